@@ -1,0 +1,191 @@
+/*
+ * scm.h — C ABI of the MI355X-native sequential SIFT feature-matching stage.
+ *
+ * Drop-in boundary for the reference's Scanner op
+ *   REGISTER_OP(SequentialMatchingCPU) / SequentialMatchingCPUKernel
+ *   (reference integration/op_cpp/sequential_matching.cc:27-205)
+ * loaded by integration/feature_matching.py:39-54.
+ *
+ * All buffers crossing this boundary are host memory laid out exactly as the
+ * reference's io.cc codecs write them (integration/op_cpp/io.cc), so a Scanner
+ * kernel (see scanner_colmap_amd/csrc/scanner_op/) or any FFI (ctypes, see
+ * scanner_colmap_amd/_abi.py) can call it with the bytes Scanner hands over.
+ * Plain C types only: no torch / HIP types in the signatures.
+ *
+ * Error convention: every int-returning entry point returns SCM_OK (0) on
+ * success and a negative SCM_E_* code otherwise; scm_last_error() returns a
+ * thread-local message.  The reference aborts the worker through glog CHECK
+ * (no return codes); the Scanner-side op maps a non-zero status to the same
+ * fatal abort (scanner_op/sequential_matching_gpu.cc).
+ *
+ * Threading (reference: one kernel instance per Scanner pipeline instance,
+ * execute() serial per instance, sequential_matching.cc:103): an scm_context
+ * is NOT re-entrant; distinct contexts may be used from distinct threads.
+ */
+#ifndef SCM_H_
+#define SCM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SCM_ABI_VERSION 1
+
+enum {
+  SCM_OK = 0,
+  SCM_E_INVALID = -1,   /* malformed argument / element bytes            */
+  SCM_E_DEVICE = -2,    /* HIP runtime error, or no gfx950 device        */
+  SCM_E_NOMEM = -3,     /* host or device allocation failed              */
+  SCM_E_CAPACITY = -4,  /* caller buffer too small (size written back)   */
+  SCM_E_STATE = -5      /* call order (e.g. table_run before table_load) */
+};
+
+/* colmap::TwoViewGeometry::ConfigurationType [upstream
+ * estimators/two_view_geometry.h], SURVEY.md §8a a18. */
+enum {
+  SCM_TVG_UNDEFINED = 0,
+  SCM_TVG_DEGENERATE = 1,
+  SCM_TVG_CALIBRATED = 2,
+  SCM_TVG_UNCALIBRATED = 3,
+  SCM_TVG_PLANAR = 4,
+  SCM_TVG_PANORAMIC = 5,
+  SCM_TVG_PLANAR_OR_PANORAMIC = 6,
+  SCM_TVG_WATERMARK = 7,
+  SCM_TVG_MULTIPLE = 8
+};
+
+/* Options.  Fields 1-14 mirror siftFeatureMatchingArgs (reference
+ * integration/op_cpp/colmap.proto:6-49), overlap/loop fields mirror
+ * SequentialMatchingArgs (colmap.proto:55-65), and the remaining fields are
+ * the colmap::TwoViewGeometry::Options / RANSACOptions defaults that
+ * sequential_matching.cc:64-75 leaves untouched.  scm_default_options() fills
+ * the proto2 defaults — the values the reference runs with, because
+ * feature_matching.py:50-54 passes no op args. */
+typedef struct scm_matching_options {
+  int32_t use_gpu;                   /* colmap.proto:7   default 0      */
+  int32_t gpu_index;                 /* colmap.proto:11  default "-1"   */
+  double max_ratio;                  /* colmap.proto:14  default 0.8    */
+  double max_distance;               /* colmap.proto:17  default 0.7    */
+  int32_t cross_check;               /* colmap.proto:20  default 1      */
+  int32_t max_num_matches;           /* colmap.proto:23  default 32768  */
+  float max_error;                   /* colmap.proto:26  default 4.0    */
+  double confidence;                 /* colmap.proto:29  default 0.999  */
+  int32_t min_num_trials;            /* colmap.proto:33  default 30     */
+  int32_t max_num_trials;            /* colmap.proto:34  default 10000  */
+  double min_inlier_ratio;           /* colmap.proto:38  default 0.25   */
+  int32_t min_num_inliers;           /* colmap.proto:42  default 15     */
+  int32_t multiple_models;           /* colmap.proto:45  default 0      */
+  int32_t guided_matching;           /* colmap.proto:48  default 0      */
+  int32_t loop_detection;            /* colmap.proto:57  default 0      */
+  int32_t overlap;                   /* colmap.proto:59  default 10     */
+  int32_t quadratic_overlap;         /* colmap.proto:62  default 0      */
+  double min_E_F_inlier_ratio;       /* COLMAP default 0.95             */
+  double max_H_inlier_ratio;         /* COLMAP default 0.8              */
+  double watermark_min_inlier_ratio; /* COLMAP default 0.7              */
+  double watermark_border_size;      /* COLMAP default 0.1              */
+  int32_t detect_watermark;          /* COLMAP default 1                */
+  double dyn_num_trials_multiplier;  /* COLMAP RANSACOptions default 3  */
+  /* The reference's RANSAC PRNG is thread-local and time-seeded (COLMAP
+   * SetPRNGSeed is never called), so its geometry output is not reproducible.
+   * Here every pair draws from a fresh std::mt19937 seeded with
+   * scm_pair_seed(ransac_seed, image_id1, image_id2). */
+  uint32_t ransac_seed;              /* default 0                       */
+} scm_matching_options;
+
+/* One Scanner element: a borrowed, read-only byte range (scanner::Element,
+ * reference io.cc:67-68). */
+typedef struct scm_element {
+  const uint8_t* buffer;
+  size_t size;
+} scm_element;
+
+/* An output element produced by the library (scanner::new_buffer +
+ * insert_element, io.cc:157/272/86).  Release with scm_blob_free. */
+typedef struct scm_blob {
+  uint8_t* data;
+  size_t size;
+} scm_blob;
+
+typedef struct scm_context scm_context;
+
+/* ---- options / utilities -------------------------------------------- */
+int32_t scm_abi_version(void);
+const char* scm_last_error(void);
+void scm_default_options(scm_matching_options* opts);
+/* Decode a serialised SequentialMatchingArgs (proto2 wire format) into opts,
+ * starting from the defaults — replaces SequentialMatchingArgs::ParseFromArray
+ * + parseConfigs (sequential_matching.cc:36-76). */
+int scm_parse_args(const uint8_t* bytes, size_t size, scm_matching_options* opts);
+uint32_t scm_pair_seed(uint32_t base_seed, uint32_t image_id1, uint32_t image_id2);
+void scm_blob_free(scm_blob* blob);
+
+/* ---- kernel instance (SequentialMatchingCPUKernel ctor, :30-33) ------- */
+/* Binds one HIP device (Scanner KernelConfig.devices[0]); owns one stream
+ * and its HBM workspace.  Fails with SCM_E_DEVICE if no gfx950 device. */
+int scm_context_create(int32_t device_index, const scm_matching_options* opts,
+                       scm_context** out);
+void scm_context_destroy(scm_context* ctx);
+
+/* ---- hot path, pair granularity -------------------------------------- */
+/* colmap::MatchSiftFeaturesCPU replacement (sequential_matching.cc:154-155):
+ * u8 descriptors, row-major N x 128.  Writes the cross-checked matches as
+ * (idx1, idx2) uint32 pairs sorted by idx1 into matches[0 .. 2*cap).  On
+ * SCM_E_CAPACITY *num_matches holds the required count. */
+int scm_match_pair(scm_context* ctx, const uint8_t* desc1, int64_t n1,
+                   const uint8_t* desc2, int64_t n2, uint32_t* matches,
+                   int64_t cap, int64_t* num_matches);
+
+/* verifyTwoViewGeometry + post-filter replacement (sequential_matching.cc:
+ * 84-101, 164-178): keypoints are FeatureKeypoint rows {x,y,a11,a12,a21,a22}
+ * (float32, 24 B).  Writes one TwoViewGeometry in the io.cc per-TVG byte
+ * layout (io.cc:279-292) to *tvg_out. */
+int scm_verify_pair(scm_context* ctx, const float* kp1, int64_t n1,
+                    const float* kp2, int64_t n2, const uint32_t* matches,
+                    int64_t num_matches, uint32_t image_id1, uint32_t image_id2,
+                    scm_blob* tvg_out);
+
+/* ---- hot path, op granularity ---------------------------------------- */
+/* SequentialMatchingCPUKernel::execute replacement (:103-185) for ONE output
+ * row: stencil_size elements of each input column (image_ids: size_t id,
+ * io.cc:67; keypoints: io.cc:115-147 vector blob; descriptors: io.cc:180-194
+ * matrix blob).  Produces the two output elements pair_image_ids
+ * (io.cc:151-176) and two_view_geometries (io.cc:256-297). */
+int scm_execute_stencil(scm_context* ctx, int64_t stencil_size,
+                        const scm_element* image_ids,
+                        const scm_element* keypoints,
+                        const scm_element* descriptors,
+                        scm_blob* pair_image_ids_out, scm_blob* tvgs_out);
+
+/* ---- table granularity (HBM-resident batch path) ---------------------- */
+/* Decode and upload num_rows rows of the `extraction` table (columns
+ * image_id / keypoints / descriptors, feature_matching.py:61-68) into HBM. */
+int scm_table_load(scm_context* ctx, int64_t num_rows,
+                   const scm_element* image_ids, const scm_element* keypoints,
+                   const scm_element* descriptors);
+/* Run the stencil range(0, overlap) (feature_matching.py:43) for output rows
+ * [row_begin, row_end) of the loaded table; writes (row_end - row_begin)
+ * pair_image_ids and two_view_geometries elements.  Row i is paired with rows
+ * i+1 .. min(i+overlap-1, num_rows-1). */
+int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin,
+                  int64_t row_end, scm_blob* pair_image_ids_out,
+                  scm_blob* tvgs_out);
+/* Raw cross-checked matches of the most recent scm_table_run for the pair
+ * (row, row + offset), offset in [1, overlap); the debug `matches` output the
+ * bit-exact checks read. */
+int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset,
+                      uint32_t* matches, int64_t cap, int64_t* num_matches);
+
+/* Per-stage device time of the most recent scm_table_run, milliseconds,
+ * measured with HIP events on the context's stream:
+ * t[0] = descriptor-distance + top-2 kernel, t[1] = match finalize,
+ * t[2] = RANSAC hypothesis kernels, t[3] = whole run (wall). */
+int scm_table_timings(scm_context* ctx, double* t, int32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SCM_H_ */

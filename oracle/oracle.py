@@ -1,0 +1,179 @@
+"""ctypes wrapper of the CPU oracle (oracle/build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, always as the checker / the timed CPU baseline.
+See oracle.cc for what it restates and its parity status ("parity unpinned"
+at the COLMAP boundary; pinned by known-answer tests).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from ctypes import (POINTER, byref, c_double, c_float, c_int, c_int32, c_int64,
+                    c_size_t, c_uint8, c_uint32, c_void_p)
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB):
+        build()
+    from scanner_colmap_amd._abi import Element, MatchingOptions  # struct layouts only
+    L = ctypes.CDLL(LIB)
+    L.oracle_default_options.argtypes = [POINTER(MatchingOptions)]
+    L.oracle_default_options.restype = None
+    L.oracle_pair_seed.argtypes = [c_uint32, c_uint32, c_uint32]
+    L.oracle_pair_seed.restype = c_uint32
+    L.oracle_match_pair.argtypes = [POINTER(MatchingOptions), c_void_p, c_int64, c_void_p,
+                                    c_int64, c_void_p, c_int64, POINTER(c_int64)]
+    L.oracle_row_top2.argtypes = [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
+                                  c_void_p]
+    L.oracle_acosf_normed.argtypes = [c_int32]
+    L.oracle_acosf_normed.restype = c_float
+    L.oracle_verify_pair.argtypes = [POINTER(MatchingOptions), c_void_p, c_int64, c_void_p,
+                                     c_int64, c_void_p, c_int64, c_uint32, c_uint32,
+                                     POINTER(POINTER(c_uint8)), POINTER(c_size_t)]
+    L.oracle_loransac.argtypes = [POINTER(MatchingOptions), c_int32, c_void_p, c_void_p,
+                                  c_int64, c_uint32, c_void_p, POINTER(c_int64),
+                                  POINTER(c_double), POINTER(c_int64), c_void_p]
+    L.oracle_std_uniform.argtypes = [c_uint32, c_void_p, c_void_p, c_int64, c_void_p]
+    L.oracle_execute_stencil.argtypes = [POINTER(MatchingOptions), c_int64, POINTER(Element),
+                                         POINTER(Element), POINTER(Element),
+                                         POINTER(POINTER(c_uint8)), POINTER(c_size_t),
+                                         POINTER(POINTER(c_uint8)), POINTER(c_size_t)]
+    L.oracle_table_run.argtypes = [POINTER(MatchingOptions), c_int64, POINTER(Element),
+                                   POINTER(Element), POINTER(Element), c_int64, c_int64,
+                                   c_int64, POINTER(POINTER(c_uint8)), POINTER(c_size_t),
+                                   POINTER(POINTER(c_uint8)), POINTER(c_size_t)]
+    L.oracle_free.argtypes = [POINTER(c_uint8)]
+    L.oracle_free.restype = None
+    _lib = L
+    return L
+
+
+def default_options():
+    from scanner_colmap_amd._abi import MatchingOptions
+    o = MatchingOptions()
+    lib().oracle_default_options(byref(o))
+    return o
+
+
+def pair_seed(base, id1, id2) -> int:
+    return int(lib().oracle_pair_seed(base, id1, id2))
+
+
+def _take(p, n) -> bytes:
+    b = ctypes.string_at(p, n) if n else b""
+    lib().oracle_free(p)
+    return b
+
+
+def match_pair(d1, d2, opts=None) -> np.ndarray:
+    opts = opts or default_options()
+    a = np.ascontiguousarray(d1, dtype=np.uint8).reshape(-1, 128)
+    b = np.ascontiguousarray(d2, dtype=np.uint8).reshape(-1, 128)
+    cap = max(1, min(len(a), len(b)))
+    out = np.zeros((cap, 2), dtype=np.uint32)
+    m = c_int64()
+    rc = lib().oracle_match_pair(byref(opts), a.ctypes.data, len(a), b.ctypes.data, len(b),
+                                 out.ctypes.data, cap, byref(m))
+    assert rc == 0, rc
+    return out[: m.value].copy()
+
+
+def row_top2(d1, d2):
+    a = np.ascontiguousarray(d1, dtype=np.uint8).reshape(-1, 128)
+    b = np.ascontiguousarray(d2, dtype=np.uint8).reshape(-1, 128)
+    best = np.zeros(len(a), np.int32)
+    second = np.zeros(len(a), np.int32)
+    idx = np.zeros(len(a), np.int32)
+    lib().oracle_row_top2(a.ctypes.data, len(a), b.ctypes.data, len(b), best.ctypes.data,
+                          second.ctypes.data, idx.ctypes.data)
+    return best, second, idx
+
+
+def acosf_normed(d: int) -> float:
+    return float(lib().oracle_acosf_normed(int(d)))
+
+
+def verify_pair(kp1, kp2, matches, id1, id2, opts=None) -> bytes:
+    opts = opts or default_options()
+    k1 = np.ascontiguousarray(kp1, dtype=np.float32).reshape(-1, 6)
+    k2 = np.ascontiguousarray(kp2, dtype=np.float32).reshape(-1, 6)
+    m = np.ascontiguousarray(matches, dtype=np.uint32).reshape(-1, 2)
+    p = POINTER(c_uint8)()
+    n = c_size_t()
+    rc = lib().oracle_verify_pair(byref(opts), k1.ctypes.data, len(k1), k2.ctypes.data, len(k2),
+                                  m.ctypes.data, len(m), id1, id2, byref(p), byref(n))
+    assert rc == 0
+    return _take(p, n.value)
+
+
+def loransac(kind, x1, x2, seed, opts=None):
+    opts = opts or default_options()
+    a = np.ascontiguousarray(x1, dtype=np.float64).reshape(-1, 2)
+    b = np.ascontiguousarray(x2, dtype=np.float64).reshape(-1, 2)
+    model = np.zeros(9)
+    ni, nt = c_int64(), c_int64()
+    rs = c_double()
+    mask = np.zeros(len(a), np.uint8)
+    ok = lib().oracle_loransac(byref(opts), kind, a.ctypes.data, b.ctypes.data, len(a), seed,
+                               model.ctypes.data, byref(ni), byref(rs), byref(nt),
+                               mask.ctypes.data)
+    return dict(success=bool(ok), model=model, num_inliers=ni.value, residual_sum=rs.value,
+                num_trials=nt.value, mask=mask.astype(bool))
+
+
+def std_uniform(seed, lo, hi) -> np.ndarray:
+    lo = np.ascontiguousarray(lo, dtype=np.uint32)
+    hi = np.ascontiguousarray(hi, dtype=np.uint32)
+    out = np.zeros(len(lo), np.uint32)
+    lib().oracle_std_uniform(seed, lo.ctypes.data, hi.ctypes.data, len(lo), out.ctypes.data)
+    return out
+
+
+def _elements(chunks):
+    from scanner_colmap_amd._abi import _elements as e
+    return e(chunks)
+
+
+def execute_stencil(ids, kps, descs, opts=None):
+    opts = opts or default_options()
+    e1, k1 = _elements(ids)
+    e2, k2 = _elements(kps)
+    e3, k3 = _elements(descs)
+    pa, pb = POINTER(c_uint8)(), POINTER(c_uint8)()
+    na, nb = c_size_t(), c_size_t()
+    rc = lib().oracle_execute_stencil(byref(opts), len(ids), e1, e2, e3, byref(pa), byref(na),
+                                      byref(pb), byref(nb))
+    assert rc == 0, rc
+    return _take(pa, na.value), _take(pb, nb.value)
+
+
+def table_run(ids, kps, descs, overlap, row_begin, row_end, opts=None):
+    opts = opts or default_options()
+    e1, k1 = _elements(ids)
+    e2, k2 = _elements(kps)
+    e3, k3 = _elements(descs)
+    n = row_end - row_begin
+    pa = (POINTER(c_uint8) * n)()
+    pb = (POINTER(c_uint8) * n)()
+    na = (c_size_t * n)()
+    nb = (c_size_t * n)()
+    rc = lib().oracle_table_run(byref(opts), len(ids), e1, e2, e3, overlap, row_begin, row_end,
+                                pa, na, pb, nb)
+    assert rc == 0, rc
+    return ([_take(pa[i], na[i]) for i in range(n)], [_take(pb[i], nb[i]) for i in range(n)])

@@ -1,0 +1,245 @@
+"""ctypes binding of the product C ABI (include/scm.h, lib/libscm.so).
+
+This is the Python-side FFI a Scanner job script (reference
+integration/feature_matching.py:39-54) would use in place of
+``db.load_op(libsequential_matching.so)``.  There is no CPU fallback: if
+the HIP library cannot be loaded, or no gfx950 device is visible,
+``Context`` raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (POINTER, Structure, byref, c_char_p, c_double, c_float,
+                    c_int, c_int32, c_int64, c_size_t, c_uint8, c_uint32,
+                    c_void_p)
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libscm.so")
+
+SCM_OK = 0
+SCM_E_INVALID = -1
+SCM_E_DEVICE = -2
+SCM_E_NOMEM = -3
+SCM_E_CAPACITY = -4
+SCM_E_STATE = -5
+
+# Every function include/scm.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "scm_abi_version", "scm_last_error", "scm_default_options",
+    "scm_parse_args", "scm_pair_seed", "scm_blob_free",
+    "scm_context_create", "scm_context_destroy", "scm_match_pair",
+    "scm_verify_pair", "scm_execute_stencil", "scm_table_load",
+    "scm_table_run", "scm_table_matches", "scm_table_timings",
+)
+
+
+class MatchingOptions(Structure):
+    """scm_matching_options (include/scm.h) = colmap.proto:6-65 + COLMAP
+    TwoViewGeometry / RANSAC defaults."""
+    _fields_ = [
+        ("use_gpu", c_int32), ("gpu_index", c_int32),
+        ("max_ratio", c_double), ("max_distance", c_double),
+        ("cross_check", c_int32), ("max_num_matches", c_int32),
+        ("max_error", c_float), ("confidence", c_double),
+        ("min_num_trials", c_int32), ("max_num_trials", c_int32),
+        ("min_inlier_ratio", c_double), ("min_num_inliers", c_int32),
+        ("multiple_models", c_int32), ("guided_matching", c_int32),
+        ("loop_detection", c_int32), ("overlap", c_int32),
+        ("quadratic_overlap", c_int32),
+        ("min_E_F_inlier_ratio", c_double), ("max_H_inlier_ratio", c_double),
+        ("watermark_min_inlier_ratio", c_double),
+        ("watermark_border_size", c_double), ("detect_watermark", c_int32),
+        ("dyn_num_trials_multiplier", c_double), ("ransac_seed", c_uint32),
+    ]
+
+
+class Element(Structure):
+    _fields_ = [("buffer", POINTER(c_uint8)), ("size", c_size_t)]
+
+
+class Blob(Structure):
+    _fields_ = [("data", POINTER(c_uint8)), ("size", c_size_t)]
+
+
+class ScmError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"scm error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libscm.so (raises OSError if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise OSError(f"{path} not built: run `make -C scanner_colmap_amd/csrc` "
+                      "or __graft_entry__.build()")
+    lib = ctypes.CDLL(path)
+    lib.scm_abi_version.restype = c_int32
+    lib.scm_last_error.restype = c_char_p
+    lib.scm_default_options.argtypes = [POINTER(MatchingOptions)]
+    lib.scm_parse_args.argtypes = [c_void_p, c_size_t, POINTER(MatchingOptions)]
+    lib.scm_pair_seed.argtypes = [c_uint32, c_uint32, c_uint32]
+    lib.scm_pair_seed.restype = c_uint32
+    lib.scm_blob_free.argtypes = [POINTER(Blob)]
+    lib.scm_context_create.argtypes = [c_int32, POINTER(MatchingOptions), POINTER(c_void_p)]
+    lib.scm_context_destroy.argtypes = [c_void_p]
+    lib.scm_match_pair.argtypes = [c_void_p, c_void_p, c_int64, c_void_p, c_int64,
+                                   c_void_p, c_int64, POINTER(c_int64)]
+    lib.scm_verify_pair.argtypes = [c_void_p, c_void_p, c_int64, c_void_p, c_int64,
+                                    c_void_p, c_int64, c_uint32, c_uint32, POINTER(Blob)]
+    lib.scm_execute_stencil.argtypes = [c_void_p, c_int64, POINTER(Element),
+                                        POINTER(Element), POINTER(Element),
+                                        POINTER(Blob), POINTER(Blob)]
+    lib.scm_table_load.argtypes = [c_void_p, c_int64, POINTER(Element),
+                                   POINTER(Element), POINTER(Element)]
+    lib.scm_table_run.argtypes = [c_void_p, c_int64, c_int64, c_int64,
+                                  POINTER(Blob), POINTER(Blob)]
+    lib.scm_table_matches.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64,
+                                      POINTER(c_int64)]
+    lib.scm_table_timings.argtypes = [c_void_p, POINTER(c_double), c_int32]
+    for name in EXPORTS:
+        if name not in ("scm_abi_version", "scm_last_error", "scm_default_options",
+                        "scm_pair_seed", "scm_blob_free", "scm_context_destroy"):
+            getattr(lib, name).restype = c_int
+    lib.scm_default_options.restype = None
+    lib.scm_blob_free.restype = None
+    lib.scm_context_destroy.restype = None
+    _lib = lib
+    return lib
+
+
+def default_options() -> MatchingOptions:
+    o = MatchingOptions()
+    load_library().scm_default_options(byref(o))
+    return o
+
+
+def parse_args(data: bytes) -> MatchingOptions:
+    o = MatchingOptions()
+    buf = ctypes.create_string_buffer(data, len(data)) if data else None
+    _check(load_library().scm_parse_args(buf, len(data), byref(o)))
+    return o
+
+
+def pair_seed(base: int, id1: int, id2: int) -> int:
+    return int(load_library().scm_pair_seed(base, id1, id2))
+
+
+def _check(rc: int) -> None:
+    if rc != SCM_OK:
+        msg = load_library().scm_last_error()
+        raise ScmError(rc, msg.decode() if msg else "")
+
+
+def _blob_bytes(b: Blob) -> bytes:
+    out = ctypes.string_at(b.data, b.size) if b.size else b""
+    load_library().scm_blob_free(byref(b))
+    return out
+
+
+def _elements(chunks) -> tuple:
+    """Build a ctypes Element array over a list of bytes / numpy buffers
+    (kept alive by the returned tuple)."""
+    keep = []
+    arr = (Element * max(1, len(chunks)))()
+    for i, c in enumerate(chunks):
+        a = np.frombuffer(c, dtype=np.uint8) if isinstance(c, (bytes, bytearray)) else c
+        a = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
+        keep.append(a)
+        arr[i].buffer = a.ctypes.data_as(POINTER(c_uint8))
+        arr[i].size = a.nbytes
+    return arr, keep
+
+
+class Context:
+    """One kernel instance on one HIP device (SequentialMatchingCPUKernel
+    constructor, sequential_matching.cc:30-33)."""
+
+    def __init__(self, device: int = 0, options: MatchingOptions | None = None):
+        self._lib = load_library()
+        self._ptr = c_void_p()
+        opts = options if options is not None else default_options()
+        self.options = opts
+        _check(self._lib.scm_context_create(device, byref(opts), byref(self._ptr)))
+
+    def close(self) -> None:
+        if self._ptr:
+            self._lib.scm_context_destroy(self._ptr)
+            self._ptr = c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --- pair granularity -------------------------------------------------
+    def match_pair(self, desc1: np.ndarray, desc2: np.ndarray) -> np.ndarray:
+        d1 = np.ascontiguousarray(desc1, dtype=np.uint8).reshape(-1, 128)
+        d2 = np.ascontiguousarray(desc2, dtype=np.uint8).reshape(-1, 128)
+        cap = max(1, min(len(d1), len(d2)))
+        out = np.zeros((cap, 2), dtype=np.uint32)
+        n = c_int64()
+        _check(self._lib.scm_match_pair(self._ptr, d1.ctypes.data, len(d1), d2.ctypes.data,
+                                        len(d2), out.ctypes.data, cap, byref(n)))
+        return out[: n.value].copy()
+
+    def verify_pair(self, kp1: np.ndarray, kp2: np.ndarray, matches: np.ndarray,
+                    id1: int, id2: int) -> bytes:
+        k1 = np.ascontiguousarray(kp1, dtype=np.float32).reshape(-1, 6)
+        k2 = np.ascontiguousarray(kp2, dtype=np.float32).reshape(-1, 6)
+        m = np.ascontiguousarray(matches, dtype=np.uint32).reshape(-1, 2)
+        b = Blob()
+        _check(self._lib.scm_verify_pair(self._ptr, k1.ctypes.data, len(k1), k2.ctypes.data,
+                                         len(k2), m.ctypes.data, len(m), id1, id2, byref(b)))
+        return _blob_bytes(b)
+
+    # --- op granularity ---------------------------------------------------
+    def execute_stencil(self, ids, kps, descs) -> tuple[bytes, bytes]:
+        e_ids, k1 = _elements(ids)
+        e_kps, k2 = _elements(kps)
+        e_desc, k3 = _elements(descs)
+        a, b = Blob(), Blob()
+        _check(self._lib.scm_execute_stencil(self._ptr, len(ids), e_ids, e_kps, e_desc,
+                                             byref(a), byref(b)))
+        return _blob_bytes(a), _blob_bytes(b)
+
+    # --- table granularity ------------------------------------------------
+    def table_load(self, ids, kps, descs) -> None:
+        e_ids, k1 = _elements(ids)
+        e_kps, k2 = _elements(kps)
+        e_desc, k3 = _elements(descs)
+        _check(self._lib.scm_table_load(self._ptr, len(ids), e_ids, e_kps, e_desc))
+
+    def table_run(self, overlap: int, row_begin: int, row_end: int):
+        n = row_end - row_begin
+        a = (Blob * max(1, n))()
+        b = (Blob * max(1, n))()
+        _check(self._lib.scm_table_run(self._ptr, overlap, row_begin, row_end, a, b))
+        return [_blob_bytes(a[i]) for i in range(n)], [_blob_bytes(b[i]) for i in range(n)]
+
+    def table_matches(self, row: int, offset: int, cap: int = 1 << 16) -> np.ndarray:
+        out = np.zeros((max(1, cap), 2), dtype=np.uint32)
+        n = c_int64()
+        _check(self._lib.scm_table_matches(self._ptr, row, offset, out.ctypes.data, cap,
+                                           byref(n)))
+        return out[: n.value].copy()
+
+    def table_timings(self) -> dict:
+        t = (c_double * 4)()
+        _check(self._lib.scm_table_timings(self._ptr, t, 4))
+        return {"match_ms": t[0], "finalize_ms": t[1], "verify_ms": t[2], "wall_ms": t[3]}

@@ -1,0 +1,48 @@
+// Shared constants / job descriptors of the matcher kernels (match_kernels.hip)
+// and their host launchers (scm_runtime.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace scm {
+
+constexpr int kMatchWaves = 8;                   // waves per workgroup
+constexpr int kMatchThreads = kMatchWaves * 64;  // 512
+constexpr int kRowsPerBlock = kMatchWaves * 64;  // pivot rows per workgroup
+constexpr int kTileBytes = 32 * 256;             // 32 bf16 descriptors
+constexpr int kTilesPerSeg = 256;                // 8 tile-index bits per key
+constexpr int kColsPerSeg = kTilesPerSeg * 32;   // 8192 columns per segment
+constexpr int kIdxBits = 13;
+constexpr uint32_t kIdxMask = (1u << kIdxBits) - 1u;
+constexpr uint32_t kLutMax = 1u << 18;           // acosf LUT covers [0, 2^18]
+constexpr int kFinThreads = 1024;
+
+// One workgroup of match_tiles_kernel: 512 rows of a pivot image against
+// every column of `npairs` neighbour images (pairs[pair0 .. pair0+npairs)).
+struct MatchJob {
+  int64_t a_row;   // table row of the pivot image's descriptor 0
+  int32_t rb;      // row block
+  int32_t n1;      // pivot keypoints
+  int32_t pair0;   // first PairDesc of this pivot
+  int32_t npairs;
+};
+
+struct PairDesc {
+  int64_t b_row;        // table row of the neighbour's descriptor 0
+  int64_t rowres_off;   // uint2 offset: [nseg][n1]
+  int64_t colpart_off;  // uint2 offset: [nrb][n2pad]
+  int64_t m21_off;      // int32 offset: [n2]
+  int64_t match_off;    // uint2 offset: [n1]
+  int32_t n1, n2, n2pad, nseg, nrb, pad_;
+};
+
+hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int njobs,
+                              const PairDesc* pairs, uint2* rowres, uint2* colpart,
+                              bool clamp, hipStream_t stream);
+hipError_t launch_match_finalize(const PairDesc* pairs, int npairs, const uint2* rowres,
+                                 const uint2* colpart, int32_t* m21, const float* lut,
+                                 float max_ratio, float max_distance, int cross_check,
+                                 uint2* matches, int32_t* counts, hipStream_t stream);
+hipError_t launch_u8_to_bf16(const uint8_t* in, uint16_t* out, int64_t n, hipStream_t stream);
+
+}  // namespace scm

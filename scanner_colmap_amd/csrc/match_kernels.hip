@@ -1,0 +1,390 @@
+// Kernel 1 of the sequential-matching stage: brute-force SIFT descriptor
+// similarity on bf16 MFMA with a fused, bit-exact two-way top-2 reduction,
+// plus the finalize kernel (ratio / distance tests, cross-check, ordered
+// compaction).
+//
+// Replaces colmap::MatchSiftFeaturesCPU as called from
+// SequentialMatchingCPUKernel::execute (reference
+// integration/op_cpp/sequential_matching.cc:154-155), i.e. the upstream
+// ComputeSiftDistanceMatrix + FindBestMatchesOneWay x2 + FindBestMatches
+// (SURVEY.md §8a a5-a7).  The int32 N1 x N2 matrix is never materialised.
+//
+// Exactness (SURVEY.md §8a "Exactness facts"):
+//  * u8 descriptors are exact in bf16; each MFMA chain starts from an
+//    accumulator tuple holding 2^23, so every partial sum is an integer in
+//    [2^23, 2^24) — exact in f32 — and the f32 bit pattern of the result is
+//    0x4B000000 | dot (dot <= 128*255^2 < 2^23).  Verified on gfx950
+//    (probes/probe_mfma.hip, including all-255 operands).
+//  * Ordering keys are 32-bit: key = (dot << 13) | 13 index bits, where the
+//    index bits are [row code i (4 bits) | spare | tile index t (8 bits)].
+//    Fast variant: the pivot's bf16 operand is pre-scaled by 16 (exact) and
+//    the accumulator of register i starts at 2^23 + (15 - i), so the MFMA
+//    result bits are 0x4B000000 | dot << 4 | (15 - i) and ONE v_lshl_or_b32
+//    (acc << 9 | t-bits from an SGPR) forms the key.  This needs dot < 2^19
+//    for every pair of rows, which the host guarantees from exact squared
+//    norms (|a||b| < 2^19; RootSIFT u8 descriptors have |a|^2 ~ 2^18).
+//  * Otherwise the CLAMP variant (unscaled operand, accumulator 2^23) uses
+//    min(dot, 2^18), which changes no output: acosf(min(d * 2^-18, 1)) is 0
+//    for every d >= 2^18, so any (best, second) >= 2^18 fails the ratio test
+//    and a unique best above 2^18 keeps its index.
+//  * max(key) = largest dot, lowest index among ties (FindBestMatchesOneWay
+//    keeps the first maximum; equal values fall to "second"); the running
+//    second is med3(key, best, second).  Both merges are associative, so the
+//    tile-parallel reduction equals the sequential scan bit for bit.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "match_kernels.h"
+
+namespace scm {
+
+typedef __attribute__((ext_vector_type(8))) short bf16x8;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+
+__device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t d;
+  asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+__device__ __forceinline__ uint32_t merge_second(uint32_t b1a, uint32_t b2a,
+                                                 uint32_t b1b, uint32_t b2b) {
+  const uint32_t lo = min(b1a, b1b) & ~kIdxMask;
+  return max(max(b2a, b2b), lo);
+}
+
+// One workgroup = one MatchJob = 512 rows of the pivot image (8 waves x 64
+// rows, two 32-row MFMA sub-tiles per wave, A fragments register-resident)
+// swept against every column of every neighbour image of the job, 32 columns
+// per LDS tile.  Per element (fast variant): 1 v_lshl_or (key) + 2 row-state
+// ops + 2 column-state ops.
+template <bool CLAMP>
+__global__ __launch_bounds__(kMatchThreads, 2) void match_tiles_kernel(
+    const uint16_t* __restrict__ desc,        // bf16 table, [rows][128]
+    const MatchJob* __restrict__ jobs,
+    const PairDesc* __restrict__ pairs,
+    uint2* __restrict__ rowres,               // per pair [nseg][n1]
+    uint2* __restrict__ colpart) {            // per pair [nrb][n2pad]
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kTileBytes + 2 * kMatchWaves * 32 * 8];
+  uint2* colscratch = reinterpret_cast<uint2*>(lds + 2 * kTileBytes);
+
+  const MatchJob job = jobs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+
+  // ---- A fragments: rows rb*512 + wave*64 + 32*s + r, 16-B chunks h*8+q.
+  bf16x8 afrag[2][8];
+  {
+    const int64_t a_base = job.a_row;  // first table row of the pivot image
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int row = job.rb * kRowsPerBlock + wave * 64 + 32 * s + r;
+      const bool ok = row < job.n1;
+      const uint4* src = reinterpret_cast<const uint4*>(desc + (a_base + (ok ? row : 0)) * 128) + h * 8;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        uint4 v = ok ? src[q] : make_uint4(0, 0, 0, 0);
+        if (!CLAMP) {  // x16: +4 on the bf16 exponent of every non-zero element
+          uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const uint32_t lo = w[e] & 0xFFFFu, hi = w[e] >> 16;
+            w[e] = (lo ? lo + 0x200u : 0u) | ((hi ? hi + 0x200u : 0u) << 16);
+          }
+          v = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+        afrag[s][q] = *reinterpret_cast<bf16x8*>(&v);
+      }
+    }
+  }
+  f32x16 cinit;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) cinit[i] = CLAMP ? 8388608.0f : 8388608.0f + (float)(15 - i);
+
+  // Staging role of this thread: one 16-B chunk of the 8 KiB B tile.
+  const int st_col = tid >> 4;    // 0..31
+  const int st_chunk = tid & 15;  // 0..15
+  const int st_lds = st_col * 256 + ((st_chunk ^ (st_col & 15)) << 4);
+
+  int tile_parity = 0;
+  for (int p = 0; p < job.npairs; ++p) {
+    const PairDesc pd = pairs[job.pair0 + p];
+    const int ntiles_total = (pd.n2 + 31) >> 5;
+    uint2* colp = colpart + pd.colpart_off + (int64_t)job.rb * pd.n2pad;
+    for (int seg = 0; seg < pd.nseg; ++seg) {
+      const int t_begin = seg * kTilesPerSeg;
+      const int t_end = min(ntiles_total, t_begin + kTilesPerSeg);
+      uint32_t b1r[2][16], b2r[2][16];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { b1r[s][i] = 0u; b2r[s][i] = 0u; }
+
+      // Prologue: stage tile t_begin.
+      {
+        const uint4* src = reinterpret_cast<const uint4*>(
+            desc + (pd.b_row + (int64_t)t_begin * 32 + st_col) * 128) + st_chunk;
+        *reinterpret_cast<uint4*>(lds + tile_parity * kTileBytes + st_lds) = *src;
+      }
+      __syncthreads();
+
+      for (int t = t_begin; t < t_end; ++t) {
+        const int cur = tile_parity;
+        uint4 nxt = make_uint4(0, 0, 0, 0);
+        const bool has_next = (t + 1) < t_end;
+        if (has_next) {
+          nxt = *(reinterpret_cast<const uint4*>(
+                      desc + (pd.b_row + (int64_t)(t + 1) * 32 + st_col) * 128) + st_chunk);
+        }
+        // ---- B fragments from LDS (swizzled 16-B chunks).
+        const uint8_t* bt = lds + cur * kTileBytes + r * 256;
+        bf16x8 bfrag[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int ch = (h * 8 + q) ^ (r & 15);
+          bfrag[q] = *reinterpret_cast<const bf16x8*>(bt + (ch << 4));
+        }
+        f32x16 acc[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag[s][0], bfrag[0], cinit, 0, 0, 0);
+#pragma unroll
+          for (int q = 1; q < 8; ++q)
+            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag[s][q], bfrag[q], acc[s], 0, 0, 0);
+        }
+        // ---- Epilogue: keys, row state, column state.
+        const uint32_t tbits = (uint32_t)(kTilesPerSeg - 1 - (t - t_begin));
+        uint32_t b1c[2], b2c[2];
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          b1c[s] = 0u;
+          b2c[s] = 0u;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const uint32_t bits = __float_as_uint(acc[s][i]);
+            uint32_t key;
+            if (CLAMP)
+              key = (min(bits, 0x4B040000u) << 13) | tbits | ((uint32_t)(15 - i) << 9);
+            else
+              key = (bits << 9) | tbits;
+            b2r[s][i] = med3_u32(key, b1r[s][i], b2r[s][i]);
+            b1r[s][i] = max(b1r[s][i], key);
+            b2c[s] = med3_u32(key, b1c[s], b2c[s]);
+            b1c[s] = max(b1c[s], key);
+          }
+        }
+        // Column partial of this wave: re-key with the row inside the block,
+        // merge the two sub-tiles and the two half-waves.
+        {
+          uint32_t B1 = 0u, B2 = 0u;
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const uint32_t ii = 15u - ((b1c[s] >> 9) & 15u);
+            const uint32_t row_in_blk = (uint32_t)wave * 64u + 32u * s + (ii & 3u) + 8u * (ii >> 2) + 4u * (uint32_t)h;
+            const uint32_t k1 = (b1c[s] & ~kIdxMask) | (kIdxMask - row_in_blk);
+            const uint32_t k2 = b2c[s] & ~kIdxMask;
+            if (s == 0) { B1 = k1; B2 = k2; }
+            else { B2 = merge_second(B1, B2, k1, k2); B1 = max(B1, k1); }
+          }
+          const uint32_t o1 = __shfl_xor(B1, 32);
+          const uint32_t o2 = __shfl_xor(B2, 32);
+          B2 = merge_second(B1, B2, o1, o2);
+          B1 = max(B1, o1);
+          if (h == 0) colscratch[(cur * kMatchWaves + wave) * 32 + r] = make_uint2(B1, B2);
+        }
+        if (has_next) *reinterpret_cast<uint4*>(lds + (cur ^ 1) * kTileBytes + st_lds) = nxt;
+        __syncthreads();
+        // One wave merges the 8 wave partials of this tile and stores them.
+        if (wave == (t & (kMatchWaves - 1)) && h == 0) {
+          uint2 m = colscratch[(cur * kMatchWaves + 0) * 32 + r];
+#pragma unroll
+          for (int w = 1; w < kMatchWaves; ++w) {
+            const uint2 o = colscratch[(cur * kMatchWaves + w) * 32 + r];
+            m.y = merge_second(m.x, m.y, o.x, o.y);
+            m.x = max(m.x, o.x);
+          }
+          colp[t * 32 + r] = m;
+        }
+        tile_parity ^= 1;
+      }
+
+      // ---- Row flush for this segment: re-key with the column inside the
+      // segment, reduce over the 32 lanes of each half, store.
+      uint2* rr = rowres + pd.rowres_off + (int64_t)seg * pd.n1;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t k1 = b1r[s][i];
+          const uint32_t tl = (uint32_t)(kTilesPerSeg - 1) - (k1 & 255u);
+          const uint32_t col = tl * 32u + (uint32_t)r;
+          uint32_t B1 = (k1 & ~kIdxMask) | (kIdxMask - col);
+          uint32_t B2 = b2r[s][i] & ~kIdxMask;
+#pragma unroll
+          for (int x = 1; x < 32; x <<= 1) {
+            const uint32_t o1 = __shfl_xor(B1, x);
+            const uint32_t o2 = __shfl_xor(B2, x);
+            B2 = merge_second(B1, B2, o1, o2);
+            B1 = max(B1, o1);
+          }
+          const int row = job.rb * kRowsPerBlock + wave * 64 + 32 * s + (i & 3) + 8 * (i >> 2) + 4 * h;
+          if (r == i + 16 * s && row < pd.n1) rr[row] = make_uint2(B1, B2);
+        }
+      }
+    }
+  }
+}
+
+// Upper bound, acosf LUT: lut[d] = acosf(min(d * 2^-18, 1.0f)), d in [0, 2^18],
+// built on the host with the host libm (the reference's own acosf).
+__device__ __forceinline__ float lut_at(const float* lut, uint32_t v) {
+  return lut[v < kLutMax ? v : kLutMax];
+}
+
+// Ratio + distance test of FindBestMatchesOneWay on (best, second) values.
+__device__ __forceinline__ bool passes(const float* lut, uint32_t best, uint32_t second,
+                                       float max_ratio, float max_distance) {
+  if (best == 0u) return false;  // best_i2 == -1
+  const float bn = lut_at(lut, best);
+  if (bn > max_distance) return false;
+  const float sn = lut_at(lut, second);
+  return !(bn >= max_ratio * sn);
+}
+
+// Finalize: one workgroup per pair.  Merges column partials over row blocks
+// (ascending block order; strict '>' keeps the lowest row on ties), merges
+// row results over column segments, applies the tests, the cross-check and an
+// order-preserving compaction (matches sorted by idx1, as FindBestMatches).
+__global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
+    const PairDesc* __restrict__ pairs, const uint2* __restrict__ rowres,
+    const uint2* __restrict__ colpart, int32_t* __restrict__ m21_scratch,
+    const float* __restrict__ lut, float max_ratio, float max_distance,
+    int cross_check, uint2* __restrict__ matches, int32_t* __restrict__ counts) {
+  __shared__ int32_t wave_tot[kFinThreads / 64];
+  __shared__ int32_t wave_off[kFinThreads / 64];
+  const PairDesc pd = pairs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  int32_t* m21 = m21_scratch + pd.m21_off;
+  const uint2* cp = colpart + pd.colpart_off;
+  const uint2* rr = rowres + pd.rowres_off;
+
+  if (cross_check) {
+    for (int j = tid; j < pd.n2; j += kFinThreads) {
+      uint2 m = cp[j];
+      int best_rb = 0;
+      for (int b = 1; b < pd.nrb; ++b) {
+        const uint2 o = cp[(int64_t)b * pd.n2pad + j];
+        m.y = merge_second(m.x, m.y, o.x, o.y);
+        if (o.x > m.x) { m.x = o.x; best_rb = b; }
+      }
+      const uint32_t best = m.x >> kIdxBits, second = m.y >> kIdxBits;
+      const int32_t row = best_rb * kRowsPerBlock + (int32_t)(kIdxMask - (m.x & kIdxMask));
+      m21[j] = passes(lut, best, second, max_ratio, max_distance) ? row : -1;
+    }
+    __syncthreads();
+  }
+  // Rows: contiguous chunk per thread for the ordered compaction.
+  const int per = (pd.n1 + kFinThreads - 1) / kFinThreads;
+  const int i0 = min(pd.n1, tid * per), i1 = min(pd.n1, i0 + per);
+  int cnt = 0;
+  for (int pass = 0; pass < 2; ++pass) {
+    int out = 0;
+    if (pass == 1) {
+      // exclusive scan of cnt over the block
+      int x = cnt;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+      }
+      if (lane == 63) wave_tot[wave] = x;
+      __syncthreads();
+      if (tid == 0) {
+        int acc = 0;
+        for (int w = 0; w < kFinThreads / 64; ++w) { wave_off[w] = acc; acc += wave_tot[w]; }
+        counts[blockIdx.x] = acc;
+      }
+      __syncthreads();
+      out = wave_off[wave] + x - cnt;
+    }
+    for (int i = i0; i < i1; ++i) {
+      uint2 m = rr[i];
+      int best_seg = 0;
+      for (int sg = 1; sg < pd.nseg; ++sg) {
+        const uint2 o = rr[(int64_t)sg * pd.n1 + i];
+        m.y = merge_second(m.x, m.y, o.x, o.y);
+        if (o.x > m.x) { m.x = o.x; best_seg = sg; }
+      }
+      const uint32_t best = m.x >> kIdxBits, second = m.y >> kIdxBits;
+      const int32_t col = best_seg * (kTilesPerSeg * 32) + (int32_t)(kIdxMask - (m.x & kIdxMask));
+      bool ok = passes(lut, best, second, max_ratio, max_distance);
+      if (ok && cross_check) ok = (m21[col] == i);
+      if (ok) {
+        if (pass == 0) ++cnt;
+        else matches[pd.match_off + out++] = make_uint2((uint32_t)i, (uint32_t)col);
+      }
+    }
+  }
+}
+
+// u8 -> bf16 descriptor conversion at table load (exact: integers < 256).
+__global__ void u8_to_bf16_kernel(const uint8_t* __restrict__ in,
+                                  uint16_t* __restrict__ out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t base = i * 8;
+  if (base >= n) return;
+  if (base + 8 <= n) {
+    const uint2 v = *reinterpret_cast<const uint2*>(in + base);
+    uint32_t w[2] = {v.x, v.y};
+    uint16_t o[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const float f = (float)((w[k >> 2] >> (8 * (k & 3))) & 255u);
+      o[k] = (uint16_t)(__float_as_uint(f) >> 16);
+    }
+    *reinterpret_cast<uint4*>(out + base) = *reinterpret_cast<uint4*>(o);
+  } else {
+    for (int64_t k = base; k < n; ++k) out[k] = (uint16_t)(__float_as_uint((float)in[k]) >> 16);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host launchers.
+// ---------------------------------------------------------------------------
+hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int njobs,
+                              const PairDesc* pairs, uint2* rowres, uint2* colpart,
+                              bool clamp, hipStream_t stream) {
+  if (njobs <= 0) return hipSuccess;
+  if (clamp)
+    hipLaunchKernelGGL(match_tiles_kernel<true>, dim3(njobs), dim3(kMatchThreads), 0, stream,
+                       desc, jobs, pairs, rowres, colpart);
+  else
+    hipLaunchKernelGGL(match_tiles_kernel<false>, dim3(njobs), dim3(kMatchThreads), 0, stream,
+                       desc, jobs, pairs, rowres, colpart);
+  return hipGetLastError();
+}
+
+hipError_t launch_match_finalize(const PairDesc* pairs, int npairs, const uint2* rowres,
+                                 const uint2* colpart, int32_t* m21, const float* lut,
+                                 float max_ratio, float max_distance, int cross_check,
+                                 uint2* matches, int32_t* counts, hipStream_t stream) {
+  if (npairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(match_finalize_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
+                     rowres, colpart, m21, lut, max_ratio, max_distance, cross_check, matches,
+                     counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_u8_to_bf16(const uint8_t* in, uint16_t* out, int64_t n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int64_t threads = (n + 7) / 8;
+  hipLaunchKernelGGL(u8_to_bf16_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     stream, in, out, n);
+  return hipGetLastError();
+}
+
+}  // namespace scm

@@ -1,0 +1,112 @@
+// Internal declarations shared by the host runtime translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/scm.h"
+#include "match_kernels.h"
+
+namespace scm {
+
+void set_error(const std::string& msg);
+
+#define SCM_HIP(call)                                                        \
+  do {                                                                       \
+    hipError_t e_ = (call);                                                  \
+    if (e_ != hipSuccess) {                                                  \
+      ::scm::set_error(std::string(#call) + ": " + hipGetErrorString(e_));   \
+      return SCM_E_DEVICE;                                                   \
+    }                                                                        \
+  } while (0)
+
+#define SCM_TRY(call)        \
+  do {                       \
+    int rc_ = (call);        \
+    if (rc_ != SCM_OK) return rc_; \
+  } while (0)
+
+// Grow-only device buffer (allocation happens outside the launch sequence).
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return SCM_OK;
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    size_t want = need + need / 4 + 4096;
+    if (hipMalloc(&ptr, want) != hipSuccess) {
+      set_error("hipMalloc of " + std::to_string(want) + " bytes failed");
+      return SCM_E_NOMEM;
+    }
+    bytes = want;
+    return SCM_OK;
+  }
+  template <typename T> T* as() const { return reinterpret_cast<T*>(ptr); }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+};
+
+// Pinned host staging buffer.
+struct HostBuf {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return SCM_OK;
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+    size_t want = need + need / 4 + 4096;
+    if (hipHostMalloc(&ptr, want, hipHostMallocDefault) != hipSuccess) {
+      set_error("hipHostMalloc failed");
+      return SCM_E_NOMEM;
+    }
+    bytes = want;
+    return SCM_OK;
+  }
+  template <typename T> T* as() const { return reinterpret_cast<T*>(ptr); }
+  void release() {
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = nullptr;
+    bytes = 0;
+  }
+};
+
+struct Match {
+  uint32_t idx1, idx2;
+};
+
+// Decoded view of one table row (borrowed pointers into Scanner elements).
+struct RowView {
+  uint32_t id = 0;
+  const float* kp = nullptr;  // FeatureKeypoint rows, 6 floats
+  int64_t nkp = 0;
+  const uint8_t* desc = nullptr;
+  int64_t ndesc = 0;
+};
+
+int decode_row(const scm_element& id, const scm_element& kp, const scm_element& desc,
+               RowView* out);
+
+// One TwoViewGeometry as the op emits it (F, H row-major in memory).
+struct Tvg {
+  int32_t config = SCM_TVG_UNDEFINED;
+  double F[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  double H[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+  double tri_angle = 0.0;
+  std::vector<Match> inlier_matches;
+};
+
+void append_tvg(std::vector<uint8_t>* out, const Tvg& t);
+int make_blob(const std::vector<uint8_t>& bytes, scm_blob* out);
+std::vector<uint8_t> tvg_list_bytes(const std::vector<Tvg>& list);
+std::vector<uint8_t> id_list_bytes(const std::vector<uint32_t>& ids);
+
+}  // namespace scm

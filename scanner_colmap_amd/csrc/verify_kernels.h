@@ -1,0 +1,71 @@
+// Descriptors and launchers of the two-view-geometry kernel (verify_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace scm {
+
+constexpr int kVerifyThreads = 256;   // 4 waves per pair
+constexpr int kTrialBatch = 64;       // hypotheses solved in parallel per round
+constexpr int kLdsSampleIdx = 8192;   // sample index vector kept in LDS up to this M
+
+// Scalar options of TwoViewGeometry::EstimateUncalibrated (SURVEY.md §8a a2,
+// a9-a14) after the op's parseConfigs (sequential_matching.cc:64-75).
+struct VerifyParams {
+  double max_residual;            // max_error^2
+  double confidence;
+  double dyn_num_trials_multiplier;
+  double max_H_inlier_ratio;
+  double watermark_min_inlier_ratio;
+  double watermark_border_size;
+  int32_t min_num_trials;
+  int32_t max_trials_F;           // min(max_num_trials, ComputeNumTrials(min_inlier_ratio))
+  int32_t max_trials_H;
+  int32_t max_trials_T;           // watermark translation RANSAC (ratio 0.7)
+  int32_t min_num_inliers;
+  int32_t detect_watermark;
+  uint32_t base_seed;
+  int32_t pad_;
+};
+
+struct VerifyPair {
+  int64_t pts_off;   // double offset of xy1/xy2 (2 doubles per match)
+  int64_t scr_off;   // double offset of the per-pair scratch (6 doubles per match)
+  int64_t idx_off;   // uint32 offset of the global sample-index scratch (M > kLdsSampleIdx)
+  int64_t mask_off;  // byte offset of the F inlier mask
+  int32_t m;         // number of matches
+  uint32_t id1, id2;
+  int32_t pad_;
+};
+
+struct VerifyOut {
+  int32_t config;
+  int32_t num_inliers;   // F inliers = |inlier_matches| (0 after the post-filter)
+  int32_t f_trials, h_trials;
+  int32_t f_inliers_raw, h_inliers_raw;
+  int32_t watermark, pad_;
+  double F[9];
+  double H[9];
+};
+
+hipError_t launch_verify(const VerifyPair* pairs, int npairs, const double* xy1,
+                         const double* xy2, double* scratch, uint32_t* idx_scratch,
+                         uint8_t* masks, VerifyOut* out, const VerifyParams& params,
+                         hipStream_t stream);
+
+// Gathers the matched keypoint coordinates of each pair (float -> double,
+// FeatureKeypointsToPointsVector, sequential_matching.cc:91-92).
+struct GatherPair {
+  int64_t match_off;  // uint2 offset into the matcher's match buffer
+  int64_t kp1_off;    // float2 offset of image 1 / image 2 keypoint xy
+  int64_t kp2_off;
+  int64_t pts_off;    // destination double offset / 2
+  int32_t m;
+  int32_t pad_;
+};
+// Also packs each pair's matches contiguously at pts_off (packed).
+hipError_t launch_gather(const GatherPair* pairs, int npairs, const uint2* matches,
+                         const float2* kpxy, double* xy1, double* xy2, uint2* packed,
+                         hipStream_t stream);
+
+}  // namespace scm

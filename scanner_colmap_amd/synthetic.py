@@ -1,0 +1,125 @@
+"""Deterministic synthetic `extraction` tables (SURVEY.md §8d "Synthetic
+inputs"): a camera moving along a corridor of 3-D points, each image seeing a
+sliding window of the points so that its overlap with the next image decays
+over about `overlap` images; keypoints are noisy projections plus uniform
+outliers; descriptors are per-point base vectors perturbed per view and
+RootSIFT-normalised to uint8 like COLMAP's extractor output
+(min(255, round(512 * v))).
+
+No dataset or checkpoint is downloaded anywhere; every configuration of
+BASELINE.json is generated from a seed.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def rootsift_u8(v: np.ndarray) -> np.ndarray:
+    """L1-normalise, sqrt, L2-normalise, u8 = min(255, round(512 v))."""
+    v = np.abs(v).astype(np.float32)
+    v /= np.maximum(v.sum(axis=1, keepdims=True), 1e-12)
+    v = np.sqrt(v)
+    v /= np.maximum(np.linalg.norm(v, axis=1, keepdims=True), 1e-12)
+    return np.minimum(255.0, np.round(512.0 * v)).astype(np.uint8)
+
+
+class Corridor:
+    """Point cloud + trajectory; images are generated on demand."""
+
+    def __init__(self, num_images: int, num_kpts: int, overlap: int, seed: int,
+                 outlier_frac: float = 0.3, noise_px: float = 0.5,
+                 desc_noise: float = 0.35, focal: float = 1200.0,
+                 confuser_frac: float = 0.1):
+        self.num_images = num_images
+        self.num_kpts = num_kpts
+        self.seed = seed
+        self.outlier_frac = outlier_frac
+        self.noise_px = noise_px
+        self.desc_noise = desc_noise
+        self.focal = focal
+        self.confuser_frac = confuser_frac
+        self.overlap = overlap
+        self.visible = max(8, int(round(num_kpts * (1.0 - outlier_frac))))
+        self.step = max(1, self.visible // max(2, overlap))
+        self.num_points = self.visible + self.step * num_images
+        rng = np.random.default_rng(seed)
+        dx = 0.004
+        self.points = np.stack([
+            np.arange(self.num_points) * dx + rng.uniform(-0.5, 0.5, self.num_points) * dx,
+            rng.uniform(-3.0, 3.0, self.num_points),
+            rng.uniform(8.0, 25.0, self.num_points)], axis=1)
+        self.dx = dx
+        # Sparse, heavy-tailed base descriptors (SIFT-like histograms).
+        self.base = rng.gamma(0.5, 1.0, size=(self.num_points, 128)).astype(np.float32)
+
+    def camera(self, i: int):
+        rng = np.random.default_rng((self.seed, 7, i))
+        c = np.array([(i * self.step + self.visible / 2) * self.dx,
+                      0.2 * np.sin(i / 5.0), -0.5])
+        yaw = rng.uniform(-0.03, 0.03)
+        pitch = rng.uniform(-0.02, 0.02)
+        cy, sy, cp, sp = np.cos(yaw), np.sin(yaw), np.cos(pitch), np.sin(pitch)
+        Ry = np.array([[cy, 0, sy], [0, 1, 0], [-sy, 0, cy]])
+        Rx = np.array([[1, 0, 0], [0, cp, -sp], [0, sp, cp]])
+        return Rx @ Ry, c
+
+    def image(self, i: int):
+        """(image_id, keypoints N x 6 float32, descriptors N x 128 uint8)."""
+        rng = np.random.default_rng((self.seed, 11, i))
+        n = self.num_kpts
+        nvis = min(self.visible, n)
+        idx = np.arange(i * self.step, i * self.step + nvis)
+        R, c = self.camera(i)
+        Xc = (self.points[idx] - c) @ R.T
+        u = self.focal * Xc[:, 0] / Xc[:, 2] + 960.0 + rng.normal(0, self.noise_px, nvis)
+        v = self.focal * Xc[:, 1] / Xc[:, 2] + 540.0 + rng.normal(0, self.noise_px, nvis)
+        b = self.base[idx]
+        d_in = b + self.desc_noise * rng.gamma(0.5, 1.0, size=b.shape).astype(np.float32)
+        nout = n - nvis
+        d_out = rng.gamma(0.5, 1.0, size=(nout, 128)).astype(np.float32)
+        # Confusers: outlier keypoints carrying the descriptor of a point that
+        # is NOT visible here but is in the next images -> geometrically wrong
+        # matches that pass the ratio test (RANSAC outliers).
+        ncf = min(nout, int(round(self.confuser_frac * n)))
+        if ncf > 0:
+            lo = i * self.step + nvis
+            hi = min(self.num_points, lo + self.step * max(1, self.overlap))
+            if hi > lo:
+                pts = rng.integers(lo, hi, size=ncf)
+                d_out[:ncf] = self.base[pts] + self.desc_noise * rng.gamma(
+                    0.5, 1.0, size=(ncf, 128)).astype(np.float32)
+        xy_out = np.stack([rng.uniform(0, 1920, nout), rng.uniform(0, 1080, nout)], axis=1)
+        xy = np.concatenate([np.stack([u, v], axis=1), xy_out]).astype(np.float32)
+        desc = rootsift_u8(np.concatenate([d_in, d_out]))
+        perm = rng.permutation(n)
+        kp = np.zeros((n, 6), dtype=np.float32)
+        kp[:, 0:2] = xy[perm]
+        kp[:, 2] = 1.0
+        kp[:, 5] = 1.0
+        return i + 1, kp, np.ascontiguousarray(desc[perm])
+
+    def images(self):
+        return [self.image(i) for i in range(self.num_images)]
+
+
+def random_descriptors(n: int, seed: int) -> np.ndarray:
+    rng = np.random.default_rng(seed)
+    return rootsift_u8(rng.gamma(0.5, 1.0, size=(n, 128)))
+
+
+def tie_stress_pair(n1: int, n2: int, seed: int):
+    """Descriptor pair with duplicate rows, exact ties, zero rows and
+    saturated (255) entries: exercises lowest-index tie breaking and the
+    best == second ratio-test branch."""
+    rng = np.random.default_rng(seed)
+    a = random_descriptors(n1, seed)
+    b = random_descriptors(n2, seed + 1)
+    k = min(n1, n2) // 4
+    b[:k] = a[rng.permutation(n1)[:k]]                 # true matches
+    b[k:2 * k] = b[:k]                                   # duplicated columns -> ties
+    a[n1 // 2: n1 // 2 + k // 2] = a[: k // 2]           # duplicated rows
+    a[-3:] = 0                                           # zero rows
+    b[-2:] = 0
+    a[5, :] = 255                                        # saturated rows
+    b[7, :] = 255
+    return a, b

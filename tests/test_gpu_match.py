@@ -1,0 +1,76 @@
+"""GPU parity of kernel 1 (descriptor matching) against the CPU oracle:
+match indices must be bit-exact (BASELINE north star).
+Sizes are chosen so the oracle's faithful scalar matcher finishes in seconds."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from scanner_colmap_amd.synthetic import Corridor, random_descriptors, tie_stress_pair
+
+pytestmark = pytest.mark.gpu
+
+
+def _same(ctx, a, b):
+    got = ctx.match_pair(a, b)
+    ref = oracle.match_pair(a, b)
+    assert got.shape == ref.shape, (got.shape, ref.shape)
+    np.testing.assert_array_equal(got, ref)
+    return len(ref)
+
+
+def test_random_ragged(gpu_ctx):
+    a = random_descriptors(700, 1)
+    b = random_descriptors(901, 2)
+    b[:300] = a[100:400]
+    _same(gpu_ctx, a, b)
+
+
+def test_corridor_pairs(gpu_ctx):
+    c = Corridor(4, 1500, 3, seed=5)
+    imgs = c.images()
+    n = [_same(gpu_ctx, imgs[0][2], imgs[j][2]) for j in (1, 2, 3)]
+    assert n[0] > 100
+
+
+def test_tie_stress(gpu_ctx):
+    a, b = tie_stress_pair(1000, 777, 3)
+    _same(gpu_ctx, a, b)
+    _same(gpu_ctx, b, a)
+
+
+def test_clamp_variant_large_norms(gpu_ctx):
+    # Non-normalised descriptors (|a||b| >= 2^19) take the CLAMP kernel.
+    rng = np.random.default_rng(9)
+    a = rng.integers(0, 256, size=(600, 128), dtype=np.uint8)
+    b = rng.integers(0, 256, size=(650, 128), dtype=np.uint8)
+    b[:200] = a[:200]
+    a[10] = 255
+    b[20] = 255
+    _same(gpu_ctx, a, b)
+
+
+@pytest.mark.parametrize("n1,n2", [(0, 10), (10, 0), (1, 1), (1, 33), (33, 1), (31, 65),
+                                   (513, 47)])
+def test_edge_sizes(gpu_ctx, n1, n2):
+    a = random_descriptors(max(n1, 1), 11)[:n1]
+    b = random_descriptors(max(n2, 1), 12)[:n2]
+    if n1 and n2:
+        k = min(n1, n2)
+        b[:k // 2] = a[:k // 2]
+    _same(gpu_ctx, a, b)
+
+
+def test_zero_descriptors(gpu_ctx):
+    a = np.zeros((64, 128), np.uint8)
+    b = random_descriptors(64, 3)
+    _same(gpu_ctx, a, b)
+    _same(gpu_ctx, b, a)
+
+
+def test_segmented_columns(gpu_ctx):
+    # n2 > 8192 exercises the column segments of the row state.
+    a = random_descriptors(300, 21)
+    b = random_descriptors(8192 + 700, 22)
+    b[8500:8800] = a
+    b[100:200] = a[:100]
+    _same(gpu_ctx, a, b)
