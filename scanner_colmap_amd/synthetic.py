@@ -42,15 +42,40 @@ class Corridor:
         self.visible = max(8, int(round(num_kpts * (1.0 - outlier_frac))))
         self.step = max(1, self.visible // max(2, overlap))
         self.num_points = self.visible + self.step * num_images
-        rng = np.random.default_rng(seed)
-        dx = 0.004
-        self.points = np.stack([
-            np.arange(self.num_points) * dx + rng.uniform(-0.5, 0.5, self.num_points) * dx,
-            rng.uniform(-3.0, 3.0, self.num_points),
-            rng.uniform(8.0, 25.0, self.num_points)], axis=1)
-        self.dx = dx
-        # Sparse, heavy-tailed base descriptors (SIFT-like histograms).
-        self.base = rng.gamma(0.5, 1.0, size=(self.num_points, 128)).astype(np.float32)
+        self.dx = 0.004
+        self._blocks = {}
+
+    # Point positions and base descriptors are generated lazily in blocks of
+    # 4096 points (seeded per block), so any image of a very long sequence
+    # can be produced without materialising the whole corridor.
+    _BLOCK = 4096
+
+    def _block(self, b: int):
+        blk = self._blocks.get(b)
+        if blk is None:
+            rng = np.random.default_rng((self.seed, 3, b))
+            n = self._BLOCK
+            j = np.arange(b * n, (b + 1) * n)
+            pts = np.stack([j * self.dx + rng.uniform(-0.5, 0.5, n) * self.dx,
+                            rng.uniform(-3.0, 3.0, n), rng.uniform(8.0, 25.0, n)], axis=1)
+            # Sparse, heavy-tailed base descriptors (SIFT-like histograms).
+            base = rng.gamma(0.5, 1.0, size=(n, 128)).astype(np.float32)
+            if len(self._blocks) > 64:
+                self._blocks.clear()
+            blk = self._blocks[b] = (pts, base)
+        return blk
+
+    def _points(self, idx: np.ndarray):
+        idx = np.asarray(idx)
+        pts = np.empty((len(idx), 3))
+        base = np.empty((len(idx), 128), np.float32)
+        blocks = idx // self._BLOCK
+        for b in np.unique(blocks):
+            sel = blocks == b
+            p, d = self._block(int(b))
+            pts[sel] = p[idx[sel] - b * self._BLOCK]
+            base[sel] = d[idx[sel] - b * self._BLOCK]
+        return pts, base
 
     def camera(self, i: int):
         rng = np.random.default_rng((self.seed, 7, i))
@@ -70,10 +95,10 @@ class Corridor:
         nvis = min(self.visible, n)
         idx = np.arange(i * self.step, i * self.step + nvis)
         R, c = self.camera(i)
-        Xc = (self.points[idx] - c) @ R.T
+        P, b = self._points(idx)
+        Xc = (P - c) @ R.T
         u = self.focal * Xc[:, 0] / Xc[:, 2] + 960.0 + rng.normal(0, self.noise_px, nvis)
         v = self.focal * Xc[:, 1] / Xc[:, 2] + 540.0 + rng.normal(0, self.noise_px, nvis)
-        b = self.base[idx]
         d_in = b + self.desc_noise * rng.gamma(0.5, 1.0, size=b.shape).astype(np.float32)
         nout = n - nvis
         d_out = rng.gamma(0.5, 1.0, size=(nout, 128)).astype(np.float32)
@@ -86,7 +111,7 @@ class Corridor:
             hi = min(self.num_points, lo + self.step * max(1, self.overlap))
             if hi > lo:
                 pts = rng.integers(lo, hi, size=ncf)
-                d_out[:ncf] = self.base[pts] + self.desc_noise * rng.gamma(
+                d_out[:ncf] = self._points(pts)[1] + self.desc_noise * rng.gamma(
                     0.5, 1.0, size=(ncf, 128)).astype(np.float32)
         xy_out = np.stack([rng.uniform(0, 1920, nout), rng.uniform(0, 1080, nout)], axis=1)
         xy = np.concatenate([np.stack([u, v], axis=1), xy_out]).astype(np.float32)
@@ -98,8 +123,24 @@ class Corridor:
         kp[:, 5] = 1.0
         return i + 1, kp, np.ascontiguousarray(desc[perm])
 
-    def images(self):
-        return [self.image(i) for i in range(self.num_images)]
+    def images(self, start: int = 0, stop: int | None = None, workers: int = 1):
+        """Images [start, stop); `workers` > 1 generates in forked processes
+        (call before any GPU runtime is initialised in this process)."""
+        stop = self.num_images if stop is None else min(stop, self.num_images)
+        if workers <= 1 or stop - start < 2 * workers:
+            return [self.image(i) for i in range(start, stop)]
+        import multiprocessing as mp
+        global _POOL_CORRIDOR
+        _POOL_CORRIDOR = self
+        with mp.get_context("fork").Pool(workers) as pool:
+            return pool.map(_pool_image, range(start, stop), chunksize=4)
+
+
+_POOL_CORRIDOR = None
+
+
+def _pool_image(i):
+    return _POOL_CORRIDOR.image(i)
 
 
 def random_descriptors(n: int, seed: int) -> np.ndarray:
