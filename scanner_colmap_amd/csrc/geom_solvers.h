@@ -37,8 +37,10 @@
 
 #if defined(__HIPCC__)
 #define SCM_HD __host__ __device__
+#define SCM_UNROLL _Pragma("unroll")
 #else
 #define SCM_HD
+#define SCM_UNROLL
 #endif
 
 #include <math.h>
@@ -49,12 +51,14 @@ namespace geom {
 
 // ---------------------------------------------------------------------------
 // Canonical reduction order: item i goes to partial (i mod 64), each partial
-// accumulates its items in ascending order starting from 0.0, then the
-// partials are combined as p[l] += p[l + w] for w = 32, 16, ..., 1.  A
-// 64-lane wavefront evaluates exactly the same additions (one partial per
-// lane, butterfly-free tree through LDS or DPP with the same pairing).
+// accumulates its items in ascending order starting from -0.0 (the additive
+// identity: -0.0 + x == x for every x, so an empty partial changes nothing),
+// then the partials are combined as p[l] += p[l + w] for w = 32, 16, ..., 1.
+// A 64-lane wavefront evaluates exactly the same additions (one partial per
+// lane, the tree as shuffle-downs with the same pairing).
 // ---------------------------------------------------------------------------
 constexpr int kCanon = 64;
+constexpr double kCanonZero = -0.0;
 
 SCM_HD inline double canon_tree(double* p) {
   for (int w = kCanon / 2; w >= 1; w >>= 1)
@@ -188,14 +192,14 @@ SCM_HD inline void mat3_mul(const double* A, const double* B, double* C) {
 // xy interleaved (x0,y0,...).  Writes T (row-major 3x3).
 SCM_HD inline void normalize_transform(const double* xy, int n, double* T) {
   double p0[kCanon], p1[kCanon];
-  for (int l = 0; l < kCanon; ++l) { p0[l] = 0.0; p1[l] = 0.0; }
+  for (int l = 0; l < kCanon; ++l) { p0[l] = kCanonZero; p1[l] = kCanonZero; }
   for (int i = 0; i < n; ++i) {
     p0[i & (kCanon - 1)] += xy[2 * i];
     p1[i & (kCanon - 1)] += xy[2 * i + 1];
   }
   const double c0 = canon_tree(p0) / (double)n;
   const double c1 = canon_tree(p1) / (double)n;
-  for (int l = 0; l < kCanon; ++l) p0[l] = 0.0;
+  for (int l = 0; l < kCanon; ++l) p0[l] = kCanonZero;
   for (int i = 0; i < n; ++i) {
     const double d0 = xy[2 * i] - c0;
     const double d1 = xy[2 * i + 1] - c1;
@@ -243,98 +247,135 @@ SCM_HD inline void ata_accumulate(double* part45, const double* a) {
     for (int q = p; q < 9; ++q) part45[k++] += a[p] * a[q];
 }
 
-// Orthonormal basis of the null space of a full-row-rank m x 9 matrix A
-// (row-major, m <= 8) from a Householder QR of A^T: the last 9-m columns of Q.
-// W (scratch, 9*m) receives A^T and is destroyed.  ns receives (9-m) vectors
-// of 9 entries each, ns[j*9 + r].
-SCM_HD inline void householder_nullspace(const double* A, int m, double* W,
-                                         double* V, double* vn2, double* ns) {
+// Orthonormal basis of the null space of a full-row-rank M x 9 matrix A
+// (row-major, M <= 8) from a Householder QR of A^T: the last 9-M columns of Q.
+// Reflector k is stored in place in column k of W = A^T.  ns receives (9-M)
+// vectors of 9 entries each, ns[j*9 + r].  Fixed trip counts: the loops
+// unroll completely, so on the GPU everything stays in registers.
+template <int M>
+SCM_HD inline void householder_nullspace(const double* A, double* ns) {
+  double W[9][M];
+  double vn2[M];
+SCM_UNROLL
   for (int r = 0; r < 9; ++r)
-    for (int c = 0; c < m; ++c) W[r * m + c] = A[c * 9 + r];
-  for (int k = 0; k < m; ++k) {
+SCM_UNROLL
+    for (int c = 0; c < M; ++c) W[r][c] = A[c * 9 + r];
+SCM_UNROLL
+  for (int k = 0; k < M; ++k) {
     double nrm2 = 0.0;
-    for (int r = k; r < 9; ++r) nrm2 += W[r * m + k] * W[r * m + k];
+SCM_UNROLL
+    for (int r = k; r < 9; ++r) nrm2 += W[r][k] * W[r][k];
     const double nrm = sqrt(nrm2);
-    double* v = V + k * 9;
-    for (int r = 0; r < 9; ++r) v[r] = 0.0;
     vn2[k] = 0.0;
     if (nrm == 0.0) continue;
-    const double x0 = W[k * m + k];
+    const double x0 = W[k][k];
     const double alpha = x0 > 0.0 ? -nrm : nrm;
-    for (int r = k; r < 9; ++r) v[r] = W[r * m + k];
-    v[k] = x0 - alpha;
+    W[k][k] = x0 - alpha;  // v = (x0 - alpha, x1, ..., x_{8-k})
     double v2 = 0.0;
-    for (int r = k; r < 9; ++r) v2 += v[r] * v[r];
+SCM_UNROLL
+    for (int r = k; r < 9; ++r) v2 += W[r][k] * W[r][k];
     vn2[k] = v2;
     if (v2 == 0.0) continue;
-    for (int c = k; c < m; ++c) {
+SCM_UNROLL
+    for (int c = k + 1; c < M; ++c) {
       double dot = 0.0;
-      for (int r = k; r < 9; ++r) dot += v[r] * W[r * m + c];
+SCM_UNROLL
+      for (int r = k; r < 9; ++r) dot += W[r][k] * W[r][c];
       const double f = 2.0 * dot / v2;
-      for (int r = k; r < 9; ++r) W[r * m + c] = W[r * m + c] - f * v[r];
+SCM_UNROLL
+      for (int r = k; r < 9; ++r) W[r][c] = W[r][c] - f * W[r][k];
     }
   }
-  for (int j = m; j < 9; ++j) {
-    double* q = ns + (j - m) * 9;
+SCM_UNROLL
+  for (int j = M; j < 9; ++j) {
+    double q[9];
+SCM_UNROLL
     for (int r = 0; r < 9; ++r) q[r] = (r == j) ? 1.0 : 0.0;
-    for (int k = m - 1; k >= 0; --k) {
+SCM_UNROLL
+    for (int k = M - 1; k >= 0; --k) {
       if (vn2[k] == 0.0) continue;
-      const double* v = V + k * 9;
       double dot = 0.0;
-      for (int r = k; r < 9; ++r) dot += v[r] * q[r];
+SCM_UNROLL
+      for (int r = k; r < 9; ++r) dot += W[r][k] * q[r];
       const double f = 2.0 * dot / vn2[k];
-      for (int r = k; r < 9; ++r) q[r] = q[r] - f * v[r];
+SCM_UNROLL
+      for (int r = k; r < 9; ++r) q[r] = q[r] - f * W[r][k];
     }
+SCM_UNROLL
+    for (int r = 0; r < 9; ++r) ns[(j - M) * 9 + r] = q[r];
   }
 }
 
-// Cyclic Jacobi eigen-decomposition of a symmetric n x n matrix (row-major,
-// n <= 9).  On return the diagonal of a holds the eigenvalues and column j of
-// v (row-major, v[r*n+j]) the j-th eigenvector.  Returns the index of the
-// smallest eigenvalue (lowest index on ties).
-SCM_HD inline int jacobi_eigen_min(double* a, double* v, int n) {
-  for (int r = 0; r < n; ++r)
-    for (int c = 0; c < n; ++c) v[r * n + c] = (r == c) ? 1.0 : 0.0;
-  for (int sweep = 0; sweep < 64; ++sweep) {
+// Cyclic Jacobi eigen-decomposition of a symmetric N x N matrix (row-major).
+// On return the diagonal of a holds the eigenvalues and column j of v
+// (row-major, v[r*N+j]) the j-th eigenvector.  Returns the index of the
+// smallest eigenvalue (lowest index on ties).  Sweep structure (rotation
+// order, convergence test, zeroing of a_pq) is the definition the GPU's
+// lane-distributed 9x9 version (verify_kernels.hip) reproduces exactly.
+constexpr int kJacobiMaxSweeps = 64;
+
+SCM_HD inline void jacobi_params(double app, double aqq, double apq, double* c, double* s) {
+  const double theta = (aqq - app) / (2.0 * apq);
+  double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
+  if (theta < 0.0) t = -t;
+  *c = 1.0 / sqrt(t * t + 1.0);
+  *s = t * *c;
+}
+
+template <int N>
+SCM_HD inline int jacobi_eigen_min(double* a, double* v) {
+SCM_UNROLL
+  for (int r = 0; r < N; ++r)
+SCM_UNROLL
+    for (int c = 0; c < N; ++c) v[r * N + c] = (r == c) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < kJacobiMaxSweeps; ++sweep) {
     double off = 0.0, diag = 0.0;
-    for (int p = 0; p < n; ++p) {
-      diag += a[p * n + p] * a[p * n + p];
-      for (int q = p + 1; q < n; ++q) off += a[p * n + q] * a[p * n + q];
+SCM_UNROLL
+    for (int p = 0; p < N; ++p) {
+      diag += a[p * N + p] * a[p * N + p];
+SCM_UNROLL
+      for (int q = p + 1; q < N; ++q) off += a[p * N + q] * a[p * N + q];
     }
     if (off <= 1e-36 * diag || off == 0.0) break;
-    for (int p = 0; p < n - 1; ++p) {
-      for (int q = p + 1; q < n; ++q) {
-        const double apq = a[p * n + q];
+SCM_UNROLL
+    for (int p = 0; p < N - 1; ++p) {
+SCM_UNROLL
+      for (int q = p + 1; q < N; ++q) {
+        const double apq = a[p * N + q];
         if (apq == 0.0) continue;
-        const double app = a[p * n + p], aqq = a[q * n + q];
-        const double theta = (aqq - app) / (2.0 * apq);
-        double t = 1.0 / (fabs(theta) + sqrt(theta * theta + 1.0));
-        if (theta < 0.0) t = -t;
-        const double c = 1.0 / sqrt(t * t + 1.0);
-        const double s = t * c;
-        for (int k = 0; k < n; ++k) {
-          const double akp = a[k * n + p], akq = a[k * n + q];
-          a[k * n + p] = c * akp - s * akq;
-          a[k * n + q] = s * akp + c * akq;
+        double c, s;
+        jacobi_params(a[p * N + p], a[q * N + q], apq, &c, &s);
+SCM_UNROLL
+        for (int k = 0; k < N; ++k) {
+          const double akp = a[k * N + p], akq = a[k * N + q];
+          a[k * N + p] = c * akp - s * akq;
+          a[k * N + q] = s * akp + c * akq;
         }
-        for (int k = 0; k < n; ++k) {
-          const double apk = a[p * n + k], aqk = a[q * n + k];
-          a[p * n + k] = c * apk - s * aqk;
-          a[q * n + k] = s * apk + c * aqk;
+SCM_UNROLL
+        for (int k = 0; k < N; ++k) {
+          const double apk = a[p * N + k], aqk = a[q * N + k];
+          a[p * N + k] = c * apk - s * aqk;
+          a[q * N + k] = s * apk + c * aqk;
         }
-        a[p * n + q] = 0.0;
-        a[q * n + p] = 0.0;
-        for (int k = 0; k < n; ++k) {
-          const double vkp = v[k * n + p], vkq = v[k * n + q];
-          v[k * n + p] = c * vkp - s * vkq;
-          v[k * n + q] = s * vkp + c * vkq;
+        a[p * N + q] = 0.0;
+        a[q * N + p] = 0.0;
+SCM_UNROLL
+        for (int k = 0; k < N; ++k) {
+          const double vkp = v[k * N + p], vkq = v[k * N + q];
+          v[k * N + p] = c * vkp - s * vkq;
+          v[k * N + q] = s * vkp + c * vkq;
         }
       }
     }
   }
   int best = 0;
-  for (int j = 1; j < n; ++j)
-    if (a[j * n + j] < a[best * n + best]) best = j;
+  double bv = a[0];
+SCM_UNROLL
+  for (int j = 1; j < N; ++j)
+    if (a[j * N + j] < bv) {
+      bv = a[j * N + j];
+      best = j;
+    }
   return best;
 }
 
@@ -426,34 +467,52 @@ SCM_HD inline int poly3_real_roots(const double* c, double* r) {
   if (fabs(C) > R) R = fabs(C);
   if (fabs(D) > R) R = fabs(D);
   R = 1.0 + R;  // Cauchy bound: every root has |x| < R.
-  double pts[4];
-  int np = 0;
-  pts[np++] = -R;
-  // Critical points of p: 3x^2 + 2Bx + C = 0 (stable quadratic formula).
+  // Bracket points -R <= e0 <= e1 <= R; e0 / e1 are the critical points of p
+  // (3x^2 + 2Bx + C = 0, stable quadratic formula) when they exist inside
+  // (-R, R), otherwise duplicates of the neighbouring point (an empty
+  // interval, skipped).
+  double e0 = -R, e1 = -R;
   const double disc = B * B - 3.0 * C;
   if (disc > 0.0) {
     const double sd = sqrt(disc);
     const double q = (B >= 0.0) ? -(B + sd) : -(B - sd);
-    double e0 = q / 3.0, e1 = C / q;
-    if (e1 < e0) { const double t = e0; e0 = e1; e1 = t; }
-    if (e0 > -R && e0 < R) pts[np++] = e0;
-    if (e1 > -R && e1 < R && e1 > pts[np - 1]) pts[np++] = e1;
+    double c0 = q / 3.0, c1 = C / q;
+    if (c1 < c0) { const double t = c0; c0 = c1; c1 = t; }
+    if (c0 > -R && c0 < R) e0 = c0;
+    e1 = e0;
+    if (c1 > -R && c1 < R && c1 > e0) e1 = c1;
   }
-  pts[np++] = R;
+  const double pts[4] = {-R, e0, e1, R};
   int nr = 0;
+  double r0 = 0.0, r1 = 0.0, r2 = 0.0;
   double plo = cubic_eval(B, C, D, pts[0]);
-  for (int k = 0; k + 1 < np; ++k) {
+  SCM_UNROLL
+  for (int k = 0; k < 3; ++k) {
     const double lo = pts[k], hi = pts[k + 1];
+    if (!(lo < hi)) continue;  // empty interval (plo unchanged: p(hi) == p(lo))
     const double phi = cubic_eval(B, C, D, hi);
+    double x = 0.0;
+    bool found = false;
     if (plo == 0.0) {
-      if (nr == 0 || r[nr - 1] != lo) r[nr++] = lo;
+      const double last = nr == 1 ? r0 : (nr == 2 ? r1 : r2);
+      if (nr == 0 || last != lo) { x = lo; found = true; }
     } else if (phi != 0.0 && ((plo < 0.0) != (phi < 0.0))) {
-      r[nr++] = cubic_refine(B, C, D, lo, hi, plo);
+      x = cubic_refine(B, C, D, lo, hi, plo);
+      found = true;
     }
-    if (phi == 0.0 && k + 2 == np) r[nr++] = hi;
+    if (found && nr < 3) {
+      if (nr == 0) r0 = x; else if (nr == 1) r1 = x; else r2 = x;
+      ++nr;
+    }
+    if (phi == 0.0 && k == 2 && nr < 3) {
+      if (nr == 0) r0 = hi; else if (nr == 1) r1 = hi; else r2 = hi;
+      ++nr;
+    }
     plo = phi;
-    if (nr == 3) break;
   }
+  r[0] = r0;
+  r[1] = r1;
+  r[2] = r2;
   return nr;
 }
 
@@ -476,8 +535,8 @@ SCM_HD inline int fundamental_7pt(const double* x1, const double* x2,
     a[3] = yy1 * x0; a[4] = yy1 * y0; a[5] = yy1;
     a[6] = x0;       a[7] = y0;       a[8] = 1.0;
   }
-  double W[9 * 7], V[7 * 9], vn2[7], ns[2 * 9];
-  householder_nullspace(A, 7, W, V, vn2, ns);
+  double ns[2 * 9];
+  householder_nullspace<7>(A, ns);
   double f1[9], f2[9];
   for (int i = 0; i < 9; ++i) {
     f2[i] = ns[9 + i];
@@ -509,19 +568,34 @@ SCM_HD inline int fundamental_7pt(const double* x1, const double* x2,
   coeffs[3] = f2[0] * t3 - f2[1] * t4 + f2[2] * t5;
   double roots[3];
   const int nroots = poly3_real_roots(coeffs, roots);
+  // Models in root order, skipping |F(2,2)| < 1e-10; written with static
+  // indices (register-resident on the GPU).
+  double out[3][9];
   int nm = 0;
-  for (int k = 0; k < nroots; ++k) {
+  SCM_UNROLL
+  for (int k = 0; k < 3; ++k) {
+    if (k >= nroots) continue;
     const double lambda = roots[k];
     double F[9];
     // Eigen: lambda * f1 + mu * f2 with mu = 1, reshaped column-major 3x3 and
     // transposed on return => row-major F[r][c] = f[3r + c].
+    SCM_UNROLL
     for (int i = 0; i < 9; ++i) F[i] = lambda * f1[i] + 1.0 * f2[i];
     if (fabs(F[8]) < 1e-10) continue;
     const double s = F[8];
-    double* M = models + 9 * nm;
-    for (int i = 0; i < 9; ++i) M[i] = F[i] / s;
+    SCM_UNROLL
+    for (int i = 0; i < 9; ++i) {
+      const double v = F[i] / s;
+      if (nm == 0) out[0][i] = v;
+      else if (nm == 1) out[1][i] = v;
+      else out[2][i] = v;
+    }
     ++nm;
   }
+  SCM_UNROLL
+  for (int k = 0; k < 3; ++k)
+    SCM_UNROLL
+    for (int i = 0; i < 9; ++i) models[9 * k + i] = k < nm ? out[k][i] : 0.0;
   return nm;
 }
 
@@ -535,7 +609,7 @@ SCM_HD inline void ata_null_vector(const double* ata45, double* out9) {
       a[q * 9 + p] = ata45[k];
       ++k;
     }
-  const int jmin = jacobi_eigen_min(a, v, 9);
+  const int jmin = jacobi_eigen_min<9>(a, v);
   for (int i = 0; i < 9; ++i) out9[i] = v[i * 9 + jmin];
 }
 
@@ -550,8 +624,11 @@ SCM_HD inline void fundamental_8pt_finish(const double* f, const double* T1,
     for (int q = 0; q < 3; ++q)
       g[p * 3 + q] = f[0 + p] * f[0 + q] + f[3 + p] * f[3 + q] + f[6 + p] * f[6 + q];
   double w[9];
-  const int kmin = jacobi_eigen_min(g, w, 3);
-  const double v3[3] = {w[0 * 3 + kmin], w[1 * 3 + kmin], w[2 * 3 + kmin]};
+  const int kmin = jacobi_eigen_min<3>(g, w);
+  double v3[3];
+SCM_UNROLL
+  for (int r = 0; r < 3; ++r)
+    v3[r] = kmin == 0 ? w[r * 3] : (kmin == 1 ? w[r * 3 + 1] : w[r * 3 + 2]);
   double Fr[9];
   for (int r = 0; r < 3; ++r) {
     const double fv = f[3 * r] * v3[0] + f[3 * r + 1] * v3[1] + f[3 * r + 2] * v3[2];
@@ -571,7 +648,7 @@ SCM_HD inline int fundamental_8pt(const double* xy1, const double* xy2, int n, d
   normalize_transform(xy2, n, T2);
   double part[kCanon][45];
   for (int l = 0; l < kCanon; ++l)
-    for (int k = 0; k < 45; ++k) part[l][k] = 0.0;
+    for (int k = 0; k < 45; ++k) part[l][k] = kCanonZero;
   for (int i = 0; i < n; ++i) {
     double x0, y0, x1, y1, a[9];
     apply_normalize(T1, xy1[2 * i], xy1[2 * i + 1], &x0, &y0);
@@ -620,12 +697,11 @@ SCM_HD inline int homography_dlt(const double* xy1, const double* xy2, int n, do
       apply_normalize(T2, xy2[2 * i], xy2[2 * i + 1], &d0, &d1);
       h_rows(s0, s1, d0, d1, A + 9 * i, A + 9 * (i + 4));
     }
-    double W[9 * 8], V[8 * 9], vn2[8];
-    householder_nullspace(A, 8, W, V, vn2, h);
+    householder_nullspace<8>(A, h);
   } else {
     double part[kCanon][45];
     for (int l = 0; l < kCanon; ++l)
-      for (int k = 0; k < 45; ++k) part[l][k] = 0.0;
+      for (int k = 0; k < 45; ++k) part[l][k] = kCanonZero;
     for (int i = 0; i < n; ++i) {
       double s0, s1, d0, d1, a[9], b[9];
       apply_normalize(T1, xy1[2 * i], xy1[2 * i + 1], &s0, &s1);
@@ -652,7 +728,7 @@ SCM_HD inline void translation_estimate(const double* xy1, const double* xy2, in
                                         double* t) {
   double p[4][kCanon];
   for (int c = 0; c < 4; ++c)
-    for (int l = 0; l < kCanon; ++l) p[c][l] = 0.0;
+    for (int l = 0; l < kCanon; ++l) p[c][l] = kCanonZero;
   for (int i = 0; i < n; ++i) {
     const int l = i & (kCanon - 1);
     p[0][l] += xy1[2 * i];

@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -73,6 +74,11 @@ struct scm_context {
   // verification workspace
   DevBuf d_gpairs, d_vpairs, d_xy1, d_xy2, d_packed, d_scratch, d_idx, d_masks, d_vout;
   HostBuf h_stage;
+  // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
+  bool profile = false;
+  DevBuf d_prof;
+  std::vector<uint64_t> prof_sum;
+  int64_t prof_pairs = 0;
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
   // last table run, for scm_table_matches
@@ -317,10 +323,15 @@ int verify_stage(scm_context* ctx, const ImageTable& t, const std::vector<PairSp
   std::vector<GatherPair> gp;
   std::vector<VerifyPair> vp;
   std::vector<int64_t> vsrc, gsrc;
-  int64_t pts = 0, scr = 0, idx = 0;
+  int64_t pts = 0, scr = 0;
+  int max_m = 0;
   for (int64_t i = 0; i < P; ++i) {
     const int32_t m = counts[i];
     if (m <= 0) continue;
+    if (m > kMaxVerifyMatches) {
+      set_error("more than 65535 matches in one pair");
+      return SCM_E_INVALID;
+    }
     GatherPair g;
     std::memset(&g, 0, sizeof(g));
     g.match_off = pds[i].match_off;
@@ -335,15 +346,14 @@ int verify_stage(scm_context* ctx, const ImageTable& t, const std::vector<PairSp
       std::memset(&v, 0, sizeof(v));
       v.pts_off = 2 * pts;
       v.scr_off = scr;
-      v.idx_off = idx;
       v.mask_off = pts;
       v.m = m;
       v.id1 = t.ids[specs[i].a];
       v.id2 = t.ids[specs[i].b];
       vp.push_back(v);
       vsrc.push_back(i);
-      scr += 10 * (int64_t)m;
-      if (m > kLdsSampleIdx) idx += m;
+      scr += 10 * (int64_t)m + kVerifyModelDoubles;
+      max_m = std::max(max_m, m);
     }
     pts += m;
   }
@@ -363,16 +373,23 @@ int verify_stage(scm_context* ctx, const ImageTable& t, const std::vector<PairSp
   if (V > 0) {
     SCM_TRY(ctx->d_vpairs.ensure(V * sizeof(VerifyPair)));
     SCM_TRY(ctx->d_scratch.ensure(std::max<int64_t>(scr, 1) * sizeof(double)));
-    SCM_TRY(ctx->d_idx.ensure(std::max<int64_t>(idx, 1) * sizeof(uint32_t)));
+    SCM_TRY(ctx->d_idx.ensure(V * 640 * sizeof(uint32_t)));
     SCM_TRY(ctx->d_vout.ensure(V * sizeof(VerifyOut)));
     SCM_HIP(hipMemcpyAsync(ctx->d_vpairs.ptr, vp.data(), V * sizeof(VerifyPair),
                            hipMemcpyHostToDevice, ctx->stream));
     const VerifyParams params = make_params(ctx->opts);
     SCM_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
-    SCM_HIP(launch_verify(ctx->d_vpairs.as<VerifyPair>(), (int)V, ctx->d_xy1.as<double>(),
+    uint64_t* prof = nullptr;
+    if (ctx->profile) {
+      SCM_TRY(ctx->d_prof.ensure(V * kVerifyProfSlots * sizeof(uint64_t)));
+      SCM_HIP(hipMemsetAsync(ctx->d_prof.ptr, 0, V * kVerifyProfSlots * sizeof(uint64_t),
+                             ctx->stream));
+      prof = ctx->d_prof.as<uint64_t>();
+    }
+    SCM_HIP(launch_verify(ctx->d_vpairs.as<VerifyPair>(), (int)V, max_m, ctx->d_xy1.as<double>(),
                           ctx->d_xy2.as<double>(), ctx->d_scratch.as<double>(),
                           ctx->d_idx.as<uint32_t>(), ctx->d_masks.as<uint8_t>(),
-                          ctx->d_vout.as<VerifyOut>(), params, ctx->stream));
+                          ctx->d_vout.as<VerifyOut>(), params, prof, ctx->stream));
     SCM_HIP(hipEventRecord(ctx->ev[4], ctx->stream));
     SCM_HIP(hipMemcpyAsync(vout.data(), ctx->d_vout.ptr, V * sizeof(VerifyOut),
                            hipMemcpyDeviceToHost, ctx->stream));
@@ -385,6 +402,15 @@ int verify_stage(scm_context* ctx, const ImageTable& t, const std::vector<PairSp
                          ctx->stream));
   SCM_HIP(hipStreamSynchronize(ctx->stream));
   if (V > 0) ctx->t_verify += event_ms(ctx->ev[3], ctx->ev[4]);
+  if (V > 0 && ctx->profile) {
+    std::vector<uint64_t> pr(V * kVerifyProfSlots);
+    SCM_HIP(hipMemcpy(pr.data(), ctx->d_prof.ptr, pr.size() * sizeof(uint64_t),
+                      hipMemcpyDeviceToHost));
+    ctx->prof_sum.resize(kVerifyProfSlots, 0);
+    for (int64_t k = 0; k < V; ++k)
+      for (int j = 0; j < kVerifyProfSlots; ++j) ctx->prof_sum[j] += pr[k * kVerifyProfSlots + j];
+    ctx->prof_pairs += V;
+  }
   for (int64_t k = 0; k < G; ++k) {
     PairResult& r = (*results)[gsrc[k]];
     r.matches.assign(packed.begin() + gp[k].pts_off, packed.begin() + gp[k].pts_off + gp[k].m);
@@ -491,6 +517,7 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   scm_context* ctx = new scm_context();
   ctx->device = device_index;
   ctx->opts = o;
+  if (const char* e = std::getenv("SCM_PROFILE")) ctx->profile = e[0] == '1';
   if (hipSetDevice(device_index) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     set_error("failed to create HIP stream");
@@ -512,6 +539,16 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
 
 void scm_context_destroy(scm_context* ctx) {
   if (!ctx) return;
+  if (ctx->profile && ctx->prof_pairs > 0) {
+    static const char* names[] = {"sample", "solve", "score", "cand_res", "seqsum", "lo_gather",
+                                  "lo_est", "lo_res", "other", "n_batch", "n_cand", "n_lo",
+                                  "n_trials", "n_points", "n_seqsum", "-"};
+    std::fprintf(stderr, "[scm verify profile] pairs=%lld (per pair: cycles / counts)\n",
+                 (long long)ctx->prof_pairs);
+    for (int j = 0; j < 15; ++j)
+      std::fprintf(stderr, "  %-10s %14.1f\n", names[j],
+                   (double)ctx->prof_sum[j] / (double)ctx->prof_pairs);
+  }
   (void)hipSetDevice(ctx->device);
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   ctx->table.release();
@@ -519,7 +556,7 @@ void scm_context_destroy(scm_context* ctx) {
   for (DevBuf* b : {&ctx->lut, &ctx->d_jobs, &ctx->d_pairs, &ctx->d_rowres, &ctx->d_colpart,
                     &ctx->d_m21, &ctx->d_matches, &ctx->d_counts, &ctx->d_gpairs, &ctx->d_vpairs,
                     &ctx->d_xy1, &ctx->d_xy2, &ctx->d_packed, &ctx->d_scratch, &ctx->d_idx,
-                    &ctx->d_masks, &ctx->d_vout})
+                    &ctx->d_masks, &ctx->d_vout, &ctx->d_prof})
     b->release();
   ctx->h_stage.release();
   for (auto& e : ctx->ev)

@@ -5,9 +5,10 @@
 
 namespace scm {
 
-constexpr int kVerifyThreads = 256;   // 4 waves per pair
-constexpr int kTrialBatch = 64;       // hypotheses solved in parallel per round
-constexpr int kLdsSampleIdx = 8192;   // sample index vector kept in LDS up to this M
+constexpr int kVerifyThreads = 64;    // one wavefront per pair
+constexpr int kTrialBatch = 64;       // hypotheses solved in parallel per round (one per lane)
+constexpr int kMaxVerifyMatches = 65535;  // uint16 sample indices in LDS
+constexpr int kVerifyModelDoubles = kTrialBatch * 27;  // per-pair model buffer
 
 // Scalar options of TwoViewGeometry::EstimateUncalibrated (SURVEY.md §8a a2,
 // a9-a14) after the op's parseConfigs (sequential_matching.cc:64-75).
@@ -30,8 +31,8 @@ struct VerifyParams {
 
 struct VerifyPair {
   int64_t pts_off;   // double offset of xy1/xy2 (2 doubles per match)
-  int64_t scr_off;   // double offset of the per-pair scratch (6 doubles per match)
-  int64_t idx_off;   // uint32 offset of the global sample-index scratch (M > kLdsSampleIdx)
+  int64_t scr_off;   // double offset of the per-pair scratch (10 m + kVerifyModelDoubles)
+  int64_t idx_off;   // unused (kept for layout stability)
   int64_t mask_off;  // byte offset of the F inlier mask
   int32_t m;         // number of matches
   uint32_t id1, id2;
@@ -48,10 +49,13 @@ struct VerifyOut {
   double H[9];
 };
 
-hipError_t launch_verify(const VerifyPair* pairs, int npairs, const double* xy1,
-                         const double* xy2, double* scratch, uint32_t* idx_scratch,
-                         uint8_t* masks, VerifyOut* out, const VerifyParams& params,
+// snaps: 640 uint32 per pair (PRNG snapshot for the abort rewind).
+hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
+                         const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
+                         VerifyOut* out, const VerifyParams& params, uint64_t* prof,
                          hipStream_t stream);
+size_t verify_lds_bytes(int max_m);
+constexpr int kVerifyProfSlots = 16;
 
 // Gathers the matched keypoint coordinates of each pair (float -> double,
 // FeatureKeypointsToPointsVector, sequential_matching.cc:91-92).

@@ -3,20 +3,23 @@
 // the op's post-filter, reference integration/op_cpp/sequential_matching.cc:
 // 84-101 and 164-178; upstream EstimateUncalibrated).
 //
-// One 256-thread workgroup owns one image pair and runs, in order and with
-// the pair's own std::mt19937 stream (LDS-resident):
+// One wavefront owns one image pair (many pairs resident per CU hide each
+// other's serial sections) and runs, in order and with the pair's own
+// std::mt19937 stream (LDS-resident):
 //   LO-RANSAC<7-pt F, 8-pt F>  ->  LO-RANSAC<4-pt H, N-pt H>
 //   -> configuration -> DetectWatermark (LO-RANSAC<translation>) -> post-filter.
-// Each RANSAC round solves kTrialBatch hypotheses in parallel (one lane per
-// trial), scores every resulting model with one wavefront per model over the
-// pair's matches (fp64 Sampson / transfer error, exact inlier counts), then
+// Each round solves kTrialBatch minimal samples in parallel (one hypothesis
+// per lane, models kept in that lane's registers), scores every model over
+// the pair's matches (points streamed once per round in register chunks,
+// models broadcast with v_readlane, inlier bits counted with ballot), then
 // replays the trials in order exactly as the sequential LO-RANSAC does
 // (Compare, recursive local optimisation, dynamic trial bound, early abort);
 // hypotheses past the abort point are discarded and the PRNG is rewound to
-// the last consumed draw.  Residual sums that decide a Compare are summed
-// sequentially in index order, as InlierSupportMeasurer::Evaluate does.  The
-// estimator arithmetic is the shared geom_solvers.h, so every model is
-// bit-identical to the CPU oracle's.
+// the last consumed draw.  Residual sums are only needed when two inlier
+// counts tie; they are then summed in index order, as
+// InlierSupportMeasurer::Evaluate does.  The estimator arithmetic is the
+// shared geom_solvers.h (the 9x9 Jacobi is its lane-distributed twin), so
+// every model is bit-identical to the CPU oracle's.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -31,30 +34,74 @@ using namespace geom;
 enum { KIND_F = 0, KIND_H = 1, KIND_T = 2 };
 
 template <int K> struct KindTraits;
-template <> struct KindTraits<KIND_F> { static constexpr int kmin = 7, kmin_local = 8, max_models = 3, msize = 9; };
-template <> struct KindTraits<KIND_H> { static constexpr int kmin = 4, kmin_local = 4, max_models = 1, msize = 9; };
-template <> struct KindTraits<KIND_T> { static constexpr int kmin = 1, kmin_local = 1, max_models = 1, msize = 2; };
+template <> struct KindTraits<KIND_F> { static constexpr int kmin = 7, kmin_local = 8, mm = 3, ms = 9; };
+template <> struct KindTraits<KIND_H> { static constexpr int kmin = 4, kmin_local = 4, mm = 1, ms = 9; };
+template <> struct KindTraits<KIND_T> { static constexpr int kmin = 1, kmin_local = 1, mm = 1, ms = 2; };
 
+// Fixed part of the per-pair LDS; the sample-index vector (uint16, one per
+// match) follows it in dynamic LDS.
 struct __attribute__((aligned(16))) VerifyLds {
-  double models[kTrialBatch][3][9];
-  double red[45 * kCanon];
   double best_model[9];
-  double local_model[9];
-  double T1[9], T2[9];
+  double ata[45];
+  double jA[81], jV[81];
   double best_sum;
-  double bcast_d;
+  uint64_t prof_t;
   uint32_t mt[624];
-  uint32_t mt_snap[624];
-  uint32_t sidx[kLdsSampleIdx];
-  uint32_t samples[kTrialBatch][8];
+  uint32_t counts[kTrialBatch * 3];
   int32_t nmodels[kTrialBatch];
-  int32_t counts[kTrialBatch][3];
-  int32_t wave_cnt[kVerifyThreads / 64];
-  int32_t scan[kVerifyThreads];
-  int32_t mt_idx, mt_idx_snap;
+  uint16_t samples[kTrialBatch][8];
+  int32_t mt_idx;
   int32_t best_n;
-  int32_t bcast_i;
+  int32_t best_sum_valid;
+  int32_t pad_;
 };
+
+// ---------------------------------------------------------------------------
+// Diagnostic phase timer (only when the launcher passes a profile buffer; no
+// stamp executes in the production launch).
+// ---------------------------------------------------------------------------
+struct Prof {  // passed by value; the last stamp lives in *tp (LDS)
+  uint64_t* p;
+  uint64_t* tp;
+  __device__ void start() {
+    if (p && threadIdx.x == 0) *tp = __builtin_amdgcn_s_memtime();
+  }
+  __device__ void lap(int k) {
+    if (p && threadIdx.x == 0) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      p[k] += now - *tp;
+      *tp = now;
+    }
+  }
+  __device__ void count(int k, uint64_t v = 1) {
+    if (p && threadIdx.x == 0) p[k] += v;
+  }
+};
+enum { PR_SAMPLE = 0, PR_SOLVE, PR_SCORE, PR_CAND, PR_SEQSUM, PR_GATHER, PR_LOEST, PR_LORES,
+       PR_OTHER, PR_N_BATCH, PR_N_CAND, PR_N_LO, PR_N_TRIALS, PR_N_POINTS, PR_N_SEQSUM };
+
+__device__ __forceinline__ void wsync() { __syncthreads(); }  // one wavefront: cheap
+
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+  const uint64_t u = (uint64_t)__double_as_longlong(v);
+  const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)u, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(u >> 32), lane);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
+  return v;
+}
+
+// Canonical tree (geom_solvers.h): lane l accumulates p[l] + p[l + w] for
+// w = 32 .. 1; lane 0 holds the canonical sum, returned to every lane.
+__device__ __forceinline__ double canon_tree_wave(double v) {
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) v = v + __shfl_down(v, w);
+  return readlane_d(v, 0);
+}
 
 // ---------------------------------------------------------------------------
 // std::mt19937 + std::uniform_int_distribution<uint32_t> (libstdc++ 11,
@@ -101,231 +148,257 @@ __device__ uint32_t uniform_u32(VerifyLds& s, uint32_t a, uint32_t b) {
 }
 
 // ---------------------------------------------------------------------------
-// Workgroup helpers.
+// Residuals and supports.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int wave_sum_i(int v) {
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d);
-  return v;
-}
-
-// Sum of v over the workgroup (all threads receive it).
-__device__ int wg_sum_i(VerifyLds& s, int v) {
-  v = wave_sum_i(v);
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) s.wave_cnt[wave] = v;
-  __syncthreads();
-  int t = 0;
-#pragma unroll
-  for (int w = 0; w < kVerifyThreads / 64; ++w) t += s.wave_cnt[w];
-  __syncthreads();
-  return t;
-}
-
 template <int K>
-__device__ __forceinline__ double residual(const double* m, const double* xy1,
-                                           const double* xy2, int i) {
-  const double a0 = xy1[2 * i], a1 = xy1[2 * i + 1];
-  const double b0 = xy2[2 * i], b1 = xy2[2 * i + 1];
+__device__ __forceinline__ double residual_pt(const double* m, double a0, double a1, double b0,
+                                              double b1) {
   if (K == KIND_F) return sampson_sq(m, a0, a1, b0, b1);
   if (K == KIND_H) return homography_sq(m, a0, a1, b0, b1);
   return translation_sq(m, a0, a1, b0, b1);
 }
 
-// Residuals of one model over all points into res, returns the inlier count.
+// Inlier test r <= maxr of the squared Sampson error WITHOUT the division in
+// the common case: num and den are computed exactly as sampson_sq does, and
+// the correctly rounded quotient fl(num / den) <= maxr is decided from
+// num <= maxr * den * (1 - 2^-50)  (surely inside) and
+// num >= maxr * den * (1 + 2^-50)  (surely outside: exceeds maxr by > 2 ulp),
+// each side carrying at most 2^-52 relative rounding; anything else
+// (ties within the band, den <= 0, overflow, NaN) takes the exact division.
+__device__ __forceinline__ bool sampson_inlier(const double* F, double x1_0, double x1_1,
+                                               double x2_0, double x2_1, double maxr) {
+  const double Fx1_0 = F[0] * x1_0 + F[1] * x1_1 + F[2];
+  const double Fx1_1 = F[3] * x1_0 + F[4] * x1_1 + F[5];
+  const double Fx1_2 = F[6] * x1_0 + F[7] * x1_1 + F[8];
+  const double Ftx2_0 = F[0] * x2_0 + F[3] * x2_1 + F[6];
+  const double Ftx2_1 = F[1] * x2_0 + F[4] * x2_1 + F[7];
+  const double x2tFx1 = x2_0 * Fx1_0 + x2_1 * Fx1_1 + Fx1_2;
+  const double num = x2tFx1 * x2tFx1;
+  const double den = Fx1_0 * Fx1_0 + Fx1_1 * Fx1_1 + Ftx2_0 * Ftx2_0 + Ftx2_1 * Ftx2_1;
+  const double md = maxr * den;
+  const bool sane = den > 0.0 && den < 1e300 && num < 1e300;
+  const bool in = sane && num <= md * (1.0 - 0x1p-50);
+  const bool out = sane && num >= md * (1.0 + 0x1p-50);
+  if (in | out) return in;
+  return num / den <= maxr;
+}
+
+// Residuals of one model over all points into res; returns the inlier count.
 template <int K>
-__device__ int residuals_wg(VerifyLds& s, const double* m, const double* xy1,
-                            const double* xy2, int n, double maxr, double* res) {
+__device__ int residuals_wave(const double* m, const double* xy1, const double* xy2, int n,
+                              double maxr, double* res) {
   int c = 0;
-  for (int i = threadIdx.x; i < n; i += kVerifyThreads) {
-    const double r = residual<K>(m, xy1, xy2, i);
+  for (int i = threadIdx.x; i < n; i += 64) {
+    const double r = residual_pt<K>(m, xy1[2 * i], xy1[2 * i + 1], xy2[2 * i], xy2[2 * i + 1]);
     res[i] = r;
     c += (r <= maxr) ? 1 : 0;
   }
-  return wg_sum_i(s, c);
+  return wave_sum_i(c);
 }
 
-// InlierSupportMeasurer::Evaluate's residual_sum: inlier residuals summed in
-// index order (one lane), broadcast to the workgroup.
-__device__ double seq_inlier_sum(VerifyLds& s, const double* res, int n, double maxr) {
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double sum = 0.0;
-    for (int i = 0; i < n; ++i) {
-      const double r = res[i];
+// InlierSupportMeasurer::Evaluate's residual_sum: inlier residuals summed
+// in index order.  The wave loads 64 residuals at a time; the ordered
+// accumulation runs on values broadcast with v_readlane (every lane computes
+// the same scalar sum).
+__device__ double seq_inlier_sum(const double* res, int n, double maxr) {
+  double sum = 0.0;
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + threadIdx.x;
+    const double v = i < n ? res[i] : 1.7976931348623157e308;
+    const int cnt = min(64, n - base);
+    for (int j = 0; j < cnt; ++j) {
+      const double r = readlane_d(v, j);
       if (r <= maxr) sum += r;
     }
-    s.bcast_d = sum;
   }
-  __syncthreads();
-  const double v = s.bcast_d;
-  __syncthreads();
-  return v;
+  return sum;
 }
 
-// Ordered compaction of the points whose residual is <= maxr into
-// xin1 / xin2; returns the number of inliers.
-__device__ int gather_inliers(VerifyLds& s, const double* res, int n, double maxr,
-                              const double* xy1, const double* xy2, double* xin1,
-                              double* xin2) {
-  const int tid = threadIdx.x;
-  const int per = (n + kVerifyThreads - 1) / kVerifyThreads;
-  const int i0 = min(n, tid * per), i1 = min(n, i0 + per);
-  int c = 0;
-  for (int i = i0; i < i1; ++i) c += (res[i] <= maxr) ? 1 : 0;
-  s.scan[tid] = c;
-  __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int t = 0; t < kVerifyThreads; ++t) {
-      const int v = s.scan[t];
-      s.scan[t] = acc;
-      acc += v;
-    }
-    s.bcast_i = acc;
-  }
-  __syncthreads();
-  int o = s.scan[tid];
-  for (int i = i0; i < i1; ++i) {
-    if (res[i] <= maxr) {
+// Ordered compaction of the points whose residual is <= maxr.
+__device__ int gather_inliers(const double* res, int n, double maxr, const double* xy1,
+                              const double* xy2, double* xin1, double* xin2) {
+  const int lane = threadIdx.x;
+  int base_out = 0;
+  for (int base = 0; base < n; base += 64) {
+    const int i = base + lane;
+    const bool in = i < n && res[i] <= maxr;
+    const uint64_t bal = __ballot(in);
+    if (in) {
+      const int o = base_out + (int)__builtin_amdgcn_mbcnt_hi(
+                                   (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
       xin1[2 * o] = xy1[2 * i];
       xin1[2 * o + 1] = xy1[2 * i + 1];
       xin2[2 * o] = xy2[2 * i];
       xin2[2 * o + 1] = xy2[2 * i + 1];
-      ++o;
     }
+    base_out += __popcll(bal);
   }
-  const int total = s.bcast_i;
-  __syncthreads();
-  return total;
+  return base_out;
 }
 
-// Canonical partial sums (geom_solvers.h kCanon order) of up to 4 per-point
-// quantities, computed by wave 0 (lane l owns points i = l mod 64), then the
-// fixed tree by one lane per quantity.  Results in s.red[q * 64].
-template <typename F>
-__device__ void canon_sums(VerifyLds& s, int n, int nq, F f) {
-  const int tid = threadIdx.x;
-  if (tid < kCanon) {
-    double p[4] = {0.0, 0.0, 0.0, 0.0};
-    for (int i = tid; i < n; i += kCanon) {
-      double v[4];
-      f(i, v);
-      for (int q = 0; q < nq; ++q) p[q] += v[q];
+// LDS twin of jacobi_eigen_min<9> (geom_solvers.h): the 9x9 matrices live
+// in LDS, lane k < 9 owns row k for the column / V updates and column k for
+// the row update; identical operations in identical order.  Returns the
+// eigenvector of the smallest eigenvalue in f (every lane).
+__device__ void jacobi9_wave(const double* ata45, double* A, double* V, double* f) {
+  const int lane = threadIdx.x;
+  if (lane < 9) {
+#pragma unroll
+    for (int c = 0; c < 9; ++c) {
+      const int p = lane < c ? lane : c, q = lane < c ? c : lane;
+      A[lane * 9 + c] = ata45[ata_index(p, q)];
+      V[lane * 9 + c] = (lane == c) ? 1.0 : 0.0;
     }
-    for (int q = 0; q < nq; ++q) s.red[q * kCanon + tid] = p[q];
   }
-  __syncthreads();
-  if (tid < nq) canon_tree(&s.red[tid * kCanon]);
-  __syncthreads();
+  wsync();
+  for (int sweep = 0; sweep < kJacobiMaxSweeps; ++sweep) {
+    double off = 0.0, diag = 0.0;
+    for (int p = 0; p < 9; ++p) {
+      diag += A[p * 9 + p] * A[p * 9 + p];
+      for (int q = p + 1; q < 9; ++q) off += A[p * 9 + q] * A[p * 9 + q];
+    }
+    if (off <= 1e-36 * diag || off == 0.0) break;
+    for (int p = 0; p < 8; ++p) {
+      for (int q = p + 1; q < 9; ++q) {
+        const double apq = A[p * 9 + q];
+        if (apq == 0.0) continue;
+        double c, s;
+        jacobi_params(A[p * 9 + p], A[q * 9 + q], apq, &c, &s);
+        wsync();
+        if (lane < 9) {  // columns p, q of row `lane`
+          const double akp = A[lane * 9 + p], akq = A[lane * 9 + q];
+          A[lane * 9 + p] = c * akp - s * akq;
+          A[lane * 9 + q] = s * akp + c * akq;
+          const double vkp = V[lane * 9 + p], vkq = V[lane * 9 + q];
+          V[lane * 9 + p] = c * vkp - s * vkq;
+          V[lane * 9 + q] = s * vkp + c * vkq;
+        }
+        wsync();
+        if (lane < 9) {  // rows p, q at column `lane`
+          const double apk = A[p * 9 + lane], aqk = A[q * 9 + lane];
+          A[p * 9 + lane] = c * apk - s * aqk;
+          A[q * 9 + lane] = s * apk + c * aqk;
+        }
+        wsync();
+        if (lane == 0) {
+          A[p * 9 + q] = 0.0;
+          A[q * 9 + p] = 0.0;
+        }
+        wsync();
+      }
+    }
+  }
+  int best = 0;
+  for (int j = 1; j < 9; ++j)
+    if (A[j * 9 + j] < A[best * 9 + best]) best = j;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) f[i] = V[i * 9 + best];
 }
 
-// normalize_transform (geom_solvers.h) of both point sets, in parallel.
-__device__ void normalize_pair_wg(VerifyLds& s, const double* xy1, const double* xy2, int n) {
-  canon_sums(s, n, 4, [&](int i, double* v) {
-    v[0] = xy1[2 * i];
-    v[1] = xy1[2 * i + 1];
-    v[2] = xy2[2 * i];
-    v[3] = xy2[2 * i + 1];
-  });
-  const double c10 = s.red[0] / (double)n, c11 = s.red[kCanon] / (double)n;
-  const double c20 = s.red[2 * kCanon] / (double)n, c21 = s.red[3 * kCanon] / (double)n;
-  __syncthreads();
-  canon_sums(s, n, 2, [&](int i, double* v) {
+// normalize_transform (geom_solvers.h) of both point sets, canonical sums.
+__device__ void normalize_pair_wave(const double* xy1, const double* xy2, int n, double* T1,
+                                    double* T2) {
+  const int lane = threadIdx.x;
+  double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
+  for (int i = lane; i < n; i += 64) {
+    p0 += xy1[2 * i];
+    p1 += xy1[2 * i + 1];
+    p2 += xy2[2 * i];
+    p3 += xy2[2 * i + 1];
+  }
+  const double c10 = canon_tree_wave(p0) / (double)n, c11 = canon_tree_wave(p1) / (double)n;
+  const double c20 = canon_tree_wave(p2) / (double)n, c21 = canon_tree_wave(p3) / (double)n;
+  p0 = kCanonZero;
+  p1 = kCanonZero;
+  for (int i = lane; i < n; i += 64) {
     const double d0 = xy1[2 * i] - c10, d1 = xy1[2 * i + 1] - c11;
     const double e0 = xy2[2 * i] - c20, e1 = xy2[2 * i + 1] - c21;
-    v[0] = d0 * d0 + d1 * d1;
-    v[1] = e0 * e0 + e1 * e1;
-  });
-  if (threadIdx.x == 0) {
-    const double rms1 = sqrt(s.red[0] / (double)n);
-    const double rms2 = sqrt(s.red[kCanon] / (double)n);
-    const double sc1 = sqrt(2.0) / rms1, sc2 = sqrt(2.0) / rms2;
-    double* T1 = s.T1;
-    double* T2 = s.T2;
-    T1[0] = sc1; T1[1] = 0.0; T1[2] = -sc1 * c10;
-    T1[3] = 0.0; T1[4] = sc1; T1[5] = -sc1 * c11;
-    T1[6] = 0.0; T1[7] = 0.0; T1[8] = 1.0;
-    T2[0] = sc2; T2[1] = 0.0; T2[2] = -sc2 * c20;
-    T2[3] = 0.0; T2[4] = sc2; T2[5] = -sc2 * c21;
-    T2[6] = 0.0; T2[7] = 0.0; T2[8] = 1.0;
+    p0 += d0 * d0 + d1 * d1;
+    p1 += e0 * e0 + e1 * e1;
   }
-  __syncthreads();
+  const double rms1 = sqrt(canon_tree_wave(p0) / (double)n);
+  const double rms2 = sqrt(canon_tree_wave(p1) / (double)n);
+  const double s1 = sqrt(2.0) / rms1, s2 = sqrt(2.0) / rms2;
+  T1[0] = s1; T1[1] = 0.0; T1[2] = -s1 * c10;
+  T1[3] = 0.0; T1[4] = s1; T1[5] = -s1 * c11;
+  T1[6] = 0.0; T1[7] = 0.0; T1[8] = 1.0;
+  T2[0] = s2; T2[1] = 0.0; T2[2] = -s2 * c20;
+  T2[3] = 0.0; T2[4] = s2; T2[5] = -s2 * c21;
+  T2[6] = 0.0; T2[7] = 0.0; T2[8] = 1.0;
 }
 
-// Local (least-squares) estimators on n gathered inliers; result in
-// s.local_model.  Same arithmetic as geom_solvers.h fundamental_8pt /
-// homography_dlt (n > 4) / translation_estimate.
+// Local (least-squares) estimators on n gathered inliers (geom_solvers.h
+// fundamental_8pt / homography_dlt n > 4 / translation_estimate); every lane
+// returns the model.
 template <int K>
-__device__ void local_estimate_wg(VerifyLds& s, const double* xin1, const double* xin2, int n) {
-  const int tid = threadIdx.x;
+__device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const double* xin2, int n,
+                                    double* model) {
+  const int lane = threadIdx.x;
   if (K == KIND_T) {
-    canon_sums(s, n, 4, [&](int i, double* v) {
-      v[0] = xin1[2 * i];
-      v[1] = xin1[2 * i + 1];
-      v[2] = xin2[2 * i];
-      v[3] = xin2[2 * i + 1];
-    });
-    if (tid == 0) {
-      const double s0 = s.red[0] / (double)n, s1 = s.red[kCanon] / (double)n;
-      const double d0 = s.red[2 * kCanon] / (double)n, d1 = s.red[3 * kCanon] / (double)n;
-      s.local_model[0] = d0 - s0;
-      s.local_model[1] = d1 - s1;
+    double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
+    for (int i = lane; i < n; i += 64) {
+      p0 += xin1[2 * i];
+      p1 += xin1[2 * i + 1];
+      p2 += xin2[2 * i];
+      p3 += xin2[2 * i + 1];
     }
-    __syncthreads();
+    const double s0 = canon_tree_wave(p0) / (double)n, s1 = canon_tree_wave(p1) / (double)n;
+    const double d0 = canon_tree_wave(p2) / (double)n, d1 = canon_tree_wave(p3) / (double)n;
+    model[0] = d0 - s0;
+    model[1] = d1 - s1;
     return;
   }
-  normalize_pair_wg(s, xin1, xin2, n);
-  // A^T A partials: wave w owns entries k = w, w+4, ...; lane l owns points l mod 64.
-  {
-    const int wave = tid >> 6, lane = tid & 63;
-    double part[12];
+  double T1[9], T2[9];
+  normalize_pair_wave(xin1, xin2, n, T1, T2);
+  // A^T A in canonical order, 15 packed entries per pass (register budget);
+  // every entry accumulates exactly the terms of ata_accumulate in order.
 #pragma unroll
-    for (int j = 0; j < 12; ++j) part[j] = 0.0;
-    const double* T1 = s.T1;
-    const double* T2 = s.T2;
-    for (int i = lane; i < n; i += kCanon) {
+  for (int pass = 0; pass < 3; ++pass) {
+    double part[15];
+#pragma unroll
+    for (int k = 0; k < 15; ++k) part[k] = kCanonZero;
+    for (int i = lane; i < n; i += 64) {
       double x0, y0, x1, y1;
       apply_normalize(T1, xin1[2 * i], xin1[2 * i + 1], &x0, &y0);
       apply_normalize(T2, xin2[2 * i], xin2[2 * i + 1], &x1, &y1);
       double a[9], b[9];
       if (K == KIND_F) f_row(x0, y0, x1, y1, a);
       else h_rows(x0, y0, x1, y1, a, b);
-      int k = 0, j = 0;
+      int k = 0;
 #pragma unroll
       for (int p = 0; p < 9; ++p)
 #pragma unroll
         for (int q = p; q < 9; ++q) {
-          if ((k & 3) == wave) {
-            double v = part[j] + a[p] * a[q];
-            if (K == KIND_H) v = v + b[p] * b[q];
-            part[j] = v;
+          if (k >= 15 * pass && k < 15 * pass + 15) {
+            double v = part[k - 15 * pass] + a[p] * a[q];
+            part[k - 15 * pass] = v;
           }
-          if ((k & 3) == wave) ++j;
           ++k;
         }
-    }
-    int k = 0, j = 0;
+      if (K == KIND_H) {
+        k = 0;
 #pragma unroll
-    for (int p = 0; p < 9; ++p)
+        for (int p = 0; p < 9; ++p)
 #pragma unroll
-      for (int q = p; q < 9; ++q) {
-        if ((k & 3) == wave) s.red[k * kCanon + lane] = part[j++];
-        ++k;
+          for (int q = p; q < 9; ++q) {
+            if (k >= 15 * pass && k < 15 * pass + 15)
+              part[k - 15 * pass] = part[k - 15 * pass] + b[p] * b[q];
+            ++k;
+          }
       }
+    }
+#pragma unroll
+    for (int k = 0; k < 15; ++k) {
+      const double t = canon_tree_wave(part[k]);
+      if (lane == 0) s.ata[15 * pass + k] = t;
+    }
   }
-  __syncthreads();
-  if (tid < 45) canon_tree(&s.red[tid * kCanon]);
-  __syncthreads();
-  if (tid == 0) {
-    double ata[45];
-    for (int k = 0; k < 45; ++k) ata[k] = s.red[k * kCanon];
-    double f[9];
-    ata_null_vector(ata, f);
-    if (K == KIND_F) fundamental_8pt_finish(f, s.T1, s.T2, s.local_model);
-    else homography_finish(f, s.T1, s.T2, s.local_model);
-  }
-  __syncthreads();
+  wsync();
+  double f[9];
+  jacobi9_wave(s.ata, s.jA, s.jV, f);
+  wsync();
+  if (K == KIND_F) fundamental_8pt_finish(f, T1, T2, model);
+  else homography_finish(f, T1, T2, model);
 }
 
 struct RansacResult {
@@ -335,183 +408,280 @@ struct RansacResult {
   int res_sel;  // which residual buffer holds the best model's residuals
 };
 
+// Makes s.best_sum the exact (index-order) sum of the best model's inlier
+// residuals, computing it lazily from res_best the first time a tie needs it.
+__device__ void ensure_best_sum(VerifyLds& s, const double* res_best, int n, double maxr) {
+  if (s.best_sum_valid) return;
+  const double bs = seq_inlier_sum(res_best, n, maxr);
+  wsync();
+  if (threadIdx.x == 0) {
+    s.best_sum = bs;
+    s.best_sum_valid = 1;
+  }
+  wsync();
+}
+
 // LORANSAC<Estimator, LocalEstimator>::Estimate on n points (xy1, xy2).
-// res[0] / res[1]: residual buffers (n doubles each); xin1 / xin2 inlier
-// gather buffers (2n doubles each).  Best model ends in s.best_model.
+// res0 / res1: residual buffers (n doubles each); xin1 / xin2 inlier gather
+// buffers (2n doubles each); snap: 625-word PRNG snapshot (global).  The
+// best model ends in s.best_model.
 template <int K>
-__device__ RansacResult loransac_wg(VerifyLds& s, const double* xy1, const double* xy2,
-                                    int n, int max_trials, const VerifyParams& P,
-                                    double* res0, double* res1, double* xin1, double* xin2,
-                                    uint32_t* sidx_global) {
+__device__ RansacResult loransac_wave(VerifyLds& s, uint16_t* sidx, const double* xy1,
+                                      const double* xy2, int n, int max_trials,
+                                      const VerifyParams P, double* res0, double* res1,
+                                      double* xin1, double* xin2, uint32_t* snap,
+                                      double* mbuf, Prof pf) {
   using Tr = KindTraits<K>;
-  const int tid = threadIdx.x;
-  const int wave = tid >> 6, lane = tid & 63;
+  constexpr int MM = Tr::mm, MS = Tr::ms;
+  const int lane = threadIdx.x;
   const double maxr = P.max_residual;
   RansacResult out = {0, 0, 0, 0};
-  if (tid < 9) s.best_model[tid] = 0.0;  // report.model when no model is found
-  __syncthreads();
-  if (n < Tr::kmin) return out;
-
-  uint32_t* sidx = (n <= kLdsSampleIdx) ? s.sidx : sidx_global;
-  for (int i = tid; i < n; i += kVerifyThreads) sidx[i] = (uint32_t)i;
-  if (tid == 0) {
+  if (lane < 9) s.best_model[lane] = 0.0;  // report.model when no model is found
+  if (lane == 0) {
     s.best_n = 0;
-    s.best_sum = 1.7976931348623157e308;  // DBL_MAX
+    s.best_sum = 1.7976931348623157e308;  // Support() default: DBL_MAX
+    s.best_sum_valid = 1;
   }
+  wsync();
+  if (n < Tr::kmin) return out;
+  for (int i = lane; i < n; i += 64) sidx[i] = (uint16_t)i;
   double* res[2] = {res0, res1};
-  int best_sel = 0;          // res[best_sel] = residuals of the best model
+  int best_sel = 0;
   int dyn_max = max_trials;
   int trial = 0;
   bool abort = false;
   int abort_trial = -1;
-  __syncthreads();
+  wsync();
 
   while (trial < max_trials && !abort) {
     const int B = min(kTrialBatch, max_trials - trial);
-    // -- snapshot the PRNG, draw B samples (Shuffle of the persistent index vector).
-    for (int i = tid; i < 624; i += kVerifyThreads) s.mt_snap[i] = s.mt[i];
-    if (tid == 0) s.mt_idx_snap = s.mt_idx;
-    __syncthreads();
-    if (tid == 0) {
+    pf.lap(PR_OTHER);
+    pf.count(PR_N_BATCH);
+    // -- snapshot the PRNG (global), draw B samples (Shuffle of the persistent
+    //    index vector, RandomSampler::Sample).
+    for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
+    if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
+    wsync();
+    if (lane == 0) {
       const uint32_t last = (uint32_t)(n - 1);
       for (int b = 0; b < B; ++b)
         for (int i = 0; i < Tr::kmin; ++i) {
           const uint32_t j = uniform_u32(s, (uint32_t)i, last);
-          const uint32_t t = sidx[i];
+          const uint16_t t = sidx[i];
           sidx[i] = sidx[j];
           sidx[j] = t;
           s.samples[b][i] = sidx[i];
         }
     }
-    __syncthreads();
-    // -- solve the B minimal samples, one lane each.
-    if (tid < B) {
+    for (int i = lane; i < kTrialBatch * 3; i += 64) s.counts[i] = 0u;
+    wsync();
+    pf.lap(PR_SAMPLE);
+    // -- solve the B minimal samples, one lane each; models go to the pair's
+    //    model buffer (global, L1/L2-resident), counts of models to LDS.
+    if (lane < B) {
       double a[2 * 7], b[2 * 7];
+#pragma unroll
       for (int i = 0; i < Tr::kmin; ++i) {
-        const uint32_t k = s.samples[tid][i];
+        const uint32_t k = s.samples[lane][i];
         a[2 * i] = xy1[2 * k];
         a[2 * i + 1] = xy1[2 * k + 1];
         b[2 * i] = xy2[2 * k];
         b[2 * i + 1] = xy2[2 * k + 1];
       }
-      int nm = 0;
-      if (K == KIND_F) {
-        nm = fundamental_7pt(a, b, &s.models[tid][0][0]);
-      } else if (K == KIND_H) {
-        homography_dlt(a, b, 4, &s.models[tid][0][0]);
-        nm = 1;
-      } else {
-        translation_estimate(a, b, 1, &s.models[tid][0][0]);
-        nm = 1;
+      double* mo = mbuf + lane * (MM * MS);
+      int nm = 1;
+      if (K == KIND_F) nm = fundamental_7pt(a, b, mo);
+      else if (K == KIND_H) homography_dlt(a, b, 4, mo);
+      else translation_estimate(a, b, 1, mo);
+      s.nmodels[lane] = nm;
+    }
+    wsync();
+    pf.lap(PR_SOLVE);
+    // -- score: every lane reloads its own trial's models into registers; the
+    //    points are streamed once in register chunks and each model is
+    //    broadcast with v_readlane; exact inlier counts via ballot.
+    double m[MM][MS];
+    int nm = 0;
+    if (lane < B) {
+      nm = s.nmodels[lane];
+      const double* src = mbuf + lane * (MM * MS);
+#pragma unroll
+      for (int k = 0; k < MM; ++k)
+#pragma unroll
+        for (int j = 0; j < MS; ++j) m[k][j] = src[k * MS + j];
+    } else {
+#pragma unroll
+      for (int k = 0; k < MM; ++k)
+#pragma unroll
+        for (int j = 0; j < MS; ++j) m[k][j] = 0.0;
+    }
+    constexpr int PC = 8;  // points per lane per chunk
+    for (int base = 0; base < n; base += 64 * PC) {
+      double pa0[PC], pa1[PC], pb0[PC], pb1[PC];
+      bool ok[PC];
+#pragma unroll
+      for (int p = 0; p < PC; ++p) {
+        const int i = base + p * 64 + lane;
+        ok[p] = i < n;
+        const int ii = ok[p] ? i : 0;
+        pa0[p] = xy1[2 * ii];
+        pa1[p] = xy1[2 * ii + 1];
+        pb0[p] = xy2[2 * ii];
+        pb1[p] = xy2[2 * ii + 1];
       }
-      s.nmodels[tid] = nm;
-    }
-    __syncthreads();
-    // -- score: one wavefront per model, exact inlier counts.
-    for (int slot = wave; slot < B * Tr::max_models; slot += kVerifyThreads / 64) {
-      const int b = slot / Tr::max_models, k = slot % Tr::max_models;
-      if (k >= s.nmodels[b]) continue;
-      const double* m = &s.models[b][k][0];
-      int c = 0;
-      for (int i = lane; i < n; i += 64) c += (residual<K>(m, xy1, xy2, i) <= maxr) ? 1 : 0;
-      c = wave_sum_i(c);
-      if (lane == 0) s.counts[b][k] = c;
-    }
-    __syncthreads();
-    // -- replay the trials in order.
-    for (int b = 0; b < B && !abort; ++b) {
-      const int t = trial + b;
-      const int nm = s.nmodels[b];
-      for (int k = 0; k < nm; ++k) {
-        const int c = s.counts[b][k];
-        const int bn = s.best_n;
-        if (c >= bn) {
-          const double* m = &s.models[b][k][0];
-          double* rt = res[best_sel ^ 1];
-          residuals_wg<K>(s, m, xy1, xy2, n, maxr, rt);
-          const double sum = seq_inlier_sum(s, rt, n, maxr);
-          const bool better = (c > bn) || (sum < s.best_sum);
-          if (better) {
-            if (tid == 0) {
-              s.best_n = c;
-              s.best_sum = sum;
+      for (int t = 0; t < B; ++t) {
+        const int nmt = __builtin_amdgcn_readlane(nm, t);
+#pragma unroll
+        for (int k = 0; k < MM; ++k) {
+          if (k < nmt) {
+            double mk[MS];
+#pragma unroll
+            for (int j = 0; j < MS; ++j) mk[j] = readlane_d(m[k][j], t);
+            int c = 0;
+#pragma unroll
+            for (int p = 0; p < PC; ++p) {
+              bool in;
+              if (K == KIND_F) in = sampson_inlier(mk, pa0[p], pa1[p], pb0[p], pb1[p], maxr);
+              else in = residual_pt<K>(mk, pa0[p], pa1[p], pb0[p], pb1[p]) <= maxr;
+              c += __popcll(__ballot(ok[p] && in));
             }
-            if (tid < Tr::msize) s.best_model[tid] = m[tid];
-            best_sel ^= 1;
-            __syncthreads();
-            // Recursive local optimisation.
-            if (c > Tr::kmin && c >= Tr::kmin_local) {
-              for (int lt = 0; lt < 10; ++lt) {
-                const int ni = gather_inliers(s, res[best_sel], n, maxr, xy1, xy2, xin1, xin2);
-                local_estimate_wg<K>(s, xin1, xin2, ni);
-                const int prev = s.best_n;
-                double* rl = res[best_sel ^ 1];
-                const int lc = residuals_wg<K>(s, s.local_model, xy1, xy2, n, maxr, rl);
-                bool lbetter = lc > prev;
-                double lsum = 0.0;
-                if (lc >= prev) {
-                  lsum = seq_inlier_sum(s, rl, n, maxr);
-                  lbetter = (lc > prev) || (lsum < s.best_sum);
-                }
-                if (lbetter) {
-                  if (tid == 0) {
-                    s.best_n = lc;
-                    s.best_sum = lsum;
-                  }
-                  if (tid < Tr::msize) s.best_model[tid] = s.local_model[tid];
-                  best_sel ^= 1;
-                }
-                __syncthreads();
-                if (s.best_n <= prev) break;
-              }
-            }
-            dyn_max = (int)min((uint64_t)0x7FFFFFFF,
-                               num_trials((uint64_t)s.best_n, (uint64_t)n, P.confidence,
-                                          P.dyn_num_trials_multiplier, Tr::kmin));
+            if (lane == 0) s.counts[t * MM + k] += (uint32_t)c;
           }
         }
-        if (t >= dyn_max && t >= P.min_num_trials) {
-          abort = true;
-          abort_trial = t;
-          break;
+      }
+    }
+    wsync();
+    pf.lap(PR_SCORE);
+    // -- replay the trials in order.
+    for (int t = 0; t < B && !abort; ++t) {
+      const int tt = trial + t;
+      const int nmt = s.nmodels[t];
+      for (int k = 0; k < MM; ++k) {
+        if (k < nmt && !abort) {
+          const int c = (int)s.counts[t * MM + k];
+          const int bn = s.best_n;
+          if (c >= bn) {
+            double mk[MS];
+            const double* src = mbuf + (t * MM + k) * MS;
+#pragma unroll
+            for (int j = 0; j < MS; ++j) mk[j] = src[j];
+            pf.lap(PR_OTHER);
+            pf.count(PR_N_CAND);
+            double* rt = res[best_sel ^ 1];
+            residuals_wave<K>(mk, xy1, xy2, n, maxr, rt);
+            pf.lap(PR_CAND);
+            bool better = c > bn;
+            double sum = 0.0;
+            if (!better) {  // tie on the inlier count: Compare the residual sums
+              sum = seq_inlier_sum(rt, n, maxr);
+              ensure_best_sum(s, res[best_sel], n, maxr);
+              better = sum < s.best_sum;
+              pf.count(PR_N_SEQSUM);
+              pf.lap(PR_SEQSUM);
+            }
+            if (better) {
+              wsync();
+              if (lane == 0) {
+#pragma unroll
+                for (int j = 0; j < MS; ++j) s.best_model[j] = mk[j];
+                s.best_n = c;
+                s.best_sum = sum;
+                s.best_sum_valid = c == bn ? 1 : 0;
+              }
+              best_sel ^= 1;
+              wsync();
+              // Recursive local optimisation.
+              if (c > Tr::kmin && c >= Tr::kmin_local) {
+                for (int lt = 0; lt < 10; ++lt) {
+                  pf.lap(PR_OTHER);
+                  pf.count(PR_N_LO);
+                  const int ni = gather_inliers(res[best_sel], n, maxr, xy1, xy2, xin1, xin2);
+                  pf.lap(PR_GATHER);
+                  double lm[9];
+                  local_estimate_wave<K>(s, xin1, xin2, ni, lm);
+                  pf.lap(PR_LOEST);
+                  const int prev = s.best_n;
+                  double* rl = res[best_sel ^ 1];
+                  const int lc = residuals_wave<K>(lm, xy1, xy2, n, maxr, rl);
+                  pf.lap(PR_LORES);
+                  bool lbetter = lc > prev;
+                  double lsum = 0.0;
+                  if (lc == prev) {
+                    lsum = seq_inlier_sum(rl, n, maxr);
+                    ensure_best_sum(s, res[best_sel], n, maxr);
+                    lbetter = lsum < s.best_sum;
+                    pf.count(PR_N_SEQSUM);
+                    pf.lap(PR_SEQSUM);
+                  }
+                  if (lbetter) {
+                    wsync();
+                    if (lane == 0) {
+#pragma unroll
+                      for (int j = 0; j < MS; ++j) s.best_model[j] = lm[j];
+                      s.best_n = lc;
+                      s.best_sum = lsum;
+                      s.best_sum_valid = lc == prev ? 1 : 0;
+                    }
+                    best_sel ^= 1;
+                  }
+                  wsync();
+                  if (s.best_n <= prev) break;
+                }
+              }
+              dyn_max = (int)min((uint64_t)0x7FFFFFFF,
+                                 num_trials((uint64_t)s.best_n, (uint64_t)n, P.confidence,
+                                            P.dyn_num_trials_multiplier, Tr::kmin));
+            }
+          }
+          if (tt >= dyn_max && tt >= P.min_num_trials) {
+            abort = true;
+            abort_trial = tt;
+          }
         }
       }
     }
     if (abort) {
-      // Rewind the PRNG to the state after trial abort_trial's sample.
-      __syncthreads();
-      for (int i = tid; i < 624; i += kVerifyThreads) s.mt[i] = s.mt_snap[i];
-      if (tid == 0) s.mt_idx = s.mt_idx_snap;
-      __syncthreads();
-      if (tid == 0) {
+      // Rewind the PRNG to the state right after trial abort_trial's sample.
+      wsync();
+      for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
+      wsync();
+      if (lane == 0) {
+        s.mt_idx = (int32_t)snap[624];
         const uint32_t last = (uint32_t)(n - 1);
         for (int b = 0; b <= abort_trial - trial; ++b)
           for (int i = 0; i < Tr::kmin; ++i) (void)uniform_u32(s, (uint32_t)i, last);
       }
-      __syncthreads();
+      wsync();
       out.num_trials = abort_trial + 2;
     } else {
       trial += B;
       out.num_trials = trial;
     }
   }
+  pf.lap(PR_OTHER);
+  pf.count(PR_N_TRIALS, (uint64_t)out.num_trials);
+  pf.count(PR_N_POINTS, (uint64_t)n);
   // res[best_sel] holds the residuals of the best model (every accepted
   // model had its residuals written to the buffer that became res[best_sel]).
   out.num_inliers = s.best_n;
   out.success = s.best_n >= Tr::kmin ? 1 : 0;
   out.res_sel = best_sel;
-  __syncthreads();
+  wsync();
   return out;
 }
 
 __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
     const double* __restrict__ xy2_all, double* __restrict__ scratch,
-    uint32_t* __restrict__ idx_scratch, uint8_t* __restrict__ masks,
-    VerifyOut* __restrict__ out, VerifyParams P) {
-  __shared__ VerifyLds s;
+    uint32_t* __restrict__ snaps, uint8_t* __restrict__ masks,
+    VerifyOut* __restrict__ out, VerifyParams P, uint64_t* __restrict__ prof) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
+  uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
+  Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
+  pf.start();
   const VerifyPair pp = pairs[blockIdx.x];
-  const int tid = threadIdx.x;
+  const int lane = threadIdx.x;
   const int n = pp.m;
   VerifyOut o;
   o.config = 0;
@@ -522,32 +692,34 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
   o.pad_ = 0;
   for (int i = 0; i < 9; ++i) { o.F[i] = 0.0; o.H[i] = 0.0; }
   uint8_t* mask = masks + pp.mask_off;
-  for (int i = tid; i < n; i += kVerifyThreads) mask[i] = 0;
+  for (int i = lane; i < n; i += 64) mask[i] = 0;
+  uint32_t* snap = snaps + (int64_t)blockIdx.x * 640;
 
   if (n >= P.min_num_inliers && n > 0) {
     const double* xy1 = xy1_all + pp.pts_off;
     const double* xy2 = xy2_all + pp.pts_off;
-    double* res0 = scratch + pp.scr_off;
-    double* res1 = res0 + n;
-    double* xin1 = res1 + n;
-    double* xin2 = xin1 + 2 * n;
-    uint32_t* sg = idx_scratch + pp.idx_off;
-    if (tid == 0) mt_seed(s, pair_seed(P.base_seed, pp.id1, pp.id2));
-    __syncthreads();
+    double* base = scratch + pp.scr_off;  // 10 n + kVerifyModelDoubles doubles
+    double* res0 = base;
+    double* res1 = base + n;
+    double* xin1 = base + 2 * n;
+    double* xin2 = base + 4 * n;
+    double* mbuf = base + 10 * n;  // kTrialBatch * 27 doubles
+    if (lane == 0) mt_seed(s, pair_seed(P.base_seed, pp.id1, pp.id2));
+    wsync();
 
     // ---- F: LORANSAC<7-pt, 8-pt>.
-    const RansacResult rf = loransac_wg<KIND_F>(s, xy1, xy2, n, P.max_trials_F, P, res0, res1,
-                                                xin1, xin2, sg);
+    const RansacResult rf = loransac_wave<KIND_F>(s, sidx, xy1, xy2, n, P.max_trials_F, P, res0,
+                                                  res1, xin1, xin2, snap, mbuf, pf);
     double Fm[9];
     for (int i = 0; i < 9; ++i) Fm[i] = s.best_model[i];
     const double* resF = rf.res_sel ? res1 : res0;
     // F inlier mask (ExtractInlierMatches input) before the buffers are reused.
     if (rf.success)
-      for (int i = tid; i < n; i += kVerifyThreads) mask[i] = resF[i] <= P.max_residual ? 1 : 0;
-    __syncthreads();
+      for (int i = lane; i < n; i += 64) mask[i] = resF[i] <= P.max_residual ? 1 : 0;
+    wsync();
     // ---- H: LORANSAC<H, H> (same PRNG stream).
-    const RansacResult rh = loransac_wg<KIND_H>(s, xy1, xy2, n, P.max_trials_H, P, res0, res1,
-                                                xin1, xin2, sg);
+    const RansacResult rh = loransac_wave<KIND_H>(s, sidx, xy1, xy2, n, P.max_trials_H, P, res0,
+                                                  res1, xin1, xin2, snap, mbuf, pf);
     double Hm[9];
     for (int i = 0; i < 9; ++i) Hm[i] = s.best_model[i];
     o.f_trials = rf.num_trials;
@@ -569,7 +741,7 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
         // DetectWatermark with the dummy cameras (width = height = 0): a point
         // is inside the [0,0]x[0,0] box only if it is exactly (0, 0).
         int nb = 0;
-        for (int i = tid; i < n; i += kVerifyThreads) {
+        for (int i = lane; i < n; i += 64) {
           if (!mask[i]) continue;
           const bool in1 = xy1[2 * i] >= 0.0 && xy1[2 * i] <= 0.0 && xy1[2 * i + 1] >= 0.0 &&
                            xy1[2 * i + 1] <= 0.0;
@@ -577,50 +749,37 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
                            xy2[2 * i + 1] <= 0.0;
           nb += (!in1 && !in2) ? 1 : 0;
         }
-        nb = wg_sum_i(s, nb);
+        nb = wave_sum_i(nb);
         const int ni = rf.num_inliers;
         const double bratio = (double)nb / (double)ni;
         if (!(bratio < P.watermark_min_inlier_ratio)) {
           // Inlier points in index order -> translation LO-RANSAC.  Scratch
-          // layout (10n doubles per pair, res0 = base): tin1 [0,2ni) tin2
-          // [2n,2n+2ni) tres0 [4n,4n+ni) tres1 [5n,5n+ni) tx1 [6n,6n+2ni)
-          // tx2 [8n,8n+2ni).
-          double* base = res0;
+          // layout (10n doubles): tin1 [0,2ni) tin2 [2n,2n+2ni) tres0
+          // [4n,4n+ni) tres1 [5n,5n+ni) tx1 [6n,6n+2ni) tx2 [8n,8n+2ni).
           double* tin1 = base;
           double* tin2 = base + 2 * n;
-          {
-            const int per = (n + kVerifyThreads - 1) / kVerifyThreads;
-            const int i0 = min(n, tid * per), i1 = min(n, i0 + per);
-            int c = 0;
-            for (int i = i0; i < i1; ++i) c += mask[i] ? 1 : 0;
-            s.scan[tid] = c;
-            __syncthreads();
-            if (tid == 0) {
-              int acc = 0;
-              for (int t = 0; t < kVerifyThreads; ++t) {
-                const int v = s.scan[t];
-                s.scan[t] = acc;
-                acc += v;
-              }
+          int w = 0;
+          for (int b0 = 0; b0 < n; b0 += 64) {
+            const int i = b0 + lane;
+            const bool in = i < n && mask[i];
+            const uint64_t bal = __ballot(in);
+            if (in) {
+              const int o2 = w + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+              tin1[2 * o2] = xy1[2 * i];
+              tin1[2 * o2 + 1] = xy1[2 * i + 1];
+              tin2[2 * o2] = xy2[2 * i];
+              tin2[2 * o2 + 1] = xy2[2 * i + 1];
             }
-            __syncthreads();
-            int w = s.scan[tid];
-            for (int i = i0; i < i1; ++i)
-              if (mask[i]) {
-                tin1[2 * w] = xy1[2 * i];
-                tin1[2 * w + 1] = xy1[2 * i + 1];
-                tin2[2 * w] = xy2[2 * i];
-                tin2[2 * w + 1] = xy2[2 * i + 1];
-                ++w;
-              }
-            __syncthreads();
+            w += __popcll(bal);
           }
+          wsync();
           double* tres0 = base + 4 * n;
           double* tres1 = base + 5 * n;
           double* tx1 = base + 6 * n;
           double* tx2 = base + 8 * n;
-          const RansacResult rt = loransac_wg<KIND_T>(s, tin1, tin2, ni, P.max_trials_T, P, tres0,
-                                                      tres1, tx1, tx2, sg);
+          const RansacResult rt = loransac_wave<KIND_T>(s, sidx, tin1, tin2, ni, P.max_trials_T,
+                                                        P, tres0, tres1, tx1, tx2, snap, mbuf, pf);
           const double iratio = (double)rt.num_inliers / (double)ni;
           if (iratio >= P.watermark_min_inlier_ratio) {
             o.config = SCM_TVG_WATERMARK;
@@ -635,10 +794,8 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
       o.num_inliers = 0;
       for (int i = 0; i < 9; ++i) { o.F[i] = 0.0; o.H[i] = 0.0; }
     }
-  } else {
-    o.config = 0;  // DEGENERATE, then the post-filter's TwoViewGeometry()
   }
-  if (tid == 0) out[blockIdx.x] = o;
+  if (lane == 0) out[blockIdx.x] = o;
 }
 
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
@@ -657,13 +814,24 @@ __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2*
   }
 }
 
-hipError_t launch_verify(const VerifyPair* pairs, int npairs, const double* xy1,
-                         const double* xy2, double* scratch, uint32_t* idx_scratch,
-                         uint8_t* masks, VerifyOut* out, const VerifyParams& params,
+size_t verify_lds_bytes(int max_m) {
+  return sizeof(VerifyLds) + (size_t)((max_m + 7) / 8 * 8) * sizeof(uint16_t);
+}
+
+hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
+                         const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
+                         VerifyOut* out, const VerifyParams& params, uint64_t* prof,
                          hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(verify_kernel, dim3(npairs), dim3(kVerifyThreads), 0, stream, pairs, xy1,
-                     xy2, scratch, idx_scratch, masks, out, params);
+  const size_t lds = verify_lds_bytes(max_m);
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)verify_kernel,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(verify_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs, xy1,
+                     xy2, scratch, snaps, masks, out, params, prof);
   return hipGetLastError();
 }
 
