@@ -140,9 +140,9 @@ def main():
             gdesc += float(n_per_img[r]) * n_per_img[j]
 
     def step():
-        pa, pb = ctx.table_run(overlap, lr_b, lr_e)
+        packed = ctx.table_run_packed(overlap, lr_b, lr_e)
         if world > 1:
-            sd.gather_to_root(sd.pack_rows(pa, pb), device=device)
+            sd.gather_to_root(sd.pack_packed(packed.offsets, packed.data), device=device)
         return ctx.table_timings()
 
     for _ in range(args.warmup):

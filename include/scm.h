@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SCM_ABI_VERSION 1
+#define SCM_ABI_VERSION 2
 
 enum {
   SCM_OK = 0,
@@ -172,9 +172,22 @@ int scm_table_load(scm_context* ctx, int64_t num_rows,
 int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin,
                   int64_t row_end, scm_blob* pair_image_ids_out,
                   scm_blob* tvgs_out);
+/* Same run, one packed output: rows_out receives a single buffer holding, for
+ * each output row r in order, the pair_image_ids element followed by the
+ * two_view_geometries element; row_offsets (2 * (row_end - row_begin) + 1
+ * entries, caller-allocated) receives the byte offset of each element and the
+ * total size last: element 2r spans [row_offsets[2r], row_offsets[2r+1]),
+ * element 2r+1 spans [row_offsets[2r+1], row_offsets[2r+2]).  Saves one
+ * allocation per element on the serving path (the bytes are identical). */
+int scm_table_run_packed(scm_context* ctx, int64_t overlap, int64_t row_begin,
+                         int64_t row_end, scm_blob* rows_out,
+                         int64_t* row_offsets);
+/* Keep (keep != 0) the raw cross-checked matches of every pair of the
+ * following table runs for scm_table_matches; off by default. */
+int scm_set_keep_matches(scm_context* ctx, int32_t keep);
 /* Raw cross-checked matches of the most recent scm_table_run for the pair
  * (row, row + offset), offset in [1, overlap); the debug `matches` output the
- * bit-exact checks read. */
+ * bit-exact checks read.  Requires scm_set_keep_matches. */
 int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset,
                       uint32_t* matches, int64_t cap, int64_t* num_matches);
 

@@ -635,6 +635,14 @@ uint32_t oracle_pair_seed(uint32_t base, uint32_t id1, uint32_t id2) {
   return h;
 }
 
+// ComputeNumTrials as the oracle evaluates it (test support: the
+// libm-free restatement is compared with std::log/std::pow in tests).
+uint64_t oracle_num_trials(uint64_t num_inliers, uint64_t num_samples,
+                           double confidence, double multiplier, int32_t kmin) {
+  return (uint64_t)compute_num_trials(num_inliers, num_samples, confidence,
+                                      multiplier, kmin);
+}
+
 int oracle_match_pair(const scm_matching_options* o, const uint8_t* d1,
                       int64_t n1, const uint8_t* d2, int64_t n2,
                       uint32_t* out, int64_t cap, int64_t* m) {

@@ -10,7 +10,7 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
-from ctypes import (POINTER, byref, c_double, c_float, c_int, c_int32, c_int64,
+from ctypes import (POINTER, byref, c_double, c_float, c_int, c_int32, c_int64, c_uint64,
                     c_size_t, c_uint8, c_uint32, c_void_p)
 
 import numpy as np
@@ -58,6 +58,8 @@ def lib() -> ctypes.CDLL:
                                    POINTER(Element), POINTER(Element), c_int64, c_int64,
                                    c_int64, POINTER(POINTER(c_uint8)), POINTER(c_size_t),
                                    POINTER(POINTER(c_uint8)), POINTER(c_size_t)]
+    L.oracle_num_trials.argtypes = [c_uint64, c_uint64, c_double, c_double, c_int32]
+    L.oracle_num_trials.restype = c_uint64
     L.oracle_free.argtypes = [POINTER(c_uint8)]
     L.oracle_free.restype = None
     _lib = L
@@ -135,6 +137,10 @@ def loransac(kind, x1, x2, seed, opts=None):
                                mask.ctypes.data)
     return dict(success=bool(ok), model=model, num_inliers=ni.value, residual_sum=rs.value,
                 num_trials=nt.value, mask=mask.astype(bool))
+
+
+def num_trials(num_inliers, num_samples, confidence=0.999, multiplier=3.0, kmin=7) -> int:
+    return int(lib().oracle_num_trials(num_inliers, num_samples, confidence, multiplier, kmin))
 
 
 def std_uniform(seed, lo, hi) -> np.ndarray:

@@ -32,7 +32,8 @@ EXPORTS = (
     "scm_parse_args", "scm_pair_seed", "scm_blob_free",
     "scm_context_create", "scm_context_destroy", "scm_match_pair",
     "scm_verify_pair", "scm_execute_stencil", "scm_table_load",
-    "scm_table_run", "scm_table_matches", "scm_table_timings",
+    "scm_table_run", "scm_table_run_packed", "scm_set_keep_matches",
+    "scm_table_matches", "scm_table_timings",
 )
 
 
@@ -102,6 +103,9 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                    POINTER(Element), POINTER(Element)]
     lib.scm_table_run.argtypes = [c_void_p, c_int64, c_int64, c_int64,
                                   POINTER(Blob), POINTER(Blob)]
+    lib.scm_table_run_packed.argtypes = [c_void_p, c_int64, c_int64, c_int64,
+                                         POINTER(Blob), c_void_p]
+    lib.scm_set_keep_matches.argtypes = [c_void_p, c_int32]
     lib.scm_table_matches.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64,
                                       POINTER(c_int64)]
     lib.scm_table_timings.argtypes = [c_void_p, POINTER(c_double), c_int32]
@@ -157,6 +161,39 @@ def _elements(chunks) -> tuple:
         arr[i].buffer = a.ctypes.data_as(POINTER(c_uint8))
         arr[i].size = a.nbytes
     return arr, keep
+
+
+class PackedRows:
+    """Output of scm_table_run_packed: one library-owned buffer (freed with
+    scm_blob_free when this object dies) plus the element offsets.  Element
+    2r is row r's pair_image_ids, element 2r+1 its two_view_geometries."""
+
+    def __init__(self, blob: Blob, offsets: np.ndarray):
+        self._blob = blob
+        self.offsets = offsets
+        n = int(blob.size)
+        self.data = (np.ctypeslib.as_array(blob.data, shape=(n,)) if n
+                     else np.zeros(0, dtype=np.uint8))
+
+    def __len__(self) -> int:
+        return (len(self.offsets) - 1) // 2
+
+    def element(self, k: int) -> bytes:
+        return self.data[self.offsets[k]:self.offsets[k + 1]].tobytes()
+
+    def rows(self) -> tuple[list[bytes], list[bytes]]:
+        n = len(self)
+        return ([self.element(2 * r) for r in range(n)],
+                [self.element(2 * r + 1) for r in range(n)])
+
+    def __del__(self):
+        try:
+            if self._blob is not None and self._blob.data:
+                self.data = None
+                load_library().scm_blob_free(byref(self._blob))
+                self._blob = None
+        except Exception:
+            pass
 
 
 class Context:
@@ -231,6 +268,17 @@ class Context:
         b = (Blob * max(1, n))()
         _check(self._lib.scm_table_run(self._ptr, overlap, row_begin, row_end, a, b))
         return [_blob_bytes(a[i]) for i in range(n)], [_blob_bytes(b[i]) for i in range(n)]
+
+    def table_run_packed(self, overlap: int, row_begin: int, row_end: int) -> PackedRows:
+        n = row_end - row_begin
+        offs = np.zeros(2 * n + 1, dtype=np.int64)
+        b = Blob()
+        _check(self._lib.scm_table_run_packed(self._ptr, overlap, row_begin, row_end, byref(b),
+                                              offs.ctypes.data))
+        return PackedRows(b, offs)
+
+    def set_keep_matches(self, keep: bool = True) -> None:
+        _check(self._lib.scm_set_keep_matches(self._ptr, 1 if keep else 0))
 
     def table_matches(self, row: int, offset: int, cap: int = 1 << 16) -> np.ndarray:
         out = np.zeros((max(1, cap), 2), dtype=np.uint32)

@@ -268,6 +268,10 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
   const PairDesc pd = pairs[blockIdx.x];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
+  if (pd.n1 == 0 || pd.n2 == 0) {  // no descriptors on one side: no matches
+    if (tid == 0) counts[blockIdx.x] = 0;
+    return;
+  }
   int32_t* m21 = m21_scratch + pd.m21_off;
   const uint2* cp = colpart + pd.colpart_off;
   const uint2* rr = rowres + pd.rowres_off;

@@ -4,15 +4,27 @@
 // (reference integration/op_cpp/sequential_matching.cc:27-205): one context
 // = one kernel instance bound to one device with its own stream and HBM
 // workspace; execute() over a stencil, or the batched table path that keeps
-// every descriptor resident in HBM and runs all pairs of a row range in
-// large launches.
+// every descriptor resident in HBM.
+//
+// Batch pipeline (table path): pairs are cut into batches of whole pivot
+// rows; each batch is enqueued as
+//   match tiles -> finalize -> gather -> verify -> scan + compact
+// on the context's stream with no host synchronisation in between (the
+// verifier reads the match counts from device memory; buffers are laid out
+// for the worst case, one match slot per pivot keypoint).  The compact kernel
+// writes counts, matches and F-inlier masks, and the verifier its geometry
+// records, straight into host-mapped pinned memory.  Two batch buffer sets
+// alternate, so the host serialises batch b's io.cc rows (multithreaded)
+// while the GPU runs batch b+1.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "geom_solvers.h"
@@ -26,7 +38,7 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 
 namespace {
 
-constexpr int64_t kMaxPairsPerBatch = 4096;
+constexpr int64_t kMaxPairsPerBatch = 2048;
 
 struct ImageTable {
   int64_t n = 0;
@@ -36,9 +48,9 @@ struct ImageTable {
   std::vector<int64_t> kp_off;    // first float2 keypoint
   std::vector<uint64_t> max_norm2;
   int64_t total_rows = 0, total_kp = 0;
-  DevBuf desc;   // uint16 bf16 [total_rows][128]
-  DevBuf kpxy;   // float2 [total_kp]
-  DevBuf u8;     // upload staging
+  DevBuf desc;  // uint16 bf16 [total_rows][128]
+  DevBuf kpxy;  // float2 [total_kp]
+  DevBuf u8;    // upload staging
   void release() {
     desc.release();
     kpxy.release();
@@ -50,10 +62,67 @@ struct PairSpec {
   int32_t a, b;  // image indices in the table
 };
 
-struct PairResult {
-  std::vector<Match> matches;
-  VerifyOut vo;
-  std::vector<uint8_t> mask;
+// Host-mapped pinned buffer (device writes, host reads after the event).
+struct MappedBuf {
+  void* host = nullptr;
+  void* dev = nullptr;
+  size_t bytes = 0;
+  int ensure(size_t need) {
+    if (need <= bytes) return SCM_OK;
+    release();
+    const size_t want = need + need / 4 + 4096;
+    if (hipHostMalloc(&host, want, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+      host = nullptr;
+      set_error("hipHostMalloc(mapped) of " + std::to_string(want) + " bytes failed");
+      return SCM_E_NOMEM;
+    }
+    if (hipHostGetDevicePointer(&dev, host, 0) != hipSuccess) {
+      set_error("hipHostGetDevicePointer failed");
+      return SCM_E_DEVICE;
+    }
+    bytes = want;
+    return SCM_OK;
+  }
+  void release() {
+    if (host) (void)hipHostFree(host);
+    host = dev = nullptr;
+    bytes = 0;
+  }
+};
+
+// One in-flight batch: device workspace, descriptor staging, results.
+struct BatchSet {
+  DevBuf jobs, pairs, rowres, colpart, m21, matches, counts, gpairs, vpairs, xy1, xy2, scratch,
+      snaps, masks, offsets, match_off, prof;
+  HostBuf stage;
+  MappedBuf out;
+  size_t off_counts = 0, off_offsets = 0, off_vout = 0, off_matches = 0, off_masks = 0;
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  int64_t P = 0;
+  bool verify = false;
+  bool pending = false;
+  bool matched = false;
+  void release() {
+    for (DevBuf* b : {&jobs, &pairs, &rowres, &colpart, &m21, &matches, &counts, &gpairs, &vpairs,
+                      &xy1, &xy2, &scratch, &snaps, &masks, &offsets, &match_off, &prof})
+      b->release();
+    stage.release();
+    out.release();
+    for (auto& e : ev) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+  }
+};
+
+// Collected results of one batch (views into the mapped buffer).
+struct BatchView {
+  int64_t P = 0;
+  const int32_t* counts = nullptr;
+  const int64_t* offsets = nullptr;
+  const VerifyOut* vout = nullptr;  // P entries (verify runs only)
+  const Match* matches = nullptr;   // pair p at offsets[p]
+  const uint8_t* masks = nullptr;
 };
 
 }  // namespace
@@ -65,24 +134,21 @@ struct scm_context {
   int device = 0;
   hipStream_t stream = nullptr;
   scm_matching_options opts;
-  std::vector<float> lut_host;
   DevBuf lut;
   ImageTable table, scratch_table;
   bool table_loaded = false;
-  // matcher workspace
-  DevBuf d_jobs, d_pairs, d_rowres, d_colpart, d_m21, d_matches, d_counts;
-  // verification workspace
-  DevBuf d_gpairs, d_vpairs, d_xy1, d_xy2, d_packed, d_scratch, d_idx, d_masks, d_vout;
-  HostBuf h_stage;
+  BatchSet sets[2];
+  HostBuf h_stage;  // table upload staging
+  int threads = 1;
+  int64_t batch_pairs = kMaxPairsPerBatch;  // SCM_BATCH_PAIRS overrides (tests)
+  double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
   bool profile = false;
-  DevBuf d_prof;
   std::vector<uint64_t> prof_sum;
   int64_t prof_pairs = 0;
-  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
-  // last table run, for scm_table_matches
-  int64_t last_begin = 0, last_end = 0, last_overlap = 0;
+  // raw matches of the last table run (scm_set_keep_matches)
+  bool keep_matches = false;
+  int64_t last_begin = 0, last_end = 0;
   std::vector<std::vector<std::pair<int64_t, std::vector<Match>>>> last_matches;
 };
 
@@ -96,6 +162,29 @@ void build_lut(std::vector<float>* lut) {
   const float kDistNorm = 1.0f / (512.0f * 512.0f);
   for (uint32_t d = 0; d <= kLutMax; ++d)
     (*lut)[d] = std::acos(std::min(kDistNorm * (float)(int32_t)d, 1.0f));
+}
+
+double event_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
+  return (double)ms;
+}
+
+template <typename F>
+void parallel_for(int threads, int64_t n, F f) {
+  if (threads <= 1 || n < 64) {
+    for (int64_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> ts;
+  const int T = (int)std::min<int64_t>(threads, n);
+  const int64_t chunk = (n + T - 1) / T;
+  for (int t = 0; t < T; ++t)
+    ts.emplace_back([&, t] {
+      const int64_t e = std::min(n, (t + 1) * chunk);
+      for (int64_t i = t * chunk; i < e; ++i) f(i);
+    });
+  for (auto& th : ts) th.join();
 }
 
 int upload_table(scm_context* ctx, ImageTable* t, const std::vector<RowView>& rows,
@@ -128,7 +217,7 @@ int upload_table(scm_context* ctx, ImageTable* t, const std::vector<RowView>& ro
     const size_t bytes = (size_t)total_rows * 128;
     SCM_TRY(ctx->h_stage.ensure(bytes));
     uint8_t* h = ctx->h_stage.as<uint8_t>();
-    for (int64_t i = 0; i < t->n; ++i) {
+    parallel_for(ctx->threads, t->n, [&](int64_t i) {
       const RowView& r = rows[i];
       uint8_t* dst = h + (size_t)t->desc_row[i] * 128;
       const size_t nb = (size_t)r.ndesc * 128;
@@ -143,7 +232,7 @@ int upload_table(scm_context* ctx, ImageTable* t, const std::vector<RowView>& ro
         mx = std::max<uint64_t>(mx, s);
       }
       t->max_norm2[i] = mx;
-    }
+    });
     SCM_TRY(t->u8.ensure(bytes));
     SCM_TRY(t->desc.ensure(bytes * 2));
     SCM_HIP(hipMemcpyAsync(t->u8.ptr, h, bytes, hipMemcpyHostToDevice, ctx->stream));
@@ -196,252 +285,357 @@ VerifyParams make_params(const scm_matching_options& o) {
   return p;
 }
 
-double event_ms(hipEvent_t a, hipEvent_t b) {
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.0;
-  return (double)ms;
-}
+size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 
-// Descriptor matching of the given pairs (pairs of one pivot consecutive).
-// Leaves per-pair matches on the device at PairDesc.match_off and counts in
-// d_counts; returns host copies of both descriptors arrays for the verifier.
-int match_stage(scm_context* ctx, const ImageTable& t, const std::vector<PairSpec>& specs,
-                std::vector<PairDesc>* pds_out, std::vector<int32_t>* counts_out) {
+// Enqueue one batch on the context stream.  given != nullptr: skip matching
+// and verify the given matches of the single pair specs[0] instead.
+int enqueue_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
+                  const std::vector<PairSpec>& specs, bool verify, const uint32_t* given,
+                  int64_t given_m) {
   const int64_t P = (int64_t)specs.size();
+  bs.P = P;
+  bs.verify = verify;
+  bs.matched = given == nullptr;
+  bs.pending = false;
+  for (auto& e : bs.ev)
+    if (!e) SCM_HIP(hipEventCreate(&e));
+  if (P == 0) return SCM_OK;
+  // ---- descriptors (worst-case layout: one match slot per pivot keypoint).
   std::vector<PairDesc> pds(P);
-  std::vector<MatchJob> jobs_fast, jobs_clamp;
-  int64_t rr = 0, cp = 0, m21 = 0, mo = 0;
-  std::vector<char> active(P, 0);
-  // Active pairs are packed first so the finalize grid covers exactly them.
-  std::vector<int64_t> order;
-  for (int64_t i = 0; i < P; ++i)
-    if (t.ndesc[specs[i].a] > 0 && t.ndesc[specs[i].b] > 0) active[i] = 1;
-  int64_t i = 0;
-  std::vector<PairDesc> packed;
-  std::vector<int64_t> packed_src;
-  while (i < P) {
+  std::vector<int64_t> moff(P), soff(P);
+  std::vector<MatchJob> jobs, jobs_clamp;
+  int64_t rr = 0, cp = 0, m21 = 0, mo = 0, scr = 0;
+  int max_slots = 0;
+  for (int64_t i = 0; i < P;) {
     const int32_t a = specs[i].a;
     int64_t j = i;
     while (j < P && specs[j].a == a) ++j;
-    const int32_t pair0 = (int32_t)packed.size();
     bool clamp = false;
-    int32_t np = 0;
+    // match slots of every pair of this pivot
+    const int32_t slots = given ? (int32_t)std::max<int64_t>(given_m, 1) : t.ndesc[a];
     for (int64_t k = i; k < j; ++k) {
-      if (!active[k]) continue;
       const int32_t b = specs[k].b;
-      PairDesc pd;
+      PairDesc& pd = pds[k];
       std::memset(&pd, 0, sizeof(pd));
-      pd.n1 = t.ndesc[a];
-      pd.n2 = t.ndesc[b];
+      pd.n1 = given ? 0 : t.ndesc[a];
+      pd.n2 = given ? 0 : t.ndesc[b];
       pd.n2pad = (pd.n2 + 31) / 32 * 32;
       pd.nseg = (pd.n2 + kColsPerSeg - 1) / kColsPerSeg;
       pd.nrb = (pd.n1 + kRowsPerBlock - 1) / kRowsPerBlock;
-      pd.b_row = t.desc_row[b];
+      pd.b_row = given ? 0 : t.desc_row[b];
       pd.rowres_off = rr;
       pd.colpart_off = cp;
       pd.m21_off = m21;
       pd.match_off = mo;
+      moff[k] = mo;
+      soff[k] = scr;
       rr += (int64_t)pd.nseg * pd.n1;
       cp += (int64_t)pd.nrb * pd.n2pad;
       m21 += pd.n2;
-      mo += pd.n1;
-      // |a||b| < 2^19 for every row pair  <=>  max|a|^2 * max|b|^2 < 2^38.
-      const unsigned __int128 prod = (unsigned __int128)t.max_norm2[a] * t.max_norm2[b];
-      if (prod >= ((unsigned __int128)1 << 38)) clamp = true;
-      packed.push_back(pd);
-      packed_src.push_back(k);
-      ++np;
+      mo += slots;
+      scr += 10 * (int64_t)slots + kVerifyModelDoubles;
+      max_slots = std::max(max_slots, slots);
+      if (!given) {
+        // |a||b| < 2^19 for every row pair  <=>  max|a|^2 * max|b|^2 < 2^38.
+        const unsigned __int128 prod = (unsigned __int128)t.max_norm2[a] * t.max_norm2[b];
+        if (prod >= ((unsigned __int128)1 << 38)) clamp = true;
+      }
     }
-    if (np > 0) {
+    if (!given && t.ndesc[a] > 0) {
+      // Jobs over runs of consecutive active pairs of this pivot.
       const int32_t n1 = t.ndesc[a];
       const int32_t nrb = (n1 + kRowsPerBlock - 1) / kRowsPerBlock;
-      for (int32_t rb = 0; rb < nrb; ++rb) {
-        MatchJob jb;
-        jb.a_row = t.desc_row[a];
-        jb.rb = rb;
-        jb.n1 = n1;
-        jb.pair0 = pair0;
-        jb.npairs = np;
-        (clamp ? jobs_clamp : jobs_fast).push_back(jb);
+      for (int64_t k = i; k < j;) {
+        while (k < j && pds[k].n2 == 0) ++k;
+        int64_t e = k;
+        while (e < j && pds[e].n2 > 0) ++e;
+        if (e > k)
+          for (int32_t rb = 0; rb < nrb; ++rb) {
+            MatchJob jb;
+            jb.a_row = t.desc_row[a];
+            jb.rb = rb;
+            jb.n1 = n1;
+            jb.pair0 = (int32_t)k;
+            jb.npairs = (int32_t)(e - k);
+            (clamp ? jobs_clamp : jobs).push_back(jb);
+          }
+        k = e;
       }
     }
     i = j;
   }
-  const int64_t PA = (int64_t)packed.size();
-  pds_out->assign(P, PairDesc());
-  counts_out->assign(P, 0);
-  for (int64_t k = 0; k < PA; ++k) (*pds_out)[packed_src[k]] = packed[k];
-  if (PA == 0) return SCM_OK;
-  const int64_t nj = (int64_t)(jobs_fast.size() + jobs_clamp.size());
-  SCM_TRY(ctx->d_jobs.ensure(nj * sizeof(MatchJob)));
-  SCM_TRY(ctx->d_pairs.ensure(PA * sizeof(PairDesc)));
-  SCM_TRY(ctx->d_rowres.ensure(std::max<int64_t>(rr, 1) * sizeof(uint2)));
-  SCM_TRY(ctx->d_colpart.ensure(std::max<int64_t>(cp, 1) * sizeof(uint2)));
-  SCM_TRY(ctx->d_m21.ensure(std::max<int64_t>(m21, 1) * sizeof(int32_t)));
-  SCM_TRY(ctx->d_matches.ensure(std::max<int64_t>(mo, 1) * sizeof(uint2)));
-  SCM_TRY(ctx->d_counts.ensure(PA * sizeof(int32_t)));
-  std::vector<MatchJob> jobs(jobs_fast);
-  jobs.insert(jobs.end(), jobs_clamp.begin(), jobs_clamp.end());
-  SCM_HIP(hipMemcpyAsync(ctx->d_jobs.ptr, jobs.data(), nj * sizeof(MatchJob),
-                         hipMemcpyHostToDevice, ctx->stream));
-  SCM_HIP(hipMemcpyAsync(ctx->d_pairs.ptr, packed.data(), PA * sizeof(PairDesc),
-                         hipMemcpyHostToDevice, ctx->stream));
-  SCM_HIP(hipEventRecord(ctx->ev[0], ctx->stream));
-  SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), ctx->d_jobs.as<MatchJob>(),
-                             (int)jobs_fast.size(), ctx->d_pairs.as<PairDesc>(),
-                             ctx->d_rowres.as<uint2>(), ctx->d_colpart.as<uint2>(), false,
-                             ctx->stream));
-  SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), ctx->d_jobs.as<MatchJob>() + jobs_fast.size(),
-                             (int)jobs_clamp.size(), ctx->d_pairs.as<PairDesc>(),
-                             ctx->d_rowres.as<uint2>(), ctx->d_colpart.as<uint2>(), true,
-                             ctx->stream));
-  SCM_HIP(hipEventRecord(ctx->ev[1], ctx->stream));
-  SCM_HIP(launch_match_finalize(ctx->d_pairs.as<PairDesc>(), (int)PA, ctx->d_rowres.as<uint2>(),
-                                ctx->d_colpart.as<uint2>(), ctx->d_m21.as<int32_t>(),
-                                ctx->lut.as<float>(), (float)ctx->opts.max_ratio,
-                                (float)ctx->opts.max_distance, ctx->opts.cross_check,
-                                ctx->d_matches.as<uint2>(), ctx->d_counts.as<int32_t>(),
-                                ctx->stream));
-  SCM_HIP(hipEventRecord(ctx->ev[2], ctx->stream));
-  std::vector<int32_t> cnt(PA);
-  SCM_HIP(hipMemcpyAsync(cnt.data(), ctx->d_counts.ptr, PA * sizeof(int32_t),
-                         hipMemcpyDeviceToHost, ctx->stream));
-  SCM_HIP(hipStreamSynchronize(ctx->stream));
-  ctx->t_match += event_ms(ctx->ev[0], ctx->ev[1]);
-  ctx->t_final += event_ms(ctx->ev[1], ctx->ev[2]);
-  for (int64_t k = 0; k < PA; ++k) (*counts_out)[packed_src[k]] = cnt[k];
-  return SCM_OK;
-}
-
-// Geometry of the given pairs from matches already on the device
-// (d_matches at pds[i].match_off, counts[i] entries); fills results.
-int verify_stage(scm_context* ctx, const ImageTable& t, const std::vector<PairSpec>& specs,
-                 const std::vector<PairDesc>& pds, const std::vector<int32_t>& counts,
-                 bool verify, std::vector<PairResult>* results) {
-  const int64_t P = (int64_t)specs.size();
-  results->assign(P, PairResult());
-  std::vector<GatherPair> gp;
-  std::vector<VerifyPair> vp;
-  std::vector<int64_t> vsrc, gsrc;
-  int64_t pts = 0, scr = 0;
-  int max_m = 0;
-  for (int64_t i = 0; i < P; ++i) {
-    const int32_t m = counts[i];
-    if (m <= 0) continue;
-    if (m > kMaxVerifyMatches) {
-      set_error("more than 65535 matches in one pair");
-      return SCM_E_INVALID;
-    }
-    GatherPair g;
-    std::memset(&g, 0, sizeof(g));
-    g.match_off = pds[i].match_off;
-    g.kp1_off = t.kp_off[specs[i].a];
-    g.kp2_off = t.kp_off[specs[i].b];
-    g.pts_off = pts;
-    g.m = m;
-    gp.push_back(g);
-    gsrc.push_back(i);
-    if (verify && m >= ctx->opts.min_num_inliers) {
-      VerifyPair v;
-      std::memset(&v, 0, sizeof(v));
-      v.pts_off = 2 * pts;
-      v.scr_off = scr;
-      v.mask_off = pts;
-      v.m = m;
-      v.id1 = t.ids[specs[i].a];
-      v.id2 = t.ids[specs[i].b];
-      vp.push_back(v);
-      vsrc.push_back(i);
-      scr += 10 * (int64_t)m + kVerifyModelDoubles;
-      max_m = std::max(max_m, m);
-    }
-    pts += m;
+  if (verify && max_slots > kMaxVerifyMatches) {
+    set_error("more than 65535 keypoints in a pivot image (verifier index limit)");
+    return SCM_E_INVALID;
   }
-  if (gp.empty()) return SCM_OK;
-  const int64_t G = (int64_t)gp.size(), V = (int64_t)vp.size();
-  SCM_TRY(ctx->d_gpairs.ensure(G * sizeof(GatherPair)));
-  SCM_TRY(ctx->d_xy1.ensure(2 * pts * sizeof(double)));
-  SCM_TRY(ctx->d_xy2.ensure(2 * pts * sizeof(double)));
-  SCM_TRY(ctx->d_packed.ensure(pts * sizeof(uint2)));
-  SCM_TRY(ctx->d_masks.ensure(pts));
-  SCM_HIP(hipMemcpyAsync(ctx->d_gpairs.ptr, gp.data(), G * sizeof(GatherPair),
-                         hipMemcpyHostToDevice, ctx->stream));
-  SCM_HIP(launch_gather(ctx->d_gpairs.as<GatherPair>(), (int)G, ctx->d_matches.as<uint2>(),
-                        t.kpxy.as<float2>(), ctx->d_xy1.as<double>(), ctx->d_xy2.as<double>(),
-                        ctx->d_packed.as<uint2>(), ctx->stream));
-  std::vector<VerifyOut> vout(V);
-  if (V > 0) {
-    SCM_TRY(ctx->d_vpairs.ensure(V * sizeof(VerifyPair)));
-    SCM_TRY(ctx->d_scratch.ensure(std::max<int64_t>(scr, 1) * sizeof(double)));
-    SCM_TRY(ctx->d_idx.ensure(V * 640 * sizeof(uint32_t)));
-    SCM_TRY(ctx->d_vout.ensure(V * sizeof(VerifyOut)));
-    SCM_HIP(hipMemcpyAsync(ctx->d_vpairs.ptr, vp.data(), V * sizeof(VerifyPair),
-                           hipMemcpyHostToDevice, ctx->stream));
-    const VerifyParams params = make_params(ctx->opts);
-    SCM_HIP(hipEventRecord(ctx->ev[3], ctx->stream));
+  const int64_t nfast = (int64_t)jobs.size();
+  jobs.insert(jobs.end(), jobs_clamp.begin(), jobs_clamp.end());
+  const int64_t NJ = (int64_t)jobs.size();
+  std::vector<GatherPair> gps(P);
+  std::vector<VerifyPair> vps(P);
+  for (int64_t k = 0; k < P; ++k) {
+    GatherPair& g = gps[k];
+    std::memset(&g, 0, sizeof(g));
+    g.match_off = moff[k];
+    g.kp1_off = t.kp_off[specs[k].a];
+    g.kp2_off = t.kp_off[specs[k].b];
+    g.pts_off = moff[k];
+    g.cidx = (int32_t)k;
+    VerifyPair& v = vps[k];
+    std::memset(&v, 0, sizeof(v));
+    v.pts_off = 2 * moff[k];
+    v.scr_off = soff[k];
+    v.mask_off = moff[k];
+    v.cidx = (int32_t)k;
+    v.id1 = t.ids[specs[k].a];
+    v.id2 = t.ids[specs[k].b];
+    v.out_idx = (int32_t)k;
+  }
+  // ---- buffers.
+  SCM_TRY(bs.jobs.ensure(std::max<int64_t>(NJ, 1) * sizeof(MatchJob)));
+  SCM_TRY(bs.pairs.ensure(P * sizeof(PairDesc)));
+  SCM_TRY(bs.rowres.ensure(std::max<int64_t>(rr, 1) * sizeof(uint2)));
+  SCM_TRY(bs.colpart.ensure(std::max<int64_t>(cp, 1) * sizeof(uint2)));
+  SCM_TRY(bs.m21.ensure(std::max<int64_t>(m21, 1) * sizeof(int32_t)));
+  SCM_TRY(bs.matches.ensure(std::max<int64_t>(mo, 1) * sizeof(uint2)));
+  SCM_TRY(bs.masks.ensure(std::max<int64_t>(mo, 1)));
+  SCM_TRY(bs.counts.ensure(P * sizeof(int32_t)));
+  SCM_TRY(bs.offsets.ensure((P + 1) * sizeof(int64_t)));
+  SCM_TRY(bs.match_off.ensure(P * sizeof(int64_t)));
+  SCM_TRY(bs.gpairs.ensure(P * sizeof(GatherPair)));
+  SCM_TRY(bs.vpairs.ensure(P * sizeof(VerifyPair)));
+  if (verify) {
+    SCM_TRY(bs.xy1.ensure(2 * std::max<int64_t>(mo, 1) * sizeof(double)));
+    SCM_TRY(bs.xy2.ensure(2 * std::max<int64_t>(mo, 1) * sizeof(double)));
+    SCM_TRY(bs.scratch.ensure(std::max<int64_t>(scr, 1) * sizeof(double)));
+    SCM_TRY(bs.snaps.ensure(P * 640 * sizeof(uint32_t)));
+  }
+  bs.off_counts = 0;
+  bs.off_offsets = align256(bs.off_counts + P * sizeof(int32_t));
+  bs.off_vout = align256(bs.off_offsets + (P + 1) * sizeof(int64_t));
+  bs.off_matches = align256(bs.off_vout + P * sizeof(VerifyOut));
+  bs.off_masks = align256(bs.off_matches + mo * sizeof(uint2));
+  SCM_TRY(bs.out.ensure(bs.off_masks + mo + 256));
+  // ---- descriptor upload from pinned staging.
+  const size_t s_pairs = align256(NJ * sizeof(MatchJob));
+  const size_t s_g = align256(s_pairs + P * sizeof(PairDesc));
+  const size_t s_v = align256(s_g + P * sizeof(GatherPair));
+  const size_t s_mo = align256(s_v + P * sizeof(VerifyPair));
+  const size_t s_cnt = align256(s_mo + P * sizeof(int64_t));
+  const size_t s_given = align256(s_cnt + sizeof(int32_t));
+  const size_t s_end = s_given + (given ? (size_t)given_m * sizeof(uint2) : 0);
+  SCM_TRY(bs.stage.ensure(s_end));
+  uint8_t* st = bs.stage.as<uint8_t>();
+  if (NJ) std::memcpy(st, jobs.data(), NJ * sizeof(MatchJob));
+  std::memcpy(st + s_pairs, pds.data(), P * sizeof(PairDesc));
+  std::memcpy(st + s_g, gps.data(), P * sizeof(GatherPair));
+  std::memcpy(st + s_v, vps.data(), P * sizeof(VerifyPair));
+  std::memcpy(st + s_mo, moff.data(), P * sizeof(int64_t));
+  hipStream_t sm = ctx->stream;
+  if (NJ)
+    SCM_HIP(hipMemcpyAsync(bs.jobs.ptr, st, NJ * sizeof(MatchJob), hipMemcpyHostToDevice, sm));
+  SCM_HIP(hipMemcpyAsync(bs.pairs.ptr, st + s_pairs, P * sizeof(PairDesc), hipMemcpyHostToDevice,
+                         sm));
+  SCM_HIP(hipMemcpyAsync(bs.gpairs.ptr, st + s_g, P * sizeof(GatherPair), hipMemcpyHostToDevice,
+                         sm));
+  SCM_HIP(hipMemcpyAsync(bs.vpairs.ptr, st + s_v, P * sizeof(VerifyPair), hipMemcpyHostToDevice,
+                         sm));
+  SCM_HIP(hipMemcpyAsync(bs.match_off.ptr, st + s_mo, P * sizeof(int64_t), hipMemcpyHostToDevice,
+                         sm));
+  if (given) {
+    const int32_t gm = (int32_t)given_m;
+    std::memcpy(st + s_cnt, &gm, sizeof(gm));
+    SCM_HIP(hipMemcpyAsync(bs.counts.ptr, st + s_cnt, sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    if (given_m > 0) {
+      std::memcpy(st + s_given, given, (size_t)given_m * sizeof(uint2));
+      SCM_HIP(hipMemcpyAsync(bs.matches.ptr, st + s_given, (size_t)given_m * sizeof(uint2),
+                             hipMemcpyHostToDevice, sm));
+    }
+  }
+  // ---- kernels.
+  SCM_HIP(hipEventRecord(bs.ev[0], sm));
+  if (!given) {
+    SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), bs.jobs.as<MatchJob>(), (int)nfast,
+                               bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
+                               bs.colpart.as<uint2>(), false, sm));
+    SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), bs.jobs.as<MatchJob>() + nfast,
+                               (int)(NJ - nfast), bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
+                               bs.colpart.as<uint2>(), true, sm));
+  }
+  SCM_HIP(hipEventRecord(bs.ev[1], sm));
+  if (!given)
+    SCM_HIP(launch_match_finalize(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
+                                  bs.colpart.as<uint2>(), bs.m21.as<int32_t>(),
+                                  ctx->lut.as<float>(), (float)ctx->opts.max_ratio,
+                                  (float)ctx->opts.max_distance, ctx->opts.cross_check,
+                                  bs.matches.as<uint2>(), bs.counts.as<int32_t>(), sm));
+  SCM_HIP(hipEventRecord(bs.ev[2], sm));
+  uint8_t* outd = reinterpret_cast<uint8_t*>(bs.out.dev);
+  if (verify) {
+    SCM_HIP(launch_gather(bs.gpairs.as<GatherPair>(), (int)P, bs.matches.as<uint2>(),
+                          t.kpxy.as<float2>(), bs.xy1.as<double>(), bs.xy2.as<double>(),
+                          bs.counts.as<int32_t>(), sm));
     uint64_t* prof = nullptr;
     if (ctx->profile) {
-      SCM_TRY(ctx->d_prof.ensure(V * kVerifyProfSlots * sizeof(uint64_t)));
-      SCM_HIP(hipMemsetAsync(ctx->d_prof.ptr, 0, V * kVerifyProfSlots * sizeof(uint64_t),
-                             ctx->stream));
-      prof = ctx->d_prof.as<uint64_t>();
+      SCM_TRY(bs.prof.ensure(P * kVerifyProfSlots * sizeof(uint64_t)));
+      SCM_HIP(hipMemsetAsync(bs.prof.ptr, 0, P * kVerifyProfSlots * sizeof(uint64_t), sm));
+      prof = bs.prof.as<uint64_t>();
     }
-    SCM_HIP(launch_verify(ctx->d_vpairs.as<VerifyPair>(), (int)V, max_m, ctx->d_xy1.as<double>(),
-                          ctx->d_xy2.as<double>(), ctx->d_scratch.as<double>(),
-                          ctx->d_idx.as<uint32_t>(), ctx->d_masks.as<uint8_t>(),
-                          ctx->d_vout.as<VerifyOut>(), params, prof, ctx->stream));
-    SCM_HIP(hipEventRecord(ctx->ev[4], ctx->stream));
-    SCM_HIP(hipMemcpyAsync(vout.data(), ctx->d_vout.ptr, V * sizeof(VerifyOut),
-                           hipMemcpyDeviceToHost, ctx->stream));
+    SCM_HIP(hipEventRecord(bs.ev[3], sm));
+    SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)P, max_slots, bs.xy1.as<double>(),
+                          bs.xy2.as<double>(), bs.scratch.as<double>(), bs.snaps.as<uint32_t>(),
+                          bs.masks.as<uint8_t>(),
+                          reinterpret_cast<VerifyOut*>(outd + bs.off_vout), make_params(ctx->opts),
+                          prof, bs.counts.as<int32_t>(), sm));
+  } else {
+    SCM_HIP(hipEventRecord(bs.ev[3], sm));
   }
-  std::vector<Match> packed(pts);
-  std::vector<uint8_t> masks(pts);
-  SCM_HIP(hipMemcpyAsync(packed.data(), ctx->d_packed.ptr, pts * sizeof(uint2),
-                         hipMemcpyDeviceToHost, ctx->stream));
-  SCM_HIP(hipMemcpyAsync(masks.data(), ctx->d_masks.ptr, pts, hipMemcpyDeviceToHost,
-                         ctx->stream));
-  SCM_HIP(hipStreamSynchronize(ctx->stream));
-  if (V > 0) ctx->t_verify += event_ms(ctx->ev[3], ctx->ev[4]);
-  if (V > 0 && ctx->profile) {
-    std::vector<uint64_t> pr(V * kVerifyProfSlots);
-    SCM_HIP(hipMemcpy(pr.data(), ctx->d_prof.ptr, pr.size() * sizeof(uint64_t),
+  SCM_HIP(hipEventRecord(bs.ev[4], sm));
+  SCM_HIP(launch_compact(bs.counts.as<int32_t>(), (int)P, bs.offsets.as<int64_t>(),
+                         reinterpret_cast<int64_t*>(outd + bs.off_offsets),
+                         reinterpret_cast<int32_t*>(outd + bs.off_counts),
+                         bs.match_off.as<int64_t>(), bs.matches.as<uint2>(),
+                         bs.masks.as<uint8_t>(), reinterpret_cast<uint2*>(outd + bs.off_matches),
+                         outd + bs.off_masks, sm));
+  SCM_HIP(hipEventRecord(bs.ev[5], sm));
+  bs.pending = true;
+  return SCM_OK;
+}
+
+int collect_batch(scm_context* ctx, BatchSet& bs, BatchView* v) {
+  *v = BatchView();
+  v->P = bs.P;
+  if (!bs.pending) return SCM_OK;
+  SCM_HIP(hipEventSynchronize(bs.ev[5]));
+  bs.pending = false;
+  if (bs.matched) {
+    ctx->t_match += event_ms(bs.ev[0], bs.ev[1]);
+    ctx->t_final += event_ms(bs.ev[1], bs.ev[2]);
+  }
+  if (bs.verify) ctx->t_verify += event_ms(bs.ev[3], bs.ev[4]);
+  const uint8_t* o = reinterpret_cast<const uint8_t*>(bs.out.host);
+  v->counts = reinterpret_cast<const int32_t*>(o + bs.off_counts);
+  v->offsets = reinterpret_cast<const int64_t*>(o + bs.off_offsets);
+  v->vout = bs.verify ? reinterpret_cast<const VerifyOut*>(o + bs.off_vout) : nullptr;
+  v->matches = reinterpret_cast<const Match*>(o + bs.off_matches);
+  v->masks = o + bs.off_masks;
+  if (ctx->profile && bs.verify && bs.P > 0) {
+    std::vector<uint64_t> pr(bs.P * kVerifyProfSlots);
+    SCM_HIP(hipMemcpy(pr.data(), bs.prof.ptr, pr.size() * sizeof(uint64_t),
                       hipMemcpyDeviceToHost));
     ctx->prof_sum.resize(kVerifyProfSlots, 0);
-    for (int64_t k = 0; k < V; ++k)
+    for (int64_t k = 0; k < bs.P; ++k)
       for (int j = 0; j < kVerifyProfSlots; ++j) ctx->prof_sum[j] += pr[k * kVerifyProfSlots + j];
-    ctx->prof_pairs += V;
-  }
-  for (int64_t k = 0; k < G; ++k) {
-    PairResult& r = (*results)[gsrc[k]];
-    r.matches.assign(packed.begin() + gp[k].pts_off, packed.begin() + gp[k].pts_off + gp[k].m);
-  }
-  for (int64_t k = 0; k < V; ++k) {
-    PairResult& r = (*results)[vsrc[k]];
-    r.vo = vout[k];
-    r.mask.assign(masks.begin() + vp[k].mask_off, masks.begin() + vp[k].mask_off + vp[k].m);
+    ctx->prof_pairs += bs.P;
   }
   return SCM_OK;
 }
 
-Tvg to_tvg(const PairResult& r) {
-  Tvg t;
-  t.config = r.vo.config;
-  if (t.config == 0) return t;  // TwoViewGeometry()
-  for (int i = 0; i < 9; ++i) {
-    t.F[i] = r.vo.F[i];
-    t.H[i] = r.vo.H[i];
-  }
-  for (size_t i = 0; i < r.mask.size(); ++i)
-    if (r.mask[i]) t.inlier_matches.push_back(r.matches[i]);
-  return t;
+// Number of F inliers emitted for pair p (TwoViewGeometry() after the
+// post-filter emits none, sequential_matching.cc:96-99).
+int64_t inlier_count(const BatchView& v, int64_t p) {
+  if (!v.vout || v.vout[p].config == 0) return 0;
+  const uint8_t* m = v.masks + v.offsets[p];
+  int64_t c = 0;
+  for (int32_t i = 0; i < v.counts[p]; ++i) c += m[i];
+  return c;
 }
 
-int run_pairs(scm_context* ctx, const ImageTable& t, const std::vector<PairSpec>& specs,
-              bool verify, std::vector<PairResult>* results) {
-  std::vector<PairDesc> pds;
-  std::vector<int32_t> counts;
-  SCM_TRY(match_stage(ctx, t, specs, &pds, &counts));
-  return verify_stage(ctx, t, specs, pds, counts, verify, results);
+// Bytes of one TVG in the io.cc layout (io.cc:279-292): config, E, F, H,
+// qvec, tvec, tri_angle, inlier count.
+constexpr size_t kTvgFixed = 4 + 8 * 35 + 8;
+
+uint8_t* write_tvg(uint8_t* d, const BatchView& v, int64_t p, int64_t ninl) {
+  const VerifyOut* vo = v.vout ? &v.vout[p] : nullptr;
+  const int32_t config = vo ? vo->config : 0;
+  std::memcpy(d, &config, 4);
+  d += 4;
+  double blk[35];
+  std::memset(blk, 0, sizeof(blk));
+  if (vo && config != 0)
+    for (int c = 0; c < 3; ++c)
+      for (int r = 0; r < 3; ++r) {  // Eigen column-major
+        blk[9 + 3 * c + r] = vo->F[3 * r + c];
+        blk[18 + 3 * c + r] = vo->H[3 * r + c];
+      }
+  std::memcpy(d, blk, sizeof(blk));
+  d += sizeof(blk);
+  const uint64_t n = (uint64_t)ninl;
+  std::memcpy(d, &n, 8);
+  d += 8;
+  if (ninl > 0) {
+    const int64_t o = v.offsets[p];
+    int64_t w = 0;
+    for (int32_t i = 0; i < v.counts[p]; ++i)
+      if (v.masks[o + i]) {
+        std::memcpy(d + 8 * w, &v.matches[o + i], 8);
+        ++w;
+      }
+    d += 8 * ninl;
+  }
+  return d;
+}
+
+// Growable malloc'd output (realloc of large blocks remaps, no copy).
+struct Packed {
+  uint8_t* data = nullptr;
+  size_t size = 0, cap = 0;
+  std::vector<int64_t> row_off;  // [ids_r, tvgs_r] per row, then the end
+  bool reserve(size_t need) {
+    if (need <= cap) return true;
+    const size_t want = std::max(need, cap + cap / 2);
+    uint8_t* p = (uint8_t*)std::realloc(data, want);
+    if (!p) return false;
+    data = p;
+    cap = want;
+    return true;
+  }
+};
+
+// Serialises one batch's output rows: row r's pairs are
+// pairs_begin[r] .. pairs_begin[r + 1] of the batch.
+int serialize_rows(scm_context* ctx, const BatchView& v, const std::vector<uint32_t>& pair_ids,
+                   const std::vector<int64_t>& pairs_begin, Packed* out) {
+  const int64_t nrows = (int64_t)pairs_begin.size() - 1;
+  std::vector<int64_t> ninl(v.P);
+  parallel_for(ctx->threads, v.P, [&](int64_t p) { ninl[p] = inlier_count(v, p); });
+  std::vector<size_t> rstart(nrows + 1);
+  size_t at = out->size;
+  for (int64_t r = 0; r < nrows; ++r) {
+    rstart[r] = at;
+    const int64_t np = pairs_begin[r + 1] - pairs_begin[r];
+    at += 8 + 4 * (size_t)np + 12;
+    for (int64_t p = pairs_begin[r]; p < pairs_begin[r + 1]; ++p) at += kTvgFixed + 8 * ninl[p];
+  }
+  rstart[nrows] = at;
+  if (!out->reserve(at)) {
+    set_error("output allocation failed");
+    return SCM_E_NOMEM;
+  }
+  parallel_for(ctx->threads, nrows, [&](int64_t r) {
+    uint8_t* d = out->data + rstart[r];
+    const int64_t pb = pairs_begin[r], pe = pairs_begin[r + 1];
+    const uint64_t np = (uint64_t)(pe - pb);
+    std::memcpy(d, &np, 8);  // createVectorBuffer<vector<image_t>> (io.cc:151-162)
+    d += 8;
+    for (int64_t p = pb; p < pe; ++p) {
+      std::memcpy(d, &pair_ids[p], 4);
+      d += 4;
+    }
+    // create_two_view_geometries_buffer (io.cc:256-297): total size, count.
+    const uint64_t tb = (uint64_t)(rstart[r + 1] - rstart[r] - 8 - 4 * np);
+    const int32_t cnt = (int32_t)np;
+    std::memcpy(d, &tb, 8);
+    std::memcpy(d + 8, &cnt, 4);
+    d += 12;
+    for (int64_t p = pb; p < pe; ++p) d = write_tvg(d, v, p, ninl[p]);
+  });
+  for (int64_t r = 0; r < nrows; ++r) {
+    out->row_off.push_back((int64_t)rstart[r]);
+    out->row_off.push_back((int64_t)(rstart[r] + 8 + 4 * (pairs_begin[r + 1] - pairs_begin[r])));
+  }
+  out->size = at;
+  return SCM_OK;
 }
 
 int decode_rows(int64_t n, const scm_element* ids, const scm_element* kps,
@@ -472,6 +666,74 @@ void row_pairs(const std::vector<uint32_t>& stencil_ids, std::vector<int64_t>* s
     seen.push_back(id2);
     sel->push_back((int64_t)s);
   }
+}
+
+// Runs the sequential stencil over table rows [row_begin, row_end) through
+// the double-buffered batch pipeline into one packed output.
+int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
+              Packed* out) {
+  const ImageTable& t = ctx->table;
+  struct Batch {
+    std::vector<PairSpec> specs;
+    std::vector<uint32_t> pair_ids;
+    std::vector<int64_t> pairs_begin;
+  };
+  std::vector<Batch> batches;
+  std::vector<uint32_t> ids(overlap);
+  std::vector<int64_t> rows(overlap), sel;
+  Batch cur;
+  for (int64_t r = row_begin; r < row_end; ++r) {
+    for (int64_t s = 0; s < overlap; ++s) {
+      rows[s] = std::min(r + s, t.n - 1);  // stencil clamped at the table end
+      ids[s] = t.ids[rows[s]];
+    }
+    row_pairs(ids, &sel);
+    if (!cur.specs.empty() && (int64_t)(cur.specs.size() + sel.size()) > ctx->batch_pairs) {
+      cur.pairs_begin.push_back((int64_t)cur.specs.size());
+      batches.push_back(std::move(cur));
+      cur = Batch();
+    }
+    cur.pairs_begin.push_back((int64_t)cur.specs.size());
+    for (int64_t s : sel) {
+      cur.specs.push_back({(int32_t)r, (int32_t)rows[s]});
+      cur.pair_ids.push_back(ids[s]);
+    }
+  }
+  if (!cur.pairs_begin.empty()) {
+    cur.pairs_begin.push_back((int64_t)cur.specs.size());
+    batches.push_back(std::move(cur));
+  }
+  if (ctx->keep_matches) {
+    ctx->last_begin = row_begin;
+    ctx->last_end = row_end;
+    ctx->last_matches.assign(row_end - row_begin, {});
+  }
+  auto finish = [&](const Batch& b, BatchSet& bs) -> int {
+    BatchView v;
+    SCM_TRY(collect_batch(ctx, bs, &v));
+    SCM_TRY(serialize_rows(ctx, v, b.pair_ids, b.pairs_begin, out));
+    if (ctx->keep_matches)
+      for (int64_t p = 0; p < v.P; ++p) {
+        const int64_t row = b.specs[p].a, o = v.offsets[p];
+        ctx->last_matches[row - row_begin].push_back(
+            {b.specs[p].b - row, std::vector<Match>(v.matches + o, v.matches + o + v.counts[p])});
+      }
+    return SCM_OK;
+  };
+  out->row_off.reserve(2 * (row_end - row_begin) + 1);
+  for (size_t k = 0; k < batches.size(); ++k) {
+    SCM_TRY(enqueue_batch(ctx, ctx->sets[k & 1], t, batches[k].specs, true, nullptr, 0));
+    if (k > 0) SCM_TRY(finish(batches[k - 1], ctx->sets[(k - 1) & 1]));
+  }
+  if (!batches.empty()) SCM_TRY(finish(batches.back(), ctx->sets[(batches.size() - 1) & 1]));
+  out->row_off.push_back((int64_t)out->size);
+  return SCM_OK;
+}
+
+// Drains any batch left in flight by an error path.
+void drain(scm_context* ctx) {
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  ctx->sets[0].pending = ctx->sets[1].pending = false;
 }
 
 }  // namespace
@@ -508,8 +770,10 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
     return SCM_E_DEVICE;
   }
   scm_matching_options o;
-  if (opts) o = *opts;
-  else scm_default_options(&o);
+  if (opts)
+    o = *opts;
+  else
+    scm_default_options(&o);
   if (o.multiple_models) {
     set_error("multiple_models (TwoViewGeometry::EstimateMultiple) is not supported");
     return SCM_E_INVALID;
@@ -518,17 +782,22 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   ctx->device = device_index;
   ctx->opts = o;
   if (const char* e = std::getenv("SCM_PROFILE")) ctx->profile = e[0] == '1';
+  int hw = (int)std::thread::hardware_concurrency();
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::max(1, std::atoi(e));
+  ctx->threads = std::max(1, std::min(16, hw));
+  if (const char* e = std::getenv("SCM_BATCH_PAIRS"))
+    ctx->batch_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
   if (hipSetDevice(device_index) != hipSuccess ||
       hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
     set_error("failed to create HIP stream");
     delete ctx;
     return SCM_E_DEVICE;
   }
-  for (auto& e : ctx->ev) (void)hipEventCreate(&e);
-  build_lut(&ctx->lut_host);
-  if (ctx->lut.ensure(ctx->lut_host.size() * sizeof(float)) != SCM_OK ||
-      hipMemcpy(ctx->lut.ptr, ctx->lut_host.data(), ctx->lut_host.size() * sizeof(float),
-                hipMemcpyHostToDevice) != hipSuccess) {
+  std::vector<float> lut;
+  build_lut(&lut);
+  if (ctx->lut.ensure(lut.size() * sizeof(float)) != SCM_OK ||
+      hipMemcpy(ctx->lut.ptr, lut.data(), lut.size() * sizeof(float), hipMemcpyHostToDevice) !=
+          hipSuccess) {
     set_error("failed to upload the acosf table");
     scm_context_destroy(ctx);
     return SCM_E_DEVICE;
@@ -539,28 +808,24 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
 
 void scm_context_destroy(scm_context* ctx) {
   if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  drain(ctx);
   if (ctx->profile && ctx->prof_pairs > 0) {
-    static const char* names[] = {"sample", "solve", "score", "cand_res", "seqsum", "lo_gather",
-                                  "lo_est", "lo_res", "other", "n_batch", "n_cand", "n_lo",
-                                  "n_trials", "n_points", "n_seqsum", "-"};
+    static const char* names[] = {"sample",    "solve",   "score",  "cand_res", "seqsum",
+                                  "lo_gather", "lo_est",  "lo_res", "other",    "n_batch",
+                                  "n_cand",    "n_lo",    "n_trials", "n_points", "n_seqsum"};
     std::fprintf(stderr, "[scm verify profile] pairs=%lld (per pair: cycles / counts)\n",
                  (long long)ctx->prof_pairs);
     for (int j = 0; j < 15; ++j)
       std::fprintf(stderr, "  %-10s %14.1f\n", names[j],
                    (double)ctx->prof_sum[j] / (double)ctx->prof_pairs);
   }
-  (void)hipSetDevice(ctx->device);
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   ctx->table.release();
   ctx->scratch_table.release();
-  for (DevBuf* b : {&ctx->lut, &ctx->d_jobs, &ctx->d_pairs, &ctx->d_rowres, &ctx->d_colpart,
-                    &ctx->d_m21, &ctx->d_matches, &ctx->d_counts, &ctx->d_gpairs, &ctx->d_vpairs,
-                    &ctx->d_xy1, &ctx->d_xy2, &ctx->d_packed, &ctx->d_scratch, &ctx->d_idx,
-                    &ctx->d_masks, &ctx->d_vout, &ctx->d_prof})
-    b->release();
+  ctx->lut.release();
+  ctx->sets[0].release();
+  ctx->sets[1].release();
   ctx->h_stage.release();
-  for (auto& e : ctx->ev)
-    if (e) (void)hipEventDestroy(e);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -573,25 +838,32 @@ int scm_match_pair(scm_context* ctx, const uint8_t* desc1, int64_t n1, const uin
   }
   SCM_HIP(hipSetDevice(ctx->device));
   std::vector<RowView> rows(2);
-  rows[0].id = 1; rows[0].desc = desc1; rows[0].ndesc = n1;
-  rows[1].id = 2; rows[1].desc = desc2; rows[1].ndesc = n2;
+  rows[0].id = 1;
+  rows[0].desc = desc1;
+  rows[0].ndesc = n1;
+  rows[1].id = 2;
+  rows[1].desc = desc2;
+  rows[1].ndesc = n2;
   SCM_TRY(upload_table(ctx, &ctx->scratch_table, rows, true, false));
-  std::vector<PairSpec> specs = {{0, 1}};
-  std::vector<PairDesc> pds;
-  std::vector<int32_t> counts;
-  SCM_TRY(match_stage(ctx, ctx->scratch_table, specs, &pds, &counts));
-  *num_matches = counts[0];
-  if (counts[0] > cap) {
+  BatchSet& bs = ctx->sets[0];
+  const int rc = enqueue_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, false, nullptr, 0);
+  if (rc != SCM_OK) {
+    drain(ctx);
+    return rc;
+  }
+  BatchView v;
+  SCM_TRY(collect_batch(ctx, bs, &v));
+  *num_matches = v.counts[0];
+  if (v.counts[0] > cap) {
     set_error("match buffer too small");
     return SCM_E_CAPACITY;
   }
-  if (counts[0] > 0) {
+  if (v.counts[0] > 0) {
     if (!matches) {
       set_error("null match buffer");
       return SCM_E_INVALID;
     }
-    SCM_HIP(hipMemcpy(matches, ctx->d_matches.as<uint2>() + pds[0].match_off,
-                      (size_t)counts[0] * sizeof(uint2), hipMemcpyDeviceToHost));
+    std::memcpy(matches, v.matches + v.offsets[0], (size_t)v.counts[0] * sizeof(Match));
   }
   return SCM_OK;
 }
@@ -604,6 +876,10 @@ int scm_verify_pair(scm_context* ctx, const float* kp1, int64_t n1, const float*
     set_error("invalid arguments");
     return SCM_E_INVALID;
   }
+  if (num_matches > kMaxVerifyMatches) {
+    set_error("more than 65535 matches in one pair");
+    return SCM_E_INVALID;
+  }
   for (int64_t i = 0; i < num_matches; ++i)
     if ((int64_t)matches[2 * i] >= n1 || (int64_t)matches[2 * i + 1] >= n2) {
       set_error("match index out of range");
@@ -611,21 +887,24 @@ int scm_verify_pair(scm_context* ctx, const float* kp1, int64_t n1, const float*
     }
   SCM_HIP(hipSetDevice(ctx->device));
   std::vector<RowView> rows(2);
-  rows[0].id = image_id1; rows[0].kp = kp1; rows[0].nkp = n1;
-  rows[1].id = image_id2; rows[1].kp = kp2; rows[1].nkp = n2;
+  rows[0].id = image_id1;
+  rows[0].kp = kp1;
+  rows[0].nkp = n1;
+  rows[1].id = image_id2;
+  rows[1].kp = kp2;
+  rows[1].nkp = n2;
   SCM_TRY(upload_table(ctx, &ctx->scratch_table, rows, false, true));
-  std::vector<PairSpec> specs = {{0, 1}};
-  std::vector<PairDesc> pds(1);
-  std::memset(&pds[0], 0, sizeof(PairDesc));
-  std::vector<int32_t> counts = {(int32_t)num_matches};
-  SCM_TRY(ctx->d_matches.ensure(std::max<int64_t>(num_matches, 1) * sizeof(uint2)));
-  if (num_matches > 0)
-    SCM_HIP(hipMemcpy(ctx->d_matches.ptr, matches, (size_t)num_matches * sizeof(uint2),
-                      hipMemcpyHostToDevice));
-  std::vector<PairResult> res;
-  SCM_TRY(verify_stage(ctx, ctx->scratch_table, specs, pds, counts, true, &res));
-  std::vector<uint8_t> bytes;
-  append_tvg(&bytes, to_tvg(res[0]));
+  BatchSet& bs = ctx->sets[0];
+  const int rc = enqueue_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, true, matches, num_matches);
+  if (rc != SCM_OK) {
+    drain(ctx);
+    return rc;
+  }
+  BatchView v;
+  SCM_TRY(collect_batch(ctx, bs, &v));
+  const int64_t ninl = inlier_count(v, 0);
+  std::vector<uint8_t> bytes(kTvgFixed + 8 * ninl);
+  write_tvg(bytes.data(), v, 0, ninl);
   return make_blob(bytes, tvg_out);
 }
 
@@ -645,17 +924,41 @@ int scm_execute_stencil(scm_context* ctx, int64_t stencil_size, const scm_elemen
   row_pairs(ids, &sel);
   SCM_TRY(upload_table(ctx, &ctx->scratch_table, rows, true, true));
   std::vector<PairSpec> specs;
-  for (int64_t s : sel) specs.push_back({0, (int32_t)s});
-  std::vector<PairResult> res;
-  SCM_TRY(run_pairs(ctx, ctx->scratch_table, specs, true, &res));
   std::vector<uint32_t> pair_ids;
-  std::vector<Tvg> tvgs;
-  for (size_t k = 0; k < sel.size(); ++k) {
-    pair_ids.push_back(ids[sel[k]]);
-    tvgs.push_back(to_tvg(res[k]));
+  for (int64_t s : sel) {
+    specs.push_back({0, (int32_t)s});
+    pair_ids.push_back(ids[s]);
   }
-  SCM_TRY(make_blob(id_list_bytes(pair_ids), pair_image_ids_out));
-  return make_blob(tvg_list_bytes(tvgs), tvgs_out);
+  BatchSet& bs = ctx->sets[0];
+  int rc = enqueue_batch(ctx, bs, ctx->scratch_table, specs, true, nullptr, 0);
+  if (rc != SCM_OK) {
+    drain(ctx);
+    return rc;
+  }
+  BatchView v;
+  SCM_TRY(collect_batch(ctx, bs, &v));
+  Packed pk;
+  rc = serialize_rows(ctx, v, pair_ids, {0, (int64_t)specs.size()}, &pk);
+  if (rc != SCM_OK) {
+    std::free(pk.data);
+    return rc;
+  }
+  const size_t split = (size_t)pk.row_off[1];
+  scm_blob a{(uint8_t*)std::malloc(split), split};
+  scm_blob b{(uint8_t*)std::malloc(pk.size - split), pk.size - split};
+  if (!a.data || !b.data) {
+    std::free(a.data);
+    std::free(b.data);
+    std::free(pk.data);
+    set_error("malloc failed");
+    return SCM_E_NOMEM;
+  }
+  std::memcpy(a.data, pk.data, split);
+  std::memcpy(b.data, pk.data + split, pk.size - split);
+  std::free(pk.data);
+  *pair_image_ids_out = a;
+  *tvgs_out = b;
+  return SCM_OK;
 }
 
 int scm_table_load(scm_context* ctx, int64_t num_rows, const scm_element* image_ids,
@@ -673,72 +976,88 @@ int scm_table_load(scm_context* ctx, int64_t num_rows, const scm_element* image_
   return SCM_OK;
 }
 
-int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
-                  scm_blob* pair_image_ids_out, scm_blob* tvgs_out) {
-  if (!ctx || !pair_image_ids_out || !tvgs_out) {
-    set_error("invalid arguments");
-    return SCM_E_INVALID;
-  }
+static int table_run_common(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
+                            Packed* pk) {
   if (!ctx->table_loaded) {
     set_error("scm_table_run before scm_table_load");
     return SCM_E_STATE;
   }
-  const ImageTable& t = ctx->table;
-  if (overlap < 1 || row_begin < 0 || row_end > t.n || row_begin > row_end) {
+  if (overlap < 1 || row_begin < 0 || row_end > ctx->table.n || row_begin > row_end) {
     set_error("invalid row range / overlap");
     return SCM_E_INVALID;
   }
   SCM_HIP(hipSetDevice(ctx->device));
-  hipEvent_t w0 = ctx->ev[5];
-  SCM_HIP(hipEventRecord(w0, ctx->stream));
   ctx->t_match = ctx->t_final = ctx->t_verify = 0.0;
+  const auto w0 = std::chrono::steady_clock::now();
+  const int rc = run_table(ctx, overlap, row_begin, row_end, pk);
+  if (rc != SCM_OK) drain(ctx);
+  ctx->t_wall =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+  return rc;
+}
+
+int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
+                  scm_blob* pair_image_ids_out, scm_blob* tvgs_out) {
+  if (!ctx || ((!pair_image_ids_out || !tvgs_out) && row_end > row_begin)) {
+    set_error("invalid arguments");
+    return SCM_E_INVALID;
+  }
+  Packed pk;
+  const int rc = table_run_common(ctx, overlap, row_begin, row_end, &pk);
+  if (rc != SCM_OK) {
+    std::free(pk.data);
+    return rc;
+  }
   const int64_t nrows = row_end - row_begin;
-  ctx->last_begin = row_begin;
-  ctx->last_end = row_end;
-  ctx->last_overlap = overlap;
-  ctx->last_matches.assign(nrows, {});
-  std::vector<std::vector<int64_t>> row_sel(nrows);  // neighbour table rows per output row
-  for (int64_t r = row_begin; r < row_end; ++r) {
-    std::vector<uint32_t> ids(overlap);
-    std::vector<int64_t> rows(overlap);
-    for (int64_t s = 0; s < overlap; ++s) {
-      rows[s] = std::min(r + s, t.n - 1);  // stencil clamped at the table end
-      ids[s] = t.ids[rows[s]];
-    }
-    std::vector<int64_t> sel;
-    row_pairs(ids, &sel);
-    for (int64_t s : sel) row_sel[r - row_begin].push_back(rows[s]);
-  }
-  std::vector<std::vector<Tvg>> tvgs(nrows);
-  std::vector<std::vector<uint32_t>> pids(nrows);
-  int64_t r = row_begin;
-  while (r < row_end) {
-    std::vector<PairSpec> specs;
-    std::vector<std::pair<int64_t, int64_t>> where;  // (output row, neighbour row)
-    while (r < row_end && (specs.empty() ||
-                           (int64_t)(specs.size() + row_sel[r - row_begin].size()) <= kMaxPairsPerBatch)) {
-      for (int64_t nb : row_sel[r - row_begin]) {
-        specs.push_back({(int32_t)r, (int32_t)nb});
-        where.push_back({r, nb});
+  for (int64_t r = 0; r < nrows; ++r) {
+    const int64_t a = pk.row_off[2 * r], b = pk.row_off[2 * r + 1], c = pk.row_off[2 * r + 2];
+    uint8_t* pa = (uint8_t*)std::malloc((size_t)(b - a));
+    uint8_t* pb = (uint8_t*)std::malloc((size_t)(c - b));
+    if (!pa || !pb) {
+      std::free(pa);
+      std::free(pb);
+      for (int64_t q = 0; q < r; ++q) {
+        scm_blob_free(&pair_image_ids_out[q]);
+        scm_blob_free(&tvgs_out[q]);
       }
-      ++r;
+      std::free(pk.data);
+      set_error("malloc failed");
+      return SCM_E_NOMEM;
     }
-    std::vector<PairResult> res;
-    SCM_TRY(run_pairs(ctx, t, specs, true, &res));
-    for (size_t k = 0; k < specs.size(); ++k) {
-      const int64_t orow = where[k].first - row_begin;
-      pids[orow].push_back(t.ids[where[k].second]);
-      tvgs[orow].push_back(to_tvg(res[k]));
-      ctx->last_matches[orow].push_back({where[k].second - where[k].first, std::move(res[k].matches)});
-    }
+    std::memcpy(pa, pk.data + a, (size_t)(b - a));
+    std::memcpy(pb, pk.data + b, (size_t)(c - b));
+    pair_image_ids_out[r] = scm_blob{pa, (size_t)(b - a)};
+    tvgs_out[r] = scm_blob{pb, (size_t)(c - b)};
   }
-  for (int64_t k = 0; k < nrows; ++k) {
-    SCM_TRY(make_blob(id_list_bytes(pids[k]), &pair_image_ids_out[k]));
-    SCM_TRY(make_blob(tvg_list_bytes(tvgs[k]), &tvgs_out[k]));
+  std::free(pk.data);
+  return SCM_OK;
+}
+
+int scm_table_run_packed(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
+                         scm_blob* rows_out, int64_t* row_offsets) {
+  if (!ctx || !rows_out || !row_offsets) {
+    set_error("invalid arguments");
+    return SCM_E_INVALID;
   }
-  SCM_HIP(hipEventRecord(ctx->ev[4], ctx->stream));
-  SCM_HIP(hipEventSynchronize(ctx->ev[4]));
-  ctx->t_wall = event_ms(w0, ctx->ev[4]);
+  Packed pk;
+  const int rc = table_run_common(ctx, overlap, row_begin, row_end, &pk);
+  if (rc != SCM_OK) {
+    std::free(pk.data);
+    return rc;
+  }
+  std::memcpy(row_offsets, pk.row_off.data(), pk.row_off.size() * sizeof(int64_t));
+  rows_out->data = pk.data ? pk.data : (uint8_t*)std::malloc(1);
+  rows_out->size = pk.size;
+  return SCM_OK;
+}
+
+int scm_set_keep_matches(scm_context* ctx, int32_t keep) {
+  if (!ctx) {
+    set_error("null context");
+    return SCM_E_INVALID;
+  }
+  ctx->keep_matches = keep != 0;
+  if (!keep) ctx->last_matches.clear();
   return SCM_OK;
 }
 
@@ -748,7 +1067,12 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset, uint32_t* m
     set_error("invalid arguments");
     return SCM_E_INVALID;
   }
-  if (row < ctx->last_begin || row >= ctx->last_end) {
+  if (!ctx->keep_matches) {
+    set_error("call scm_set_keep_matches(ctx, 1) before scm_table_run");
+    return SCM_E_STATE;
+  }
+  if (row < ctx->last_begin || row >= ctx->last_end ||
+      ctx->last_matches.size() != (size_t)(ctx->last_end - ctx->last_begin)) {
     set_error("row outside the last scm_table_run");
     return SCM_E_INVALID;
   }
@@ -759,7 +1083,13 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset, uint32_t* m
       set_error("match buffer too small");
       return SCM_E_CAPACITY;
     }
-    if (*num_matches > 0) std::memcpy(matches, e.second.data(), e.second.size() * sizeof(Match));
+    if (*num_matches > 0) {
+      if (!matches) {
+        set_error("null match buffer");
+        return SCM_E_INVALID;
+      }
+      std::memcpy(matches, e.second.data(), e.second.size() * sizeof(Match));
+    }
     return SCM_OK;
   }
   set_error("no pair (row, row + offset) in the last run");

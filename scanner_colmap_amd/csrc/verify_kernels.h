@@ -32,10 +32,11 @@ struct VerifyParams {
 struct VerifyPair {
   int64_t pts_off;   // double offset of xy1/xy2 (2 doubles per match)
   int64_t scr_off;   // double offset of the per-pair scratch (10 m + kVerifyModelDoubles)
-  int64_t idx_off;   // unused (kept for layout stability)
   int64_t mask_off;  // byte offset of the F inlier mask
-  int32_t m;         // number of matches
+  int32_t m;         // number of matches when cidx < 0
+  int32_t cidx;      // index into the device match counts (>= 0: read m there)
   uint32_t id1, id2;
+  int32_t out_idx;   // VerifyOut slot
   int32_t pad_;
 };
 
@@ -53,7 +54,7 @@ struct VerifyOut {
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
-                         hipStream_t stream);
+                         const int32_t* counts, hipStream_t stream);
 size_t verify_lds_bytes(int max_m);
 constexpr int kVerifyProfSlots = 16;
 
@@ -64,12 +65,17 @@ struct GatherPair {
   int64_t kp1_off;    // float2 offset of image 1 / image 2 keypoint xy
   int64_t kp2_off;
   int64_t pts_off;    // destination double offset / 2
-  int32_t m;
-  int32_t pad_;
+  int32_t m;          // number of matches when cidx < 0
+  int32_t cidx;       // index into the device match counts (>= 0: read m there)
 };
-// Also packs each pair's matches contiguously at pts_off (packed).
 hipError_t launch_gather(const GatherPair* pairs, int npairs, const uint2* matches,
-                         const float2* kpxy, double* xy1, double* xy2, uint2* packed,
+                         const float2* kpxy, double* xy1, double* xy2, const int32_t* counts,
                          hipStream_t stream);
+// Exclusive scan of counts (device + host-mapped copies) and packing of each
+// pair's matches / F-inlier mask into host-mapped memory.
+hipError_t launch_compact(const int32_t* counts, int npairs, int64_t* offsets,
+                          int64_t* host_offsets, int32_t* host_counts, const int64_t* match_off,
+                          const uint2* matches, const uint8_t* masks, uint2* out_matches,
+                          uint8_t* out_masks, hipStream_t stream);
 
 }  // namespace scm

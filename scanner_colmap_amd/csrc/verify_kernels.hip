@@ -674,7 +674,8 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
     const double* __restrict__ xy2_all, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, uint8_t* __restrict__ masks,
-    VerifyOut* __restrict__ out, VerifyParams P, uint64_t* __restrict__ prof) {
+    VerifyOut* __restrict__ out, VerifyParams P, uint64_t* __restrict__ prof,
+    const int32_t* __restrict__ counts) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
@@ -682,7 +683,7 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
   pf.start();
   const VerifyPair pp = pairs[blockIdx.x];
   const int lane = threadIdx.x;
-  const int n = pp.m;
+  const int n = pp.cidx >= 0 ? counts[pp.cidx] : pp.m;
   VerifyOut o;
   o.config = 0;
   o.num_inliers = 0;
@@ -795,22 +796,72 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
       for (int i = 0; i < 9; ++i) { o.F[i] = 0.0; o.H[i] = 0.0; }
     }
   }
-  if (lane == 0) out[blockIdx.x] = o;
+  if (lane == 0) out[pp.out_idx] = o;
 }
 
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
                               const float2* __restrict__ kpxy, double* __restrict__ xy1,
-                              double* __restrict__ xy2, uint2* __restrict__ packed) {
+                              double* __restrict__ xy2, const int32_t* __restrict__ counts) {
   const GatherPair g = pairs[blockIdx.x];
-  for (int i = threadIdx.x; i < g.m; i += blockDim.x) {
+  const int m = g.cidx >= 0 ? counts[g.cidx] : g.m;
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
     const uint2 mt = matches[g.match_off + i];
-    packed[g.pts_off + i] = mt;
     const float2 a = kpxy[g.kp1_off + mt.x];
     const float2 b = kpxy[g.kp2_off + mt.y];
     xy1[2 * (g.pts_off + i)] = (double)a.x;
     xy1[2 * (g.pts_off + i) + 1] = (double)a.y;
     xy2[2 * (g.pts_off + i)] = (double)b.x;
     xy2[2 * (g.pts_off + i) + 1] = (double)b.y;
+  }
+}
+
+// Exclusive scan of the per-pair match counts (one block).
+__global__ __launch_bounds__(1024) void scan_counts_kernel(const int32_t* __restrict__ counts,
+                                                           int npairs,
+                                                           int64_t* __restrict__ offsets,
+                                                           int64_t* __restrict__ host_offsets,
+                                                           int32_t* __restrict__ host_counts) {
+  __shared__ int64_t wsum[16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int per = (npairs + 1023) / 1024;
+  const int i0 = min(npairs, tid * per), i1 = min(npairs, i0 + per);
+  int64_t c = 0;
+  for (int i = i0; i < i1; ++i) c += counts[i];
+  int64_t x = c;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int64_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wsum[wave] = x;
+  __syncthreads();
+  int64_t before = 0;
+  for (int w = 0; w < wave; ++w) before += wsum[w];
+  int64_t o = before + x - c;
+  for (int i = i0; i < i1; ++i) {
+    offsets[i] = o;
+    host_offsets[i] = o;
+    host_counts[i] = counts[i];
+    o += counts[i];
+  }
+  if (tid == 1023) {
+    offsets[npairs] = o;
+    host_offsets[npairs] = o;
+  }
+}
+
+// Packs each pair's matches and F-inlier mask contiguously (offsets from the
+// scan) into the host-mapped result buffer.
+__global__ void compact_kernel(const int32_t* __restrict__ counts, const int64_t* __restrict__ offsets,
+                               const int64_t* __restrict__ match_off, const uint2* __restrict__ matches,
+                               const uint8_t* __restrict__ masks, uint2* __restrict__ out_matches,
+                               uint8_t* __restrict__ out_masks) {
+  const int p = blockIdx.x;
+  const int m = counts[p];
+  const int64_t o = offsets[p], s = match_off[p];
+  for (int i = threadIdx.x; i < m; i += blockDim.x) {
+    out_matches[o + i] = matches[s + i];
+    out_masks[o + i] = masks[s + i];
   }
 }
 
@@ -821,7 +872,7 @@ size_t verify_lds_bytes(int max_m) {
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
-                         hipStream_t stream) {
+                         const int32_t* counts, hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
   const size_t lds = verify_lds_bytes(max_m);
   static bool attr = false;
@@ -831,16 +882,28 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     attr = true;
   }
   hipLaunchKernelGGL(verify_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs, xy1,
-                     xy2, scratch, snaps, masks, out, params, prof);
+                     xy2, scratch, snaps, masks, out, params, prof, counts);
   return hipGetLastError();
 }
 
 hipError_t launch_gather(const GatherPair* pairs, int npairs, const uint2* matches,
-                         const float2* kpxy, double* xy1, double* xy2, uint2* packed,
+                         const float2* kpxy, double* xy1, double* xy2, const int32_t* counts,
                          hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(gather_kernel, dim3(npairs), dim3(256), 0, stream, pairs, matches, kpxy,
-                     xy1, xy2, packed);
+                     xy1, xy2, counts);
+  return hipGetLastError();
+}
+
+hipError_t launch_compact(const int32_t* counts, int npairs, int64_t* offsets,
+                          int64_t* host_offsets, int32_t* host_counts, const int64_t* match_off,
+                          const uint2* matches, const uint8_t* masks, uint2* out_matches,
+                          uint8_t* out_masks, hipStream_t stream) {
+  if (npairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(1024), 0, stream, counts, npairs, offsets,
+                     host_offsets, host_counts);
+  hipLaunchKernelGGL(compact_kernel, dim3(npairs), dim3(256), 0, stream, counts, offsets,
+                     match_off, matches, masks, out_matches, out_masks);
   return hipGetLastError();
 }
 

@@ -30,7 +30,11 @@ def shard_rows(num_rows: int, overlap: int, world: int, rank: int) -> tuple[int,
     total = c[-1]
     bounds = [0]
     for r in range(1, world):
-        bounds.append(int(np.searchsorted(c, total * r / world, side="left")))
+        target = total * r / world
+        k = int(np.searchsorted(c, target, side="left"))  # first cut with c[k] >= target
+        if k > 0 and target - c[k - 1] < c[min(k, num_rows)] - target:
+            k -= 1  # the cut before it is closer to the ideal split
+        bounds.append(k)
     bounds.append(num_rows)
     bounds = np.maximum.accumulate(np.array(bounds))
     return int(bounds[rank]), int(bounds[rank + 1])
@@ -64,8 +68,30 @@ def unpack_rows(buf: bytes) -> tuple[list[bytes], list[bytes]]:
     return pa, pb
 
 
-def gather_to_root(payload: bytes, device=None) -> list[bytes] | None:
-    """Gather every rank's byte payload to rank 0 (None elsewhere).
+def pack_packed(offsets: np.ndarray, data: np.ndarray) -> np.ndarray:
+    """Payload of one rank's scm_table_run_packed output: element count,
+    the 2n+1 element offsets, then the packed element bytes."""
+    offs = np.ascontiguousarray(offsets, dtype=np.int64)
+    head = np.array([offs.size], dtype=np.int64)
+    return np.concatenate([head.view(np.uint8), offs.view(np.uint8),
+                           np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)])
+
+
+def unpack_packed(buf) -> tuple[list[bytes], list[bytes]]:
+    """Inverse of pack_packed, split into (pair_image_ids, tvgs) rows."""
+    b = np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf
+    (n,) = b[:8].view(np.int64)
+    offs = b[8:8 + 8 * n].view(np.int64)
+    data = b[8 + 8 * n:]
+    rows = (n - 1) // 2
+    pa = [data[offs[2 * r]:offs[2 * r + 1]].tobytes() for r in range(rows)]
+    pb = [data[offs[2 * r + 1]:offs[2 * r + 2]].tobytes() for r in range(rows)]
+    return pa, pb
+
+
+def gather_to_root(payload, device=None) -> list[bytes] | None:
+    """Gather every rank's byte payload (bytes or a uint8 numpy array) to
+    rank 0 (None elsewhere).
 
     Sizes are exchanged with an all_gather of one int64 per rank, then each
     rank ships its payload (padded to the largest) with dist.gather — on the
@@ -82,8 +108,10 @@ def gather_to_root(payload: bytes, device=None) -> list[bytes] | None:
     sizes = [int(s.item()) for s in sizes]
     mx = max(1, max(sizes))
     t = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    if payload:
-        t[: len(payload)] = torch.frombuffer(bytearray(payload), dtype=torch.uint8).to(dev)
+    if len(payload):
+        src = (np.frombuffer(payload, dtype=np.uint8) if isinstance(payload, (bytes, bytearray))
+               else np.ascontiguousarray(payload, dtype=np.uint8).reshape(-1))
+        t[: len(payload)] = torch.from_numpy(src.copy() if not src.flags.writeable else src).to(dev)
     bufs = [torch.zeros(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
     dist.gather(t, gather_list=bufs, dst=0)
     if rank != 0:

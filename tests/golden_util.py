@@ -1,0 +1,25 @@
+"""Loader of the committed golden vectors (tests/golden/golden_v1.npz, made
+by tests/golden/make_golden.py).  Plain arrays only: allow_pickle=False."""
+import os
+
+import numpy as np
+
+PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_v1.npz")
+MATCH_CASES = ("random_ragged", "tie_stress", "corridor")
+VERIFY_CASES = ("01", "03", "23")
+
+
+def load():
+    with np.load(PATH, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def blobs(g, name):
+    offs, data = g[f"{name}_offs"], g[f"{name}_data"]
+    return [data[offs[i]:offs[i + 1]].tobytes() for i in range(len(offs) - 1)]
+
+
+def table(g):
+    from scanner_colmap_amd.codecs import encode_image_id
+    ids = [encode_image_id(int(i)) for i in g["table_ids"]]
+    return ids, blobs(g, "table_kps"), blobs(g, "table_descs")

@@ -1,0 +1,95 @@
+"""Multi-rank plumbing on the CPU: pair-balanced sharding
+with halos, and the rank-0 gather of packed io.cc rows over a world-size-2
+gloo group.  Each rank computes its shard with the CPU oracle standing in
+for the GPU stage; rank 0 checks the gathered rows against a one-rank run."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from scanner_colmap_amd import distributed as sd
+
+
+@pytest.mark.parametrize("n,K,world", [(100, 10, 8), (1000, 20, 8), (128, 128, 8), (7, 4, 2),
+                                       (3, 10, 4), (0, 5, 2)])
+def test_shard_rows_partition(n, K, world):
+    ppr = sd.pairs_per_row(n, K)
+    bounds = [sd.shard_rows(n, K, world, r) for r in range(world)]
+    assert bounds[0][0] == 0 and bounds[-1][1] == n
+    for (a, b), (c, _) in zip(bounds, bounds[1:]):
+        assert b == c and a <= b
+    loads = [int(ppr[a:b].sum()) for a, b in bounds]
+    if n > 0 and ppr.sum() > 0:
+        assert max(loads) - min(loads) <= max(ppr) + 1 or min(loads) == 0
+        assert sum(loads) == ppr.sum()
+    for a, b in bounds:
+        ta, tb = sd.table_range(a, b, n, K)
+        assert ta == a and tb == min(n, b + K - 1)
+
+
+def test_pack_unpack_packed():
+    rows_a = [b"\x01\x00\x00\x00\x00\x00\x00\x00\x05\x00\x00\x00", b"\x00" * 8]
+    rows_b = [b"abc" * 5, b"\x0c" + b"\x00" * 11]
+    data = b"".join(x for pair in zip(rows_a, rows_b) for x in pair)
+    offs = np.cumsum([0] + [len(x) for pair in zip(rows_a, rows_b) for x in pair])
+    payload = sd.pack_packed(offs, np.frombuffer(data, np.uint8))
+    assert sd.unpack_packed(payload.tobytes()) == (rows_a, rows_b)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, n, K, q):
+    import torch.distributed as dist
+
+    from oracle import oracle
+    from scanner_colmap_amd.codecs import table_rows
+    from scanner_colmap_amd.synthetic import Corridor
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = Corridor(n, 400, K, seed=53)
+        a, b = sd.shard_rows(n, K, world, rank)
+        ta, tb = sd.table_range(a, b, n, K)
+        ids, kps, descs = table_rows(c.images(ta, tb))
+        pa, pb = oracle.table_run(ids, kps, descs, K, a - ta, b - ta)
+        # same layout scm_table_run_packed returns
+        elems = [x for pair in zip(pa, pb) for x in pair]
+        offs = np.cumsum([0] + [len(x) for x in elems]).astype(np.int64)
+        data = np.frombuffer(b"".join(elems), np.uint8) if elems else np.zeros(0, np.uint8)
+        got = sd.gather_to_root(sd.pack_packed(offs, data))
+        if rank == 0:
+            rows_a, rows_b = [], []
+            for payload in got:
+                x, y = sd.unpack_packed(payload)
+                rows_a += x
+                rows_b += y
+            ids, kps, descs = table_rows(c.images())
+            ref = oracle.table_run(ids, kps, descs, K, 0, n)
+            q.put((rows_a == ref[0], rows_b == ref[1], len(rows_a)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_gather_world2():
+    n, K, world = 9, 4, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, K, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    assert codes == [0, 0], codes
+    ok_a, ok_b, nrows = q.get(timeout=5)
+    assert ok_a and ok_b and nrows == n

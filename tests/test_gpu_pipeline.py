@@ -1,0 +1,88 @@
+"""Batch pipeline of the table path: packed output, kept matches, several
+batches in flight (SCM_BATCH_PAIRS forces small batches), ragged tables.
+Every output byte is compared with the CPU oracle (oracle/oracle.cc)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from scanner_colmap_amd import Context
+from scanner_colmap_amd.codecs import (decode_descriptors, decode_keypoints, encode_descriptors,
+                                       encode_keypoints, table_rows)
+from scanner_colmap_amd.synthetic import Corridor
+
+pytestmark = pytest.mark.gpu
+
+
+def _table(n, kpts, seed, overlap=4):
+    imgs = Corridor(n, kpts, overlap, seed=seed).images()
+    return imgs, table_rows(imgs)
+
+
+def test_packed_equals_rows_and_oracle(gpu_ctx):
+    imgs, (ids, kps, descs) = _table(9, 600, 31)
+    ref = oracle.table_run(ids, kps, descs, 5, 0, len(imgs))
+    gpu_ctx.table_load(ids, kps, descs)
+    packed = gpu_ctx.table_run_packed(5, 0, len(imgs))
+    pa, pb = packed.rows()
+    assert pa == ref[0] and pb == ref[1]
+    assert packed.offsets[-1] == packed.data.size
+    rows = gpu_ctx.table_run(5, 0, len(imgs))
+    assert rows[0] == pa and rows[1] == pb
+
+
+def test_sub_range(gpu_ctx):
+    imgs, (ids, kps, descs) = _table(8, 500, 37)
+    ref = oracle.table_run(ids, kps, descs, 3, 2, 7)
+    gpu_ctx.table_load(ids, kps, descs)
+    got = gpu_ctx.table_run(3, 2, 7)
+    assert got == ref
+    empty = gpu_ctx.table_run_packed(3, 4, 4)
+    assert len(empty) == 0 and empty.data.size == 0
+
+
+def test_keep_matches(gpu_ctx):
+    imgs, (ids, kps, descs) = _table(5, 800, 41)
+    gpu_ctx.table_load(ids, kps, descs)
+    gpu_ctx.set_keep_matches(True)
+    try:
+        gpu_ctx.table_run(3, 0, len(imgs))
+        for r in range(len(imgs) - 1):
+            for off in (1, 2):
+                if r + off >= len(imgs):
+                    continue
+                got = gpu_ctx.table_matches(r, off)
+                ref = oracle.match_pair(imgs[r][2], imgs[r + off][2])
+                assert got.shape == ref.shape and (got == ref).all(), (r, off)
+    finally:
+        gpu_ctx.set_keep_matches(False)
+
+
+def test_many_batches_in_flight():
+    """Batches of 3 pairs: exercises the double-buffered enqueue/collect
+    alternation and per-batch serialisation against the oracle."""
+    imgs, (ids, kps, descs) = _table(12, 400, 43)
+    ref = oracle.table_run(ids, kps, descs, 4, 0, len(imgs))
+    os.environ["SCM_BATCH_PAIRS"] = "3"
+    try:
+        with Context(0) as ctx:
+            ctx.table_load(ids, kps, descs)
+            got = ctx.table_run(4, 0, len(imgs))
+            got2 = ctx.table_run_packed(4, 0, len(imgs)).rows()
+    finally:
+        del os.environ["SCM_BATCH_PAIRS"]
+    assert got == ref
+    assert got2 == ref
+
+
+def test_ragged_table_with_empty_images(gpu_ctx):
+    """Images with 0, 1, 31 and 2000 keypoints in one table."""
+    sizes = [700, 0, 1, 700, 31, 2000, 650]
+    _, (ids, kps, descs) = _table(len(sizes), 2000, 47)
+    kps2 = [encode_keypoints(decode_keypoints(k)[:s]) for s, k in zip(sizes, kps)]
+    descs2 = [encode_descriptors(decode_descriptors(d)[:s]) for s, d in zip(sizes, descs)]
+    ref = oracle.table_run(ids, kps2, descs2, 4, 0, len(sizes))
+    gpu_ctx.table_load(ids, kps2, descs2)
+    got = gpu_ctx.table_run(4, 0, len(sizes))
+    assert got == ref
