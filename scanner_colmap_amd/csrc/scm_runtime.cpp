@@ -8,14 +8,14 @@
 //
 // Batch pipeline (table path): pairs are cut into batches of whole pivot
 // rows; each batch is enqueued as
-//   match tiles -> finalize -> gather -> verify -> scan + compact
-// on the context's stream with no host synchronisation in between (the
-// verifier reads the match counts from device memory; buffers are laid out
-// for the worst case, one match slot per pivot keypoint).  The compact kernel
-// writes counts, matches and F-inlier masks, and the verifier its geometry
-// records, straight into host-mapped pinned memory.  Two batch buffer sets
-// alternate, so the host serialises batch b's io.cc rows (multithreaded)
-// while the GPU runs batch b+1.
+//   match tiles -> finalize -> gather -> verify -> compact
+// Matching runs on one stream with buffers laid out for the worst case (one
+// match slot per pivot keypoint), so it never waits for the host.  Only the
+// per-pair match counts come back early; the host then launches verification
+// of exactly the pairs that need it (longest first) on the batch's own
+// stream, compacts matches and F-inlier masks in HBM and DMAs the results to
+// pinned memory.  Three batch buffer sets rotate: while batch b+1 is matched
+// and batch b verified, the host serialises batch b-1's io.cc rows.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -38,7 +38,8 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 
 namespace {
 
-constexpr int64_t kMaxPairsPerBatch = 2048;
+constexpr int64_t kMaxPairsPerBatch = 16384;
+constexpr int64_t kDefaultPairsPerBatch = 8192;
 
 struct ImageTable {
   int64_t n = 0;
@@ -62,30 +63,25 @@ struct PairSpec {
   int32_t a, b;  // image indices in the table
 };
 
-// Host-mapped pinned buffer (device writes, host reads after the event).
-struct MappedBuf {
+// Pinned host result buffer: the DMA target of each batch's results.
+struct PinnedOut {
   void* host = nullptr;
-  void* dev = nullptr;
   size_t bytes = 0;
   int ensure(size_t need) {
     if (need <= bytes) return SCM_OK;
     release();
     const size_t want = need + need / 4 + 4096;
-    if (hipHostMalloc(&host, want, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
+    if (hipHostMalloc(&host, want, hipHostMallocDefault) != hipSuccess) {
       host = nullptr;
-      set_error("hipHostMalloc(mapped) of " + std::to_string(want) + " bytes failed");
+      set_error("hipHostMalloc of " + std::to_string(want) + " bytes failed");
       return SCM_E_NOMEM;
-    }
-    if (hipHostGetDevicePointer(&dev, host, 0) != hipSuccess) {
-      set_error("hipHostGetDevicePointer failed");
-      return SCM_E_DEVICE;
     }
     bytes = want;
     return SCM_OK;
   }
   void release() {
     if (host) (void)hipHostFree(host);
-    host = dev = nullptr;
+    host = nullptr;
     bytes = 0;
   }
 };
@@ -93,20 +89,29 @@ struct MappedBuf {
 // One in-flight batch: device workspace, descriptor staging, results.
 struct BatchSet {
   DevBuf jobs, pairs, rowres, colpart, m21, matches, counts, gpairs, vpairs, xy1, xy2, scratch,
-      snaps, masks, offsets, match_off, prof;
-  HostBuf stage;
-  MappedBuf out;
+      snaps, masks, offsets, match_off, prof, xyf, dvout, dpack, dpmask;
+  HostBuf stage, vstage;
+  PinnedOut out;
   size_t off_counts = 0, off_offsets = 0, off_vout = 0, off_matches = 0, off_masks = 0;
-  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  int64_t P = 0;
+  // 0 match start, 1 tiles done, 2 finalize done, 3 counts on host (match
+  // stream); 4 verify start, 5 verify done, 6 compaction done (verify stream)
+  hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipStream_t vstream = nullptr;  // verification stream of this set
+  const ImageTable* table = nullptr;
+  std::vector<PairSpec> specs;
+  std::vector<int64_t> moff;  // first match slot of each pair
+  int64_t P = 0, slots = 0, nprof = 0;
   bool verify = false;
-  bool pending = false;
+  bool pending = false;  // stage 1 enqueued, results not collected
+  bool posted = false;   // stage 2 enqueued
   bool matched = false;
   void release() {
     for (DevBuf* b : {&jobs, &pairs, &rowres, &colpart, &m21, &matches, &counts, &gpairs, &vpairs,
-                      &xy1, &xy2, &scratch, &snaps, &masks, &offsets, &match_off, &prof})
+                      &xy1, &xy2, &scratch, &snaps, &masks, &offsets, &match_off, &prof, &xyf, &dvout,
+                      &dpack, &dpmask})
       b->release();
     stage.release();
+    vstage.release();
     out.release();
     for (auto& e : ev) {
       if (e) (void)hipEventDestroy(e);
@@ -132,15 +137,16 @@ using namespace scm;
 
 struct scm_context {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // matching stream
   scm_matching_options opts;
   DevBuf lut;
   ImageTable table, scratch_table;
   bool table_loaded = false;
-  BatchSet sets[2];
+  BatchSet sets[3];
   HostBuf h_stage;  // table upload staging
   int threads = 1;
-  int64_t batch_pairs = kMaxPairsPerBatch;  // SCM_BATCH_PAIRS overrides (tests)
+  int64_t batch_pairs = kDefaultPairsPerBatch;  // SCM_BATCH_PAIRS overrides
+  bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
   bool profile = false;
@@ -287,25 +293,27 @@ VerifyParams make_params(const scm_matching_options& o) {
 
 size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 
-// Enqueue one batch on the context stream.  given != nullptr: skip matching
-// and verify the given matches of the single pair specs[0] instead.
-int enqueue_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
-                  const std::vector<PairSpec>& specs, bool verify, const uint32_t* given,
-                  int64_t given_m) {
+// Stage 1 of a batch, on the matching stream: upload the pair descriptors,
+// run the tile + finalize kernels (or upload the given matches of the single
+// pair specs[0]), and copy the match counts into the mapped result buffer.
+// Buffers are laid out for the worst case (one match slot per pivot
+// keypoint) so nothing waits for the counts.
+int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
+                  const std::vector<PairSpec>& specs, const uint32_t* given, int64_t given_m) {
   const int64_t P = (int64_t)specs.size();
   bs.P = P;
-  bs.verify = verify;
+  bs.verify = false;
   bs.matched = given == nullptr;
   bs.pending = false;
+  bs.table = &t;
+  bs.specs = specs;
   for (auto& e : bs.ev)
     if (!e) SCM_HIP(hipEventCreate(&e));
   if (P == 0) return SCM_OK;
-  // ---- descriptors (worst-case layout: one match slot per pivot keypoint).
   std::vector<PairDesc> pds(P);
-  std::vector<int64_t> moff(P), soff(P);
   std::vector<MatchJob> jobs, jobs_clamp;
-  int64_t rr = 0, cp = 0, m21 = 0, mo = 0, scr = 0;
-  int max_slots = 0;
+  bs.moff.resize(P);
+  int64_t rr = 0, cp = 0, m21 = 0, mo = 0;
   for (int64_t i = 0; i < P;) {
     const int32_t a = specs[i].a;
     int64_t j = i;
@@ -327,14 +335,11 @@ int enqueue_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
       pd.colpart_off = cp;
       pd.m21_off = m21;
       pd.match_off = mo;
-      moff[k] = mo;
-      soff[k] = scr;
+      bs.moff[k] = mo;
       rr += (int64_t)pd.nseg * pd.n1;
       cp += (int64_t)pd.nrb * pd.n2pad;
       m21 += pd.n2;
       mo += slots;
-      scr += 10 * (int64_t)slots + kVerifyModelDoubles;
-      max_slots = std::max(max_slots, slots);
       if (!given) {
         // |a||b| < 2^19 for every row pair  <=>  max|a|^2 * max|b|^2 < 2^38.
         const unsigned __int128 prod = (unsigned __int128)t.max_norm2[a] * t.max_norm2[b];
@@ -364,33 +369,10 @@ int enqueue_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
     }
     i = j;
   }
-  if (verify && max_slots > kMaxVerifyMatches) {
-    set_error("more than 65535 keypoints in a pivot image (verifier index limit)");
-    return SCM_E_INVALID;
-  }
+  bs.slots = mo;
   const int64_t nfast = (int64_t)jobs.size();
   jobs.insert(jobs.end(), jobs_clamp.begin(), jobs_clamp.end());
   const int64_t NJ = (int64_t)jobs.size();
-  std::vector<GatherPair> gps(P);
-  std::vector<VerifyPair> vps(P);
-  for (int64_t k = 0; k < P; ++k) {
-    GatherPair& g = gps[k];
-    std::memset(&g, 0, sizeof(g));
-    g.match_off = moff[k];
-    g.kp1_off = t.kp_off[specs[k].a];
-    g.kp2_off = t.kp_off[specs[k].b];
-    g.pts_off = moff[k];
-    g.cidx = (int32_t)k;
-    VerifyPair& v = vps[k];
-    std::memset(&v, 0, sizeof(v));
-    v.pts_off = 2 * moff[k];
-    v.scr_off = soff[k];
-    v.mask_off = moff[k];
-    v.cidx = (int32_t)k;
-    v.id1 = t.ids[specs[k].a];
-    v.id2 = t.ids[specs[k].b];
-    v.out_idx = (int32_t)k;
-  }
   // ---- buffers.
   SCM_TRY(bs.jobs.ensure(std::max<int64_t>(NJ, 1) * sizeof(MatchJob)));
   SCM_TRY(bs.pairs.ensure(P * sizeof(PairDesc)));
@@ -402,14 +384,6 @@ int enqueue_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   SCM_TRY(bs.counts.ensure(P * sizeof(int32_t)));
   SCM_TRY(bs.offsets.ensure((P + 1) * sizeof(int64_t)));
   SCM_TRY(bs.match_off.ensure(P * sizeof(int64_t)));
-  SCM_TRY(bs.gpairs.ensure(P * sizeof(GatherPair)));
-  SCM_TRY(bs.vpairs.ensure(P * sizeof(VerifyPair)));
-  if (verify) {
-    SCM_TRY(bs.xy1.ensure(2 * std::max<int64_t>(mo, 1) * sizeof(double)));
-    SCM_TRY(bs.xy2.ensure(2 * std::max<int64_t>(mo, 1) * sizeof(double)));
-    SCM_TRY(bs.scratch.ensure(std::max<int64_t>(scr, 1) * sizeof(double)));
-    SCM_TRY(bs.snaps.ensure(P * 640 * sizeof(uint32_t)));
-  }
   bs.off_counts = 0;
   bs.off_offsets = align256(bs.off_counts + P * sizeof(int32_t));
   bs.off_vout = align256(bs.off_offsets + (P + 1) * sizeof(int64_t));
@@ -418,9 +392,7 @@ int enqueue_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   SCM_TRY(bs.out.ensure(bs.off_masks + mo + 256));
   // ---- descriptor upload from pinned staging.
   const size_t s_pairs = align256(NJ * sizeof(MatchJob));
-  const size_t s_g = align256(s_pairs + P * sizeof(PairDesc));
-  const size_t s_v = align256(s_g + P * sizeof(GatherPair));
-  const size_t s_mo = align256(s_v + P * sizeof(VerifyPair));
+  const size_t s_mo = align256(s_pairs + P * sizeof(PairDesc));
   const size_t s_cnt = align256(s_mo + P * sizeof(int64_t));
   const size_t s_given = align256(s_cnt + sizeof(int32_t));
   const size_t s_end = s_given + (given ? (size_t)given_m * sizeof(uint2) : 0);
@@ -428,17 +400,11 @@ int enqueue_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   uint8_t* st = bs.stage.as<uint8_t>();
   if (NJ) std::memcpy(st, jobs.data(), NJ * sizeof(MatchJob));
   std::memcpy(st + s_pairs, pds.data(), P * sizeof(PairDesc));
-  std::memcpy(st + s_g, gps.data(), P * sizeof(GatherPair));
-  std::memcpy(st + s_v, vps.data(), P * sizeof(VerifyPair));
-  std::memcpy(st + s_mo, moff.data(), P * sizeof(int64_t));
+  std::memcpy(st + s_mo, bs.moff.data(), P * sizeof(int64_t));
   hipStream_t sm = ctx->stream;
   if (NJ)
     SCM_HIP(hipMemcpyAsync(bs.jobs.ptr, st, NJ * sizeof(MatchJob), hipMemcpyHostToDevice, sm));
   SCM_HIP(hipMemcpyAsync(bs.pairs.ptr, st + s_pairs, P * sizeof(PairDesc), hipMemcpyHostToDevice,
-                         sm));
-  SCM_HIP(hipMemcpyAsync(bs.gpairs.ptr, st + s_g, P * sizeof(GatherPair), hipMemcpyHostToDevice,
-                         sm));
-  SCM_HIP(hipMemcpyAsync(bs.vpairs.ptr, st + s_v, P * sizeof(VerifyPair), hipMemcpyHostToDevice,
                          sm));
   SCM_HIP(hipMemcpyAsync(bs.match_off.ptr, st + s_mo, P * sizeof(int64_t), hipMemcpyHostToDevice,
                          sm));
@@ -452,7 +418,6 @@ int enqueue_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
                              hipMemcpyHostToDevice, sm));
     }
   }
-  // ---- kernels.
   SCM_HIP(hipEventRecord(bs.ev[0], sm));
   if (!given) {
     SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), bs.jobs.as<MatchJob>(), (int)nfast,
@@ -470,35 +435,137 @@ int enqueue_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
                                   (float)ctx->opts.max_distance, ctx->opts.cross_check,
                                   bs.matches.as<uint2>(), bs.counts.as<int32_t>(), sm));
   SCM_HIP(hipEventRecord(bs.ev[2], sm));
-  uint8_t* outd = reinterpret_cast<uint8_t*>(bs.out.dev);
+  uint8_t* outh = reinterpret_cast<uint8_t*>(bs.out.host);
+  SCM_HIP(hipMemcpyAsync(outh + bs.off_counts, bs.counts.ptr, P * sizeof(int32_t),
+                         hipMemcpyDeviceToHost, sm));
+  SCM_HIP(hipEventRecord(bs.ev[3], sm));
+  bs.pending = true;
+  return SCM_OK;
+}
+
+// Stage 2 of a batch, on the verification stream: waits (host side) for the
+// batch's match counts, then verifies exactly the pairs the reference
+// verifies (>= min_num_inliers matches, sequential_matching.cc:164-178 /
+// EstimateUncalibrated), longest first so the launch tail is short, with the
+// LDS sample buffer sized to the largest match count; finally compacts the
+// matches and F-inlier masks into the mapped result buffer.
+int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
+  bs.verify = verify;
+  if (!bs.pending || bs.P == 0) return SCM_OK;
+  const int64_t P = bs.P;
+  const ImageTable& t = *bs.table;
+  SCM_HIP(hipEventSynchronize(bs.ev[3]));
+  uint8_t* outh = reinterpret_cast<uint8_t*>(bs.out.host);
+  const int32_t* counts = reinterpret_cast<const int32_t*>(outh + bs.off_counts);
+  hipStream_t sv = bs.vstream;
+  SCM_HIP(hipStreamWaitEvent(sv, bs.ev[3], 0));
+  std::vector<int64_t> order;
   if (verify) {
-    SCM_HIP(launch_gather(bs.gpairs.as<GatherPair>(), (int)P, bs.matches.as<uint2>(),
-                          t.kpxy.as<float2>(), bs.xy1.as<double>(), bs.xy2.as<double>(),
-                          bs.counts.as<int32_t>(), sm));
+    for (int64_t k = 0; k < P; ++k)
+      if (counts[k] >= std::max(1, ctx->opts.min_num_inliers)) {
+        if (counts[k] > kMaxVerifyMatches) {
+          set_error("more than 65535 matches in one pair (verifier index limit)");
+          return SCM_E_INVALID;
+        }
+        order.push_back(k);
+      }
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int64_t x, int64_t y) { return counts[x] > counts[y]; });
+  }
+  // Packed output offsets (exclusive scan of the counts) on the host.
+  int64_t* offs = reinterpret_cast<int64_t*>(outh + bs.off_offsets);
+  int64_t total = 0;
+  for (int64_t k = 0; k < P; ++k) {
+    offs[k] = total;
+    total += counts[k];
+  }
+  offs[P] = total;
+  const int64_t V = (int64_t)order.size();
+  SCM_HIP(hipEventRecord(bs.ev[4], sv));
+  if (verify) {
+    SCM_TRY(bs.dvout.ensure(P * sizeof(VerifyOut)));
+    SCM_HIP(hipMemsetAsync(bs.dvout.ptr, 0, P * sizeof(VerifyOut), sv));  // TwoViewGeometry()
+  }
+  if (V > 0) {
+    std::vector<GatherPair> gps(V);
+    std::vector<VerifyPair> vps(V);
+    int64_t scr = 0;
+    for (int64_t q = 0; q < V; ++q) {
+      const int64_t k = order[q];
+      const int32_t m = counts[k];
+      GatherPair& g = gps[q];
+      std::memset(&g, 0, sizeof(g));
+      g.match_off = bs.moff[k];
+      g.kp1_off = t.kp_off[bs.specs[k].a];
+      g.kp2_off = t.kp_off[bs.specs[k].b];
+      g.pts_off = bs.moff[k];
+      g.m = m;
+      g.cidx = -1;
+      VerifyPair& v = vps[q];
+      std::memset(&v, 0, sizeof(v));
+      v.pts_off = 2 * bs.moff[k];
+      v.scr_off = scr;
+      v.mask_off = bs.moff[k];
+      v.m = m;
+      v.cidx = -1;
+      v.id1 = t.ids[bs.specs[k].a];
+      v.id2 = t.ids[bs.specs[k].b];
+      v.out_idx = (int32_t)k;
+      scr += 10 * (int64_t)m + kVerifyModelDoubles;
+    }
+    const int max_m = counts[order[0]];
+    SCM_TRY(bs.gpairs.ensure(V * sizeof(GatherPair)));
+    SCM_TRY(bs.vpairs.ensure(V * sizeof(VerifyPair)));
+    SCM_TRY(bs.xy1.ensure(2 * std::max<int64_t>(bs.slots, 1) * sizeof(double)));
+    SCM_TRY(bs.xy2.ensure(2 * std::max<int64_t>(bs.slots, 1) * sizeof(double)));
+    SCM_TRY(bs.xyf.ensure(std::max<int64_t>(bs.slots, 1) * sizeof(float4)));
+    SCM_TRY(bs.scratch.ensure(std::max<int64_t>(scr, 1) * sizeof(double)));
+    SCM_TRY(bs.snaps.ensure(V * 640 * sizeof(uint32_t)));
+    const size_t s_v = align256(V * sizeof(GatherPair));
+    SCM_TRY(bs.vstage.ensure(s_v + V * sizeof(VerifyPair)));
+    uint8_t* st = bs.vstage.as<uint8_t>();
+    std::memcpy(st, gps.data(), V * sizeof(GatherPair));
+    std::memcpy(st + s_v, vps.data(), V * sizeof(VerifyPair));
+    SCM_HIP(hipMemcpyAsync(bs.gpairs.ptr, st, V * sizeof(GatherPair), hipMemcpyHostToDevice, sv));
+    SCM_HIP(hipMemcpyAsync(bs.vpairs.ptr, st + s_v, V * sizeof(VerifyPair),
+                           hipMemcpyHostToDevice, sv));
+    SCM_HIP(launch_gather(bs.gpairs.as<GatherPair>(), (int)V, bs.matches.as<uint2>(),
+                          t.kpxy.as<float2>(), bs.xy1.as<double>(), bs.xy2.as<double>(), nullptr,
+                          bs.xyf.as<float4>(), sv));
     uint64_t* prof = nullptr;
     if (ctx->profile) {
-      SCM_TRY(bs.prof.ensure(P * kVerifyProfSlots * sizeof(uint64_t)));
-      SCM_HIP(hipMemsetAsync(bs.prof.ptr, 0, P * kVerifyProfSlots * sizeof(uint64_t), sm));
+      SCM_TRY(bs.prof.ensure(V * kVerifyProfSlots * sizeof(uint64_t)));
+      SCM_HIP(hipMemsetAsync(bs.prof.ptr, 0, V * kVerifyProfSlots * sizeof(uint64_t), sv));
       prof = bs.prof.as<uint64_t>();
     }
-    SCM_HIP(hipEventRecord(bs.ev[3], sm));
-    SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)P, max_slots, bs.xy1.as<double>(),
+    bs.nprof = V;
+    SCM_HIP(hipEventRecord(bs.ev[4], sv));
+    SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
                           bs.xy2.as<double>(), bs.scratch.as<double>(), bs.snaps.as<uint32_t>(),
-                          bs.masks.as<uint8_t>(),
-                          reinterpret_cast<VerifyOut*>(outd + bs.off_vout), make_params(ctx->opts),
-                          prof, bs.counts.as<int32_t>(), sm));
-  } else {
-    SCM_HIP(hipEventRecord(bs.ev[3], sm));
+                          bs.masks.as<uint8_t>(), bs.dvout.as<VerifyOut>(),
+                          make_params(ctx->opts), prof, nullptr, bs.xyf.as<float4>(), sv));
   }
-  SCM_HIP(hipEventRecord(bs.ev[4], sm));
+  SCM_HIP(hipEventRecord(bs.ev[5], sv));
+  // Compact matches + F-inlier masks in HBM, then DMA the results into the
+  // pinned host buffer (counts are already there).
+  SCM_TRY(bs.dpack.ensure(std::max<int64_t>(total, 1) * sizeof(uint2)));
+  SCM_TRY(bs.dpmask.ensure(std::max<int64_t>(total, 1)));
+  SCM_HIP(hipMemcpyAsync(bs.offsets.ptr, offs, (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
+                         sv));
   SCM_HIP(launch_compact(bs.counts.as<int32_t>(), (int)P, bs.offsets.as<int64_t>(),
-                         reinterpret_cast<int64_t*>(outd + bs.off_offsets),
-                         reinterpret_cast<int32_t*>(outd + bs.off_counts),
                          bs.match_off.as<int64_t>(), bs.matches.as<uint2>(),
-                         bs.masks.as<uint8_t>(), reinterpret_cast<uint2*>(outd + bs.off_matches),
-                         outd + bs.off_masks, sm));
-  SCM_HIP(hipEventRecord(bs.ev[5], sm));
-  bs.pending = true;
+                         bs.masks.as<uint8_t>(), bs.dpack.as<uint2>(), bs.dpmask.as<uint8_t>(),
+                         sv));
+  if (total > 0) {
+    SCM_HIP(hipMemcpyAsync(outh + bs.off_matches, bs.dpack.ptr, total * sizeof(uint2),
+                           hipMemcpyDeviceToHost, sv));
+    SCM_HIP(hipMemcpyAsync(outh + bs.off_masks, bs.dpmask.ptr, total, hipMemcpyDeviceToHost, sv));
+  }
+  if (verify)
+    SCM_HIP(hipMemcpyAsync(outh + bs.off_vout, bs.dvout.ptr, P * sizeof(VerifyOut),
+                           hipMemcpyDeviceToHost, sv));
+  SCM_HIP(hipEventRecord(bs.ev[6], sv));
+  bs.posted = true;
   return SCM_OK;
 }
 
@@ -506,29 +573,43 @@ int collect_batch(scm_context* ctx, BatchSet& bs, BatchView* v) {
   *v = BatchView();
   v->P = bs.P;
   if (!bs.pending) return SCM_OK;
-  SCM_HIP(hipEventSynchronize(bs.ev[5]));
-  bs.pending = false;
+  if (!bs.posted) {
+    set_error("internal: batch collected before its verification stage was enqueued");
+    return SCM_E_STATE;
+  }
+  SCM_HIP(hipEventSynchronize(bs.ev[6]));
+  bs.pending = bs.posted = false;
   if (bs.matched) {
     ctx->t_match += event_ms(bs.ev[0], bs.ev[1]);
     ctx->t_final += event_ms(bs.ev[1], bs.ev[2]);
   }
-  if (bs.verify) ctx->t_verify += event_ms(bs.ev[3], bs.ev[4]);
+  if (bs.verify) ctx->t_verify += event_ms(bs.ev[4], bs.ev[5]);
   const uint8_t* o = reinterpret_cast<const uint8_t*>(bs.out.host);
   v->counts = reinterpret_cast<const int32_t*>(o + bs.off_counts);
   v->offsets = reinterpret_cast<const int64_t*>(o + bs.off_offsets);
   v->vout = bs.verify ? reinterpret_cast<const VerifyOut*>(o + bs.off_vout) : nullptr;
   v->matches = reinterpret_cast<const Match*>(o + bs.off_matches);
   v->masks = o + bs.off_masks;
-  if (ctx->profile && bs.verify && bs.P > 0) {
-    std::vector<uint64_t> pr(bs.P * kVerifyProfSlots);
+  if (ctx->profile && bs.verify && bs.nprof > 0) {
+    std::vector<uint64_t> pr(bs.nprof * kVerifyProfSlots);
     SCM_HIP(hipMemcpy(pr.data(), bs.prof.ptr, pr.size() * sizeof(uint64_t),
                       hipMemcpyDeviceToHost));
     ctx->prof_sum.resize(kVerifyProfSlots, 0);
-    for (int64_t k = 0; k < bs.P; ++k)
+    for (int64_t k = 0; k < bs.nprof; ++k)
       for (int j = 0; j < kVerifyProfSlots; ++j) ctx->prof_sum[j] += pr[k * kVerifyProfSlots + j];
-    ctx->prof_pairs += bs.P;
+    ctx->prof_pairs += bs.nprof;
   }
+  bs.nprof = 0;
   return SCM_OK;
+}
+
+// Both stages of one batch, then its results (single-pair / stencil calls).
+int run_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
+              const std::vector<PairSpec>& specs, bool verify, const uint32_t* given,
+              int64_t given_m, BatchView* v) {
+  SCM_TRY(enqueue_match(ctx, bs, t, specs, given, given_m));
+  SCM_TRY(enqueue_verify(ctx, bs, verify));
+  return collect_batch(ctx, bs, v);
 }
 
 // Number of F inliers emitted for pair p (TwoViewGeometry() after the
@@ -721,11 +802,28 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
     return SCM_OK;
   };
   out->row_off.reserve(2 * (row_end - row_begin) + 1);
-  for (size_t k = 0; k < batches.size(); ++k) {
-    SCM_TRY(enqueue_batch(ctx, ctx->sets[k & 1], t, batches[k].specs, true, nullptr, 0));
-    if (k > 0) SCM_TRY(finish(batches[k - 1], ctx->sets[(k - 1) & 1]));
+  // Three buffer sets: at step k the GPU holds match(k) on the matching
+  // stream and verify(k-1) (+ verify(k-2)) on the verification stream while
+  // the host serialises batch k-3.
+  const size_t B = batches.size();
+  if (ctx->serial) {
+    for (size_t k = 0; k < B; ++k) {
+      BatchSet& bs = ctx->sets[k % 3];
+      if (k >= 3) SCM_TRY(finish(batches[k - 3], bs));
+      SCM_TRY(enqueue_match(ctx, bs, t, batches[k].specs, nullptr, 0));
+      SCM_TRY(enqueue_verify(ctx, bs, true));
+      if (bs.pending) SCM_HIP(hipStreamWaitEvent(ctx->stream, bs.ev[6], 0));
+    }
+  } else {
+    for (size_t k = 0; k < B; ++k) {
+      if (k >= 3) SCM_TRY(finish(batches[k - 3], ctx->sets[(k - 3) % 3]));
+      SCM_TRY(enqueue_match(ctx, ctx->sets[k % 3], t, batches[k].specs, nullptr, 0));
+      if (k >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(k - 1) % 3], true));
+    }
+    if (B >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(B - 1) % 3], true));
   }
-  if (!batches.empty()) SCM_TRY(finish(batches.back(), ctx->sets[(batches.size() - 1) & 1]));
+  for (size_t k = B >= 3 ? B - 3 : 0; k < B; ++k) SCM_TRY(finish(batches[k], ctx->sets[k % 3]));
+  (void)0;
   out->row_off.push_back((int64_t)out->size);
   return SCM_OK;
 }
@@ -733,7 +831,9 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
 // Drains any batch left in flight by an error path.
 void drain(scm_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  ctx->sets[0].pending = ctx->sets[1].pending = false;
+  for (BatchSet& bs : ctx->sets)
+    if (bs.vstream) (void)hipStreamSynchronize(bs.vstream);
+  for (BatchSet& bs : ctx->sets) bs.pending = bs.posted = false;
 }
 
 }  // namespace
@@ -785,12 +885,16 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   int hw = (int)std::thread::hardware_concurrency();
   if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::max(1, std::atoi(e));
   ctx->threads = std::max(1, std::min(16, hw));
+  if (const char* e = std::getenv("SCM_SERIAL")) ctx->serial = e[0] == '1';
   if (const char* e = std::getenv("SCM_BATCH_PAIRS"))
     ctx->batch_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
   if (hipSetDevice(device_index) != hipSuccess ||
-      hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
-    set_error("failed to create HIP stream");
-    delete ctx;
+      hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->sets[0].vstream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->sets[1].vstream, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&ctx->sets[2].vstream, hipStreamNonBlocking) != hipSuccess) {
+    scm_context_destroy(ctx);
+    set_error("failed to create HIP streams");
     return SCM_E_DEVICE;
   }
   std::vector<float> lut;
@@ -813,20 +917,22 @@ void scm_context_destroy(scm_context* ctx) {
   if (ctx->profile && ctx->prof_pairs > 0) {
     static const char* names[] = {"sample",    "solve",   "score",  "cand_res", "seqsum",
                                   "lo_gather", "lo_est",  "lo_res", "other",    "n_batch",
-                                  "n_cand",    "n_lo",    "n_trials", "n_points", "n_seqsum"};
+                                  "n_cand",    "n_lo",    "n_trials", "n_points", "n_seqsum",
+                                  "score_H"};
     std::fprintf(stderr, "[scm verify profile] pairs=%lld (per pair: cycles / counts)\n",
                  (long long)ctx->prof_pairs);
-    for (int j = 0; j < 15; ++j)
+    for (int j = 0; j < 16; ++j)
       std::fprintf(stderr, "  %-10s %14.1f\n", names[j],
                    (double)ctx->prof_sum[j] / (double)ctx->prof_pairs);
   }
   ctx->table.release();
   ctx->scratch_table.release();
   ctx->lut.release();
-  ctx->sets[0].release();
-  ctx->sets[1].release();
+  for (BatchSet& bs : ctx->sets) bs.release();
   ctx->h_stage.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  for (BatchSet& bs : ctx->sets)
+    if (bs.vstream) (void)hipStreamDestroy(bs.vstream);
   delete ctx;
 }
 
@@ -846,13 +952,12 @@ int scm_match_pair(scm_context* ctx, const uint8_t* desc1, int64_t n1, const uin
   rows[1].ndesc = n2;
   SCM_TRY(upload_table(ctx, &ctx->scratch_table, rows, true, false));
   BatchSet& bs = ctx->sets[0];
-  const int rc = enqueue_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, false, nullptr, 0);
+  BatchView v;
+  const int rc = run_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, false, nullptr, 0, &v);
   if (rc != SCM_OK) {
     drain(ctx);
     return rc;
   }
-  BatchView v;
-  SCM_TRY(collect_batch(ctx, bs, &v));
   *num_matches = v.counts[0];
   if (v.counts[0] > cap) {
     set_error("match buffer too small");
@@ -895,13 +1000,13 @@ int scm_verify_pair(scm_context* ctx, const float* kp1, int64_t n1, const float*
   rows[1].nkp = n2;
   SCM_TRY(upload_table(ctx, &ctx->scratch_table, rows, false, true));
   BatchSet& bs = ctx->sets[0];
-  const int rc = enqueue_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, true, matches, num_matches);
+  BatchView v;
+  const int rc =
+      run_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, true, matches, num_matches, &v);
   if (rc != SCM_OK) {
     drain(ctx);
     return rc;
   }
-  BatchView v;
-  SCM_TRY(collect_batch(ctx, bs, &v));
   const int64_t ninl = inlier_count(v, 0);
   std::vector<uint8_t> bytes(kTvgFixed + 8 * ninl);
   write_tvg(bytes.data(), v, 0, ninl);
@@ -930,13 +1035,12 @@ int scm_execute_stencil(scm_context* ctx, int64_t stencil_size, const scm_elemen
     pair_ids.push_back(ids[s]);
   }
   BatchSet& bs = ctx->sets[0];
-  int rc = enqueue_batch(ctx, bs, ctx->scratch_table, specs, true, nullptr, 0);
+  BatchView v;
+  int rc = run_batch(ctx, bs, ctx->scratch_table, specs, true, nullptr, 0, &v);
   if (rc != SCM_OK) {
     drain(ctx);
     return rc;
   }
-  BatchView v;
-  SCM_TRY(collect_batch(ctx, bs, &v));
   Packed pk;
   rc = serialize_rows(ctx, v, pair_ids, {0, (int64_t)specs.size()}, &pk);
   if (rc != SCM_OK) {

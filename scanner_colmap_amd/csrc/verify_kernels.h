@@ -54,7 +54,7 @@ struct VerifyOut {
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
-                         const int32_t* counts, hipStream_t stream);
+                         const int32_t* counts, const float4* xyf, hipStream_t stream);
 size_t verify_lds_bytes(int max_m);
 constexpr int kVerifyProfSlots = 16;
 
@@ -70,12 +70,10 @@ struct GatherPair {
 };
 hipError_t launch_gather(const GatherPair* pairs, int npairs, const uint2* matches,
                          const float2* kpxy, double* xy1, double* xy2, const int32_t* counts,
-                         hipStream_t stream);
-// Exclusive scan of counts (device + host-mapped copies) and packing of each
-// pair's matches / F-inlier mask into host-mapped memory.
-hipError_t launch_compact(const int32_t* counts, int npairs, int64_t* offsets,
-                          int64_t* host_offsets, int32_t* host_counts, const int64_t* match_off,
-                          const uint2* matches, const uint8_t* masks, uint2* out_matches,
-                          uint8_t* out_masks, hipStream_t stream);
+                         float4* xyf, hipStream_t stream);
+// Packs each pair's matches / F-inlier mask contiguously at offsets[p].
+hipError_t launch_compact(const int32_t* counts, int npairs, const int64_t* offsets,
+                          const int64_t* match_off, const uint2* matches, const uint8_t* masks,
+                          uint2* out_matches, uint8_t* out_masks, hipStream_t stream);
 
 }  // namespace scm

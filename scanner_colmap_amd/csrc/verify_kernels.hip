@@ -50,6 +50,7 @@ struct __attribute__((aligned(16))) VerifyLds {
   uint32_t counts[kTrialBatch * 3];
   int32_t nmodels[kTrialBatch];
   uint16_t samples[kTrialBatch][8];
+  float hcs[kTrialBatch][12];  // homography filter constants per hypothesis
   int32_t mt_idx;
   int32_t best_n;
   int32_t best_sum_valid;
@@ -78,7 +79,8 @@ struct Prof {  // passed by value; the last stamp lives in *tp (LDS)
   }
 };
 enum { PR_SAMPLE = 0, PR_SOLVE, PR_SCORE, PR_CAND, PR_SEQSUM, PR_GATHER, PR_LOEST, PR_LORES,
-       PR_OTHER, PR_N_BATCH, PR_N_CAND, PR_N_LO, PR_N_TRIALS, PR_N_POINTS, PR_N_SEQSUM };
+       PR_OTHER, PR_N_BATCH, PR_N_CAND, PR_N_LO, PR_N_TRIALS, PR_N_POINTS, PR_N_SEQSUM,
+       PR_SCORE_H };
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one wavefront: cheap
 
@@ -181,6 +183,142 @@ __device__ __forceinline__ bool sampson_inlier(const double* F, double x1_0, dou
   const bool out = sane && num >= md * (1.0 + 0x1p-50);
   if (in | out) return in;
   return num / den <= maxr;
+}
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
+// Constants of the packed-fp32 homography inlier filter (score_h_chunk).
+// For one fp64 model H and points with |coordinate| <= S (exact in fp32:
+// keypoints are float32) the filter evaluates, in fp32 with explicit FMAs,
+//   Q_i = H_i0 s0 + H_i1 s1 + H_i2,  w_j = d_j Q_2 - Q_j,
+//   lhs = w_0^2 + w_1^2,  rhs = maxr Q_2^2
+// and decides the reference test  fl64(transfer error) <= maxr  (i.e.
+// W_0^2 + W_1^2 <= maxr P_2^2 on the exact values, up to the reference's own
+// fp64 rounding, 2^29 times finer) whenever |lhs - rhs| exceeds
+//   mg = a1 |Q_2| + a2 rhs + a0.
+// Error bounds (u = 2^-24; Hf = fl32(H)): |Q_i - P_i| <= 3u A_i =: al_i with
+// A_i = (|H_i0| + |H_i1|) S + |H_i2|; |w_j - W_j| <= b + u |W_j| with
+// b = S al_2 + max(al_0, al_1); hence |lhs - L| <= 2.85 b sqrt(L) + 2.01 b^2
+// + 4.1u L and |rhs - R| <= maxr al_2 (2|Q_2| + 3 al_2) + 3.01u rhs; both
+// sides are monotone in L, so evaluating them at the threshold L = R gives
+//   a1 = 2 maxr al_2 + 2.85 b sqrt(maxr),
+//   a0 = 3 maxr al_2^2 + 2.85 b sqrt(maxr) al_2 + 2.01 b^2,  a2 = 7.2u,
+// all scaled by 1.5.  Models whose fp32 evaluation could overflow get
+// a0 = inf: every point is then undecided and takes the exact fp64 test.
+__device__ __forceinline__ void h_filter_consts(const double* H, double S, double maxr,
+                                                float* c) {
+  const double u = 0x1p-24;
+  const double A0 = (fabs(H[0]) + fabs(H[1])) * S + fabs(H[2]);
+  const double A1 = (fabs(H[3]) + fabs(H[4])) * S + fabs(H[5]);
+  const double A2 = (fabs(H[6]) + fabs(H[7])) * S + fabs(H[8]);
+  const double al0 = 3.01 * u * A0, al1 = 3.01 * u * A1, al2 = 3.01 * u * A2;
+  const double b = S * al2 + fmax(al0, al1);
+  const double sq = sqrt(maxr);
+  const double a1 = 1.5 * (2.0 * maxr * al2 + 2.85 * b * sq);
+  double a0 = 1.5 * (3.0 * maxr * al2 * al2 + 2.85 * b * sq * al2 + 2.01 * b * b) + 1e-30;
+  const double a2 = 1.5 * 7.2 * u;
+  const double wmax = S * A2 + fmax(A0, A1);
+  const double lmax = 2.0 * wmax * wmax, rmax = maxr * A2 * A2;
+  if (!(lmax < 1e36 && rmax < 1e36 && a1 < 1e36 && a0 < 1e36)) a0 = __builtin_inff();
+#pragma unroll
+  for (int j = 0; j < 9; ++j) c[j] = (float)H[j];
+  c[9] = __double2float_ru(a0);
+  c[10] = __double2float_ru(a1);
+  c[11] = __double2float_ru(a2);
+}
+
+// Lanes of point slot p (point base + 64 p + lane) that hold a point.
+__device__ __forceinline__ uint64_t slot_mask(int n, int base, int p) {
+  const int rem = n - base - 64 * p;
+  return rem >= 64 ? ~0ull : (rem <= 0 ? 0ull : ((1ull << rem) - 1ull));
+}
+
+struct HFilt {
+  f32x2 h0, h1, h2, h3, h4, h5, h6, h7, h8, a0, a1, a2, mr;
+};
+
+// Filter decisions for one packed pair of points: in = surely an inlier,
+// mb = possibly an inlier (in implies mb).
+__device__ __forceinline__ void h_filter_pair(const HFilt& f, f32x2 s0, f32x2 s1, f32x2 d0,
+                                              f32x2 d1, bool* in, bool* mb) {
+  const f32x2 q0 = __builtin_elementwise_fma(f.h0, s0, __builtin_elementwise_fma(f.h1, s1, f.h2));
+  const f32x2 q1 = __builtin_elementwise_fma(f.h3, s0, __builtin_elementwise_fma(f.h4, s1, f.h5));
+  const f32x2 q2 = __builtin_elementwise_fma(f.h6, s0, __builtin_elementwise_fma(f.h7, s1, f.h8));
+  const f32x2 w0 = __builtin_elementwise_fma(d0, q2, -q0);
+  const f32x2 w1 = __builtin_elementwise_fma(d1, q2, -q1);
+  const f32x2 lhs = __builtin_elementwise_fma(w0, w0, w1 * w1);
+  const f32x2 rhs = f.mr * (q2 * q2);
+  const f32x2 mg = __builtin_elementwise_fma(f.a1, __builtin_elementwise_abs(q2),
+                                             __builtin_elementwise_fma(f.a2, rhs, f.a0));
+  const f32x2 hi = lhs + mg, lo = lhs - mg;
+  in[0] = hi.x <= rhs.x;
+  in[1] = hi.y <= rhs.y;
+  mb[0] = !(lo.x > rhs.x);
+  mb[1] = !(lo.y > rhs.y);
+}
+
+// Inlier count of the model whose filter constants are in lane t's hc[] over
+// the points [base, base + 64 PCH) (point base + 64 p + lane in slot p),
+// with the exact fp64 transfer-error test for the undecided points.
+template <int PCH>
+__device__ __forceinline__ int score_h_chunk(const float* hc, const double* mh,
+                                             const f32x2* s0, const f32x2* s1, const f32x2* d0,
+                                             const f32x2* d1, int n, int base, const double* xy1,
+                                             const double* xy2, float maxrf, double maxr) {
+  // hc: this hypothesis' 12 constants in LDS (same address in every lane:
+  // a broadcast read); mh: its fp64 model (global, only read when needed).
+  const float4 c0 = reinterpret_cast<const float4*>(hc)[0];
+  const float4 c1 = reinterpret_cast<const float4*>(hc)[1];
+  const float4 c2 = reinterpret_cast<const float4*>(hc)[2];
+  HFilt f;
+  f.h0 = c0.x;
+  f.h1 = c0.y;
+  f.h2 = c0.z;
+  f.h3 = c0.w;
+  f.h4 = c1.x;
+  f.h5 = c1.y;
+  f.h6 = c1.z;
+  f.h7 = c1.w;
+  f.h8 = c2.x;
+  f.a0 = c2.y;
+  f.a1 = c2.z;
+  f.a2 = c2.w;
+  f.mr = maxrf;
+  int cnt = 0;
+  uint64_t any = 0;
+#pragma unroll
+  for (int q = 0; q < PCH / 2; ++q) {
+    bool in[2], mb[2];
+    h_filter_pair(f, s0[q], s1[q], d0[q], d1[q], in, mb);
+    const uint64_t ok0 = slot_mask(n, base, 2 * q), ok1 = slot_mask(n, base, 2 * q + 1);
+    const uint64_t i0 = __ballot(in[0]) & ok0, i1 = __ballot(in[1]) & ok1;
+    cnt += __popcll(i0) + __popcll(i1);
+    any |= ((__ballot(mb[0]) & ~i0) & ok0) | ((__ballot(mb[1]) & ~i1) & ok1);
+  }
+  if (any) {  // rare: exact fp64 test (HomographyMatrixEstimator::Residuals)
+    double mk[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) mk[j] = mh[j];
+    const int lane = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < PCH / 2; ++q) {
+      bool in[2], mb[2];
+      h_filter_pair(f, s0[q], s1[q], d0[q], d1[q], in, mb);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = base + (2 * q + h) * 64 + lane;
+        bool e = false;
+        if (i < n && mb[h] && !in[h])
+          e = homography_sq(mk, xy1[2 * i], xy1[2 * i + 1], xy2[2 * i], xy2[2 * i + 1]) <= maxr;
+        cnt += __popcll(__ballot(e));
+      }
+    }
+  }
+  return cnt;
 }
 
 // Residuals of one model over all points into res; returns the inlier count.
@@ -426,11 +564,12 @@ __device__ void ensure_best_sum(VerifyLds& s, const double* res_best, int n, dou
 // buffers (2n doubles each); snap: 625-word PRNG snapshot (global).  The
 // best model ends in s.best_model.
 template <int K>
-__device__ RansacResult loransac_wave(VerifyLds& s, uint16_t* sidx, const double* xy1,
+__device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& s, uint16_t* sidx, const double* xy1,
                                       const double* xy2, int n, int max_trials,
                                       const VerifyParams P, double* res0, double* res1,
                                       double* xin1, double* xin2, uint32_t* snap,
-                                      double* mbuf, Prof pf) {
+                                      double* mbuf, Prof pf, const float4* xyf = nullptr,
+                                      double S = 0.0) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   const int lane = threadIdx.x;
@@ -500,6 +639,32 @@ __device__ RansacResult loransac_wave(VerifyLds& s, uint16_t* sidx, const double
     // -- score: every lane reloads its own trial's models into registers; the
     //    points are streamed once in register chunks and each model is
     //    broadcast with v_readlane; exact inlier counts via ballot.
+    if (K == KIND_H && xyf != nullptr) {
+      // Packed-fp32 filter with exact fp64 fallback (h_filter_consts); the
+      // hypotheses' constants are broadcast from LDS.
+      if (lane < B) h_filter_consts(mbuf + lane * (MM * MS), S, maxr, &s.hcs[lane][0]);
+      wsync();
+      const float maxrf = (float)maxr;
+      constexpr int PCH = 8;
+      for (int base = 0; base < n; base += 64 * PCH) {
+        f32x2 s0[PCH / 2], s1[PCH / 2], d0[PCH / 2], d1[PCH / 2];
+#pragma unroll
+        for (int q = 0; q < PCH / 2; ++q) {
+          const int i0 = base + (2 * q) * 64 + lane, i1 = i0 + 64;
+          const float4 v0 = i0 < n ? xyf[i0] : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 v1 = i1 < n ? xyf[i1] : make_float4(0.f, 0.f, 0.f, 0.f);
+          s0[q] = f32x2{v0.x, v1.x};
+          s1[q] = f32x2{v0.y, v1.y};
+          d0[q] = f32x2{v0.z, v1.z};
+          d1[q] = f32x2{v0.w, v1.w};
+        }
+        for (int t = 0; t < B; ++t) {
+          const int c = score_h_chunk<PCH>(&s.hcs[t][0], mbuf + t * (MM * MS), s0, s1, d0, d1,
+                                           n, base, xy1, xy2, maxrf, maxr);
+          if (lane == 0) s.counts[t] += (uint32_t)c;
+        }
+      }
+    } else {
     double m[MM][MS];
     int nm = 0;
     if (lane < B) {
@@ -550,8 +715,9 @@ __device__ RansacResult loransac_wave(VerifyLds& s, uint16_t* sidx, const double
         }
       }
     }
+    }
     wsync();
-    pf.lap(PR_SCORE);
+    pf.lap(K == KIND_H ? PR_SCORE_H : PR_SCORE);
     // -- replay the trials in order.
     for (int t = 0; t < B && !abort; ++t) {
       const int tt = trial + t;
@@ -670,12 +836,12 @@ __device__ RansacResult loransac_wave(VerifyLds& s, uint16_t* sidx, const double
   return out;
 }
 
-__global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
+__global__ __launch_bounds__(kVerifyThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void verify_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
     const double* __restrict__ xy2_all, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, uint8_t* __restrict__ masks,
     VerifyOut* __restrict__ out, VerifyParams P, uint64_t* __restrict__ prof,
-    const int32_t* __restrict__ counts) {
+    const int32_t* __restrict__ counts, const float4* __restrict__ xyf_all) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
@@ -719,8 +885,17 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
       for (int i = lane; i < n; i += 64) mask[i] = resF[i] <= P.max_residual ? 1 : 0;
     wsync();
     // ---- H: LORANSAC<H, H> (same PRNG stream).
+    const float4* xyf = xyf_all + pp.pts_off / 2;
+    float smax = 0.0f;
+    for (int i = lane; i < n; i += 64) {
+      const float4 v = xyf[i];
+      smax = fmaxf(smax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) smax = fmaxf(smax, __shfl_xor(smax, d));
     const RansacResult rh = loransac_wave<KIND_H>(s, sidx, xy1, xy2, n, P.max_trials_H, P, res0,
-                                                  res1, xin1, xin2, snap, mbuf, pf);
+                                                  res1, xin1, xin2, snap, mbuf, pf, xyf,
+                                                  (double)smax);
     double Hm[9];
     for (int i = 0; i < 9; ++i) Hm[i] = s.best_model[i];
     o.f_trials = rf.num_trials;
@@ -801,7 +976,8 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_kernel(
 
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
                               const float2* __restrict__ kpxy, double* __restrict__ xy1,
-                              double* __restrict__ xy2, const int32_t* __restrict__ counts) {
+                              double* __restrict__ xy2, const int32_t* __restrict__ counts,
+                              float4* __restrict__ xyf) {
   const GatherPair g = pairs[blockIdx.x];
   const int m = g.cidx >= 0 ? counts[g.cidx] : g.m;
   for (int i = threadIdx.x; i < m; i += blockDim.x) {
@@ -812,46 +988,12 @@ __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2*
     xy1[2 * (g.pts_off + i) + 1] = (double)a.y;
     xy2[2 * (g.pts_off + i)] = (double)b.x;
     xy2[2 * (g.pts_off + i) + 1] = (double)b.y;
+    xyf[g.pts_off + i] = make_float4(a.x, a.y, b.x, b.y);
   }
 }
 
-// Exclusive scan of the per-pair match counts (one block).
-__global__ __launch_bounds__(1024) void scan_counts_kernel(const int32_t* __restrict__ counts,
-                                                           int npairs,
-                                                           int64_t* __restrict__ offsets,
-                                                           int64_t* __restrict__ host_offsets,
-                                                           int32_t* __restrict__ host_counts) {
-  __shared__ int64_t wsum[16];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int per = (npairs + 1023) / 1024;
-  const int i0 = min(npairs, tid * per), i1 = min(npairs, i0 + per);
-  int64_t c = 0;
-  for (int i = i0; i < i1; ++i) c += counts[i];
-  int64_t x = c;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int64_t y = __shfl_up(x, d);
-    if (lane >= d) x += y;
-  }
-  if (lane == 63) wsum[wave] = x;
-  __syncthreads();
-  int64_t before = 0;
-  for (int w = 0; w < wave; ++w) before += wsum[w];
-  int64_t o = before + x - c;
-  for (int i = i0; i < i1; ++i) {
-    offsets[i] = o;
-    host_offsets[i] = o;
-    host_counts[i] = counts[i];
-    o += counts[i];
-  }
-  if (tid == 1023) {
-    offsets[npairs] = o;
-    host_offsets[npairs] = o;
-  }
-}
-
-// Packs each pair's matches and F-inlier mask contiguously (offsets from the
-// scan) into the host-mapped result buffer.
+// Packs each pair's matches and F-inlier mask contiguously at offsets[p]
+// (exclusive scan of the counts, computed on the host).
 __global__ void compact_kernel(const int32_t* __restrict__ counts, const int64_t* __restrict__ offsets,
                                const int64_t* __restrict__ match_off, const uint2* __restrict__ matches,
                                const uint8_t* __restrict__ masks, uint2* __restrict__ out_matches,
@@ -872,7 +1014,7 @@ size_t verify_lds_bytes(int max_m) {
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
-                         const int32_t* counts, hipStream_t stream) {
+                         const int32_t* counts, const float4* xyf, hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
   const size_t lds = verify_lds_bytes(max_m);
   static bool attr = false;
@@ -882,26 +1024,23 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     attr = true;
   }
   hipLaunchKernelGGL(verify_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs, xy1,
-                     xy2, scratch, snaps, masks, out, params, prof, counts);
+                     xy2, scratch, snaps, masks, out, params, prof, counts, xyf);
   return hipGetLastError();
 }
 
 hipError_t launch_gather(const GatherPair* pairs, int npairs, const uint2* matches,
                          const float2* kpxy, double* xy1, double* xy2, const int32_t* counts,
-                         hipStream_t stream) {
+                         float4* xyf, hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(gather_kernel, dim3(npairs), dim3(256), 0, stream, pairs, matches, kpxy,
-                     xy1, xy2, counts);
+                     xy1, xy2, counts, xyf);
   return hipGetLastError();
 }
 
-hipError_t launch_compact(const int32_t* counts, int npairs, int64_t* offsets,
-                          int64_t* host_offsets, int32_t* host_counts, const int64_t* match_off,
-                          const uint2* matches, const uint8_t* masks, uint2* out_matches,
-                          uint8_t* out_masks, hipStream_t stream) {
+hipError_t launch_compact(const int32_t* counts, int npairs, const int64_t* offsets,
+                          const int64_t* match_off, const uint2* matches, const uint8_t* masks,
+                          uint2* out_matches, uint8_t* out_masks, hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(scan_counts_kernel, dim3(1), dim3(1024), 0, stream, counts, npairs, offsets,
-                     host_offsets, host_counts);
   hipLaunchKernelGGL(compact_kernel, dim3(npairs), dim3(256), 0, stream, counts, offsets,
                      match_off, matches, masks, out_matches, out_masks);
   return hipGetLastError();
