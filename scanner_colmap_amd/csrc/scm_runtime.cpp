@@ -520,7 +520,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
     SCM_TRY(bs.xy2.ensure(2 * std::max<int64_t>(bs.slots, 1) * sizeof(double)));
     SCM_TRY(bs.xyf.ensure(std::max<int64_t>(bs.slots, 1) * sizeof(float4)));
     SCM_TRY(bs.scratch.ensure(std::max<int64_t>(scr, 1) * sizeof(double)));
-    SCM_TRY(bs.snaps.ensure(V * 640 * sizeof(uint32_t)));
+    SCM_TRY(bs.snaps.ensure(V * kVerifySnapWords * sizeof(uint32_t)));
     const size_t s_v = align256(V * sizeof(GatherPair));
     SCM_TRY(bs.vstage.ensure(s_v + V * sizeof(VerifyPair)));
     uint8_t* st = bs.vstage.as<uint8_t>();

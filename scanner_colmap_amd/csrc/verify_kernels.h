@@ -9,6 +9,7 @@ constexpr int kVerifyThreads = 64;    // one wavefront per pair
 constexpr int kTrialBatch = 64;       // hypotheses solved in parallel per round (one per lane)
 constexpr int kMaxVerifyMatches = 65535;  // uint16 sample indices in LDS
 constexpr int kVerifyModelDoubles = kTrialBatch * 27;  // per-pair model buffer
+constexpr int kVerifySnapWords = 1280;  // per pair: handed-on PRNG state + batch snapshot
 
 // Scalar options of TwoViewGeometry::EstimateUncalibrated (SURVEY.md §8a a2,
 // a9-a14) after the op's parseConfigs (sequential_matching.cc:64-75).
@@ -50,7 +51,8 @@ struct VerifyOut {
   double H[9];
 };
 
-// snaps: 640 uint32 per pair (PRNG snapshot for the abort rewind).
+// snaps: kVerifySnapWords uint32 per pair (PRNG state between the F, H and
+// watermark kernels + the per-batch snapshot for the abort rewind).
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,

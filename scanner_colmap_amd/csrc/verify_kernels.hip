@@ -51,6 +51,7 @@ struct __attribute__((aligned(16))) VerifyLds {
   int32_t nmodels[kTrialBatch];
   uint16_t samples[kTrialBatch][8];
   float hcs[kTrialBatch][12];  // homography filter constants per hypothesis
+  uint16_t jbuf[kTrialBatch * 7];  // Shuffle targets of one batch of samples
   int32_t mt_idx;
   int32_t best_n;
   int32_t best_sum_valid;
@@ -147,6 +148,130 @@ __device__ uint32_t uniform_u32(VerifyLds& s, uint32_t a, uint32_t b) {
     }
   }
   return a + (uint32_t)(product >> 32);
+}
+
+// Wave-parallel form of the same generator, used for the sample draws of a
+// whole hypothesis batch at once.
+__device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
+  y ^= y >> 11;
+  y ^= (y << 7) & 0x9d2c5680u;
+  y ^= (y << 15) & 0xefc60000u;
+  y ^= y >> 18;
+  return y;
+}
+
+// mt19937 state regeneration in three dependency phases: words [0,227) read
+// only old words, [227,454) read the new words k-227 of phase one, and
+// [454,624) the new words k-227 of phase two (k = 623 also reads the new
+// word 0) -- exactly the values the sequential loop in mt_next sees.
+__device__ void mt_twist_wave(VerifyLds& s) {
+  const int lane = threadIdx.x;
+  const int bounds[4] = {0, 227, 454, 624};
+#pragma unroll
+  for (int ph = 0; ph < 3; ++ph) {
+    uint32_t nv[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = bounds[ph] + q * 64 + lane;
+      nv[q] = 0u;
+      if (k < bounds[ph + 1]) {
+        const uint32_t y = (s.mt[k] & 0x80000000u) | (s.mt[k + 1 < 624 ? k + 1 : 0] & 0x7fffffffu);
+        const int km = k + 397 < 624 ? k + 397 : k + 397 - 624;
+        nv[q] = s.mt[km] ^ (y >> 1) ^ ((y & 1u) ? 0x9908b0dfu : 0u);
+      }
+    }
+    wsync();
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = bounds[ph] + q * 64 + lane;
+      if (k < bounds[ph + 1]) s.mt[k] = nv[q];
+    }
+    wsync();
+  }
+}
+
+// The D = B * kmin uniform_u32(i, n - 1) draws of one batch (i = r mod kmin
+// for draw r), computed in parallel under the assumption that no draw needs
+// Lemire's rejection step; the generator state advances by exactly D words.
+// Returns false (state untouched except through the snapshot the caller
+// holds) when some draw might need a rejection; the caller then replays the
+// batch serially.  Draw r's target index goes to s.jbuf[r].
+template <int KMIN>
+__device__ bool draw_targets_wave(VerifyLds& s, int D, uint32_t n) {
+  const int lane = threadIdx.x;
+  const int idx0 = s.mt_idx;
+  const int avail = 624 - idx0;
+  uint32_t outv[KMIN];
+#pragma unroll
+  for (int q = 0; q < KMIN; ++q) {
+    const int r = lane + 64 * q;
+    outv[q] = (r < D && r < avail) ? mt_temper(s.mt[idx0 + r]) : 0u;
+  }
+  if (D > avail) {
+    wsync();
+    mt_twist_wave(s);
+#pragma unroll
+    for (int q = 0; q < KMIN; ++q) {
+      const int r = lane + 64 * q;
+      if (r < D && r >= avail) outv[q] = mt_temper(s.mt[r - avail]);
+    }
+  }
+  bool bad = false;
+#pragma unroll
+  for (int q = 0; q < KMIN; ++q) {
+    const int r = lane + 64 * q;
+    if (r < D) {
+      const uint32_t i = (uint32_t)(r % KMIN);
+      const uint32_t range = n - i;
+      const uint64_t prod = (uint64_t)outv[q] * (uint64_t)range;
+      if ((uint32_t)prod < range) bad = true;
+      s.jbuf[r] = (uint16_t)(i + (uint32_t)(prod >> 32));
+    }
+  }
+  const bool ok = __ballot(bad) == 0;
+  wsync();
+  if (lane == 0) s.mt_idx = D > avail ? D - avail : idx0 + D;
+  wsync();
+  return ok;
+}
+
+// RandomSampler::Sample's Shuffle for B samples with precomputed targets:
+// the kmin hot positions live in registers, cold targets are read from LDS
+// once per sample (several reads in flight) and written back in order.
+template <int KMIN>
+__device__ void shuffle_batch_lane0(VerifyLds& s, uint16_t* sidx, int B) {
+  uint32_t R[KMIN];
+#pragma unroll
+  for (int i = 0; i < KMIN; ++i) R[i] = sidx[i];
+  for (int b = 0; b < B; ++b) {
+    uint32_t j[KMIN], v[KMIN], w[KMIN];
+#pragma unroll
+    for (int i = 0; i < KMIN; ++i) j[i] = s.jbuf[b * KMIN + i];
+#pragma unroll
+    for (int i = 0; i < KMIN; ++i) v[i] = j[i] >= (uint32_t)KMIN ? sidx[j[i]] : 0u;
+#pragma unroll
+    for (int i = 0; i < KMIN; ++i) {
+      w[i] = 0xFFFFFFFFu;
+      if (j[i] < (uint32_t)KMIN) {  // hot swap R[i] <-> R[j] (j >= i)
+        uint32_t rj = R[i];
+#pragma unroll
+        for (int t = 0; t < KMIN; ++t) rj = (t == (int)j[i]) ? R[t] : rj;
+#pragma unroll
+        for (int t = 0; t < KMIN; ++t) R[t] = (t == (int)j[i]) ? R[i] : R[t];
+        R[i] = rj;
+      } else {
+        uint32_t cur = v[i];
+#pragma unroll
+        for (int i2 = 0; i2 < i; ++i2) cur = (j[i2] == j[i]) ? w[i2] : cur;
+        w[i] = R[i];
+        sidx[j[i]] = (uint16_t)R[i];
+        R[i] = cur;
+      }
+      s.samples[b][i] = (uint16_t)R[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < KMIN; ++i) sidx[i] = (uint16_t)R[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -601,16 +726,23 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
     for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
     if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
     wsync();
-    if (lane == 0) {
-      const uint32_t last = (uint32_t)(n - 1);
-      for (int b = 0; b < B; ++b)
-        for (int i = 0; i < Tr::kmin; ++i) {
-          const uint32_t j = uniform_u32(s, (uint32_t)i, last);
-          const uint16_t t = sidx[i];
-          sidx[i] = sidx[j];
-          sidx[j] = t;
-          s.samples[b][i] = sidx[i];
-        }
+    if (draw_targets_wave<Tr::kmin>(s, B * Tr::kmin, (uint32_t)n)) {
+      if (lane == 0) shuffle_batch_lane0<Tr::kmin>(s, sidx, B);
+    } else {  // a draw may need rejection sampling: serial replay from the snapshot
+      for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
+      wsync();
+      if (lane == 0) {
+        s.mt_idx = (int32_t)snap[624];
+        const uint32_t last = (uint32_t)(n - 1);
+        for (int b = 0; b < B; ++b)
+          for (int i = 0; i < Tr::kmin; ++i) {
+            const uint32_t j = uniform_u32(s, (uint32_t)i, last);
+            const uint16_t t = sidx[i];
+            sidx[i] = sidx[j];
+            sidx[j] = t;
+            s.samples[b][i] = sidx[i];
+          }
+      }
     }
     for (int i = lane; i < kTrialBatch * 3; i += 64) s.counts[i] = 0u;
     wsync();
@@ -836,142 +968,210 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
   return out;
 }
 
-__global__ __launch_bounds__(kVerifyThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void verify_kernel(
+// ---------------------------------------------------------------------------
+// The verification runs as three kernels over the same pairs (one wavefront
+// per pair each), so that each RANSAC flavour gets its own register budget:
+//   verify_f_kernel     seed the pair's PRNG, LORANSAC<7-pt F, 8-pt F>, F
+//                       inlier mask; the PRNG state is handed on in global
+//   verify_h_kernel     LORANSAC<4-pt H, N-pt H> on the same PRNG stream
+//   verify_final_kernel configuration, DetectWatermark (translation
+//                       LORANSAC on the F inliers), post-filter
+// The F / H models and counts travel in the pair's VerifyOut record.
+// ---------------------------------------------------------------------------
+struct PairSetup {
+  VerifyPair pp;
+  int n;
+  uint32_t* state;  // 625 words: handed-on PRNG state
+  uint32_t* snap;   // 625 words: per-batch snapshot (abort rewind)
+  double* base;     // 10 n + kVerifyModelDoubles doubles of scratch
+  VerifyOut* o;
+};
+
+__device__ __forceinline__ PairSetup pair_setup(const VerifyPair* pairs, double* scratch,
+                                                uint32_t* snaps, VerifyOut* out,
+                                                const int32_t* counts) {
+  PairSetup ps;
+  ps.pp = pairs[blockIdx.x];
+  ps.n = ps.pp.cidx >= 0 ? counts[ps.pp.cidx] : ps.pp.m;
+  ps.state = snaps + (int64_t)blockIdx.x * kVerifySnapWords;
+  ps.snap = ps.state + kVerifySnapWords / 2;
+  ps.base = scratch + ps.pp.scr_off;
+  ps.o = out + ps.pp.out_idx;
+  return ps;
+}
+
+__device__ __forceinline__ void mt_save(const VerifyLds& s, uint32_t* st) {
+  for (int i = threadIdx.x; i < 624; i += 64) st[i] = s.mt[i];
+  if (threadIdx.x == 0) st[624] = (uint32_t)s.mt_idx;
+}
+
+__device__ __forceinline__ void mt_load(VerifyLds& s, const uint32_t* st) {
+  for (int i = threadIdx.x; i < 624; i += 64) s.mt[i] = st[i];
+  if (threadIdx.x == 0) s.mt_idx = (int32_t)st[624];
+  wsync();
+}
+
+__global__ __launch_bounds__(kVerifyThreads) void verify_f_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
     const double* __restrict__ xy2_all, double* __restrict__ scratch,
-    uint32_t* __restrict__ snaps, uint8_t* __restrict__ masks,
-    VerifyOut* __restrict__ out, VerifyParams P, uint64_t* __restrict__ prof,
-    const int32_t* __restrict__ counts, const float4* __restrict__ xyf_all) {
+    uint32_t* __restrict__ snaps, uint8_t* __restrict__ masks, VerifyOut* __restrict__ out,
+    VerifyParams P, uint64_t* __restrict__ prof, const int32_t* __restrict__ counts) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
   Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
   pf.start();
-  const VerifyPair pp = pairs[blockIdx.x];
-  const int lane = threadIdx.x;
-  const int n = pp.cidx >= 0 ? counts[pp.cidx] : pp.m;
-  VerifyOut o;
-  o.config = 0;
-  o.num_inliers = 0;
-  o.f_trials = o.h_trials = 0;
-  o.f_inliers_raw = o.h_inliers_raw = 0;
-  o.watermark = 0;
-  o.pad_ = 0;
-  for (int i = 0; i < 9; ++i) { o.F[i] = 0.0; o.H[i] = 0.0; }
-  uint8_t* mask = masks + pp.mask_off;
+  const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
+  const int n = ps.n, lane = threadIdx.x;
+  uint8_t* mask = masks + ps.pp.mask_off;
   for (int i = lane; i < n; i += 64) mask[i] = 0;
-  uint32_t* snap = snaps + (int64_t)blockIdx.x * 640;
+  if (!(n >= P.min_num_inliers && n > 0)) return;
+  const double* xy1 = xy1_all + ps.pp.pts_off;
+  const double* xy2 = xy2_all + ps.pp.pts_off;
+  double* res0 = ps.base;
+  double* res1 = ps.base + n;
+  if (lane == 0) mt_seed(s, pair_seed(P.base_seed, ps.pp.id1, ps.pp.id2));
+  wsync();
+  const RansacResult rf = loransac_wave<KIND_F>(s, sidx, xy1, xy2, n, P.max_trials_F, P, res0,
+                                                res1, ps.base + 2 * n, ps.base + 4 * n, ps.snap,
+                                                ps.base + 10 * n, pf);
+  // F inlier mask (the input of ExtractInlierMatches).
+  const double* resF = rf.res_sel ? res1 : res0;
+  if (rf.success)
+    for (int i = lane; i < n; i += 64) mask[i] = resF[i] <= P.max_residual ? 1 : 0;
+  if (lane < 9) ps.o->F[lane] = s.best_model[lane];
+  if (lane == 0) {
+    ps.o->f_trials = rf.num_trials;
+    ps.o->f_inliers_raw = rf.num_inliers;
+  }
+  mt_save(s, ps.state);
+}
 
-  if (n >= P.min_num_inliers && n > 0) {
-    const double* xy1 = xy1_all + pp.pts_off;
-    const double* xy2 = xy2_all + pp.pts_off;
-    double* base = scratch + pp.scr_off;  // 10 n + kVerifyModelDoubles doubles
-    double* res0 = base;
-    double* res1 = base + n;
-    double* xin1 = base + 2 * n;
-    double* xin2 = base + 4 * n;
-    double* mbuf = base + 10 * n;  // kTrialBatch * 27 doubles
-    if (lane == 0) mt_seed(s, pair_seed(P.base_seed, pp.id1, pp.id2));
-    wsync();
-
-    // ---- F: LORANSAC<7-pt, 8-pt>.
-    const RansacResult rf = loransac_wave<KIND_F>(s, sidx, xy1, xy2, n, P.max_trials_F, P, res0,
-                                                  res1, xin1, xin2, snap, mbuf, pf);
-    double Fm[9];
-    for (int i = 0; i < 9; ++i) Fm[i] = s.best_model[i];
-    const double* resF = rf.res_sel ? res1 : res0;
-    // F inlier mask (ExtractInlierMatches input) before the buffers are reused.
-    if (rf.success)
-      for (int i = lane; i < n; i += 64) mask[i] = resF[i] <= P.max_residual ? 1 : 0;
-    wsync();
-    // ---- H: LORANSAC<H, H> (same PRNG stream).
-    const float4* xyf = xyf_all + pp.pts_off / 2;
-    float smax = 0.0f;
-    for (int i = lane; i < n; i += 64) {
-      const float4 v = xyf[i];
-      smax = fmaxf(smax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    }
+__global__ __launch_bounds__(kVerifyThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void verify_h_kernel(
+    const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
+    const double* __restrict__ xy2_all, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyParams P,
+    uint64_t* __restrict__ prof, const int32_t* __restrict__ counts,
+    const float4* __restrict__ xyf_all) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
+  uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
+  Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
+  pf.start();
+  const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
+  const int n = ps.n, lane = threadIdx.x;
+  if (!(n >= P.min_num_inliers && n > 0)) return;
+  const double* xy1 = xy1_all + ps.pp.pts_off;
+  const double* xy2 = xy2_all + ps.pp.pts_off;
+  const float4* xyf = xyf_all + ps.pp.pts_off / 2;
+  mt_load(s, ps.state);
+  float smax = 0.0f;
+  for (int i = lane; i < n; i += 64) {
+    const float4 v = xyf[i];
+    smax = fmaxf(smax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) smax = fmaxf(smax, __shfl_xor(smax, d));
-    const RansacResult rh = loransac_wave<KIND_H>(s, sidx, xy1, xy2, n, P.max_trials_H, P, res0,
-                                                  res1, xin1, xin2, snap, mbuf, pf, xyf,
-                                                  (double)smax);
-    double Hm[9];
-    for (int i = 0; i < 9; ++i) Hm[i] = s.best_model[i];
-    o.f_trials = rf.num_trials;
-    o.h_trials = rh.num_trials;
-    o.f_inliers_raw = rf.num_inliers;
-    o.h_inliers_raw = rh.num_inliers;
-    for (int i = 0; i < 9; ++i) {
-      o.F[i] = Fm[i];  // F = F_report.model, H = H_report.model
-      o.H[i] = Hm[i];
-    }
-    const int mni = P.min_num_inliers;
-    if ((!rf.success && !rh.success) || (rf.num_inliers < mni && rh.num_inliers < mni)) {
-      o.config = SCM_TVG_DEGENERATE;
-    } else {
-      const double ratio = (double)rh.num_inliers / (double)rf.num_inliers;
-      o.config = ratio > P.max_H_inlier_ratio ? SCM_TVG_PLANAR_OR_PANORAMIC : SCM_TVG_UNCALIBRATED;
-      o.num_inliers = rf.success ? rf.num_inliers : 0;
-      if (P.detect_watermark && rf.success) {
-        // DetectWatermark with the dummy cameras (width = height = 0): a point
-        // is inside the [0,0]x[0,0] box only if it is exactly (0, 0).
-        int nb = 0;
-        for (int i = lane; i < n; i += 64) {
-          if (!mask[i]) continue;
-          const bool in1 = xy1[2 * i] >= 0.0 && xy1[2 * i] <= 0.0 && xy1[2 * i + 1] >= 0.0 &&
-                           xy1[2 * i + 1] <= 0.0;
-          const bool in2 = xy2[2 * i] >= 0.0 && xy2[2 * i] <= 0.0 && xy2[2 * i + 1] >= 0.0 &&
-                           xy2[2 * i + 1] <= 0.0;
-          nb += (!in1 && !in2) ? 1 : 0;
+  for (int d = 32; d >= 1; d >>= 1) smax = fmaxf(smax, __shfl_xor(smax, d));
+  const RansacResult rh = loransac_wave<KIND_H>(s, sidx, xy1, xy2, n, P.max_trials_H, P,
+                                                ps.base, ps.base + n, ps.base + 2 * n,
+                                                ps.base + 4 * n, ps.snap, ps.base + 10 * n, pf,
+                                                xyf, (double)smax);
+  if (lane < 9) ps.o->H[lane] = s.best_model[lane];
+  if (lane == 0) {
+    ps.o->h_trials = rh.num_trials;
+    ps.o->h_inliers_raw = rh.num_inliers;
+  }
+  mt_save(s, ps.state);
+}
+
+__global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
+    const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
+    const double* __restrict__ xy2_all, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, const uint8_t* __restrict__ masks,
+    VerifyOut* __restrict__ out, VerifyParams P, uint64_t* __restrict__ prof,
+    const int32_t* __restrict__ counts) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
+  uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
+  Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
+  pf.start();
+  const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
+  const int n = ps.n, lane = threadIdx.x;
+  if (!(n >= P.min_num_inliers && n > 0)) return;
+  const double* xy1 = xy1_all + ps.pp.pts_off;
+  const double* xy2 = xy2_all + ps.pp.pts_off;
+  const uint8_t* mask = masks + ps.pp.mask_off;
+  VerifyOut* o = ps.o;
+  const int f_in = o->f_inliers_raw, h_in = o->h_inliers_raw;
+  const bool f_ok = f_in >= KindTraits<KIND_F>::kmin, h_ok = h_in >= KindTraits<KIND_H>::kmin;
+  const int mni = P.min_num_inliers;
+  int config, num_inliers = 0, watermark = 0;
+  if ((!f_ok && !h_ok) || (f_in < mni && h_in < mni)) {
+    config = SCM_TVG_DEGENERATE;
+  } else {
+    const double ratio = (double)h_in / (double)f_in;
+    config = ratio > P.max_H_inlier_ratio ? SCM_TVG_PLANAR_OR_PANORAMIC : SCM_TVG_UNCALIBRATED;
+    num_inliers = f_ok ? f_in : 0;
+    if (P.detect_watermark && f_ok) {
+      // DetectWatermark with the dummy cameras (width = height = 0): a point
+      // is inside the [0,0]x[0,0] box only if it is exactly (0, 0).
+      int nb = 0;
+      for (int i = lane; i < n; i += 64) {
+        if (!mask[i]) continue;
+        const bool in1 = xy1[2 * i] >= 0.0 && xy1[2 * i] <= 0.0 && xy1[2 * i + 1] >= 0.0 &&
+                         xy1[2 * i + 1] <= 0.0;
+        const bool in2 = xy2[2 * i] >= 0.0 && xy2[2 * i] <= 0.0 && xy2[2 * i + 1] >= 0.0 &&
+                         xy2[2 * i + 1] <= 0.0;
+        nb += (!in1 && !in2) ? 1 : 0;
+      }
+      nb = wave_sum_i(nb);
+      const int ni = f_in;
+      const double bratio = (double)nb / (double)ni;
+      if (!(bratio < P.watermark_min_inlier_ratio)) {
+        // Inlier points in index order -> translation LO-RANSAC.  Scratch
+        // layout (10n doubles): tin1 [0,2ni) tin2 [2n,2n+2ni) tres0
+        // [4n,4n+ni) tres1 [5n,5n+ni) tx1 [6n,6n+2ni) tx2 [8n,8n+2ni).
+        double* base = ps.base;
+        double* tin1 = base;
+        double* tin2 = base + 2 * n;
+        int w = 0;
+        for (int b0 = 0; b0 < n; b0 += 64) {
+          const int i = b0 + lane;
+          const bool in = i < n && mask[i];
+          const uint64_t bal = __ballot(in);
+          if (in) {
+            const int o2 = w + (int)__builtin_amdgcn_mbcnt_hi(
+                                   (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            tin1[2 * o2] = xy1[2 * i];
+            tin1[2 * o2 + 1] = xy1[2 * i + 1];
+            tin2[2 * o2] = xy2[2 * i];
+            tin2[2 * o2 + 1] = xy2[2 * i + 1];
+          }
+          w += __popcll(bal);
         }
-        nb = wave_sum_i(nb);
-        const int ni = rf.num_inliers;
-        const double bratio = (double)nb / (double)ni;
-        if (!(bratio < P.watermark_min_inlier_ratio)) {
-          // Inlier points in index order -> translation LO-RANSAC.  Scratch
-          // layout (10n doubles): tin1 [0,2ni) tin2 [2n,2n+2ni) tres0
-          // [4n,4n+ni) tres1 [5n,5n+ni) tx1 [6n,6n+2ni) tx2 [8n,8n+2ni).
-          double* tin1 = base;
-          double* tin2 = base + 2 * n;
-          int w = 0;
-          for (int b0 = 0; b0 < n; b0 += 64) {
-            const int i = b0 + lane;
-            const bool in = i < n && mask[i];
-            const uint64_t bal = __ballot(in);
-            if (in) {
-              const int o2 = w + (int)__builtin_amdgcn_mbcnt_hi(
-                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-              tin1[2 * o2] = xy1[2 * i];
-              tin1[2 * o2 + 1] = xy1[2 * i + 1];
-              tin2[2 * o2] = xy2[2 * i];
-              tin2[2 * o2 + 1] = xy2[2 * i + 1];
-            }
-            w += __popcll(bal);
-          }
-          wsync();
-          double* tres0 = base + 4 * n;
-          double* tres1 = base + 5 * n;
-          double* tx1 = base + 6 * n;
-          double* tx2 = base + 8 * n;
-          const RansacResult rt = loransac_wave<KIND_T>(s, sidx, tin1, tin2, ni, P.max_trials_T,
-                                                        P, tres0, tres1, tx1, tx2, snap, mbuf, pf);
-          const double iratio = (double)rt.num_inliers / (double)ni;
-          if (iratio >= P.watermark_min_inlier_ratio) {
-            o.config = SCM_TVG_WATERMARK;
-            o.watermark = 1;
-          }
+        mt_load(s, ps.state);
+        const RansacResult rt = loransac_wave<KIND_T>(s, sidx, tin1, tin2, ni, P.max_trials_T, P,
+                                                      base + 4 * n, base + 5 * n, base + 6 * n,
+                                                      base + 8 * n, ps.snap, base + 10 * n, pf);
+        const double iratio = (double)rt.num_inliers / (double)ni;
+        if (iratio >= P.watermark_min_inlier_ratio) {
+          config = SCM_TVG_WATERMARK;
+          watermark = 1;
         }
       }
     }
-    // ---- post-filter (sequential_matching.cc:173-178): TwoViewGeometry().
-    if (o.num_inliers < P.min_num_inliers) {
-      o.config = 0;
-      o.num_inliers = 0;
-      for (int i = 0; i < 9; ++i) { o.F[i] = 0.0; o.H[i] = 0.0; }
-    }
   }
-  if (lane == 0) out[pp.out_idx] = o;
+  // Post-filter (sequential_matching.cc:173-178): TwoViewGeometry().
+  const bool keep = num_inliers >= mni;
+  if (lane == 0) {
+    o->config = keep ? config : 0;
+    o->num_inliers = keep ? num_inliers : 0;
+    o->watermark = watermark;
+  }
+  if (!keep && lane < 9) {
+    o->F[lane] = 0.0;
+    o->H[lane] = 0.0;
+  }
 }
 
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
@@ -1019,12 +1219,17 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   const size_t lds = verify_lds_bytes(max_m);
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)verify_kernel,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    for (const void* f : {(const void*)verify_f_kernel, (const void*)verify_h_kernel,
+                          (const void*)verify_final_kernel})
+      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  hipLaunchKernelGGL(verify_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs, xy1,
-                     xy2, scratch, snaps, masks, out, params, prof, counts, xyf);
+  hipLaunchKernelGGL(verify_f_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
+                     xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
+  hipLaunchKernelGGL(verify_h_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
+                     xy1, xy2, scratch, snaps, out, params, prof, counts, xyf);
+  hipLaunchKernelGGL(verify_final_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
+                     xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
   return hipGetLastError();
 }
 
