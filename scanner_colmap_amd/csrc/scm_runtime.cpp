@@ -511,7 +511,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
       v.id1 = t.ids[bs.specs[k].a];
       v.id2 = t.ids[bs.specs[k].b];
       v.out_idx = (int32_t)k;
-      scr += 10 * (int64_t)m + kVerifyModelDoubles;
+      scr += verify_scratch_doubles(m);
     }
     const int max_m = counts[order[0]];
     SCM_TRY(bs.gpairs.ensure(V * sizeof(GatherPair)));
@@ -918,10 +918,10 @@ void scm_context_destroy(scm_context* ctx) {
     static const char* names[] = {"sample",    "solve",   "score",  "cand_res", "seqsum",
                                   "lo_gather", "lo_est",  "lo_res", "other",    "n_batch",
                                   "n_cand",    "n_lo",    "n_trials", "n_points", "n_seqsum",
-                                  "score_H"};
+                                  "score_H", "n_hchunk", "n_hslow"};
     std::fprintf(stderr, "[scm verify profile] pairs=%lld (per pair: cycles / counts)\n",
                  (long long)ctx->prof_pairs);
-    for (int j = 0; j < 16; ++j)
+    for (int j = 0; j < 18; ++j)
       std::fprintf(stderr, "  %-10s %14.1f\n", names[j],
                    (double)ctx->prof_sum[j] / (double)ctx->prof_pairs);
   }

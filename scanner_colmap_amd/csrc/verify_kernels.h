@@ -9,7 +9,12 @@ constexpr int kVerifyThreads = 64;    // one wavefront per pair
 constexpr int kTrialBatch = 64;       // hypotheses solved in parallel per round (one per lane)
 constexpr int kMaxVerifyMatches = 65535;  // uint16 sample indices in LDS
 constexpr int kVerifyModelDoubles = kTrialBatch * 27;  // per-pair model buffer
-constexpr int kVerifySnapWords = 1280;  // per pair: handed-on PRNG state + batch snapshot
+constexpr int kVerifySnapWords = 1280;
+// Per-pair scratch (doubles): residuals / inlier gathers (10 m), the model
+// buffer, then the uint16 sample-index vector.
+inline int64_t verify_scratch_doubles(int64_t m) {
+  return 10 * m + kVerifyModelDoubles + (m + 3) / 4 + 1;
+}  // per pair: handed-on PRNG state + batch snapshot
 
 // Scalar options of TwoViewGeometry::EstimateUncalibrated (SURVEY.md §8a a2,
 // a9-a14) after the op's parseConfigs (sequential_matching.cc:64-75).
@@ -32,7 +37,7 @@ struct VerifyParams {
 
 struct VerifyPair {
   int64_t pts_off;   // double offset of xy1/xy2 (2 doubles per match)
-  int64_t scr_off;   // double offset of the per-pair scratch (10 m + kVerifyModelDoubles)
+  int64_t scr_off;   // double offset of the per-pair scratch (verify_scratch_doubles(m))
   int64_t mask_off;  // byte offset of the F inlier mask
   int32_t m;         // number of matches when cidx < 0
   int32_t cidx;      // index into the device match counts (>= 0: read m there)
@@ -58,7 +63,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
                          const int32_t* counts, const float4* xyf, hipStream_t stream);
 size_t verify_lds_bytes(int max_m);
-constexpr int kVerifyProfSlots = 16;
+constexpr int kVerifyProfSlots = 20;
 
 // Gathers the matched keypoint coordinates of each pair (float -> double,
 // FeatureKeypointsToPointsVector, sequential_matching.cc:91-92).

@@ -38,8 +38,9 @@ template <> struct KindTraits<KIND_F> { static constexpr int kmin = 7, kmin_loca
 template <> struct KindTraits<KIND_H> { static constexpr int kmin = 4, kmin_local = 4, mm = 1, ms = 9; };
 template <> struct KindTraits<KIND_T> { static constexpr int kmin = 1, kmin_local = 1, mm = 1, ms = 2; };
 
-// Fixed part of the per-pair LDS; the sample-index vector (uint16, one per
-// match) follows it in dynamic LDS.
+// Per-pair LDS (one wavefront); the sample-index vector of RandomSampler
+// (uint16, one per match) lives in the pair's global scratch so that the LDS
+// footprint does not grow with the match count.
 struct __attribute__((aligned(16))) VerifyLds {
   double best_model[9];
   double ata[45];
@@ -50,7 +51,10 @@ struct __attribute__((aligned(16))) VerifyLds {
   uint32_t counts[kTrialBatch * 3];
   int32_t nmodels[kTrialBatch];
   uint16_t samples[kTrialBatch][8];
-  float hcs[kTrialBatch][12];  // homography filter constants per hypothesis
+  union {
+    float hcs[kTrialBatch][12];      // homography filter constants per hypothesis
+    float fcs[kTrialBatch * 3][12];  // Sampson filter constants per 7-point model
+  };
   uint16_t jbuf[kTrialBatch * 7];  // Shuffle targets of one batch of samples
   int32_t mt_idx;
   int32_t best_n;
@@ -81,7 +85,7 @@ struct Prof {  // passed by value; the last stamp lives in *tp (LDS)
 };
 enum { PR_SAMPLE = 0, PR_SOLVE, PR_SCORE, PR_CAND, PR_SEQSUM, PR_GATHER, PR_LOEST, PR_LORES,
        PR_OTHER, PR_N_BATCH, PR_N_CAND, PR_N_LO, PR_N_TRIALS, PR_N_POINTS, PR_N_SEQSUM,
-       PR_SCORE_H };
+       PR_SCORE_H, PR_N_HCHUNK, PR_N_HSLOW };
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one wavefront: cheap
 
@@ -320,20 +324,23 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
 // For one fp64 model H and points with |coordinate| <= S (exact in fp32:
 // keypoints are float32) the filter evaluates, in fp32 with explicit FMAs,
 //   Q_i = H_i0 s0 + H_i1 s1 + H_i2,  w_j = d_j Q_2 - Q_j,
-//   lhs = w_0^2 + w_1^2,  rhs = maxr Q_2^2
+//   lhs = w_0^2 + w_1^2,  rhs = maxr Q_2^2,  diff = lhs - rhs
 // and decides the reference test  fl64(transfer error) <= maxr  (i.e.
 // W_0^2 + W_1^2 <= maxr P_2^2 on the exact values, up to the reference's own
-// fp64 rounding, 2^29 times finer) whenever |lhs - rhs| exceeds
-//   mg = a1 |Q_2| + a2 rhs + a0.
+// fp64 rounding, 2^29 times finer) whenever |diff| > mg = a2 rhs + a0.
 // Error bounds (u = 2^-24; Hf = fl32(H)): |Q_i - P_i| <= 3u A_i =: al_i with
 // A_i = (|H_i0| + |H_i1|) S + |H_i2|; |w_j - W_j| <= b + u |W_j| with
 // b = S al_2 + max(al_0, al_1); hence |lhs - L| <= 2.85 b sqrt(L) + 2.01 b^2
 // + 4.1u L and |rhs - R| <= maxr al_2 (2|Q_2| + 3 al_2) + 3.01u rhs; both
-// sides are monotone in L, so evaluating them at the threshold L = R gives
-//   a1 = 2 maxr al_2 + 2.85 b sqrt(maxr),
-//   a0 = 3 maxr al_2^2 + 2.85 b sqrt(maxr) al_2 + 2.01 b^2,  a2 = 7.2u,
-// all scaled by 1.5.  Models whose fp32 evaluation could overflow get
-// a0 = inf: every point is then undecided and takes the exact fp64 test.
+// sides are monotone in L, so evaluating them at the threshold L = R bounds
+// the decision error by  c1 |Q_2| + c0 + 7.2u rhs  with
+//   c1 = 2 maxr al_2 + 2.85 b sqrt(maxr),
+//   c0 = 3 maxr al_2^2 + 2.85 b sqrt(maxr) al_2 + 2.01 b^2.
+// The |Q_2| term is folded into the other two with c1 |Q_2| <= c1 (Q_2^2 /
+// (2 tau) + tau / 2) for any tau > 0 (tau = |Q_2| at the image middle), and
+// Q_2^2 <= 1.01 rhs / maxr; everything is scaled by 1.5.  A model whose fp32
+// evaluation could overflow gets constants that leave every point undecided
+// (it is then scored exactly).
 __device__ __forceinline__ void h_filter_consts(const double* H, double S, double maxr,
                                                 float* c) {
   const double u = 0x1p-24;
@@ -343,17 +350,27 @@ __device__ __forceinline__ void h_filter_consts(const double* H, double S, doubl
   const double al0 = 3.01 * u * A0, al1 = 3.01 * u * A1, al2 = 3.01 * u * A2;
   const double b = S * al2 + fmax(al0, al1);
   const double sq = sqrt(maxr);
-  const double a1 = 1.5 * (2.0 * maxr * al2 + 2.85 * b * sq);
-  double a0 = 1.5 * (3.0 * maxr * al2 * al2 + 2.85 * b * sq * al2 + 2.01 * b * b) + 1e-30;
-  const double a2 = 1.5 * 7.2 * u;
+  const double c1 = 2.0 * maxr * al2 + 2.85 * b * sq;
+  const double c0 = 3.0 * maxr * al2 * al2 + 2.85 * b * sq * al2 + 2.01 * b * b;
+  double tau = fabs(H[6] * (0.5 * S) + H[7] * (0.5 * S) + H[8]);
+  if (!(tau > 1e-30 && tau < 1e30)) tau = A2 > 1e-30 ? A2 : 1e-30;
+  const double a2 = 1.5 * (7.2 * u + 1.01 * c1 / (2.0 * tau * maxr));
+  double a0 = 1.5 * (c0 + 0.5 * c1 * tau) + 1e-30;
   const double wmax = S * A2 + fmax(A0, A1);
   const double lmax = 2.0 * wmax * wmax, rmax = maxr * A2 * A2;
-  if (!(lmax < 1e36 && rmax < 1e36 && a1 < 1e36 && a0 < 1e36)) a0 = __builtin_inff();
 #pragma unroll
   for (int j = 0; j < 9; ++j) c[j] = (float)H[j];
   c[9] = __double2float_ru(a0);
-  c[10] = __double2float_ru(a1);
-  c[11] = __double2float_ru(a2);
+  c[10] = __double2float_ru(a2);
+  c[11] = 0.0f;
+  if (!(lmax < 1e36 && rmax < 1e36 && a2 < 1e30 && a0 < 1e36)) {
+    // fp32 evaluation unsafe: Q = 0, mg = 1 marks every point undecided, so
+    // every point takes the exact test.
+#pragma unroll
+    for (int j = 0; j < 9; ++j) c[j] = 0.0f;
+    c[9] = 1.0f;
+    c[10] = 0.0f;
+  }
 }
 
 // Lanes of point slot p (point base + 64 p + lane) that hold a point.
@@ -363,85 +380,268 @@ __device__ __forceinline__ uint64_t slot_mask(int n, int base, int p) {
 }
 
 struct HFilt {
-  f32x2 h0, h1, h2, h3, h4, h5, h6, h7, h8, a0, a1, a2, mr;
+  float h0, h1, h2, h3, h4, h5, h6, h7, h8, a0, a2, mr;
 };
 
-// Filter decisions for one packed pair of points: in = surely an inlier,
-// mb = possibly an inlier (in implies mb).
+// Filter quantities of one packed pair of points: surely inside iff
+// diff <= -mg, undecided iff |diff| <= mg, surely outside otherwise.
 __device__ __forceinline__ void h_filter_pair(const HFilt& f, f32x2 s0, f32x2 s1, f32x2 d0,
-                                              f32x2 d1, bool* in, bool* mb) {
-  const f32x2 q0 = __builtin_elementwise_fma(f.h0, s0, __builtin_elementwise_fma(f.h1, s1, f.h2));
-  const f32x2 q1 = __builtin_elementwise_fma(f.h3, s0, __builtin_elementwise_fma(f.h4, s1, f.h5));
-  const f32x2 q2 = __builtin_elementwise_fma(f.h6, s0, __builtin_elementwise_fma(f.h7, s1, f.h8));
+                                              f32x2 d1, f32x2* diff, f32x2* mg) {
+  const f32x2 q0 = __builtin_elementwise_fma(f32x2(f.h0), s0,
+                                             __builtin_elementwise_fma(f32x2(f.h1), s1, f32x2(f.h2)));
+  const f32x2 q1 = __builtin_elementwise_fma(f32x2(f.h3), s0,
+                                             __builtin_elementwise_fma(f32x2(f.h4), s1, f32x2(f.h5)));
+  const f32x2 q2 = __builtin_elementwise_fma(f32x2(f.h6), s0,
+                                             __builtin_elementwise_fma(f32x2(f.h7), s1, f32x2(f.h8)));
   const f32x2 w0 = __builtin_elementwise_fma(d0, q2, -q0);
   const f32x2 w1 = __builtin_elementwise_fma(d1, q2, -q1);
   const f32x2 lhs = __builtin_elementwise_fma(w0, w0, w1 * w1);
-  const f32x2 rhs = f.mr * (q2 * q2);
-  const f32x2 mg = __builtin_elementwise_fma(f.a1, __builtin_elementwise_abs(q2),
-                                             __builtin_elementwise_fma(f.a2, rhs, f.a0));
-  const f32x2 hi = lhs + mg, lo = lhs - mg;
-  in[0] = hi.x <= rhs.x;
-  in[1] = hi.y <= rhs.y;
-  mb[0] = !(lo.x > rhs.x);
-  mb[1] = !(lo.y > rhs.y);
+  const f32x2 rhs = f32x2(f.mr) * (q2 * q2);
+  *mg = __builtin_elementwise_fma(f32x2(f.a2), rhs, f32x2(f.a0));
+  *diff = lhs - rhs;
 }
 
-// Inlier count of the model whose filter constants are in lane t's hc[] over
-// the points [base, base + 64 PCH) (point base + 64 p + lane in slot p),
-// with the exact fp64 transfer-error test for the undecided points.
-template <int PCH>
-__device__ __forceinline__ int score_h_chunk(const float* hc, const double* mh,
-                                             const f32x2* s0, const f32x2* s1, const f32x2* d0,
-                                             const f32x2* d1, int n, int base, const double* xy1,
-                                             const double* xy2, float maxrf, double maxr) {
-  // hc: this hypothesis' 12 constants in LDS (same address in every lane:
-  // a broadcast read); mh: its fp64 model (global, only read when needed).
+// Exact fp64 test (HomographyMatrixEstimator::Residuals) of the undecided
+// points of one packed slot pair; the fp32 coordinates widen exactly to the
+// doubles the reference uses.
+__device__ __forceinline__ int h_exact_pair(const double* mk, const HFilt& f, f32x2 s0, f32x2 s1,
+                                            f32x2 d0, f32x2 d1, uint64_t ok0, uint64_t ok1,
+                                            double maxr) {
+  f32x2 diff, mg;
+  h_filter_pair(f, s0, s1, d0, d1, &diff, &mg);
+  const bool u0 = fabsf(diff.x) <= mg.x, u1 = fabsf(diff.y) <= mg.y;
+  int cnt = 0;
+  if (__ballot(u0) & ok0) {
+    const bool e = u0 && homography_sq(mk, (double)s0.x, (double)s1.x, (double)d0.x,
+                                       (double)d1.x) <= maxr;
+    cnt += __popcll(__ballot(e) & ok0);
+  }
+  if (__ballot(u1) & ok1) {
+    const bool e = u1 && homography_sq(mk, (double)s0.y, (double)s1.y, (double)d0.y,
+                                       (double)d1.y) <= maxr;
+    cnt += __popcll(__ballot(e) & ok1);
+  }
+  return cnt;
+}
+
+__device__ __forceinline__ float uniform_f(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+
+// The hypothesis' constants (LDS, broadcast read) moved to scalar registers.
+__device__ __forceinline__ HFilt h_filter_load(const float* hc, float maxrf) {
   const float4 c0 = reinterpret_cast<const float4*>(hc)[0];
   const float4 c1 = reinterpret_cast<const float4*>(hc)[1];
   const float4 c2 = reinterpret_cast<const float4*>(hc)[2];
   HFilt f;
-  f.h0 = c0.x;
-  f.h1 = c0.y;
-  f.h2 = c0.z;
-  f.h3 = c0.w;
-  f.h4 = c1.x;
-  f.h5 = c1.y;
-  f.h6 = c1.z;
-  f.h7 = c1.w;
-  f.h8 = c2.x;
-  f.a0 = c2.y;
-  f.a1 = c2.z;
-  f.a2 = c2.w;
+  f.h0 = uniform_f(c0.x);
+  f.h1 = uniform_f(c0.y);
+  f.h2 = uniform_f(c0.z);
+  f.h3 = uniform_f(c0.w);
+  f.h4 = uniform_f(c1.x);
+  f.h5 = uniform_f(c1.y);
+  f.h6 = uniform_f(c1.z);
+  f.h7 = uniform_f(c1.w);
+  f.h8 = uniform_f(c2.x);
+  f.a0 = uniform_f(c2.y);
+  f.a2 = uniform_f(c2.z);
   f.mr = maxrf;
+  return f;
+}
+
+// Inlier count of one hypothesis (filter f, fp64 model mk in global memory) over the
+// points [base, base + 64 PCH) (point base + 64 p + lane in slot p; FULL:
+// every slot holds a point).
+template <int PCH, bool FULL>
+__device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, const f32x2* s0,
+                                             const f32x2* s1, const f32x2* d0, const f32x2* d1,
+                                             int n, int base, double maxr, int* nslow) {
   int cnt = 0;
   uint64_t any = 0;
 #pragma unroll
   for (int q = 0; q < PCH / 2; ++q) {
-    bool in[2], mb[2];
-    h_filter_pair(f, s0[q], s1[q], d0[q], d1[q], in, mb);
-    const uint64_t ok0 = slot_mask(n, base, 2 * q), ok1 = slot_mask(n, base, 2 * q + 1);
-    const uint64_t i0 = __ballot(in[0]) & ok0, i1 = __ballot(in[1]) & ok1;
-    cnt += __popcll(i0) + __popcll(i1);
-    any |= ((__ballot(mb[0]) & ~i0) & ok0) | ((__ballot(mb[1]) & ~i1) & ok1);
-  }
-  if (any) {  // rare: exact fp64 test (HomographyMatrixEstimator::Residuals)
-    double mk[9];
-#pragma unroll
-    for (int j = 0; j < 9; ++j) mk[j] = mh[j];
-    const int lane = threadIdx.x;
-#pragma unroll
-    for (int q = 0; q < PCH / 2; ++q) {
-      bool in[2], mb[2];
-      h_filter_pair(f, s0[q], s1[q], d0[q], d1[q], in, mb);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int i = base + (2 * q + h) * 64 + lane;
-        bool e = false;
-        if (i < n && mb[h] && !in[h])
-          e = homography_sq(mk, xy1[2 * i], xy1[2 * i + 1], xy2[2 * i], xy2[2 * i + 1]) <= maxr;
-        cnt += __popcll(__ballot(e));
-      }
+    f32x2 diff, mg;
+    h_filter_pair(f, s0[q], s1[q], d0[q], d1[q], &diff, &mg);
+    uint64_t i0 = __ballot(diff.x <= -mg.x), i1 = __ballot(diff.y <= -mg.y);
+    uint64_t u0 = __ballot(fabsf(diff.x) <= mg.x), u1 = __ballot(fabsf(diff.y) <= mg.y);
+    if (!FULL) {
+      const uint64_t ok0 = slot_mask(n, base, 2 * q), ok1 = slot_mask(n, base, 2 * q + 1);
+      i0 &= ok0;
+      i1 &= ok1;
+      u0 &= ok0;
+      u1 &= ok1;
     }
+    cnt += __popcll(i0) + __popcll(i1);
+    any |= u0 | u1;
+  }
+  if (any) {  // rare: exact test of the undecided points, slot pair by slot pair
+    ++*nslow;
+    asm volatile("" ::: "memory");
+    double m[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) m[j] = mk[j];
+#pragma unroll
+    for (int q = 0; q < PCH / 2; ++q)
+      cnt += h_exact_pair(m, f, s0[q], s1[q], d0[q], d1[q],
+                          FULL ? ~0ull : slot_mask(n, base, 2 * q),
+                          FULL ? ~0ull : slot_mask(n, base, 2 * q + 1), maxr);
+  }
+  return cnt;
+}
+
+// ---------------------------------------------------------------------------
+// Packed-fp32 Sampson inlier filter (FundamentalMatrix*Estimator::Residuals,
+// SURVEY.md §8a a12) with exact fp64 fallback.  With U = F x1 (rows 0..2),
+// V = F^T x2 (rows 0, 1), e = x2^T F x1, the reference tests
+// e^2 / (U0^2 + U1^2 + V0^2 + V1^2) <= maxr, i.e. E^2 <= maxr D on exact
+// values up to its own fp64 rounding.  In fp32 (u = 2^-24, explicit FMAs):
+//   |U_i - U~_i| <= 3u A_i = al_i, A_i = (|F_i0| + |F_i1|) S + |F_i2|,
+//   |V_j - V~_j| <= 3u B_j = be_j, B_j = (|F_0j| + |F_1j|) S + |F_2j|,
+//   |e - E| <= g = S (al_0 + al_1) + al_2 + 2.01u (S (A_0 + A_1) + A_2),
+// so |num - E^2| <= 2 g |E| + g^2 + u num and, with d = max(al_0, al_1,
+// be_0, be_1) and |U0| + |U1| + |V0| + |V1| <= 2 sqrt(D),
+// |den - D| <= 4 d sqrt(D) + 2 d^2 + 4u den.  At the threshold |E| =
+// sqrt(maxr D), and sqrt(D) <= (D / tau + tau) / 2 for any tau > 0 (tau =
+// sqrt(den) at the image middle), so the decision is certain whenever
+// |num - maxr den| > a1 maxr den + a0 with
+//   c1 = 2 g sqrt(maxr) + 4 d maxr, c0 = g^2 + 2 maxr d^2,
+//   a1 = 1.01 c1 / (2 tau maxr) + 5.1u, a0 = c1 tau / 2 + c0   (x 1.5).
+// ---------------------------------------------------------------------------
+struct FFilt {
+  float f0, f1, f2, f3, f4, f5, f6, f7, f8, a0, a1, mr;
+};
+
+__device__ __forceinline__ void f_filter_consts(const double* F, double S, double maxr,
+                                                float* c) {
+  const double u = 0x1p-24;
+  const double A0 = (fabs(F[0]) + fabs(F[1])) * S + fabs(F[2]);
+  const double A1 = (fabs(F[3]) + fabs(F[4])) * S + fabs(F[5]);
+  const double A2 = (fabs(F[6]) + fabs(F[7])) * S + fabs(F[8]);
+  const double B0 = (fabs(F[0]) + fabs(F[3])) * S + fabs(F[6]);
+  const double B1 = (fabs(F[1]) + fabs(F[4])) * S + fabs(F[7]);
+  const double al0 = 3.01 * u * A0, al1 = 3.01 * u * A1, al2 = 3.01 * u * A2;
+  const double be0 = 3.01 * u * B0, be1 = 3.01 * u * B1;
+  const double g = S * (al0 + al1) + al2 + 2.01 * u * (S * (A0 + A1) + A2);
+  const double d = fmax(fmax(al0, al1), fmax(be0, be1));
+  const double sq = sqrt(maxr);
+  const double c1 = 2.0 * g * sq + 4.0 * d * maxr;
+  const double c0 = g * g + 2.0 * maxr * d * d;
+  const double h = 0.5 * S;
+  const double m0 = F[0] * h + F[1] * h + F[2], m1 = F[3] * h + F[4] * h + F[5];
+  const double n0 = F[0] * h + F[3] * h + F[6], n1 = F[1] * h + F[4] * h + F[7];
+  double tau = sqrt(m0 * m0 + m1 * m1 + n0 * n0 + n1 * n1);
+  const double tmax = A0 + A1 + B0 + B1;
+  if (!(tau > 1e-30 && tau < 1e30)) tau = tmax > 1e-30 ? tmax : 1e-30;
+  const double a1 = 1.5 * (1.01 * c1 / (2.0 * tau * maxr) + 5.1 * u);
+  const double a0 = 1.5 * (0.5 * c1 * tau + c0) + 1e-30;
+  const double emax = S * (A0 + A1) + A2;
+  const double dmax = A0 * A0 + A1 * A1 + B0 * B0 + B1 * B1;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) c[j] = (float)F[j];
+  c[9] = __double2float_ru(a0);
+  c[10] = __double2float_ru(a1);
+  c[11] = 0.0f;
+  if (!(emax * emax < 1e36 && maxr * dmax < 1e36 && a1 < 1e30 && a0 < 1e36)) {
+    // fp32 evaluation unsafe: num = den = 0, margin 1 -> every point undecided.
+#pragma unroll
+    for (int j = 0; j < 9; ++j) c[j] = 0.0f;
+    c[9] = 1.0f;
+    c[10] = 0.0f;
+  }
+}
+
+__device__ __forceinline__ FFilt f_filter_load(const float* fc, float maxrf) {
+  const float4 c0 = reinterpret_cast<const float4*>(fc)[0];
+  const float4 c1 = reinterpret_cast<const float4*>(fc)[1];
+  const float4 c2 = reinterpret_cast<const float4*>(fc)[2];
+  FFilt f;
+  f.f0 = uniform_f(c0.x);
+  f.f1 = uniform_f(c0.y);
+  f.f2 = uniform_f(c0.z);
+  f.f3 = uniform_f(c0.w);
+  f.f4 = uniform_f(c1.x);
+  f.f5 = uniform_f(c1.y);
+  f.f6 = uniform_f(c1.z);
+  f.f7 = uniform_f(c1.w);
+  f.f8 = uniform_f(c2.x);
+  f.a0 = uniform_f(c2.y);
+  f.a1 = uniform_f(c2.z);
+  f.mr = maxrf;
+  return f;
+}
+
+// diff = num - maxr den, mg = decision margin (see above).
+__device__ __forceinline__ void f_filter_pair(const FFilt& f, f32x2 x0, f32x2 x1, f32x2 y0,
+                                              f32x2 y1, f32x2* diff, f32x2* mg) {
+  typedef f32x2 V;
+  const V U0 = __builtin_elementwise_fma(V(f.f0), x0, __builtin_elementwise_fma(V(f.f1), x1, V(f.f2)));
+  const V U1 = __builtin_elementwise_fma(V(f.f3), x0, __builtin_elementwise_fma(V(f.f4), x1, V(f.f5)));
+  const V U2 = __builtin_elementwise_fma(V(f.f6), x0, __builtin_elementwise_fma(V(f.f7), x1, V(f.f8)));
+  const V V0 = __builtin_elementwise_fma(V(f.f0), y0, __builtin_elementwise_fma(V(f.f3), y1, V(f.f6)));
+  const V V1 = __builtin_elementwise_fma(V(f.f1), y0, __builtin_elementwise_fma(V(f.f4), y1, V(f.f7)));
+  const V e = __builtin_elementwise_fma(y0, U0, __builtin_elementwise_fma(y1, U1, U2));
+  const V den = __builtin_elementwise_fma(
+      U0, U0, __builtin_elementwise_fma(U1, U1, __builtin_elementwise_fma(V0, V0, V1 * V1)));
+  const V rhs = V(f.mr) * den;
+  *mg = __builtin_elementwise_fma(V(f.a1), rhs, V(f.a0));
+  *diff = __builtin_elementwise_fma(e, e, -rhs);
+}
+
+__device__ __forceinline__ int f_exact_pair(const double* mk, const FFilt& f, f32x2 x0, f32x2 x1,
+                                            f32x2 y0, f32x2 y1, uint64_t ok0, uint64_t ok1,
+                                            double maxr) {
+  f32x2 diff, mg;
+  f_filter_pair(f, x0, x1, y0, y1, &diff, &mg);
+  const bool u0 = fabsf(diff.x) <= mg.x, u1 = fabsf(diff.y) <= mg.y;
+  int cnt = 0;
+  if (__ballot(u0) & ok0) {
+    const bool e = u0 && sampson_sq(mk, (double)x0.x, (double)x1.x, (double)y0.x,
+                                    (double)y1.x) <= maxr;
+    cnt += __popcll(__ballot(e) & ok0);
+  }
+  if (__ballot(u1) & ok1) {
+    const bool e = u1 && sampson_sq(mk, (double)x0.y, (double)x1.y, (double)y0.y,
+                                    (double)y1.y) <= maxr;
+    cnt += __popcll(__ballot(e) & ok1);
+  }
+  return cnt;
+}
+
+// Inlier count of one 7-point model (filter f; fp64 model mk in global
+// memory, read only for undecided points) over one chunk of points.
+template <int PCH, bool FULL>
+__device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, const f32x2* x0,
+                                             const f32x2* x1, const f32x2* y0, const f32x2* y1,
+                                             int n, int base, double maxr, int* nslow) {
+  int cnt = 0;
+  uint64_t any = 0;
+#pragma unroll
+  for (int q = 0; q < PCH / 2; ++q) {
+    f32x2 diff, mg;
+    f_filter_pair(f, x0[q], x1[q], y0[q], y1[q], &diff, &mg);
+    uint64_t i0 = __ballot(diff.x < -mg.x), i1 = __ballot(diff.y < -mg.y);
+    uint64_t u0 = __ballot(fabsf(diff.x) <= mg.x), u1 = __ballot(fabsf(diff.y) <= mg.y);
+    if (!FULL) {
+      const uint64_t ok0 = slot_mask(n, base, 2 * q), ok1 = slot_mask(n, base, 2 * q + 1);
+      i0 &= ok0;
+      i1 &= ok1;
+      u0 &= ok0;
+      u1 &= ok1;
+    }
+    cnt += __popcll(i0) + __popcll(i1);
+    any |= u0 | u1;
+  }
+  if (any) {
+    ++*nslow;
+    asm volatile("" ::: "memory");
+    double m[9];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) m[j] = mk[j];
+#pragma unroll
+    for (int q = 0; q < PCH / 2; ++q)
+      cnt += f_exact_pair(m, f, x0[q], x1[q], y0[q], y1[q],
+                          FULL ? ~0ull : slot_mask(n, base, 2 * q),
+                          FULL ? ~0ull : slot_mask(n, base, 2 * q + 1), maxr);
   }
   return cnt;
 }
@@ -593,6 +793,51 @@ __device__ void normalize_pair_wave(const double* xy1, const double* xy2, int n,
 // Local (least-squares) estimators on n gathered inliers (geom_solvers.h
 // fundamental_8pt / homography_dlt n > 4 / translation_estimate); every lane
 // returns the model.
+// One third (15 packed entries) of the normal equations A^T A of the local
+// estimators, summed in canonical order into s.ata.
+template <int K, int PASS>
+__device__ __forceinline__ void ata_pass_wave(VerifyLds& s, const double* xin1,
+                                                        const double* xin2, int n,
+                                                        const double* T1, const double* T2) {
+  const int lane = threadIdx.x;
+  double part[15];
+#pragma unroll
+  for (int k = 0; k < 15; ++k) part[k] = kCanonZero;
+#pragma unroll 1
+  for (int i = lane; i < n; i += 64) {
+    double x0, y0, x1, y1;
+    apply_normalize(T1, xin1[2 * i], xin1[2 * i + 1], &x0, &y0);
+    apply_normalize(T2, xin2[2 * i], xin2[2 * i + 1], &x1, &y1);
+    double a[9], b[9];
+    if (K == KIND_F) f_row(x0, y0, x1, y1, a);
+    else h_rows(x0, y0, x1, y1, a, b);
+    int k = 0;
+#pragma unroll
+    for (int p = 0; p < 9; ++p)
+#pragma unroll
+      for (int q = p; q < 9; ++q) {
+        if (k >= 15 * PASS && k < 15 * PASS + 15) part[k - 15 * PASS] = part[k - 15 * PASS] + a[p] * a[q];
+        ++k;
+      }
+    if (K == KIND_H) {
+      k = 0;
+#pragma unroll
+      for (int p = 0; p < 9; ++p)
+#pragma unroll
+        for (int q = p; q < 9; ++q) {
+          if (k >= 15 * PASS && k < 15 * PASS + 15)
+            part[k - 15 * PASS] = part[k - 15 * PASS] + b[p] * b[q];
+          ++k;
+        }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 15; ++k) {
+    const double t = canon_tree_wave(part[k]);
+    if (lane == 0) s.ata[15 * PASS + k] = t;
+  }
+}
+
 template <int K>
 __device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const double* xin2, int n,
                                     double* model) {
@@ -615,47 +860,9 @@ __device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const doub
   normalize_pair_wave(xin1, xin2, n, T1, T2);
   // A^T A in canonical order, 15 packed entries per pass (register budget);
   // every entry accumulates exactly the terms of ata_accumulate in order.
-#pragma unroll
-  for (int pass = 0; pass < 3; ++pass) {
-    double part[15];
-#pragma unroll
-    for (int k = 0; k < 15; ++k) part[k] = kCanonZero;
-    for (int i = lane; i < n; i += 64) {
-      double x0, y0, x1, y1;
-      apply_normalize(T1, xin1[2 * i], xin1[2 * i + 1], &x0, &y0);
-      apply_normalize(T2, xin2[2 * i], xin2[2 * i + 1], &x1, &y1);
-      double a[9], b[9];
-      if (K == KIND_F) f_row(x0, y0, x1, y1, a);
-      else h_rows(x0, y0, x1, y1, a, b);
-      int k = 0;
-#pragma unroll
-      for (int p = 0; p < 9; ++p)
-#pragma unroll
-        for (int q = p; q < 9; ++q) {
-          if (k >= 15 * pass && k < 15 * pass + 15) {
-            double v = part[k - 15 * pass] + a[p] * a[q];
-            part[k - 15 * pass] = v;
-          }
-          ++k;
-        }
-      if (K == KIND_H) {
-        k = 0;
-#pragma unroll
-        for (int p = 0; p < 9; ++p)
-#pragma unroll
-          for (int q = p; q < 9; ++q) {
-            if (k >= 15 * pass && k < 15 * pass + 15)
-              part[k - 15 * pass] = part[k - 15 * pass] + b[p] * b[q];
-            ++k;
-          }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < 15; ++k) {
-      const double t = canon_tree_wave(part[k]);
-      if (lane == 0) s.ata[15 * pass + k] = t;
-    }
-  }
+  ata_pass_wave<K, 0>(s, xin1, xin2, n, T1, T2);
+  ata_pass_wave<K, 1>(s, xin1, xin2, n, T1, T2);
+  ata_pass_wave<K, 2>(s, xin1, xin2, n, T1, T2);
   wsync();
   double f[9];
   jacobi9_wave(s.ata, s.jA, s.jV, f);
@@ -771,12 +978,63 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
     // -- score: every lane reloads its own trial's models into registers; the
     //    points are streamed once in register chunks and each model is
     //    broadcast with v_readlane; exact inlier counts via ballot.
-    if (K == KIND_H && xyf != nullptr) {
+    if constexpr (K == KIND_F) {
+      // Packed-fp32 Sampson filter with exact fp64 fallback (f_filter_consts);
+      // up to 3 models per trial, constants broadcast from LDS.
+      if (lane < B) {
+        const int nm = s.nmodels[lane];
+        for (int k = 0; k < nm; ++k)
+          f_filter_consts(mbuf + (lane * MM + k) * MS, S, maxr, &s.fcs[lane * MM + k][0]);
+      }
+      wsync();
+      const float maxrf = (float)maxr;
+      int nslow = 0;
+      uint32_t cnt0 = 0, cnt1 = 0, cnt2 = 0;  // lane t: counts of trial t's models
+      constexpr int PCH = 8;
+      for (int base = 0; base < n; base += 64 * PCH) {
+        f32x2 x0[PCH / 2], x1[PCH / 2], y0[PCH / 2], y1[PCH / 2];
+#pragma unroll
+        for (int q = 0; q < PCH / 2; ++q) {
+          const int i0 = base + (2 * q) * 64 + lane, i1 = i0 + 64;
+          const float4 v0 = i0 < n ? xyf[i0] : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 v1 = i1 < n ? xyf[i1] : make_float4(0.f, 0.f, 0.f, 0.f);
+          x0[q] = f32x2{v0.x, v1.x};
+          x1[q] = f32x2{v0.y, v1.y};
+          y0[q] = f32x2{v0.z, v1.z};
+          y1[q] = f32x2{v0.w, v1.w};
+        }
+        const bool full = base + 64 * PCH <= n;
+        for (int t = 0; t < B; ++t) {
+          const int nmt = __builtin_amdgcn_readfirstlane(s.nmodels[t]);
+          for (int k = 0; k < nmt; ++k) {
+            const FFilt f = f_filter_load(&s.fcs[t * MM + k][0], maxrf);
+            const double* mk = mbuf + (t * MM + k) * MS;
+            const int c = full ? score_f_chunk<PCH, true>(f, mk, x0, x1, y0, y1, n, base, maxr,
+                                                          &nslow)
+                               : score_f_chunk<PCH, false>(f, mk, x0, x1, y0, y1, n, base, maxr,
+                                                           &nslow);
+            const uint32_t add = (lane == t) ? (uint32_t)c : 0u;
+            if (k == 0) cnt0 += add;
+            else if (k == 1) cnt1 += add;
+            else cnt2 += add;
+          }
+        }
+      }
+      if (lane < B) {
+        s.counts[lane * MM] = cnt0;
+        s.counts[lane * MM + 1] = cnt1;
+        s.counts[lane * MM + 2] = cnt2;
+      }
+      pf.count(PR_N_HCHUNK, (uint64_t)B * (uint64_t)((n + 64 * PCH - 1) / (64 * PCH)));
+      pf.count(PR_N_HSLOW, (uint64_t)nslow);
+    } else if constexpr (K == KIND_H) {
       // Packed-fp32 filter with exact fp64 fallback (h_filter_consts); the
       // hypotheses' constants are broadcast from LDS.
       if (lane < B) h_filter_consts(mbuf + lane * (MM * MS), S, maxr, &s.hcs[lane][0]);
       wsync();
       const float maxrf = (float)maxr;
+      int nslow = 0;
+      uint32_t cnt_lane = 0;  // lane t accumulates hypothesis t's inlier count
       constexpr int PCH = 8;
       for (int base = 0; base < n; base += 64 * PCH) {
         f32x2 s0[PCH / 2], s1[PCH / 2], d0[PCH / 2], d1[PCH / 2];
@@ -790,12 +1048,19 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
           d0[q] = f32x2{v0.z, v1.z};
           d1[q] = f32x2{v0.w, v1.w};
         }
+        const bool full = base + 64 * PCH <= n;
         for (int t = 0; t < B; ++t) {
-          const int c = score_h_chunk<PCH>(&s.hcs[t][0], mbuf + t * (MM * MS), s0, s1, d0, d1,
-                                           n, base, xy1, xy2, maxrf, maxr);
-          if (lane == 0) s.counts[t] += (uint32_t)c;
+          const HFilt f = h_filter_load(&s.hcs[t][0], maxrf);
+          const int c = full ? score_h_chunk<PCH, true>(f, mbuf + t * (MM * MS), s0, s1, d0, d1, n, base,
+                                                        maxr, &nslow)
+                             : score_h_chunk<PCH, false>(f, mbuf + t * (MM * MS), s0, s1, d0, d1, n,
+                                                         base, maxr, &nslow);
+          cnt_lane += (lane == t) ? (uint32_t)c : 0u;
         }
       }
+      if (lane < B) s.counts[lane] = cnt_lane;
+      pf.count(PR_N_HCHUNK, (uint64_t)B * (uint64_t)((n + 64 * PCH - 1) / (64 * PCH)));
+      pf.count(PR_N_HSLOW, (uint64_t)nslow);
     } else {
     double m[MM][MS];
     int nm = 0;
@@ -1011,18 +1276,19 @@ __device__ __forceinline__ void mt_load(VerifyLds& s, const uint32_t* st) {
   wsync();
 }
 
-__global__ __launch_bounds__(kVerifyThreads) void verify_f_kernel(
+__global__ __launch_bounds__(kVerifyThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void verify_f_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
     const double* __restrict__ xy2_all, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, uint8_t* __restrict__ masks, VerifyOut* __restrict__ out,
-    VerifyParams P, uint64_t* __restrict__ prof, const int32_t* __restrict__ counts) {
+    VerifyParams P, uint64_t* __restrict__ prof, const int32_t* __restrict__ counts,
+    const float4* __restrict__ xyf_all) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
-  uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
   Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
   pf.start();
   const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
   const int n = ps.n, lane = threadIdx.x;
+  uint16_t* sidx = reinterpret_cast<uint16_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
   uint8_t* mask = masks + ps.pp.mask_off;
   for (int i = lane; i < n; i += 64) mask[i] = 0;
   if (!(n >= P.min_num_inliers && n > 0)) return;
@@ -1030,11 +1296,19 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_f_kernel(
   const double* xy2 = xy2_all + ps.pp.pts_off;
   double* res0 = ps.base;
   double* res1 = ps.base + n;
+  const float4* xyf = xyf_all + ps.pp.pts_off / 2;
+  float smax = 0.0f;
+  for (int i = lane; i < n; i += 64) {
+    const float4 v = xyf[i];
+    smax = fmaxf(smax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) smax = fmaxf(smax, __shfl_xor(smax, d));
   if (lane == 0) mt_seed(s, pair_seed(P.base_seed, ps.pp.id1, ps.pp.id2));
   wsync();
   const RansacResult rf = loransac_wave<KIND_F>(s, sidx, xy1, xy2, n, P.max_trials_F, P, res0,
                                                 res1, ps.base + 2 * n, ps.base + 4 * n, ps.snap,
-                                                ps.base + 10 * n, pf);
+                                                ps.base + 10 * n, pf, xyf, (double)smax);
   // F inlier mask (the input of ExtractInlierMatches).
   const double* resF = rf.res_sel ? res1 : res0;
   if (rf.success)
@@ -1055,11 +1329,11 @@ __global__ __launch_bounds__(kVerifyThreads) __attribute__((amdgpu_waves_per_eu(
     const float4* __restrict__ xyf_all) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
-  uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
   Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
   pf.start();
   const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
   const int n = ps.n, lane = threadIdx.x;
+  uint16_t* sidx = reinterpret_cast<uint16_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
   if (!(n >= P.min_num_inliers && n > 0)) return;
   const double* xy1 = xy1_all + ps.pp.pts_off;
   const double* xy2 = xy2_all + ps.pp.pts_off;
@@ -1092,11 +1366,11 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
     const int32_t* __restrict__ counts) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
-  uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
   Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
   pf.start();
   const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
   const int n = ps.n, lane = threadIdx.x;
+  uint16_t* sidx = reinterpret_cast<uint16_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
   if (!(n >= P.min_num_inliers && n > 0)) return;
   const double* xy1 = xy1_all + ps.pp.pts_off;
   const double* xy2 = xy2_all + ps.pp.pts_off;
@@ -1207,8 +1481,11 @@ __global__ void compact_kernel(const int32_t* __restrict__ counts, const int64_t
   }
 }
 
+static_assert(sizeof(VerifyLds) <= 20 * 1024, "VerifyLds must allow 8 pairs per CU");
+
 size_t verify_lds_bytes(int max_m) {
-  return sizeof(VerifyLds) + (size_t)((max_m + 7) / 8 * 8) * sizeof(uint16_t);
+  (void)max_m;
+  return sizeof(VerifyLds);
 }
 
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
@@ -1225,7 +1502,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     attr = true;
   }
   hipLaunchKernelGGL(verify_f_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
-                     xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
+                     xy1, xy2, scratch, snaps, masks, out, params, prof, counts, xyf);
   hipLaunchKernelGGL(verify_h_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
                      xy1, xy2, scratch, snaps, out, params, prof, counts, xyf);
   hipLaunchKernelGGL(verify_final_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
