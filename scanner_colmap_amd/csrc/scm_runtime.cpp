@@ -89,7 +89,8 @@ struct PinnedOut {
 // One in-flight batch: device workspace, descriptor staging, results.
 struct BatchSet {
   DevBuf jobs, pairs, rowres, colpart, m21, matches, counts, gpairs, vpairs, xy1, xy2, scratch,
-      snaps, masks, offsets, match_off, prof, xyf, dvout, dpack, dpmask;
+      snaps, masks, offsets, match_off, prof, xyf, dvout, dpack, dpmask, rst, samp, nmod, fcon,
+      cnts, act, nact, mods, wsnap;
   HostBuf stage, vstage;
   PinnedOut out;
   size_t off_counts = 0, off_offsets = 0, off_vout = 0, off_matches = 0, off_masks = 0;
@@ -108,7 +109,8 @@ struct BatchSet {
   void release() {
     for (DevBuf* b : {&jobs, &pairs, &rowres, &colpart, &m21, &matches, &counts, &gpairs, &vpairs,
                       &xy1, &xy2, &scratch, &snaps, &masks, &offsets, &match_off, &prof, &xyf, &dvout,
-                      &dpack, &dpmask})
+                      &dpack, &dpmask, &rst, &samp, &nmod, &fcon, &cnts, &act, &nact,
+                      &mods, &wsnap})
       b->release();
     stage.release();
     vstage.release();
@@ -540,10 +542,30 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
     }
     bs.nprof = V;
     SCM_HIP(hipEventRecord(bs.ev[4], sv));
+    SCM_TRY(bs.rst.ensure(V * sizeof(RansacState)));
+    SCM_TRY(bs.samp.ensure(V * kWindowTrials * 8 * sizeof(uint16_t)));
+    SCM_TRY(bs.nmod.ensure(V * kWindowTrials * sizeof(int32_t)));
+    SCM_TRY(bs.fcon.ensure(V * kWindowTrials * 3 * 12 * sizeof(float)));
+    SCM_TRY(bs.mods.ensure(V * kWindowTrials * 3 * 9 * sizeof(double)));
+    SCM_TRY(bs.cnts.ensure(V * kWindowTrials * 3 * sizeof(uint32_t)));
+    SCM_TRY(bs.wsnap.ensure(V * kMaxWindow * 640 * sizeof(uint32_t)));
+    SCM_TRY(bs.act.ensure(2 * V * sizeof(int32_t)));
+    SCM_TRY(bs.nact.ensure(2 * sizeof(int32_t)));
+    VerifyRoundBufs rb;
+    rb.rst = bs.rst.as<RansacState>();
+    rb.samp = bs.samp.as<uint16_t>();
+    rb.nmod = bs.nmod.as<int32_t>();
+    rb.fcon = bs.fcon.as<float>();
+    rb.mods = bs.mods.as<double>();
+    rb.cnts = bs.cnts.as<uint32_t>();
+    rb.wsnap = bs.wsnap.as<uint32_t>();
+    rb.act[0] = bs.act.as<int32_t>();
+    rb.act[1] = bs.act.as<int32_t>() + V;
+    rb.nact = bs.nact.as<int32_t>();
     SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
                           bs.xy2.as<double>(), bs.scratch.as<double>(), bs.snaps.as<uint32_t>(),
                           bs.masks.as<uint8_t>(), bs.dvout.as<VerifyOut>(),
-                          make_params(ctx->opts), prof, nullptr, bs.xyf.as<float4>(), sv));
+                          make_params(ctx->opts), prof, nullptr, bs.xyf.as<float4>(), rb, sv));
   }
   SCM_HIP(hipEventRecord(bs.ev[5], sv));
   // Compact matches + F-inlier masks in HBM, then DMA the results into the

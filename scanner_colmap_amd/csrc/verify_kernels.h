@@ -56,12 +56,43 @@ struct VerifyOut {
   double H[9];
 };
 
+// Per-pair state of the round-synchronous LO-RANSAC (verify_kernels.hip).
+struct RansacState {
+  int32_t n, done, trial, dyn_max;
+  int32_t max_trials, best_n, best_sum_valid, res_sel;
+  int32_t B, num_trials, pad_, pad2_;
+  double best_sum;
+  double S;  // max |coordinate| of the pair's points (fp32 filter bound)
+  double best_model[9];
+};
+
+// Windowed verifier: up to kMaxWindow rounds of kTrialBatch hypotheses.
+constexpr int kMaxWindow = 16;
+constexpr int kWindowTrials = kMaxWindow * kTrialBatch;
+
+// Device buffers of the windowed verifier (V = pairs of a batch, T =
+// kWindowTrials): rst[V], samp[V][T*8], nmod[V][T], fcon[V][3T][12],
+// mods[V][3T][9], cnts[V][3T], wsnap[V][kMaxWindow][640], act[2][V],
+// nact[2].
+struct VerifyRoundBufs {
+  RansacState* rst;
+  uint16_t* samp;
+  int32_t* nmod;
+  float* fcon;
+  double* mods;
+  uint32_t* cnts;
+  uint32_t* wsnap;
+  int32_t* act[2];
+  int32_t* nact;
+};
+
 // snaps: kVerifySnapWords uint32 per pair (PRNG state between the F, H and
-// watermark kernels + the per-batch snapshot for the abort rewind).
+// watermark kernels + the per-round snapshot for the abort rewind).
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
-                         const int32_t* counts, const float4* xyf, hipStream_t stream);
+                         const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb,
+                         hipStream_t stream);
 size_t verify_lds_bytes(int max_m);
 constexpr int kVerifyProfSlots = 20;
 

@@ -34,9 +34,12 @@ using namespace geom;
 enum { KIND_F = 0, KIND_H = 1, KIND_T = 2 };
 
 template <int K> struct KindTraits;
-template <> struct KindTraits<KIND_F> { static constexpr int kmin = 7, kmin_local = 8, mm = 3, ms = 9; };
-template <> struct KindTraits<KIND_H> { static constexpr int kmin = 4, kmin_local = 4, mm = 1, ms = 9; };
-template <> struct KindTraits<KIND_T> { static constexpr int kmin = 1, kmin_local = 1, mm = 1, ms = 2; };
+// tb: hypotheses per round (the F round is halved so that its fp64 models
+// fit in LDS next to their filter constants).
+constexpr int kTrialBatchF = kTrialBatch / 2;
+template <> struct KindTraits<KIND_F> { static constexpr int kmin = 7, kmin_local = 8, mm = 3, ms = 9, tb = kTrialBatch; };
+template <> struct KindTraits<KIND_H> { static constexpr int kmin = 4, kmin_local = 4, mm = 1, ms = 9, tb = kTrialBatch; };
+template <> struct KindTraits<KIND_T> { static constexpr int kmin = 1, kmin_local = 1, mm = 1, ms = 2, tb = kTrialBatch; };
 
 // Per-pair LDS (one wavefront); the sample-index vector of RandomSampler
 // (uint16, one per match) lives in the pair's global scratch so that the LDS
@@ -52,8 +55,14 @@ struct __attribute__((aligned(16))) VerifyLds {
   int32_t nmodels[kTrialBatch];
   uint16_t samples[kTrialBatch][8];
   union {
-    float hcs[kTrialBatch][12];      // homography filter constants per hypothesis
-    float fcs[kTrialBatch * 3][12];  // Sampson filter constants per 7-point model
+    struct {
+      float hcs[kTrialBatch][12];   // homography filter constants per hypothesis
+      double hmod[kTrialBatch][9];  // the hypotheses' fp64 models (exact fallback)
+    };
+    struct {
+      float fcs[kTrialBatchF * 3][12];   // Sampson filter constants per 7-point model
+      double fmod[kTrialBatchF * 3][9];  // the 7-point models (exact fallback)
+    };
   };
   uint16_t jbuf[kTrialBatch * 7];  // Shuffle targets of one batch of samples
   int32_t mt_idx;
@@ -404,6 +413,13 @@ __device__ __forceinline__ void h_filter_pair(const HFilt& f, f32x2 s0, f32x2 s1
 // Exact fp64 test (HomographyMatrixEstimator::Residuals) of the undecided
 // points of one packed slot pair; the fp32 coordinates widen exactly to the
 // doubles the reference uses.
+// Exact reference test of one point (rare path; not inlined so that its
+// fp64 registers do not add to the hot loop's budget).
+__device__ __attribute__((noinline)) bool h_exact_pt(const double* mk, float sx, float sy,
+                                                     float dx, float dy, double maxr) {
+  return homography_sq(mk, (double)sx, (double)sy, (double)dx, (double)dy) <= maxr;
+}
+
 __device__ __forceinline__ int h_exact_pair(const double* mk, const HFilt& f, f32x2 s0, f32x2 s1,
                                             f32x2 d0, f32x2 d1, uint64_t ok0, uint64_t ok1,
                                             double maxr) {
@@ -412,13 +428,13 @@ __device__ __forceinline__ int h_exact_pair(const double* mk, const HFilt& f, f3
   const bool u0 = fabsf(diff.x) <= mg.x, u1 = fabsf(diff.y) <= mg.y;
   int cnt = 0;
   if (__ballot(u0) & ok0) {
-    const bool e = u0 && homography_sq(mk, (double)s0.x, (double)s1.x, (double)d0.x,
-                                       (double)d1.x) <= maxr;
+    bool e = false;
+    if (u0) e = h_exact_pt(mk, s0.x, s1.x, d0.x, d1.x, maxr);
     cnt += __popcll(__ballot(e) & ok0);
   }
   if (__ballot(u1) & ok1) {
-    const bool e = u1 && homography_sq(mk, (double)s0.y, (double)s1.y, (double)d0.y,
-                                       (double)d1.y) <= maxr;
+    bool e = false;
+    if (u1) e = h_exact_pt(mk, s0.y, s1.y, d0.y, d1.y, maxr);
     cnt += __popcll(__ballot(e) & ok1);
   }
   return cnt;
@@ -449,7 +465,7 @@ __device__ __forceinline__ HFilt h_filter_load(const float* hc, float maxrf) {
   return f;
 }
 
-// Inlier count of one hypothesis (filter f, fp64 model mk in global memory) over the
+// Inlier count of one hypothesis (filter f, fp64 model mk in LDS) over the
 // points [base, base + 64 PCH) (point base + 64 p + lane in slot p; FULL:
 // every slot holds a point).
 template <int PCH, bool FULL>
@@ -476,13 +492,9 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
   }
   if (any) {  // rare: exact test of the undecided points, slot pair by slot pair
     ++*nslow;
-    asm volatile("" ::: "memory");
-    double m[9];
-#pragma unroll
-    for (int j = 0; j < 9; ++j) m[j] = mk[j];
 #pragma unroll
     for (int q = 0; q < PCH / 2; ++q)
-      cnt += h_exact_pair(m, f, s0[q], s1[q], d0[q], d1[q],
+      cnt += h_exact_pair(mk, f, s0[q], s1[q], d0[q], d1[q],
                           FULL ? ~0ull : slot_mask(n, base, 2 * q),
                           FULL ? ~0ull : slot_mask(n, base, 2 * q + 1), maxr);
   }
@@ -587,6 +599,11 @@ __device__ __forceinline__ void f_filter_pair(const FFilt& f, f32x2 x0, f32x2 x1
   *diff = __builtin_elementwise_fma(e, e, -rhs);
 }
 
+__device__ __attribute__((noinline)) bool f_exact_pt(const double* mk, float x0, float x1,
+                                                     float y0, float y1, double maxr) {
+  return sampson_sq(mk, (double)x0, (double)x1, (double)y0, (double)y1) <= maxr;
+}
+
 __device__ __forceinline__ int f_exact_pair(const double* mk, const FFilt& f, f32x2 x0, f32x2 x1,
                                             f32x2 y0, f32x2 y1, uint64_t ok0, uint64_t ok1,
                                             double maxr) {
@@ -595,20 +612,20 @@ __device__ __forceinline__ int f_exact_pair(const double* mk, const FFilt& f, f3
   const bool u0 = fabsf(diff.x) <= mg.x, u1 = fabsf(diff.y) <= mg.y;
   int cnt = 0;
   if (__ballot(u0) & ok0) {
-    const bool e = u0 && sampson_sq(mk, (double)x0.x, (double)x1.x, (double)y0.x,
-                                    (double)y1.x) <= maxr;
+    bool e = false;
+    if (u0) e = f_exact_pt(mk, x0.x, x1.x, y0.x, y1.x, maxr);
     cnt += __popcll(__ballot(e) & ok0);
   }
   if (__ballot(u1) & ok1) {
-    const bool e = u1 && sampson_sq(mk, (double)x0.y, (double)x1.y, (double)y0.y,
-                                    (double)y1.y) <= maxr;
+    bool e = false;
+    if (u1) e = f_exact_pt(mk, x0.y, x1.y, y0.y, y1.y, maxr);
     cnt += __popcll(__ballot(e) & ok1);
   }
   return cnt;
 }
 
-// Inlier count of one 7-point model (filter f; fp64 model mk in global
-// memory, read only for undecided points) over one chunk of points.
+// Inlier count of one 7-point model (filter f; fp64 model mk in LDS, read
+// only for undecided points) over one chunk of points.
 template <int PCH, bool FULL>
 __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, const f32x2* x0,
                                              const f32x2* x1, const f32x2* y0, const f32x2* y1,
@@ -633,13 +650,9 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
   }
   if (any) {
     ++*nslow;
-    asm volatile("" ::: "memory");
-    double m[9];
-#pragma unroll
-    for (int j = 0; j < 9; ++j) m[j] = mk[j];
 #pragma unroll
     for (int q = 0; q < PCH / 2; ++q)
-      cnt += f_exact_pair(m, f, x0[q], x1[q], y0[q], y1[q],
+      cnt += f_exact_pair(mk, f, x0[q], x1[q], y0[q], y1[q],
                           FULL ? ~0ull : slot_mask(n, base, 2 * q),
                           FULL ? ~0ull : slot_mask(n, base, 2 * q + 1), maxr);
   }
@@ -925,7 +938,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
   wsync();
 
   while (trial < max_trials && !abort) {
-    const int B = min(kTrialBatch, max_trials - trial);
+    const int B = min(Tr::tb, max_trials - trial);
     pf.lap(PR_OTHER);
     pf.count(PR_N_BATCH);
     // -- snapshot the PRNG (global), draw B samples (Shuffle of the persistent
@@ -983,8 +996,12 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
       // up to 3 models per trial, constants broadcast from LDS.
       if (lane < B) {
         const int nm = s.nmodels[lane];
-        for (int k = 0; k < nm; ++k)
-          f_filter_consts(mbuf + (lane * MM + k) * MS, S, maxr, &s.fcs[lane * MM + k][0]);
+        for (int k = 0; k < nm; ++k) {
+          const double* mf = mbuf + (lane * MM + k) * MS;
+          f_filter_consts(mf, S, maxr, &s.fcs[lane * MM + k][0]);
+#pragma unroll
+          for (int j = 0; j < 9; ++j) s.fmod[lane * MM + k][j] = mf[j];
+        }
       }
       wsync();
       const float maxrf = (float)maxr;
@@ -1008,7 +1025,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
           const int nmt = __builtin_amdgcn_readfirstlane(s.nmodels[t]);
           for (int k = 0; k < nmt; ++k) {
             const FFilt f = f_filter_load(&s.fcs[t * MM + k][0], maxrf);
-            const double* mk = mbuf + (t * MM + k) * MS;
+            const double* mk = &s.fmod[t * MM + k][0];
             const int c = full ? score_f_chunk<PCH, true>(f, mk, x0, x1, y0, y1, n, base, maxr,
                                                           &nslow)
                                : score_f_chunk<PCH, false>(f, mk, x0, x1, y0, y1, n, base, maxr,
@@ -1030,7 +1047,12 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
     } else if constexpr (K == KIND_H) {
       // Packed-fp32 filter with exact fp64 fallback (h_filter_consts); the
       // hypotheses' constants are broadcast from LDS.
-      if (lane < B) h_filter_consts(mbuf + lane * (MM * MS), S, maxr, &s.hcs[lane][0]);
+      if (lane < B) {
+        const double* mh = mbuf + lane * (MM * MS);
+        h_filter_consts(mh, S, maxr, &s.hcs[lane][0]);
+#pragma unroll
+        for (int j = 0; j < 9; ++j) s.hmod[lane][j] = mh[j];
+      }
       wsync();
       const float maxrf = (float)maxr;
       int nslow = 0;
@@ -1051,9 +1073,9 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
         const bool full = base + 64 * PCH <= n;
         for (int t = 0; t < B; ++t) {
           const HFilt f = h_filter_load(&s.hcs[t][0], maxrf);
-          const int c = full ? score_h_chunk<PCH, true>(f, mbuf + t * (MM * MS), s0, s1, d0, d1, n, base,
+          const int c = full ? score_h_chunk<PCH, true>(f, &s.hmod[t][0], s0, s1, d0, d1, n, base,
                                                         maxr, &nslow)
-                             : score_h_chunk<PCH, false>(f, mbuf + t * (MM * MS), s0, s1, d0, d1, n,
+                             : score_h_chunk<PCH, false>(f, &s.hmod[t][0], s0, s1, d0, d1, n,
                                                          base, maxr, &nslow);
           cnt_lane += (lane == t) ? (uint32_t)c : 0u;
         }
@@ -1276,88 +1298,6 @@ __device__ __forceinline__ void mt_load(VerifyLds& s, const uint32_t* st) {
   wsync();
 }
 
-__global__ __launch_bounds__(kVerifyThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void verify_f_kernel(
-    const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
-    const double* __restrict__ xy2_all, double* __restrict__ scratch,
-    uint32_t* __restrict__ snaps, uint8_t* __restrict__ masks, VerifyOut* __restrict__ out,
-    VerifyParams P, uint64_t* __restrict__ prof, const int32_t* __restrict__ counts,
-    const float4* __restrict__ xyf_all) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
-  Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
-  pf.start();
-  const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
-  const int n = ps.n, lane = threadIdx.x;
-  uint16_t* sidx = reinterpret_cast<uint16_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
-  uint8_t* mask = masks + ps.pp.mask_off;
-  for (int i = lane; i < n; i += 64) mask[i] = 0;
-  if (!(n >= P.min_num_inliers && n > 0)) return;
-  const double* xy1 = xy1_all + ps.pp.pts_off;
-  const double* xy2 = xy2_all + ps.pp.pts_off;
-  double* res0 = ps.base;
-  double* res1 = ps.base + n;
-  const float4* xyf = xyf_all + ps.pp.pts_off / 2;
-  float smax = 0.0f;
-  for (int i = lane; i < n; i += 64) {
-    const float4 v = xyf[i];
-    smax = fmaxf(smax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-  }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) smax = fmaxf(smax, __shfl_xor(smax, d));
-  if (lane == 0) mt_seed(s, pair_seed(P.base_seed, ps.pp.id1, ps.pp.id2));
-  wsync();
-  const RansacResult rf = loransac_wave<KIND_F>(s, sidx, xy1, xy2, n, P.max_trials_F, P, res0,
-                                                res1, ps.base + 2 * n, ps.base + 4 * n, ps.snap,
-                                                ps.base + 10 * n, pf, xyf, (double)smax);
-  // F inlier mask (the input of ExtractInlierMatches).
-  const double* resF = rf.res_sel ? res1 : res0;
-  if (rf.success)
-    for (int i = lane; i < n; i += 64) mask[i] = resF[i] <= P.max_residual ? 1 : 0;
-  if (lane < 9) ps.o->F[lane] = s.best_model[lane];
-  if (lane == 0) {
-    ps.o->f_trials = rf.num_trials;
-    ps.o->f_inliers_raw = rf.num_inliers;
-  }
-  mt_save(s, ps.state);
-}
-
-__global__ __launch_bounds__(kVerifyThreads) __attribute__((amdgpu_waves_per_eu(2, 2))) void verify_h_kernel(
-    const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
-    const double* __restrict__ xy2_all, double* __restrict__ scratch,
-    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyParams P,
-    uint64_t* __restrict__ prof, const int32_t* __restrict__ counts,
-    const float4* __restrict__ xyf_all) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
-  Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
-  pf.start();
-  const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
-  const int n = ps.n, lane = threadIdx.x;
-  uint16_t* sidx = reinterpret_cast<uint16_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
-  if (!(n >= P.min_num_inliers && n > 0)) return;
-  const double* xy1 = xy1_all + ps.pp.pts_off;
-  const double* xy2 = xy2_all + ps.pp.pts_off;
-  const float4* xyf = xyf_all + ps.pp.pts_off / 2;
-  mt_load(s, ps.state);
-  float smax = 0.0f;
-  for (int i = lane; i < n; i += 64) {
-    const float4 v = xyf[i];
-    smax = fmaxf(smax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-  }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) smax = fmaxf(smax, __shfl_xor(smax, d));
-  const RansacResult rh = loransac_wave<KIND_H>(s, sidx, xy1, xy2, n, P.max_trials_H, P,
-                                                ps.base, ps.base + n, ps.base + 2 * n,
-                                                ps.base + 4 * n, ps.snap, ps.base + 10 * n, pf,
-                                                xyf, (double)smax);
-  if (lane < 9) ps.o->H[lane] = s.best_model[lane];
-  if (lane == 0) {
-    ps.o->h_trials = rh.num_trials;
-    ps.o->h_inliers_raw = rh.num_inliers;
-  }
-  mt_save(s, ps.state);
-}
-
 __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
     const double* __restrict__ xy2_all, double* __restrict__ scratch,
@@ -1448,6 +1388,489 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Windowed LO-RANSAC (F and H).  All pairs of a batch advance together one
+// window at a time; a window holds W rounds of up to 64 hypotheses per pair
+// (W = 1, 2, 4, 8, 16, 16, ...: most F runs stop within a round or two, the
+// long runs get wide windows):
+//   rs_sample  (one wave per pair)  RandomSampler draws + Shuffle for every
+//                                   trial of the window; the PRNG state at the
+//                                   start of each round is kept for the rewind
+//   rs_solve   (one thread per hypothesis) minimal solver + filter constants
+//   rs_score   (blocks of 256 threads over (pair, 1024-point chunk)) inlier
+//                                   counts of every model of the window
+//   rs_replay  (one wave per pair)  the sequential LO-RANSAC decisions in
+//                                   trial order (Compare, local optimisation,
+//                                   dynamic trial bound, abort + PRNG rewind)
+// Hypotheses past a pair's abort point are discarded, exactly as the serial
+// algorithm never draws them; the expensive scoring runs as a wide, regular
+// kernel and the sequential parts cost one short kernel per window.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ PairSetup pair_at(const VerifyPair* pairs, int q, double* scratch,
+                                             uint32_t* snaps, VerifyOut* out) {
+  PairSetup ps;
+  ps.pp = pairs[q];
+  ps.n = ps.pp.m;
+  ps.state = snaps + (int64_t)q * kVerifySnapWords;
+  ps.snap = ps.state + kVerifySnapWords / 2;
+  ps.base = scratch + ps.pp.scr_off;
+  ps.o = out + ps.pp.out_idx;
+  return ps;
+}
+
+__device__ __forceinline__ uint16_t* pair_sidx(const PairSetup& ps) {
+  return reinterpret_cast<uint16_t*>(ps.base + 10 * (int64_t)ps.n + kVerifyModelDoubles);
+}
+
+// Per-pair results of a finished RANSAC into the pair's VerifyOut (and, for
+// F, the inlier mask ExtractInlierMatches reads).
+template <int K>
+__device__ void rs_finish(const PairSetup& ps, const RansacState& st, uint8_t* masks,
+                          double maxr) {
+  const int lane = threadIdx.x;
+  const int n = ps.n;
+  if (K == KIND_F) {
+    uint8_t* mask = masks + ps.pp.mask_off;
+    const double* resb = ps.base + (st.res_sel ? n : 0);
+    const bool ok = st.best_n >= KindTraits<K>::kmin;
+    for (int i = lane; i < n; i += 64) mask[i] = (ok && resb[i] <= maxr) ? 1 : 0;
+    if (lane < 9) ps.o->F[lane] = st.best_model[lane];
+    if (lane == 0) {
+      ps.o->f_trials = st.num_trials;
+      ps.o->f_inliers_raw = st.best_n;
+    }
+  } else {
+    if (lane < 9) ps.o->H[lane] = st.best_model[lane];
+    if (lane == 0) {
+      ps.o->h_trials = st.num_trials;
+      ps.o->h_inliers_raw = st.best_n;
+    }
+  }
+}
+
+// Start of a RANSAC for every pair: state, sample-index vector, F seeds the
+// pair's PRNG (H continues the stream F left).  Pairs with fewer points than
+// the minimal sample finish at once (LORANSAC returns an empty report).
+template <int K>
+__global__ __launch_bounds__(64) void rs_begin_kernel(
+    const VerifyPair* __restrict__ pairs, int npairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
+    const float4* __restrict__ xyf_all, RansacState* __restrict__ rst,
+    int32_t* __restrict__ act, int32_t* __restrict__ nact, VerifyParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
+  using Tr = KindTraits<K>;
+  const int lane = threadIdx.x;
+  for (int q = blockIdx.x; q < npairs; q += gridDim.x) {
+    const PairSetup ps = pair_at(pairs, q, scratch, snaps, out);
+    const int n = ps.n;
+    const float4* xyf = xyf_all + ps.pp.pts_off / 2;
+    float smax = 0.0f;
+    for (int i = lane; i < n; i += 64) {
+      const float4 v = xyf[i];
+      smax = fmaxf(smax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) smax = fmaxf(smax, __shfl_xor(smax, d));
+    if (K == KIND_F) {
+      wsync();
+      if (lane == 0) mt_seed(s, pair_seed(P.base_seed, ps.pp.id1, ps.pp.id2));
+      wsync();
+      mt_save(s, ps.state);
+    }
+    uint16_t* sidx = pair_sidx(ps);
+    for (int i = lane; i < n; i += 64) sidx[i] = (uint16_t)i;
+    if (lane == 0) {
+      RansacState& st = rst[q];
+      st.n = n;
+      st.max_trials = K == KIND_F ? P.max_trials_F : P.max_trials_H;
+      st.trial = 0;
+      st.dyn_max = st.max_trials;
+      st.best_n = 0;
+      st.best_sum_valid = 1;
+      st.res_sel = 0;
+      st.B = 0;
+      st.num_trials = 0;
+      st.done = (n < Tr::kmin || st.max_trials <= 0) ? 1 : 0;
+      st.pad_ = 0;
+      st.best_sum = 1.7976931348623157e308;  // Support() default: DBL_MAX
+      st.S = (double)smax;
+#pragma unroll
+      for (int j = 0; j < 9; ++j) st.best_model[j] = 0.0;
+      if (!st.done) act[atomicAdd(nact, 1)] = q;
+    }
+    wsync();
+    if (rst[q].done) rs_finish<K>(ps, rst[q], masks, P.max_residual);
+  }
+}
+
+// Draws of one window: B = min(64 W, max_trials - trial) samples of kmin
+// indices (RandomSampler::Sample); the PRNG state before each round of 64 is
+// kept in wsnap for the abort rewind, the state after the window in snaps.
+template <int K>
+__global__ __launch_bounds__(64) void rs_sample_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, RansacState* __restrict__ rst,
+    const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
+    int32_t* __restrict__ nact_next, uint16_t* __restrict__ samp, uint32_t* __restrict__ cnts,
+    uint32_t* __restrict__ wsnap, int W) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
+  using Tr = KindTraits<K>;
+  const int lane = threadIdx.x;
+  if (blockIdx.x == 0 && lane == 0) *nact_next = 0;
+  const int na = *nact;
+  for (int a = blockIdx.x; a < na; a += gridDim.x) {
+    const int q = act[a];
+    const PairSetup ps = pair_at(pairs, q, scratch, snaps, out);
+    const int n = ps.n;
+    const int Btot = min(kTrialBatch * W, rst[q].max_trials - rst[q].trial);
+    wsync();
+    mt_load(s, ps.state);
+    // The sample-index vector lives in LDS for the window (dynamic LDS after
+    // VerifyLds) and goes back to the pair's scratch afterwards.
+    uint16_t* gsidx = pair_sidx(ps);
+    uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
+    for (int i = lane; i < n; i += 64) sidx[i] = gsidx[i];
+    wsync();
+    uint16_t* sq = samp + (int64_t)q * kWindowTrials * 8;
+    for (int w = 0; w * kTrialBatch < Btot; ++w) {
+      const int B = min(kTrialBatch, Btot - w * kTrialBatch);
+      uint32_t* snap = wsnap + ((int64_t)q * kMaxWindow + w) * 640;
+      for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
+      if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
+      wsync();
+      if (draw_targets_wave<Tr::kmin>(s, B * Tr::kmin, (uint32_t)n)) {
+        if (lane == 0) shuffle_batch_lane0<Tr::kmin>(s, sidx, B);
+      } else {  // a draw may need rejection sampling: serial draws from the snapshot
+        for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
+        wsync();
+        if (lane == 0) {
+          s.mt_idx = (int32_t)snap[624];
+          const uint32_t last = (uint32_t)(n - 1);
+          for (int b = 0; b < B; ++b)
+            for (int i = 0; i < Tr::kmin; ++i) {
+              const uint32_t j = uniform_u32(s, (uint32_t)i, last);
+              const uint16_t t = sidx[i];
+              sidx[i] = sidx[j];
+              sidx[j] = t;
+              s.samples[b][i] = sidx[i];
+            }
+        }
+      }
+      wsync();
+      for (int i = lane; i < B * 8; i += 64) sq[w * kTrialBatch * 8 + i] = s.samples[i >> 3][i & 7];
+      wsync();
+    }
+    mt_save(s, ps.state);
+    for (int i = lane; i < n; i += 64) gsidx[i] = sidx[i];
+    uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3;
+    for (int i = lane; i < Btot * 3; i += 64) cq[i] = 0u;
+    if (lane == 0) rst[q].B = Btot;
+  }
+}
+
+// Minimal solvers, one thread per hypothesis of the window, plus the fp32
+// filter constants of every model.
+template <int K>
+__global__ __launch_bounds__(64) void rs_solve_kernel(
+    const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
+    const double* __restrict__ xy2_all, const RansacState* __restrict__ rst,
+    const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
+    const uint16_t* __restrict__ samp, int32_t* __restrict__ nmod, float* __restrict__ fcon,
+    double* __restrict__ mods, int W, double maxr) {
+  using Tr = KindTraits<K>;
+  constexpr int MM = Tr::mm, MS = Tr::ms;
+  const int na = *nact;
+  const int per = W;  // blocks of 64 hypotheses per pair
+  for (int it = blockIdx.x; it < na * per; it += gridDim.x) {
+    const int q = act[it / per];
+    const int h = (it % per) * 64 + threadIdx.x;
+    if (h >= rst[q].B) continue;
+    const VerifyPair pp = pairs[q];
+    const double S = rst[q].S;
+    const double* xy1 = xy1_all + pp.pts_off;
+    const double* xy2 = xy2_all + pp.pts_off;
+    const uint16_t* sq = samp + ((int64_t)q * kWindowTrials + h) * 8;
+    double a_[2 * 7], b_[2 * 7];
+#pragma unroll
+    for (int i = 0; i < Tr::kmin; ++i) {
+      const uint32_t k = sq[i];
+      a_[2 * i] = xy1[2 * k];
+      a_[2 * i + 1] = xy1[2 * k + 1];
+      b_[2 * i] = xy2[2 * k];
+      b_[2 * i + 1] = xy2[2 * k + 1];
+    }
+    double* mo = mods + ((int64_t)q * kWindowTrials * 3 + h * MM) * MS;
+    int nm = 1;
+    if (K == KIND_F) nm = fundamental_7pt(a_, b_, mo);
+    else homography_dlt(a_, b_, 4, mo);
+    nmod[(int64_t)q * kWindowTrials + h] = nm;
+    float* fc = fcon + ((int64_t)q * kWindowTrials * 3 + h * MM) * 12;
+    for (int k = 0; k < nm; ++k) {
+      float c[12];
+      if (K == KIND_F) f_filter_consts(mo + k * MS, S, maxr, c);
+      else h_filter_consts(mo + k * MS, S, maxr, c);
+#pragma unroll
+      for (int j = 0; j < 12; ++j) fc[k * 12 + j] = c[j];
+    }
+  }
+}
+
+// Inlier counts of every model of the window: work item = (active pair,
+// 1024-point chunk), one wave each (16 points per lane, packed in pairs);
+// the filter constants of one round at a time are broadcast from LDS and
+// lane t accumulates the count of hypothesis t of the round.
+constexpr int kScoreThreads = 64;
+constexpr int kScorePch = 16;  // points per lane
+constexpr int kScoreChunk = kScoreThreads * kScorePch;
+
+template <int K>
+__global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
+    const VerifyPair* __restrict__ pairs, const float4* __restrict__ xyf_all,
+    const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
+    const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
+    const float* __restrict__ fcon, const double* __restrict__ mods,
+    uint32_t* __restrict__ cnts, int max_chunks, double maxr) {
+  using Tr = KindTraits<K>;
+  constexpr int MM = Tr::mm, MS = Tr::ms;
+  __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * 3][12];
+  __shared__ int32_t lnm[kTrialBatch];
+  const int lane = threadIdx.x;
+  const int na = *nact;
+  const float maxrf = (float)maxr;
+  for (int w = blockIdx.x; w < na * max_chunks; w += gridDim.x) {
+    const int q = act[w / max_chunks];
+    const int chunk = w % max_chunks;
+    const VerifyPair pp = pairs[q];
+    const int n = pp.m;
+    const int base = chunk * kScoreChunk;
+    if (base >= n) continue;
+    const int Btot = rst[q].B;
+    const float4* xyf = xyf_all + pp.pts_off / 2;
+    f32x2 x0[kScorePch / 2], x1[kScorePch / 2], y0[kScorePch / 2], y1[kScorePch / 2];
+#pragma unroll
+    for (int qq = 0; qq < kScorePch / 2; ++qq) {
+      const int i0 = base + (2 * qq) * 64 + lane, i1 = i0 + 64;
+      const float4 v0 = i0 < n ? xyf[i0] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 v1 = i1 < n ? xyf[i1] : make_float4(0.f, 0.f, 0.f, 0.f);
+      x0[qq] = f32x2{v0.x, v1.x};
+      x1[qq] = f32x2{v0.y, v1.y};
+      y0[qq] = f32x2{v0.z, v1.z};
+      y1[qq] = f32x2{v0.w, v1.w};
+    }
+    const bool full = base + kScoreChunk <= n;
+    for (int r0 = 0; r0 < Btot; r0 += kTrialBatch) {
+      const int B = min(kTrialBatch, Btot - r0);
+      __syncthreads();
+      if (lane < B) lnm[lane] = nmod[(int64_t)q * kWindowTrials + r0 + lane];
+      {
+        const float4* src = reinterpret_cast<const float4*>(
+            fcon + ((int64_t)q * kWindowTrials * 3 + r0 * MM) * 12);
+        float4* dst = reinterpret_cast<float4*>(&lc[0][0]);
+        for (int i = lane; i < B * MM * 3; i += kScoreThreads) dst[i] = src[i];
+      }
+      __syncthreads();
+      const double* mb = mods + ((int64_t)q * kWindowTrials * 3 + r0 * MM) * MS;
+      int nslow = 0;
+      uint32_t c0 = 0, c1 = 0, c2 = 0;  // lane t: counts of hypothesis t's models
+      for (int t = 0; t < B; ++t) {
+        const int nmt = K == KIND_F ? __builtin_amdgcn_readfirstlane(lnm[t]) : 1;
+        for (int k = 0; k < nmt; ++k) {
+          const int m = t * MM + k;
+          int c;
+          if (K == KIND_F) {
+            const FFilt f = f_filter_load(&lc[m][0], maxrf);
+            c = full ? score_f_chunk<kScorePch, true>(f, mb + m * MS, x0, x1, y0, y1, n, base,
+                                                      maxr, &nslow)
+                     : score_f_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
+                                                       maxr, &nslow);
+          } else {
+            const HFilt f = h_filter_load(&lc[m][0], maxrf);
+            c = full ? score_h_chunk<kScorePch, true>(f, mb + m * MS, x0, x1, y0, y1, n, base,
+                                                      maxr, &nslow)
+                     : score_h_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
+                                                       maxr, &nslow);
+          }
+          const uint32_t add = (lane == t) ? (uint32_t)c : 0u;
+          if (k == 0) c0 += add;
+          else if (k == 1) c1 += add;
+          else c2 += add;
+        }
+      }
+      uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3 + r0 * MM;
+      if (lane < B) {
+        if (c0) atomicAdd(&cq[lane * MM], c0);
+        if (MM > 1 && c1) atomicAdd(&cq[lane * MM + 1], c1);
+        if (MM > 2 && c2) atomicAdd(&cq[lane * MM + 2], c2);
+      }
+    }
+  }
+}
+
+// The sequential part of one window, in trial order, for every active pair.
+template <int K>
+__global__ __launch_bounds__(64) void rs_replay_kernel(
+    const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
+    const double* __restrict__ xy2_all, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
+    RansacState* __restrict__ rst, const int32_t* __restrict__ act,
+    const int32_t* __restrict__ nact, int32_t* __restrict__ act_next,
+    int32_t* __restrict__ nact_next, const int32_t* __restrict__ nmod,
+    const uint32_t* __restrict__ cnts, const double* __restrict__ mods,
+    const uint32_t* __restrict__ wsnap, VerifyParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
+  using Tr = KindTraits<K>;
+  constexpr int MM = Tr::mm, MS = Tr::ms;
+  const int lane = threadIdx.x;
+  const double maxr = P.max_residual;
+  const int na = *nact;
+  for (int a = blockIdx.x; a < na; a += gridDim.x) {
+    const int q = act[a];
+    const PairSetup ps = pair_at(pairs, q, scratch, snaps, out);
+    const int n = ps.n;
+    const double* xy1 = xy1_all + ps.pp.pts_off;
+    const double* xy2 = xy2_all + ps.pp.pts_off;
+    double* base = ps.base;
+    double* res[2] = {base, base + n};
+    double* xin1 = base + 2 * n;
+    double* xin2 = base + 4 * n;
+    const double* mq = mods + (int64_t)q * kWindowTrials * 3 * MS;
+    RansacState st = rst[q];
+    wsync();
+    if (lane < 9) s.best_model[lane] = st.best_model[lane];
+    if (lane == 0) {
+      s.best_n = st.best_n;
+      s.best_sum = st.best_sum;
+      s.best_sum_valid = st.best_sum_valid;
+    }
+    int best_sel = st.res_sel;
+    int dyn_max = st.dyn_max;
+    const int trial = st.trial;
+    const int Btot = st.B;
+    bool abort = false;
+    int abort_trial = -1;
+    for (int r0 = 0; r0 < Btot && !abort; r0 += kTrialBatch) {
+      const int B = min(kTrialBatch, Btot - r0);
+      wsync();
+      for (int i = lane; i < B; i += 64) s.nmodels[i] = nmod[(int64_t)q * kWindowTrials + r0 + i];
+      for (int i = lane; i < B * MM; i += 64)
+        s.counts[i] = cnts[(int64_t)q * kWindowTrials * 3 + r0 * MM + i];
+      wsync();
+      for (int t = 0; t < B && !abort; ++t) {
+        const int tt = trial + r0 + t;
+        const int nmt = s.nmodels[t];
+        for (int k = 0; k < MM; ++k) {
+          if (k < nmt && !abort) {
+            const int c = (int)s.counts[t * MM + k];
+            const int bn = s.best_n;
+            if (c >= bn) {
+              double mk[MS];
+              const double* src = mq + ((r0 + t) * MM + k) * MS;
+#pragma unroll
+              for (int j = 0; j < MS; ++j) mk[j] = src[j];
+              double* rt = res[best_sel ^ 1];
+              residuals_wave<K>(mk, xy1, xy2, n, maxr, rt);
+              bool better = c > bn;
+              double sum = 0.0;
+              if (!better) {  // tie on the inlier count: Compare the residual sums
+                sum = seq_inlier_sum(rt, n, maxr);
+                ensure_best_sum(s, res[best_sel], n, maxr);
+                better = sum < s.best_sum;
+              }
+              if (better) {
+                wsync();
+                if (lane == 0) {
+#pragma unroll
+                  for (int j = 0; j < MS; ++j) s.best_model[j] = mk[j];
+                  s.best_n = c;
+                  s.best_sum = sum;
+                  s.best_sum_valid = c == bn ? 1 : 0;
+                }
+                best_sel ^= 1;
+                wsync();
+                // Recursive local optimisation.
+                if (c > Tr::kmin && c >= Tr::kmin_local) {
+                  for (int lt = 0; lt < 10; ++lt) {
+                    const int ni = gather_inliers(res[best_sel], n, maxr, xy1, xy2, xin1, xin2);
+                    double lm[9];
+                    local_estimate_wave<K>(s, xin1, xin2, ni, lm);
+                    const int prev = s.best_n;
+                    double* rl = res[best_sel ^ 1];
+                    const int lcn = residuals_wave<K>(lm, xy1, xy2, n, maxr, rl);
+                    bool lbetter = lcn > prev;
+                    double lsum = 0.0;
+                    if (lcn == prev) {
+                      lsum = seq_inlier_sum(rl, n, maxr);
+                      ensure_best_sum(s, res[best_sel], n, maxr);
+                      lbetter = lsum < s.best_sum;
+                    }
+                    if (lbetter) {
+                      wsync();
+                      if (lane == 0) {
+#pragma unroll
+                        for (int j = 0; j < MS; ++j) s.best_model[j] = lm[j];
+                        s.best_n = lcn;
+                        s.best_sum = lsum;
+                        s.best_sum_valid = lcn == prev ? 1 : 0;
+                      }
+                      best_sel ^= 1;
+                    }
+                    wsync();
+                    if (s.best_n <= prev) break;
+                  }
+                }
+                dyn_max = (int)min((uint64_t)0x7FFFFFFF,
+                                   num_trials((uint64_t)s.best_n, (uint64_t)n, P.confidence,
+                                              P.dyn_num_trials_multiplier, Tr::kmin));
+              }
+            }
+            if (tt >= dyn_max && tt >= P.min_num_trials) {
+              abort = true;
+              abort_trial = tt;
+            }
+          }
+        }
+      }
+    }
+    wsync();
+    if (abort) {
+      // Rewind the PRNG to the state right after trial abort_trial's sample:
+      // the state before its round, then that round's draws up to it.
+      const int w = (abort_trial - trial) / kTrialBatch;
+      const uint32_t* snap = wsnap + ((int64_t)q * kMaxWindow + w) * 640;
+      for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
+      wsync();
+      if (lane == 0) {
+        s.mt_idx = (int32_t)snap[624];
+        const uint32_t last = (uint32_t)(n - 1);
+        for (int b = 0; b <= abort_trial - trial - w * kTrialBatch; ++b)
+          for (int i = 0; i < Tr::kmin; ++i) (void)uniform_u32(s, (uint32_t)i, last);
+      }
+      wsync();
+      mt_save(s, ps.state);
+      st.num_trials = abort_trial + 2;
+      st.done = 1;
+    } else {
+      st.trial = trial + Btot;
+      st.num_trials = st.trial;
+      if (st.trial >= st.max_trials) st.done = 1;
+    }
+    st.dyn_max = dyn_max;
+    st.res_sel = best_sel;
+    st.best_n = s.best_n;
+    st.best_sum = s.best_sum;
+    st.best_sum_valid = s.best_sum_valid;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) st.best_model[j] = s.best_model[j];
+    wsync();
+    if (lane == 0) rst[q] = st;
+    if (st.done) rs_finish<K>(ps, st, masks, maxr);
+    else if (lane == 0) act_next[atomicAdd(nact_next, 1)] = q;
+  }
+}
+
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
                               const float2* __restrict__ kpxy, double* __restrict__ xy1,
                               double* __restrict__ xy2, const int32_t* __restrict__ counts,
@@ -1488,23 +1911,86 @@ size_t verify_lds_bytes(int max_m) {
   return sizeof(VerifyLds);
 }
 
+namespace {
+
+template <typename F>
+void set_lds_attr(F f) {
+  (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            160 * 1024);
+}
+
+// Windows of one RANSAC kind (W = 1, 2, 4, ..., kMaxWindow rounds) until the
+// trial cap; kernels of windows with no active pair exit at once.
+template <int K>
+hipError_t run_rounds(const VerifyPair* pairs, int npairs, const double* xy1, const double* xy2,
+                      double* scratch, uint32_t* snaps, uint8_t* masks, VerifyOut* out,
+                      const VerifyParams& P, const float4* xyf, const VerifyRoundBufs& rb,
+                      int max_chunks, int max_m, hipStream_t stream) {
+  const size_t lds = sizeof(VerifyLds);
+  const size_t lds_sample = lds + (size_t)((max_m + 7) / 8 * 8) * sizeof(uint16_t);
+  const int max_trials = K == KIND_F ? P.max_trials_F : P.max_trials_H;
+  const int gw = npairs < 4096 ? npairs : 4096;
+  int covered = 0, W = 1, r = 0;
+  while (covered < max_trials) {
+    const int cur = r & 1, nxt = cur ^ 1;
+    hipLaunchKernelGGL(rs_sample_kernel<K>, dim3(gw), dim3(64), lds_sample, stream, pairs, scratch,
+                       snaps, out, rb.rst, rb.act[cur], rb.nact + cur, rb.nact + nxt, rb.samp,
+                       rb.cnts, rb.wsnap, W);
+    hipLaunchKernelGGL(rs_solve_kernel<K>, dim3(4096), dim3(64), 0, stream, pairs, xy1, xy2,
+                       rb.rst, rb.act[cur], rb.nact + cur, rb.samp, rb.nmod, rb.fcon, rb.mods, W,
+                       P.max_residual);
+    hipLaunchKernelGGL(rs_score_kernel<K>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs, xyf,
+                       rb.rst, rb.act[cur], rb.nact + cur, rb.nmod, rb.fcon, rb.mods, rb.cnts,
+                       max_chunks, P.max_residual);
+    hipLaunchKernelGGL(rs_replay_kernel<K>, dim3(gw), dim3(64), lds, stream, pairs, xy1, xy2,
+                       scratch, snaps, out, masks, rb.rst, rb.act[cur], rb.nact + cur,
+                       rb.act[nxt], rb.nact + nxt, rb.nmod, rb.cnts, rb.mods, rb.wsnap, P);
+    const hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    covered += W * kTrialBatch;
+    W = W * 2 > kMaxWindow ? kMaxWindow : W * 2;
+    ++r;
+  }
+  return hipSuccess;
+}
+
+}  // namespace
+
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
-                         const int32_t* counts, const float4* xyf, hipStream_t stream) {
+                         const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb,
+                         hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
-  const size_t lds = verify_lds_bytes(max_m);
   static bool attr = false;
   if (!attr) {
-    for (const void* f : {(const void*)verify_f_kernel, (const void*)verify_h_kernel,
-                          (const void*)verify_final_kernel})
-      (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    set_lds_attr(rs_begin_kernel<KIND_F>);
+    set_lds_attr(rs_begin_kernel<KIND_H>);
+    set_lds_attr(rs_sample_kernel<KIND_F>);
+    set_lds_attr(rs_sample_kernel<KIND_H>);
+    set_lds_attr(rs_replay_kernel<KIND_F>);
+    set_lds_attr(rs_replay_kernel<KIND_H>);
+    set_lds_attr(verify_final_kernel);
     attr = true;
   }
-  hipLaunchKernelGGL(verify_f_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
-                     xy1, xy2, scratch, snaps, masks, out, params, prof, counts, xyf);
-  hipLaunchKernelGGL(verify_h_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
-                     xy1, xy2, scratch, snaps, out, params, prof, counts, xyf);
+  const size_t lds = sizeof(VerifyLds);
+  const int gw = npairs < 4096 ? npairs : 4096;
+  const int max_chunks = (max_m + kScoreChunk - 1) / kScoreChunk;
+  hipError_t err;
+  // F: LORANSAC<7-pt, 8-pt>, then the F inlier masks.
+  if ((err = hipMemsetAsync(rb.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  hipLaunchKernelGGL(rs_begin_kernel<KIND_F>, dim3(gw), dim3(64), lds, stream, pairs, npairs,
+                     scratch, snaps, out, masks, xyf, rb.rst, rb.act[0], rb.nact, params);
+  if ((err = run_rounds<KIND_F>(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf,
+                                rb, max_chunks, max_m, stream)) != hipSuccess)
+    return err;
+  // H: LORANSAC<H, H> on the same PRNG streams.
+  if ((err = hipMemsetAsync(rb.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  hipLaunchKernelGGL(rs_begin_kernel<KIND_H>, dim3(gw), dim3(64), lds, stream, pairs, npairs,
+                     scratch, snaps, out, masks, xyf, rb.rst, rb.act[0], rb.nact, params);
+  if ((err = run_rounds<KIND_H>(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf,
+                                rb, max_chunks, max_m, stream)) != hipSuccess)
+    return err;
   hipLaunchKernelGGL(verify_final_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
                      xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
   return hipGetLastError();
