@@ -58,15 +58,81 @@ __device__ __forceinline__ uint32_t merge_second(uint32_t b1a, uint32_t b2a,
 // swept against every column of every neighbour image of the job, 32 columns
 // per LDS tile.  Per element (fast variant): 1 v_lshl_or (key) + 2 row-state
 // ops + 2 column-state ops.
+//
+// Software pipeline (per wave): the 16 MFMAs of tile t+1 are issued into one
+// accumulator pair while the epilogue of tile t runs on the other, so the
+// matrix core and the vector ALU overlap inside every wave; B tiles rotate
+// through three LDS buffers (tile t+2 is staged while t+1 is read), one
+// barrier per tile.  The loop body is branch-free (the MFMAs past the last
+// tile of a segment run on a clamped tile and are discarded) so the compiler
+// can interleave the two streams.
+constexpr int kStages = 3;
+
+__device__ __forceinline__ void load_bfrag(const uint8_t* bt, int r, int h, bf16x8 (&bfrag)[8]) {
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int ch = (h * 8 + q) ^ (r & 15);
+    bfrag[q] = *reinterpret_cast<const bf16x8*>(bt + r * 256 + (ch << 4));
+  }
+}
+
+// One 32 x 32 sub-tile over K = 128: an 8-MFMA accumulation chain.
+__device__ __forceinline__ f32x16 chain(const bf16x8 (&a)[8], const bf16x8 (&b)[8],
+                                        const f32x16& cinit) {
+  f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], cinit, 0, 0, 0);
+#pragma unroll
+  for (int q = 1; q < 8; ++q) acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b[q], acc, 0, 0, 0);
+  return acc;
+}
+
+// Keys of one finished sub-tile: row top-2 state update; returns the
+// sub-tile's column partial (best two keys of the lane's column, re-keyed
+// with the row inside the workgroup).
 template <bool CLAMP>
-__global__ __launch_bounds__(kMatchThreads, 2) void match_tiles_kernel(
+__device__ __forceinline__ uint2 subtile_epilogue(const f32x16& acc, uint32_t tbits,
+                                                  uint32_t (&b1r)[16], uint32_t (&b2r)[16],
+                                                  uint32_t row_base) {
+  uint32_t b1c = 0u, b2c = 0u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t bits = __float_as_uint(acc[i]);
+    uint32_t key;
+    if (CLAMP)
+      key = (min(bits, 0x4B040000u) << 13) | tbits | ((uint32_t)(15 - i) << 9);
+    else
+      key = (bits << 9) | tbits;
+    b2r[i] = med3_u32(key, b1r[i], b2r[i]);
+    b1r[i] = max(b1r[i], key);
+    b2c = med3_u32(key, b1c, b2c);
+    b1c = max(b1c, key);
+  }
+  const uint32_t ii = 15u - ((b1c >> 9) & 15u);
+  const uint32_t row_in_blk = row_base + (ii & 3u) + 8u * (ii >> 2);
+  return make_uint2((b1c & ~kIdxMask) | (kIdxMask - row_in_blk), b2c & ~kIdxMask);
+}
+
+// One workgroup = one MatchJob = 512 rows of the pivot image (8 waves x 64
+// rows, two 32-row MFMA sub-tiles per wave, A fragments register-resident)
+// swept against every column of every neighbour image of the job, 32 columns
+// per LDS tile.  Per element (fast variant): 1 v_lshl_or (key) + 2 row-state
+// ops + 2 column-state ops.
+//
+// Software pipeline (per wave, sub-tile granularity): the MFMA chain of
+// sub-tile (t, 1) runs while the epilogue of (t, 0) executes, and the chain of
+// (t + 1, 0) while the epilogue of (t, 1) executes, so the matrix core and
+// the vector ALU overlap inside every wave with only two accumulators.  B
+// tiles rotate through three LDS buffers (tile t+2 is staged while t+1 is
+// read); one barrier per tile.  The loop body is branch-free: past the last
+// tile of a segment the chain runs on a clamped tile and is discarded.
+template <bool CLAMP>
+__global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
     const uint16_t* __restrict__ desc,        // bf16 table, [rows][128]
     const MatchJob* __restrict__ jobs,
     const PairDesc* __restrict__ pairs,
     uint2* __restrict__ rowres,               // per pair [nseg][n1]
     uint2* __restrict__ colpart) {            // per pair [nrb][n2pad]
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kTileBytes + 2 * kMatchWaves * 32 * 8];
-  uint2* colscratch = reinterpret_cast<uint2*>(lds + 2 * kTileBytes);
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kStages * kTileBytes + 2 * kMatchWaves * 32 * 8];
+  uint2* colscratch = reinterpret_cast<uint2*>(lds + kStages * kTileBytes);
 
   const MatchJob job = jobs[blockIdx.x];
   const int tid = threadIdx.x;
@@ -103,113 +169,73 @@ __global__ __launch_bounds__(kMatchThreads, 2) void match_tiles_kernel(
   f32x16 cinit;
 #pragma unroll
   for (int i = 0; i < 16; ++i) cinit[i] = CLAMP ? 8388608.0f : 8388608.0f + (float)(15 - i);
+  const uint32_t row_base0 = (uint32_t)wave * 64u + 4u * (uint32_t)h;
 
   // Staging role of this thread: one 16-B chunk of the 8 KiB B tile.
   const int st_col = tid >> 4;    // 0..31
   const int st_chunk = tid & 15;  // 0..15
   const int st_lds = st_col * 256 + ((st_chunk ^ (st_col & 15)) << 4);
 
-  int tile_parity = 0;
   for (int p = 0; p < job.npairs; ++p) {
     const PairDesc pd = pairs[job.pair0 + p];
     const int ntiles_total = (pd.n2 + 31) >> 5;
     uint2* colp = colpart + pd.colpart_off + (int64_t)job.rb * pd.n2pad;
+    const uint16_t* bdesc = desc + pd.b_row * 128;
     for (int seg = 0; seg < pd.nseg; ++seg) {
       const int t_begin = seg * kTilesPerSeg;
       const int t_end = min(ntiles_total, t_begin + kTilesPerSeg);
+      const int tlast = t_end - 1;
       uint32_t b1r[2][16], b2r[2][16];
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
         for (int i = 0; i < 16; ++i) { b1r[s][i] = 0u; b2r[s][i] = 0u; }
 
-      // Prologue: stage tile t_begin.
-      {
-        const uint4* src = reinterpret_cast<const uint4*>(
-            desc + (pd.b_row + (int64_t)t_begin * 32 + st_col) * 128) + st_chunk;
-        *reinterpret_cast<uint4*>(lds + tile_parity * kTileBytes + st_lds) = *src;
-      }
+      const uint4* src0 = reinterpret_cast<const uint4*>(bdesc + (int64_t)st_col * 128) + st_chunk;
+      // Prologue: stage tiles t_begin, t_begin + 1; chain of (t_begin, 0).
+      *reinterpret_cast<uint4*>(lds + 0 * kTileBytes + st_lds) = src0[(int64_t)t_begin * 32 * 16];
+      *reinterpret_cast<uint4*>(lds + 1 * kTileBytes + st_lds) =
+          src0[(int64_t)min(t_begin + 1, tlast) * 32 * 16];
       __syncthreads();
+      bf16x8 bfrag[8];
+      load_bfrag(lds, r, h, bfrag);
+      f32x16 acc0 = chain(afrag[0], bfrag, cinit);
 
-      for (int t = t_begin; t < t_end; ++t) {
-        const int cur = tile_parity;
-        uint4 nxt = make_uint4(0, 0, 0, 0);
-        const bool has_next = (t + 1) < t_end;
-        if (has_next) {
-          nxt = *(reinterpret_cast<const uint4*>(
-                      desc + (pd.b_row + (int64_t)(t + 1) * 32 + st_col) * 128) + st_chunk);
-        }
-        // ---- B fragments from LDS (swizzled 16-B chunks).
-        const uint8_t* bt = lds + cur * kTileBytes + r * 256;
-        bf16x8 bfrag[8];
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int ch = (h * 8 + q) ^ (r & 15);
-          bfrag[q] = *reinterpret_cast<const bf16x8*>(bt + (ch << 4));
-        }
-        f32x16 acc[2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag[s][0], bfrag[0], cinit, 0, 0, 0);
-#pragma unroll
-          for (int q = 1; q < 8; ++q)
-            acc[s] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(afrag[s][q], bfrag[q], acc[s], 0, 0, 0);
-        }
-        // ---- Epilogue: keys, row state, column state.
-        const uint32_t tbits = (uint32_t)(kTilesPerSeg - 1 - (t - t_begin));
-        uint32_t b1c[2], b2c[2];
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          b1c[s] = 0u;
-          b2c[s] = 0u;
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const uint32_t bits = __float_as_uint(acc[s][i]);
-            uint32_t key;
-            if (CLAMP)
-              key = (min(bits, 0x4B040000u) << 13) | tbits | ((uint32_t)(15 - i) << 9);
-            else
-              key = (bits << 9) | tbits;
-            b2r[s][i] = med3_u32(key, b1r[s][i], b2r[s][i]);
-            b1r[s][i] = max(b1r[s][i], key);
-            b2c[s] = med3_u32(key, b1c[s], b2c[s]);
-            b1c[s] = max(b1c[s], key);
-          }
-        }
-        // Column partial of this wave: re-key with the row inside the block,
-        // merge the two sub-tiles and the two half-waves.
-        {
-          uint32_t B1 = 0u, B2 = 0u;
-#pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const uint32_t ii = 15u - ((b1c[s] >> 9) & 15u);
-            const uint32_t row_in_blk = (uint32_t)wave * 64u + 32u * s + (ii & 3u) + 8u * (ii >> 2) + 4u * (uint32_t)h;
-            const uint32_t k1 = (b1c[s] & ~kIdxMask) | (kIdxMask - row_in_blk);
-            const uint32_t k2 = b2c[s] & ~kIdxMask;
-            if (s == 0) { B1 = k1; B2 = k2; }
-            else { B2 = merge_second(B1, B2, k1, k2); B1 = max(B1, k1); }
-          }
-          const uint32_t o1 = __shfl_xor(B1, 32);
-          const uint32_t o2 = __shfl_xor(B2, 32);
-          B2 = merge_second(B1, B2, o1, o2);
-          B1 = max(B1, o1);
-          if (h == 0) colscratch[(cur * kMatchWaves + wave) * 32 + r] = make_uint2(B1, B2);
-        }
-        if (has_next) *reinterpret_cast<uint4*>(lds + (cur ^ 1) * kTileBytes + st_lds) = nxt;
+      for (int k = 0; k < t_end - t_begin; ++k) {
+        const int t = t_begin + k;
+        const uint4 nxt = src0[(int64_t)min(t + 2, tlast) * 32 * 16];
+        const uint32_t tbits = (uint32_t)(kTilesPerSeg - 1 - k);
+        // chain (t, 1) || epilogue (t, 0)
+        const f32x16 acc1 = chain(afrag[1], bfrag, cinit);
+        const uint2 c0 = subtile_epilogue<CLAMP>(acc0, tbits, b1r[0], b2r[0], row_base0);
+        // chain (t + 1, 0) || epilogue (t, 1).  The barrier keeps the next
+        // B fragments from being loaded while the current ones are live.
+        __builtin_amdgcn_sched_barrier(0);
+        load_bfrag(lds + ((k + 1) % kStages) * kTileBytes, r, h, bfrag);
+        acc0 = chain(afrag[0], bfrag, cinit);
+        const uint2 c1 = subtile_epilogue<CLAMP>(acc1, tbits, b1r[1], b2r[1], row_base0 + 32u);
+        // Column partial of this wave: merge the two sub-tiles and the halves.
+        uint32_t B1 = max(c0.x, c1.x), B2 = merge_second(c0.x, c0.y, c1.x, c1.y);
+        const uint32_t o1 = __shfl_xor(B1, 32);
+        const uint32_t o2 = __shfl_xor(B2, 32);
+        B2 = merge_second(B1, B2, o1, o2);
+        B1 = max(B1, o1);
+        if (h == 0) colscratch[((k & 1) * kMatchWaves + wave) * 32 + r] = make_uint2(B1, B2);
+        *reinterpret_cast<uint4*>(lds + ((k + 2) % kStages) * kTileBytes + st_lds) = nxt;
         __syncthreads();
         // One wave merges the 8 wave partials of this tile and stores them.
-        if (wave == (t & (kMatchWaves - 1)) && h == 0) {
-          uint2 m = colscratch[(cur * kMatchWaves + 0) * 32 + r];
+        if (wave == (k & (kMatchWaves - 1)) && h == 0) {
+          uint2 m = colscratch[((k & 1) * kMatchWaves + 0) * 32 + r];
 #pragma unroll
           for (int w = 1; w < kMatchWaves; ++w) {
-            const uint2 o = colscratch[(cur * kMatchWaves + w) * 32 + r];
+            const uint2 o = colscratch[((k & 1) * kMatchWaves + w) * 32 + r];
             m.y = merge_second(m.x, m.y, o.x, o.y);
             m.x = max(m.x, o.x);
           }
           colp[t * 32 + r] = m;
         }
-        tile_parity ^= 1;
       }
+      __syncthreads();  // every wave done with the LDS tiles before the next segment
 
       // ---- Row flush for this segment: re-key with the column inside the
       // segment, reduce over the 32 lanes of each half, store.
