@@ -53,19 +53,6 @@ __device__ __forceinline__ uint32_t merge_second(uint32_t b1a, uint32_t b2a,
   return max(max(b2a, b2b), lo);
 }
 
-// One workgroup = one MatchJob = 512 rows of the pivot image (8 waves x 64
-// rows, two 32-row MFMA sub-tiles per wave, A fragments register-resident)
-// swept against every column of every neighbour image of the job, 32 columns
-// per LDS tile.  Per element (fast variant): 1 v_lshl_or (key) + 2 row-state
-// ops + 2 column-state ops.
-//
-// Software pipeline (per wave): the 16 MFMAs of tile t+1 are issued into one
-// accumulator pair while the epilogue of tile t runs on the other, so the
-// matrix core and the vector ALU overlap inside every wave; B tiles rotate
-// through three LDS buffers (tile t+2 is staged while t+1 is read), one
-// barrier per tile.  The loop body is branch-free (the MFMAs past the last
-// tile of a segment run on a clamped tile and are discarded) so the compiler
-// can interleave the two streams.
 constexpr int kStages = 3;
 
 __device__ __forceinline__ void load_bfrag(const uint8_t* bt, int r, int h, bf16x8 (&bfrag)[8]) {

@@ -3,23 +3,22 @@
 // the op's post-filter, reference integration/op_cpp/sequential_matching.cc:
 // 84-101 and 164-178; upstream EstimateUncalibrated).
 //
-// One wavefront owns one image pair (many pairs resident per CU hide each
-// other's serial sections) and runs, in order and with the pair's own
-// std::mt19937 stream (LDS-resident):
+// Every pair of a batch runs, in order and with the pair's own std::mt19937
+// stream:
 //   LO-RANSAC<7-pt F, 8-pt F>  ->  LO-RANSAC<4-pt H, N-pt H>
 //   -> configuration -> DetectWatermark (LO-RANSAC<translation>) -> post-filter.
-// Each round solves kTrialBatch minimal samples in parallel (one hypothesis
-// per lane, models kept in that lane's registers), scores every model over
-// the pair's matches (points streamed once per round in register chunks,
-// models broadcast with v_readlane, inlier bits counted with ballot), then
-// replays the trials in order exactly as the sequential LO-RANSAC does
-// (Compare, recursive local optimisation, dynamic trial bound, early abort);
-// hypotheses past the abort point are discarded and the PRNG is rewound to
-// the last consumed draw.  Residual sums are only needed when two inlier
-// counts tie; they are then summed in index order, as
-// InlierSupportMeasurer::Evaluate does.  The estimator arithmetic is the
-// shared geom_solvers.h (the 9x9 Jacobi is its lane-distributed twin), so
-// every model is bit-identical to the CPU oracle's.
+// F and H run as the windowed kernels below (rs_begin / rs_sample / rs_solve /
+// rs_score / rs_replay: all pairs advance one window of W rounds of 64
+// hypotheses at a time, scoring is one wide regular kernel, the sequential
+// LO-RANSAC decisions are replayed per pair in trial order and hypotheses past
+// the abort point are discarded with the PRNG rewound), the rest in
+// verify_final_kernel (one wavefront per pair).  Residual sums are only needed
+// when two inlier counts tie; they are then summed in index order, as
+// InlierSupportMeasurer::Evaluate does.  Inlier tests run on packed fp32 with
+// rigorous error bounds and fall back to the exact fp64 residual for every
+// point the bound cannot decide.  The estimator arithmetic is the shared
+// geom_solvers.h (the 9x9 Jacobi is its lane-distributed twin), so every model
+// is bit-identical to the CPU oracle's.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -681,10 +680,12 @@ __device__ double seq_inlier_sum(const double* res, int n, double maxr) {
   for (int base = 0; base < n; base += 64) {
     const int i = base + threadIdx.x;
     const double v = i < n ? res[i] : 1.7976931348623157e308;
-    const int cnt = min(64, n - base);
-    for (int j = 0; j < cnt; ++j) {
-      const double r = readlane_d(v, j);
-      if (r <= maxr) sum += r;
+    // Only the inliers contribute: visit them in lane (= index) order.
+    uint64_t bal = __ballot(v <= maxr);
+    while (bal) {
+      const int j = __builtin_ctzll(bal);
+      sum += readlane_d(v, j);
+      bal &= bal - 1;
     }
   }
   return sum;
@@ -1256,14 +1257,9 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
 }
 
 // ---------------------------------------------------------------------------
-// The verification runs as three kernels over the same pairs (one wavefront
-// per pair each), so that each RANSAC flavour gets its own register budget:
-//   verify_f_kernel     seed the pair's PRNG, LORANSAC<7-pt F, 8-pt F>, F
-//                       inlier mask; the PRNG state is handed on in global
-//   verify_h_kernel     LORANSAC<4-pt H, N-pt H> on the same PRNG stream
-//   verify_final_kernel configuration, DetectWatermark (translation
-//                       LORANSAC on the F inliers), post-filter
-// The F / H models and counts travel in the pair's VerifyOut record.
+// Per-pair state shared by the windowed kernels and verify_final_kernel (one
+// wavefront per pair): the F / H models and counts travel in the pair's
+// VerifyOut record, the PRNG state in the pair's snapshot words.
 // ---------------------------------------------------------------------------
 struct PairSetup {
   VerifyPair pp;
