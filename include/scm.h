@@ -8,7 +8,7 @@
  *
  * All buffers crossing this boundary are host memory laid out exactly as the
  * reference's io.cc codecs write them (integration/op_cpp/io.cc), so a Scanner
- * kernel (see scanner_colmap_amd/csrc/scanner_op/) or any FFI (ctypes, see
+ * kernel (see scanner_colmap_amd/scanner_op/) or any FFI (ctypes, see
  * scanner_colmap_amd/_abi.py) can call it with the bytes Scanner hands over.
  * Plain C types only: no torch / HIP types in the signatures.
  *
@@ -16,7 +16,7 @@
  * success and a negative SCM_E_* code otherwise; scm_last_error() returns a
  * thread-local message.  The reference aborts the worker through glog CHECK
  * (no return codes); the Scanner-side op maps a non-zero status to the same
- * fatal abort (scanner_op/sequential_matching_gpu.cc).
+ * fatal abort (scanner_colmap_amd/scanner_op/sequential_matching_gpu.cc).
  *
  * Threading (reference: one kernel instance per Scanner pipeline instance,
  * execute() serial per instance, sequential_matching.cc:103): an scm_context

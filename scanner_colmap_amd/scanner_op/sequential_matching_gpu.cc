@@ -1,0 +1,99 @@
+// Scanner op `SequentialMatchingGPU`: the MI355X drop-in for the reference's
+// `SequentialMatchingCPU` (reference integration/op_cpp/sequential_matching.cc:
+// 27-205).  Same stencil inputs (image_ids, keypoints, descriptors), same two
+// outputs (pair_image_ids, two_view_geometries) in the same io.cc byte layout,
+// host (CPU_DEVICE) output buffers, one kernel instance per Scanner pipeline
+// instance bound to config.devices[0].  All computation goes through the C ABI
+// of include/scm.h (libscm.so); this file only adapts Scanner's element
+// containers to it.  Build it next to the reference ops with Scanner's
+// build_op and link libscm.so.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+#include "scanner/api/kernel.h"
+#include "scanner/api/op.h"
+#include "scanner/util/memory.h"
+#include "scm.h"
+
+namespace {
+
+// The reference aborts the worker on failure (glog CHECK inside COLMAP);
+// a non-zero status from the library does the same here.
+void scm_check(int rc, const char* what) {
+  if (rc != SCM_OK) {
+    std::fprintf(stderr, "SequentialMatchingGPU: %s failed (%d): %s\n", what, rc,
+                 scm_last_error());
+    std::abort();
+  }
+}
+
+}  // namespace
+
+class SequentialMatchingGPUKernel : public scanner::StenciledBatchedKernel,
+                                    public scanner::VideoKernel {
+ public:
+  // Reference constructor + parseConfigs (sequential_matching.cc:30-76).
+  explicit SequentialMatchingGPUKernel(const scanner::KernelConfig& config)
+      : scanner::StenciledBatchedKernel(config) {
+    scm_matching_options opts;
+    scm_check(scm_parse_args(config.args.data(), config.args.size(), &opts), "scm_parse_args");
+    const int device = config.devices.empty() ? 0 : config.devices[0].id;
+    scm_check(scm_context_create(device, &opts, &ctx_), "scm_context_create");
+  }
+
+  ~SequentialMatchingGPUKernel() override { scm_context_destroy(ctx_); }
+
+  // Reference execute (sequential_matching.cc:103-185): column c, batch
+  // element 0, stencil offset s -> input_cols[c][0][s].
+  void execute(const scanner::StenciledBatchedElements& input_cols,
+               scanner::BatchedElements& output_cols) override {
+    const auto& ids = input_cols[0][0];
+    const auto& kps = input_cols[1][0];
+    const auto& descs = input_cols[2][0];
+    const size_t k = ids.size();
+    std::vector<scm_element> e_ids(k), e_kps(k), e_descs(k);
+    for (size_t s = 0; s < k; ++s) {
+      e_ids[s] = {ids[s].buffer, ids[s].size};
+      e_kps[s] = {kps[s].buffer, kps[s].size};
+      e_descs[s] = {descs[s].buffer, descs[s].size};
+    }
+    scm_blob pair_ids{nullptr, 0}, tvgs{nullptr, 0};
+    scm_check(scm_execute_stencil(ctx_, (int64_t)k, e_ids.data(), e_kps.data(), e_descs.data(),
+                                  &pair_ids, &tvgs),
+              "scm_execute_stencil");
+    emit(output_cols[0], &pair_ids);
+    emit(output_cols[1], &tvgs);
+  }
+
+ private:
+  // io.cc:157-176: the element is a scanner::new_buffer on the CPU device,
+  // owned by Scanner after insert_element.
+  static void emit(scanner::Elements& col, scm_blob* blob) {
+    scanner::u8* buf = scanner::new_buffer(scanner::CPU_DEVICE, blob->size);
+    std::memcpy(buf, blob->data, blob->size);
+    scanner::insert_element(col, buf, blob->size);
+    scm_blob_free(blob);
+  }
+
+  scm_context* ctx_ = nullptr;
+};
+
+// Same signature as REGISTER_OP(SequentialMatchingCPU) (sequential_matching.cc:
+// 193-200).  The reference names a protobuf message that colmap.proto does not
+// define ("featureMatchingArgs"); the kernel parses SequentialMatchingArgs,
+// which is what is registered here.
+REGISTER_OP(SequentialMatchingGPU)
+    .stencil()
+    .input("image_ids")
+    .input("keypoints")
+    .input("descriptors")
+    .output("pair_image_ids")
+    .output("two_view_geometries")
+    .protobuf_name("SequentialMatchingArgs");
+
+REGISTER_KERNEL(SequentialMatchingGPU, SequentialMatchingGPUKernel)
+    .device(scanner::DeviceType::GPU)
+    .batch()
+    .num_devices(1);

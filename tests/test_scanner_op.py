@@ -1,0 +1,102 @@
+"""The Scanner op `SequentialMatchingGPU` (scanner_colmap_amd/scanner_op/
+sequential_matching_gpu.cc), the drop-in for the reference's
+`SequentialMatchingCPU` (integration/op_cpp/sequential_matching.cc:27-205):
+compiled against a test stub of the Scanner API subset it uses
+(tests/scanner_stub) and driven the way a Scanner worker drives a kernel —
+instantiate by op name with a KernelConfig, execute() on one stencil of
+io.cc elements, read the two output elements."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from scanner_colmap_amd import _abi
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+STUB = os.path.join(ROOT, "tests", "scanner_stub")
+OP_SRC = os.path.join(ROOT, "scanner_colmap_amd", "scanner_op", "sequential_matching_gpu.cc")
+LIB_DIR = os.path.dirname(_abi.LIB_PATH)
+
+
+def _build_driver(tmp_path):
+    exe = tmp_path / "drive_op"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-I", STUB, "-I",
+                    os.path.join(ROOT, "include"), os.path.join(STUB, "drive_op.cc"), OP_SRC,
+                    "-L", LIB_DIR, "-lscm", f"-Wl,-rpath,{LIB_DIR}", "-o", str(exe)], check=True)
+    return exe
+
+
+def _write_stencil(d, ids, kps, descs, args=b""):
+    for c, col in enumerate((ids, kps, descs)):
+        for s, el in enumerate(col):
+            (d / f"in_{c}_{s}").write_bytes(el)
+    if args:
+        (d / "args").write_bytes(args)
+
+
+def test_op_compiles_against_scanner_api_and_links(tmp_path):
+    _build_driver(tmp_path)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")
+def test_op_aborts_without_gpu(tmp_path):
+    """No CPU fallback: the kernel constructor aborts the worker (the
+    reference's glog CHECK behaviour) when no gfx950 device exists."""
+    from scanner_colmap_amd.codecs import table_rows
+    from scanner_colmap_amd.synthetic import Corridor
+    exe = _build_driver(tmp_path)
+    ids, kps, descs = table_rows(Corridor(2, 64, 2, seed=3).images())
+    d = tmp_path / "io"
+    d.mkdir()
+    _write_stencil(d, ids, kps, descs)
+    r = subprocess.run([str(exe), "SequentialMatchingGPU", str(d), "2"], capture_output=True,
+                       text=True)
+    assert r.returncode != 0
+    assert "scm_context_create failed" in r.stderr
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,kpts,seed", [(5, 700, 41), (3, 300, 42), (1, 200, 43)])
+def test_op_execute_matches_oracle(tmp_path, k, kpts, seed):
+    from oracle import oracle
+    from scanner_colmap_amd.codecs import table_rows
+    from scanner_colmap_amd.synthetic import Corridor
+    exe = _build_driver(tmp_path)
+    ids, kps, descs = table_rows(Corridor(k, kpts, max(k, 2), seed=seed).images())
+    d = tmp_path / "io"
+    d.mkdir()
+    _write_stencil(d, ids, kps, descs)
+    r = subprocess.run([str(exe), "SequentialMatchingGPU", str(d), str(k)], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    ref_ids, ref_tvgs = oracle.execute_stencil(ids, kps, descs)
+    assert (d / "out_0").read_bytes() == ref_ids
+    assert (d / "out_1").read_bytes() == ref_tvgs
+
+
+@pytest.mark.gpu
+def test_op_parses_scanner_args(tmp_path):
+    """Serialised SequentialMatchingArgs reach the kernel (here: a tighter
+    max_ratio and min_num_inliers), compared with the oracle under the same
+    options."""
+    from oracle import oracle
+    from scanner_colmap_amd.codecs import table_rows
+    from scanner_colmap_amd.synthetic import Corridor
+    # siftargs (field 4) { max_ratio (3, double) = 0.6, min_num_inliers (12, varint) = 40 }
+    sift = bytes([0x19]) + np.float64(0.6).tobytes() + bytes([0x60, 40])
+    args = bytes([0x22, len(sift)]) + sift
+    exe = _build_driver(tmp_path)
+    ids, kps, descs = table_rows(Corridor(4, 500, 4, seed=44).images())
+    d = tmp_path / "io"
+    d.mkdir()
+    _write_stencil(d, ids, kps, descs, args)
+    r = subprocess.run([str(exe), "SequentialMatchingGPU", str(d), "4"], capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    opts = oracle.default_options()
+    opts.max_ratio = 0.6
+    opts.min_num_inliers = 40
+    ref_ids, ref_tvgs = oracle.execute_stencil(ids, kps, descs, opts)
+    assert (d / "out_0").read_bytes() == ref_ids
+    assert (d / "out_1").read_bytes() == ref_tvgs
