@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "image-pairs/s + Gdesc-dist/s, 8192×8192-kpt pairs, 1/2/4/8 GPU"
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (spec)
+DEFAULT_BATCH_PAIRS = 8192       # scm_runtime.cpp kDefaultPairsPerBatch (one matcher launch per batch)
 
 # BASELINE.json configs (synthetic stand-ins; no dataset is present).
 WORKLOADS = {
@@ -69,10 +70,14 @@ def cpu_baseline(corridor, npairs: int, overlap: int) -> dict:
         return None
     oracle.lib()
 
+    lat = [0.0] * len(pairs)
+
     def work(k):
         i, j = pairs[k]
+        t = time.perf_counter()
         m = oracle.match_pair(imgs[i][2], imgs[j][2])
         oracle.verify_pair(imgs[i][1], imgs[j][1], m, imgs[i][0], imgs[j][0])
+        lat[k] = time.perf_counter() - t
 
     threads = [threading.Thread(target=work, args=(k,)) for k in range(len(pairs))]
     t0 = time.perf_counter()
@@ -83,9 +88,35 @@ def cpu_baseline(corridor, npairs: int, overlap: int) -> dict:
     dt = time.perf_counter() - t0
     n1 = imgs[0][2].shape[0]
     return {"value": len(pairs) / dt, "unit": "image-pairs/s", "cores": len(pairs),
-            "kind": "port",
+            "kind": "port", "cpu_model": cpu_model(),
+            "pair_latency_s": round(sum(lat) / len(lat), 2),
             "sample": f"{len(pairs)} pairs (0,1..{len(pairs)}) of {n1}x{n1} kpts, one pair per "
                       f"thread, {dt:.1f} s wall (oracle/oracle.cc, -O3 scalar restatement)"}
+
+
+def cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_traffic(workload: str, kpts: int, images: int):
+    """HBM bytes per matcher launch from the committed rocprofv3 PMC summary
+    of this workload (profiles/rNN_pmc_match.json, profiles/pmc_summary.py),
+    or None when no summary matches the configuration being run."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_match.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    wl = WORKLOADS.get(workload, {})
+    if d.get("workload") != workload or kpts != wl.get("kpts") or images != wl.get("images"):
+        return None
+    return d, os.path.relpath(files[-1], ROOT)
 
 
 def main():
@@ -126,7 +157,11 @@ def main():
         device = torch.device("cuda", local_rank)
         dist.init_process_group("nccl", device_id=device)
     ctx = Context(local_rank if world > 1 else 0)
+    t_load = time.perf_counter()
     ctx.table_load(ids, kps, descs)
+    if torch.cuda.is_available():
+        torch.cuda.synchronize()
+    table_load_ms = (time.perf_counter() - t_load) * 1e3
     del ids, kps, descs
     lr_b, lr_e = row_b - tab_b, row_e - tab_b
 
@@ -183,6 +218,10 @@ def main():
         value = total_pairs * steps / elapsed
         flops_rank = 2.0 * 128.0 * gdesc * steps
         achieved_tf = flops_rank / (match_ms * 1e-3) / 1e12 if match_ms > 0 else None
+        launches = max(1, -(-npairs // DEFAULT_BATCH_PAIRS))
+        avg_n = float(np.mean(n_per_img)) if n_per_img else 0.0
+        alg_bytes_launch = npairs / launches * 2 * avg_n * 128 * 2  # bf16 descriptors of both images
+        pmc = pmc_traffic(args.workload, kpts, per_rank) if world == 1 else None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(corridor, args.cpu_baseline_pairs, overlap)
@@ -210,13 +249,18 @@ def main():
                 "peak": BF16_DENSE_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4) if achieved_tf else None,
-                "traffic": None,
+                "traffic": round(pmc[0]["traffic_bytes_per_launch"]) if pmc else None,
+                "traffic_source": (f"{pmc[1]}: FETCH_SIZE x2 + WRITE_SIZE per launch, "
+                                   f"separate rocprofv3 --pmc passes") if pmc else None,
+                "algorithmic_bytes_per_launch": round(alg_bytes_launch),
                 "algorithmic": "2*N1*N2*128 flop per pair; per-launch time from HIP events",
             },
             "stage_ms_per_step": {"match": round(match_ms / steps, 3),
                                   "finalize": round(final_ms / steps, 3),
                                   "verify": round(verify_ms / steps, 3)},
             "cpu_baseline": cpu,
+            "table_load_ms": round(table_load_ms, 1),
+            "pcie_inclusive_pairs_per_s": round(total_pairs / (elapsed / steps + table_load_ms * 1e-3), 2),
             "gen_s": round(gen_s, 1),
         }
         print(json.dumps(out), flush=True)

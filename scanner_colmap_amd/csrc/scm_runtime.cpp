@@ -295,6 +295,36 @@ VerifyParams make_params(const scm_matching_options& o) {
 
 size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 
+// XCD-aware job order.  Workgroups are dispatched round-robin over the 8
+// XCDs (workgroup b -> XCD b mod 8), each XCD with its own L2.  The jobs of
+// one pivot run (its row blocks, which all sweep the same neighbour
+// descriptors) are kept on one XCD so that the neighbour tiles are fetched
+// into that XCD's L2 once instead of once per XCD; the runs are spread over
+// the XCDs by work (least-loaded first) and the queues interleaved, padding
+// with empty jobs.
+void xcd_order(std::vector<MatchJob>& jobs, const std::vector<PairDesc>& pds) {
+  if (jobs.size() <= (size_t)kXcds) return;
+  std::vector<std::vector<MatchJob>> q(kXcds);
+  std::vector<double> load(kXcds, 0.0);
+  for (size_t i = 0; i < jobs.size();) {
+    size_t j = i;
+    while (j < jobs.size() && jobs[j].a_row == jobs[i].a_row && jobs[j].pair0 == jobs[i].pair0) ++j;
+    double cols = 0.0;
+    for (int32_t k = 0; k < jobs[i].npairs; ++k) cols += pds[jobs[i].pair0 + k].n2;
+    const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
+    load[x] += cols * (double)(j - i);
+    q[x].insert(q[x].end(), jobs.begin() + i, jobs.begin() + j);
+    i = j;
+  }
+  size_t len = 0;
+  for (const auto& v : q) len = std::max(len, v.size());
+  MatchJob empty;
+  std::memset(&empty, 0, sizeof(empty));
+  jobs.assign(len * kXcds, empty);
+  for (int x = 0; x < kXcds; ++x)
+    for (size_t k = 0; k < q[x].size(); ++k) jobs[k * kXcds + x] = q[x][k];
+}
+
 // Stage 1 of a batch, on the matching stream: upload the pair descriptors,
 // run the tile + finalize kernels (or upload the given matches of the single
 // pair specs[0]), and copy the match counts into the mapped result buffer.
@@ -372,6 +402,8 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
     i = j;
   }
   bs.slots = mo;
+  xcd_order(jobs, pds);
+  xcd_order(jobs_clamp, pds);
   const int64_t nfast = (int64_t)jobs.size();
   jobs.insert(jobs.end(), jobs_clamp.begin(), jobs_clamp.end());
   const int64_t NJ = (int64_t)jobs.size();
