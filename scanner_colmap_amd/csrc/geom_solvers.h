@@ -599,6 +599,79 @@ SCM_HD inline int fundamental_7pt(const double* x1, const double* x2,
   return nm;
 }
 
+// Parallel-order Jacobi for the 9 x 9 normal equations.  Sweeps cover the
+// 36 index pairs in 9 rounds of 4 disjoint pairs (round-robin: round r
+// leaves index r idle and pairs (r + i) mod 9 with (r - i) mod 9, i = 1..4),
+// and the 4 rotations of a round are applied together: their parameters come
+// from the same matrix, then all column updates (B = A J), then all row
+// updates (A' = J^T B), then the rotated off-diagonal entries are zeroed.
+// Rotations of a round are independent, so a GPU wavefront evaluates the four
+// (expensive, latency-bound) parameter chains at once; the arithmetic of
+// every entry is fixed by this definition, so host and device agree bit for
+// bit.  A pair whose off-diagonal entry is zero uses (c, s) = (1, 0).
+SCM_HD inline void jacobi9_round_pairs(int r, int* P, int* Q) {
+SCM_UNROLL
+  for (int i = 0; i < 4; ++i) {
+    const int a = (r + 1 + i) % 9, b = (r + 8 - i) % 9;
+    P[i] = a < b ? a : b;
+    Q[i] = a < b ? b : a;
+  }
+}
+
+SCM_HD inline int jacobi9_par_eigen_min(double* a, double* v) {
+  for (int r = 0; r < 9; ++r)
+    for (int c = 0; c < 9; ++c) v[r * 9 + c] = (r == c) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < kJacobiMaxSweeps; ++sweep) {
+    double off = 0.0, diag = 0.0;
+    for (int p = 0; p < 9; ++p) {
+      diag += a[p * 9 + p] * a[p * 9 + p];
+      for (int q = p + 1; q < 9; ++q) off += a[p * 9 + q] * a[p * 9 + q];
+    }
+    if (off <= 1e-36 * diag || off == 0.0) break;
+    for (int r = 0; r < 9; ++r) {
+      int P[4], Q[4];
+      double C[4], S[4];
+      jacobi9_round_pairs(r, P, Q);
+      for (int i = 0; i < 4; ++i) {
+        const double apq = a[P[i] * 9 + Q[i]];
+        if (apq == 0.0) {
+          C[i] = 1.0;
+          S[i] = 0.0;
+        } else {
+          jacobi_params(a[P[i] * 9 + P[i]], a[Q[i] * 9 + Q[i]], apq, &C[i], &S[i]);
+        }
+      }
+      for (int k = 0; k < 9; ++k)
+        for (int i = 0; i < 4; ++i) {
+          const double akp = a[k * 9 + P[i]], akq = a[k * 9 + Q[i]];
+          a[k * 9 + P[i]] = C[i] * akp - S[i] * akq;
+          a[k * 9 + Q[i]] = S[i] * akp + C[i] * akq;
+          const double vkp = v[k * 9 + P[i]], vkq = v[k * 9 + Q[i]];
+          v[k * 9 + P[i]] = C[i] * vkp - S[i] * vkq;
+          v[k * 9 + Q[i]] = S[i] * vkp + C[i] * vkq;
+        }
+      for (int i = 0; i < 4; ++i)
+        for (int k = 0; k < 9; ++k) {
+          const double bpk = a[P[i] * 9 + k], bqk = a[Q[i] * 9 + k];
+          a[P[i] * 9 + k] = C[i] * bpk - S[i] * bqk;
+          a[Q[i] * 9 + k] = S[i] * bpk + C[i] * bqk;
+        }
+      for (int i = 0; i < 4; ++i) {
+        a[P[i] * 9 + Q[i]] = 0.0;
+        a[Q[i] * 9 + P[i]] = 0.0;
+      }
+    }
+  }
+  int best = 0;
+  double bv = a[0];
+  for (int j = 1; j < 9; ++j)
+    if (a[j * 9 + j] < bv) {
+      bv = a[j * 9 + j];
+      best = j;
+    }
+  return best;
+}
+
 // Least-squares null vector of a packed A^T A (45 entries) via Jacobi.
 SCM_HD inline void ata_null_vector(const double* ata45, double* out9) {
   double a[81], v[81];
@@ -609,7 +682,7 @@ SCM_HD inline void ata_null_vector(const double* ata45, double* out9) {
       a[q * 9 + p] = ata45[k];
       ++k;
     }
-  const int jmin = jacobi_eigen_min<9>(a, v);
+  const int jmin = jacobi9_par_eigen_min(a, v);
   for (int i = 0; i < 9; ++i) out9[i] = v[i * 9 + jmin];
 }
 

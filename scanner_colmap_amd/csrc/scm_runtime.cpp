@@ -978,6 +978,18 @@ void scm_context_destroy(scm_context* ctx) {
     for (int j = 0; j < 18; ++j)
       std::fprintf(stderr, "  %-10s %14.1f\n", names[j],
                    (double)ctx->prof_sum[j] / (double)ctx->prof_pairs);
+    static const char* rnames[] = {"windows", "n_cand", "n_tie", "n_newbest", "n_lo_iter",
+                                   "cyc_cand", "cyc_tie", "cyc_lo", "cyc_total", "trials"};
+    for (int kind = 0; kind < 2; ++kind)
+      for (int j = 0; j < 10; ++j)
+        std::fprintf(stderr, "  replay %s %-10s %14.1f\n", kind ? "H" : "F", rnames[j],
+                     (double)ctx->prof_sum[20 + 10 * kind + j] / (double)ctx->prof_pairs);
+    static const char* lnames[] = {"lo_gather", "lo_norm", "lo_ata", "lo_jacobi", "lo_resid",
+                                   "lo_inliers"};
+    for (int kind = 0; kind < 2; ++kind)
+      for (int j = 0; j < 6; ++j)
+        std::fprintf(stderr, "  LO %s %-10s %14.1f\n", kind ? "H" : "F", lnames[j],
+                     (double)ctx->prof_sum[40 + 10 * kind + j] / (double)ctx->prof_pairs);
   }
   ctx->table.release();
   ctx->scratch_table.release();

@@ -713,11 +713,91 @@ __device__ int gather_inliers(const double* res, int n, double maxr, const doubl
   return base_out;
 }
 
-// LDS twin of jacobi_eigen_min<9> (geom_solvers.h): the 9x9 matrices live
-// in LDS, lane k < 9 owns row k for the column / V updates and column k for
-// the row update; identical operations in identical order.  Returns the
-// eigenvector of the smallest eigenvalue in f (every lane).
-__device__ void jacobi9_wave(const double* ata45, double* A, double* V, double* f) {
+// ---------------------------------------------------------------------------
+// Point loops of the windowed replay (candidate residuals and local
+// optimisation) on the packed fp32 copy of the matches (xyf: x1, y1, x2, y2
+// per point; keypoints are float32, so widening to double reproduces the
+// reference's Eigen::Vector2d values exactly).  Each lane keeps kLoU loads in
+// flight; items are still consumed in index order per lane, so every
+// canonical-order sum performs the same additions as before.
+// ---------------------------------------------------------------------------
+constexpr int kLoU = 4;
+
+__device__ __forceinline__ void load_pts(const float4* p, int b, int n, float4 (&v)[kLoU]) {
+#pragma unroll
+  for (int u = 0; u < kLoU; ++u) {
+    const int i = b + 64 * u;
+    v[u] = i < n ? p[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// apply_normalize (geom_solvers.h) for a transform with last row (0, 0, 1):
+// np2 = 0 p0 + 0 p1 + 1 is exactly 1 and the homogeneous divide by it is the
+// identity, so it is skipped (same values bit for bit).
+__device__ __forceinline__ void apply_norm_affine(const double* T, double p0, double p1,
+                                                  double* o0, double* o1) {
+  *o0 = T[0] * p0 + T[1] * p1 + T[2];
+  *o1 = T[3] * p0 + T[4] * p1 + T[5];
+}
+
+template <int K>
+__device__ int residuals_f4(const double* m, const float4* xyf, int n, double maxr, double* res) {
+  int c = 0;
+  for (int b = threadIdx.x; b < n; b += 64 * kLoU) {
+    float4 v[kLoU];
+    load_pts(xyf, b, n, v);
+#pragma unroll
+    for (int u = 0; u < kLoU; ++u) {
+      const int i = b + 64 * u;
+      if (i < n) {
+        const double r = residual_pt<K>(m, (double)v[u].x, (double)v[u].y, (double)v[u].z,
+                                        (double)v[u].w);
+        res[i] = r;
+        c += (r <= maxr) ? 1 : 0;
+      }
+    }
+  }
+  return wave_sum_i(c);
+}
+
+// Ordered compaction of the points whose residual is <= maxr into xin.
+__device__ int gather_inliers_f4(const double* res, int n, double maxr, const float4* xyf,
+                                 float4* xin) {
+  const int lane = threadIdx.x;
+  int base_out = 0;
+  for (int b0 = 0; b0 < n; b0 += 64 * kLoU) {
+    float4 v[kLoU];
+    double r[kLoU];
+    load_pts(xyf, b0 + lane, n, v);
+#pragma unroll
+    for (int u = 0; u < kLoU; ++u) {
+      const int i = b0 + 64 * u + lane;
+      r[u] = i < n ? res[i] : 1.7976931348623157e308;
+    }
+#pragma unroll
+    for (int u = 0; u < kLoU; ++u) {
+      const bool in = r[u] <= maxr;
+      const uint64_t bal = __ballot(in);
+      if (in) {
+        const int o = base_out + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        xin[o] = v[u];
+      }
+      base_out += __popcll(bal);
+    }
+  }
+  return base_out;
+}
+
+// Wavefront twin of jacobi9_par_eigen_min (geom_solvers.h) on LDS-resident
+// A and V (row-major 9 x 9).  Per round the four rotation parameter chains
+// are evaluated together (every lane, uniform values: the latency of one
+// chain instead of four), then lane (k, i) < 36 applies the column update of
+// pair i to row k of A and V, then lane (i, c) < 36 the row update of pair i
+// at column c, then the rotated off-diagonal entries are zeroed.  Same
+// operations, same order as the host version.  Returns the eigenvector of the
+// smallest eigenvalue in f (every lane).
+__device__ void jacobi9_par_wave(const double* ata45, double* A, double* V, double* f) {
   const int lane = threadIdx.x;
   if (lane < 9) {
 #pragma unroll
@@ -730,44 +810,69 @@ __device__ void jacobi9_wave(const double* ata45, double* A, double* V, double* 
   wsync();
   for (int sweep = 0; sweep < kJacobiMaxSweeps; ++sweep) {
     double off = 0.0, diag = 0.0;
+#pragma unroll
     for (int p = 0; p < 9; ++p) {
       diag += A[p * 9 + p] * A[p * 9 + p];
+#pragma unroll
       for (int q = p + 1; q < 9; ++q) off += A[p * 9 + q] * A[p * 9 + q];
     }
     if (off <= 1e-36 * diag || off == 0.0) break;
-    for (int p = 0; p < 8; ++p) {
-      for (int q = p + 1; q < 9; ++q) {
-        const double apq = A[p * 9 + q];
-        if (apq == 0.0) continue;
-        double c, s;
-        jacobi_params(A[p * 9 + p], A[q * 9 + q], apq, &c, &s);
-        wsync();
-        if (lane < 9) {  // columns p, q of row `lane`
-          const double akp = A[lane * 9 + p], akq = A[lane * 9 + q];
-          A[lane * 9 + p] = c * akp - s * akq;
-          A[lane * 9 + q] = s * akp + c * akq;
-          const double vkp = V[lane * 9 + p], vkq = V[lane * 9 + q];
-          V[lane * 9 + p] = c * vkp - s * vkq;
-          V[lane * 9 + q] = s * vkp + c * vkq;
-        }
-        wsync();
-        if (lane < 9) {  // rows p, q at column `lane`
-          const double apk = A[p * 9 + lane], aqk = A[q * 9 + lane];
-          A[p * 9 + lane] = c * apk - s * aqk;
-          A[q * 9 + lane] = s * apk + c * aqk;
-        }
-        wsync();
-        if (lane == 0) {
-          A[p * 9 + q] = 0.0;
-          A[q * 9 + p] = 0.0;
-        }
-        wsync();
+#pragma unroll 1
+    for (int r = 0; r < 9; ++r) {
+      int P[4], Q[4];
+      jacobi9_round_pairs(r, P, Q);
+      double C[4], S[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const double apq = A[P[i] * 9 + Q[i]];
+        double c, sn;
+        jacobi_params(A[P[i] * 9 + P[i]], A[Q[i] * 9 + Q[i]], apq == 0.0 ? 1.0 : apq, &c, &sn);
+        C[i] = apq == 0.0 ? 1.0 : c;
+        S[i] = apq == 0.0 ? 0.0 : sn;
       }
+      wsync();
+      if (lane < 36) {  // B = A J, V = V J: row k, pair i
+        const int k = lane >> 2, i = lane & 3;
+        const int pi = P[0] * (i == 0) + P[1] * (i == 1) + P[2] * (i == 2) + P[3] * (i == 3);
+        const int qi = Q[0] * (i == 0) + Q[1] * (i == 1) + Q[2] * (i == 2) + Q[3] * (i == 3);
+        const double ci = i == 0 ? C[0] : (i == 1 ? C[1] : (i == 2 ? C[2] : C[3]));
+        const double si = i == 0 ? S[0] : (i == 1 ? S[1] : (i == 2 ? S[2] : S[3]));
+        const double akp = A[k * 9 + pi], akq = A[k * 9 + qi];
+        const double vkp = V[k * 9 + pi], vkq = V[k * 9 + qi];
+        A[k * 9 + pi] = ci * akp - si * akq;
+        A[k * 9 + qi] = si * akp + ci * akq;
+        V[k * 9 + pi] = ci * vkp - si * vkq;
+        V[k * 9 + qi] = si * vkp + ci * vkq;
+      }
+      wsync();
+      if (lane < 36) {  // A' = J^T B: pair i, column c
+        const int i = lane / 9, c = lane - 9 * (lane / 9);
+        const int pi = P[0] * (i == 0) + P[1] * (i == 1) + P[2] * (i == 2) + P[3] * (i == 3);
+        const int qi = Q[0] * (i == 0) + Q[1] * (i == 1) + Q[2] * (i == 2) + Q[3] * (i == 3);
+        const double ci = i == 0 ? C[0] : (i == 1 ? C[1] : (i == 2 ? C[2] : C[3]));
+        const double si = i == 0 ? S[0] : (i == 1 ? S[1] : (i == 2 ? S[2] : S[3]));
+        const double bpk = A[pi * 9 + c], bqk = A[qi * 9 + c];
+        A[pi * 9 + c] = ci * bpk - si * bqk;
+        A[qi * 9 + c] = si * bpk + ci * bqk;
+      }
+      wsync();
+      if (lane < 4) {
+        const int pi = P[0] * (lane == 0) + P[1] * (lane == 1) + P[2] * (lane == 2) + P[3] * (lane == 3);
+        const int qi = Q[0] * (lane == 0) + Q[1] * (lane == 1) + Q[2] * (lane == 2) + Q[3] * (lane == 3);
+        A[pi * 9 + qi] = 0.0;
+        A[qi * 9 + pi] = 0.0;
+      }
+      wsync();
     }
   }
   int best = 0;
+  double bv = A[0];
+#pragma unroll
   for (int j = 1; j < 9; ++j)
-    if (A[j * 9 + j] < A[best * 9 + best]) best = j;
+    if (A[j * 9 + j] < bv) {
+      bv = A[j * 9 + j];
+      best = j;
+    }
 #pragma unroll
   for (int i = 0; i < 9; ++i) f[i] = V[i * 9 + best];
 }
@@ -879,8 +984,121 @@ __device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const doub
   ata_pass_wave<K, 2>(s, xin1, xin2, n, T1, T2);
   wsync();
   double f[9];
-  jacobi9_wave(s.ata, s.jA, s.jV, f);
+  jacobi9_par_wave(s.ata, s.jA, s.jV, f);
   wsync();
+  if (K == KIND_F) fundamental_8pt_finish(f, T1, T2, model);
+  else homography_finish(f, T1, T2, model);
+}
+
+// normalize_pair_wave on packed points (canonical sums, same order).
+__device__ void normalize_pair_f4(const float4* xin, int n, double* T1, double* T2) {
+  double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
+  for (int b = threadIdx.x; b < n; b += 64 * kLoU) {
+    float4 v[kLoU];
+    load_pts(xin, b, n, v);
+#pragma unroll
+    for (int u = 0; u < kLoU; ++u)
+      if (b + 64 * u < n) {
+        p0 += (double)v[u].x;
+        p1 += (double)v[u].y;
+        p2 += (double)v[u].z;
+        p3 += (double)v[u].w;
+      }
+  }
+  const double c10 = canon_tree_wave(p0) / (double)n, c11 = canon_tree_wave(p1) / (double)n;
+  const double c20 = canon_tree_wave(p2) / (double)n, c21 = canon_tree_wave(p3) / (double)n;
+  p0 = kCanonZero;
+  p1 = kCanonZero;
+  for (int b = threadIdx.x; b < n; b += 64 * kLoU) {
+    float4 v[kLoU];
+    load_pts(xin, b, n, v);
+#pragma unroll
+    for (int u = 0; u < kLoU; ++u)
+      if (b + 64 * u < n) {
+        const double d0 = (double)v[u].x - c10, d1 = (double)v[u].y - c11;
+        const double e0 = (double)v[u].z - c20, e1 = (double)v[u].w - c21;
+        p0 += d0 * d0 + d1 * d1;
+        p1 += e0 * e0 + e1 * e1;
+      }
+  }
+  const double rms1 = sqrt(canon_tree_wave(p0) / (double)n);
+  const double rms2 = sqrt(canon_tree_wave(p1) / (double)n);
+  const double s1 = sqrt(2.0) / rms1, s2 = sqrt(2.0) / rms2;
+  T1[0] = s1; T1[1] = 0.0; T1[2] = -s1 * c10;
+  T1[3] = 0.0; T1[4] = s1; T1[5] = -s1 * c11;
+  T1[6] = 0.0; T1[7] = 0.0; T1[8] = 1.0;
+  T2[0] = s2; T2[1] = 0.0; T2[2] = -s2 * c20;
+  T2[3] = 0.0; T2[4] = s2; T2[5] = -s2 * c21;
+  T2[6] = 0.0; T2[7] = 0.0; T2[8] = 1.0;
+}
+
+// ata_pass_wave on packed points.
+template <int K, int PASS>
+__device__ __forceinline__ void ata_pass_f4(VerifyLds& s, const float4* xin, int n,
+                                            const double* T1, const double* T2) {
+  const int lane = threadIdx.x;
+  double part[15];
+#pragma unroll
+  for (int k = 0; k < 15; ++k) part[k] = kCanonZero;
+#pragma unroll 1
+  for (int b = lane; b < n; b += 64 * kLoU) {
+    float4 v[kLoU];
+    load_pts(xin, b, n, v);
+#pragma unroll
+    for (int u = 0; u < kLoU; ++u) {
+      if (b + 64 * u >= n) break;
+      double x0, y0, x1, y1;
+      apply_norm_affine(T1, (double)v[u].x, (double)v[u].y, &x0, &y0);
+      apply_norm_affine(T2, (double)v[u].z, (double)v[u].w, &x1, &y1);
+      double a[9], c[9];
+      if (K == KIND_F) f_row(x0, y0, x1, y1, a);
+      else h_rows(x0, y0, x1, y1, a, c);
+      int k = 0;
+#pragma unroll
+      for (int p = 0; p < 9; ++p)
+#pragma unroll
+        for (int q = p; q < 9; ++q) {
+          if (k >= 15 * PASS && k < 15 * PASS + 15)
+            part[k - 15 * PASS] = part[k - 15 * PASS] + a[p] * a[q];
+          ++k;
+        }
+      if (K == KIND_H) {
+        k = 0;
+#pragma unroll
+        for (int p = 0; p < 9; ++p)
+#pragma unroll
+          for (int q = p; q < 9; ++q) {
+            if (k >= 15 * PASS && k < 15 * PASS + 15)
+              part[k - 15 * PASS] = part[k - 15 * PASS] + c[p] * c[q];
+            ++k;
+          }
+      }
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 15; ++k) {
+    const double t = canon_tree_wave(part[k]);
+    if (lane == 0) s.ata[15 * PASS + k] = t;
+  }
+}
+
+// local_estimate_wave (F: 8-point, H: DLT) on packed points.
+template <int K>
+__device__ void local_estimate_f4(VerifyLds& s, const float4* xin, int n, double* model,
+                                  uint64_t* pl = nullptr) {
+  uint64_t t0 = pl ? __builtin_amdgcn_s_memtime() : 0;
+  double T1[9], T2[9];
+  normalize_pair_f4(xin, n, T1, T2);
+  if (pl && threadIdx.x == 0) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[1] += t - t0; t0 = t; }
+  ata_pass_f4<K, 0>(s, xin, n, T1, T2);
+  ata_pass_f4<K, 1>(s, xin, n, T1, T2);
+  ata_pass_f4<K, 2>(s, xin, n, T1, T2);
+  wsync();
+  if (pl && threadIdx.x == 0) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[2] += t - t0; t0 = t; }
+  double f[9];
+  jacobi9_par_wave(s.ata, s.jA, s.jV, f);
+  wsync();
+  if (pl && threadIdx.x == 0) pl[3] += __builtin_amdgcn_s_memtime() - t0;
   if (K == KIND_F) fundamental_8pt_finish(f, T1, T2, model);
   else homography_finish(f, T1, T2, model);
 }
@@ -1504,7 +1722,7 @@ __global__ __launch_bounds__(64) void rs_begin_kernel(
 // indices (RandomSampler::Sample); the PRNG state before each round of 64 is
 // kept in wsnap for the abort rewind, the state after the window in snaps.
 template <int K>
-__global__ __launch_bounds__(64) void rs_sample_kernel(
+__global__ __launch_bounds__(64) void rs_draw_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, RansacState* __restrict__ rst,
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
@@ -1523,12 +1741,6 @@ __global__ __launch_bounds__(64) void rs_sample_kernel(
     const int Btot = min(kTrialBatch * W, rst[q].max_trials - rst[q].trial);
     wsync();
     mt_load(s, ps.state);
-    // The sample-index vector lives in LDS for the window (dynamic LDS after
-    // VerifyLds) and goes back to the pair's scratch afterwards.
-    uint16_t* gsidx = pair_sidx(ps);
-    uint16_t* sidx = reinterpret_cast<uint16_t*>(dyn_lds + sizeof(VerifyLds));
-    for (int i = lane; i < n; i += 64) sidx[i] = gsidx[i];
-    wsync();
     uint16_t* sq = samp + (int64_t)q * kWindowTrials * 8;
     for (int w = 0; w * kTrialBatch < Btot; ++w) {
       const int B = min(kTrialBatch, Btot - w * kTrialBatch);
@@ -1536,34 +1748,123 @@ __global__ __launch_bounds__(64) void rs_sample_kernel(
       for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
       if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
       wsync();
-      if (draw_targets_wave<Tr::kmin>(s, B * Tr::kmin, (uint32_t)n)) {
-        if (lane == 0) shuffle_batch_lane0<Tr::kmin>(s, sidx, B);
-      } else {  // a draw may need rejection sampling: serial draws from the snapshot
+      if (!draw_targets_wave<Tr::kmin>(s, B * Tr::kmin, (uint32_t)n)) {
+        // A draw may need Lemire's rejection step: serial draws from the
+        // round's snapshot (the targets do not depend on the shuffle state).
         for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
         wsync();
         if (lane == 0) {
           s.mt_idx = (int32_t)snap[624];
           const uint32_t last = (uint32_t)(n - 1);
-          for (int b = 0; b < B; ++b)
-            for (int i = 0; i < Tr::kmin; ++i) {
-              const uint32_t j = uniform_u32(s, (uint32_t)i, last);
-              const uint16_t t = sidx[i];
-              sidx[i] = sidx[j];
-              sidx[j] = t;
-              s.samples[b][i] = sidx[i];
-            }
+          for (int r = 0; r < B * Tr::kmin; ++r)
+            s.jbuf[r] = (uint16_t)uniform_u32(s, (uint32_t)(r % Tr::kmin), last);
         }
       }
       wsync();
-      for (int i = lane; i < B * 8; i += 64) sq[w * kTrialBatch * 8 + i] = s.samples[i >> 3][i & 7];
+      for (int r = lane; r < B * Tr::kmin; r += 64)
+        sq[(w * kTrialBatch + r / Tr::kmin) * 8 + r % Tr::kmin] = s.jbuf[r];
       wsync();
     }
     mt_save(s, ps.state);
-    for (int i = lane; i < n; i += 64) gsidx[i] = sidx[i];
     uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3;
     for (int i = lane; i < Btot * 3; i += 64) cq[i] = 0u;
     if (lane == 0) rst[q].B = Btot;
   }
+}
+
+// RandomSampler::Sample's Shuffle for every trial of the window, one thread
+// per pair (the swaps of one pair are a sequential chain; 64 pairs advance
+// together in a wavefront).  The targets drawn by rs_draw_kernel are read
+// from samp and replaced by the trial's sample.  The kmin hot positions live
+// in registers.  The loop is software-pipelined: the cold values of trial
+// b + 1 are loaded before trial b stores its own, and then corrected for any
+// position trial b wrote (forwarding), so one memory latency covers a trial.
+template <int K>
+__global__ __launch_bounds__(64) void rs_shuffle_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
+    const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
+    const int32_t* __restrict__ nact, uint16_t* __restrict__ samp) {
+  using Tr = KindTraits<K>;
+  constexpr int KM = Tr::kmin;
+  const int na = *nact;
+  const int a = blockIdx.x * 64 + threadIdx.x;
+  if (a >= na) return;
+  const int q = act[a];
+  const PairSetup ps = pair_at(pairs, q, scratch, snaps, out);
+  uint16_t* sidx = pair_sidx(ps);
+  const int Btot = rst[q].B;
+  uint16_t* sq = samp + (int64_t)q * kWindowTrials * 8;
+  uint32_t R[KM];
+#pragma unroll
+  for (int i = 0; i < KM; ++i) R[i] = sidx[i];
+  uint32_t j[KM], v[KM], jb[KM];
+  auto load_targets = [&](int b, uint32_t (&t)[KM]) {
+    const uint4 raw = *reinterpret_cast<const uint4*>(sq + b * 8);
+    const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int i = 0; i < KM; ++i) t[i] = (wv[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+  };
+  // Pipeline: targets two trials ahead, cold values one trial ahead.
+#pragma unroll
+  for (int i = 0; i < KM; ++i) j[i] = jb[i] = v[i] = 0u;
+  if (Btot > 0) {
+    load_targets(0, j);
+#pragma unroll
+    for (int i = 0; i < KM; ++i) v[i] = j[i] >= (uint32_t)KM ? sidx[j[i]] : 0u;
+  }
+  if (Btot > 1) load_targets(1, jb);
+  for (int b = 0; b < Btot; ++b) {
+    uint32_t jc[KM], vn[KM];
+#pragma unroll
+    for (int i = 0; i < KM; ++i) jc[i] = vn[i] = 0u;
+    if (b + 2 < Btot) load_targets(b + 2, jc);
+    if (b + 1 < Btot) {
+#pragma unroll
+      for (int i = 0; i < KM; ++i) vn[i] = jb[i] >= (uint32_t)KM ? sidx[jb[i]] : 0u;
+    }
+    uint32_t w[KM];
+#pragma unroll
+    for (int i = 0; i < KM; ++i) {
+      w[i] = 0xFFFFFFFFu;
+      if (j[i] < (uint32_t)KM) {  // hot swap R[i] <-> R[j] (j >= i)
+        uint32_t rj = R[i];
+#pragma unroll
+        for (int t = 0; t < KM; ++t) rj = (t == (int)j[i]) ? R[t] : rj;
+#pragma unroll
+        for (int t = 0; t < KM; ++t) R[t] = (t == (int)j[i]) ? R[i] : R[t];
+        R[i] = rj;
+      } else {
+        uint32_t cur = v[i];
+#pragma unroll
+        for (int i2 = 0; i2 < i; ++i2) cur = (j[i2] == j[i]) ? w[i2] : cur;
+        w[i] = R[i];
+        sidx[j[i]] = (uint16_t)R[i];
+        R[i] = cur;
+      }
+    }
+    uint32_t ow[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < KM; ++i) ow[i >> 1] |= (R[i] & 0xFFFFu) << (16 * (i & 1));
+    *reinterpret_cast<uint4*>(sq + b * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+    // Forward this trial's cold writes into the next trial's loaded values
+    // (the last write to a position wins).
+#pragma unroll
+    for (int i = 0; i < KM; ++i) {
+      uint32_t val = vn[i];
+#pragma unroll
+      for (int i2 = 0; i2 < KM; ++i2) val = (w[i2] != 0xFFFFFFFFu && j[i2] == jb[i]) ? w[i2] : val;
+      vn[i] = val;
+    }
+#pragma unroll
+    for (int i = 0; i < KM; ++i) {
+      v[i] = vn[i];
+      j[i] = jb[i];
+      jb[i] = jc[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < KM; ++i) sidx[i] = (uint16_t)R[i];
 }
 
 // Minimal solvers, one thread per hypothesis of the window, plus the fp32
@@ -1707,14 +2008,14 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
 // The sequential part of one window, in trial order, for every active pair.
 template <int K>
 __global__ __launch_bounds__(64) void rs_replay_kernel(
-    const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
-    const double* __restrict__ xy2_all, double* __restrict__ scratch,
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
     RansacState* __restrict__ rst, const int32_t* __restrict__ act,
     const int32_t* __restrict__ nact, int32_t* __restrict__ act_next,
     int32_t* __restrict__ nact_next, const int32_t* __restrict__ nmod,
     const uint32_t* __restrict__ cnts, const double* __restrict__ mods,
-    const uint32_t* __restrict__ wsnap, VerifyParams P) {
+    const uint32_t* __restrict__ wsnap, VerifyParams P, uint64_t* __restrict__ prof,
+    const float4* __restrict__ xyf_all) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
@@ -1724,14 +2025,21 @@ __global__ __launch_bounds__(64) void rs_replay_kernel(
   const int na = *nact;
   for (int a = blockIdx.x; a < na; a += gridDim.x) {
     const int q = act[a];
+    // Diagnostic counters (SCM_PROFILE=1 only): windows, candidates, ties,
+    // new bests, LO iterations; cycles in candidate residuals, tie sums, LO,
+    // whole replay.
+    uint64_t* pc = prof ? prof + (int64_t)q * kVerifyProfSlots + (K == KIND_F ? 20 : 30) : nullptr;
+    const uint64_t t_enter = pc ? __builtin_amdgcn_s_memtime() : 0;
+    if (pc && lane == 0) pc[0] += 1;
     const PairSetup ps = pair_at(pairs, q, scratch, snaps, out);
     const int n = ps.n;
-    const double* xy1 = xy1_all + ps.pp.pts_off;
-    const double* xy2 = xy2_all + ps.pp.pts_off;
     double* base = ps.base;
     double* res[2] = {base, base + n};
-    double* xin1 = base + 2 * n;
-    double* xin2 = base + 4 * n;
+    const float4* xyf = xyf_all + ps.pp.pts_off / 2;
+    // compacted inliers (packed fp32) in the scratch after the two residual
+    // buffers, 16-B aligned
+    float4* xin = reinterpret_cast<float4*>(
+        (reinterpret_cast<uintptr_t>(base + 2 * n) + 15) & ~(uintptr_t)15);
     const double* mq = mods + (int64_t)q * kWindowTrials * 3 * MS;
     RansacState st = rst[q];
     wsync();
@@ -1762,19 +2070,32 @@ __global__ __launch_bounds__(64) void rs_replay_kernel(
             const int c = (int)s.counts[t * MM + k];
             const int bn = s.best_n;
             if (c >= bn) {
+              uint64_t t0 = pc ? __builtin_amdgcn_s_memtime() : 0;
               double mk[MS];
               const double* src = mq + ((r0 + t) * MM + k) * MS;
 #pragma unroll
               for (int j = 0; j < MS; ++j) mk[j] = src[j];
               double* rt = res[best_sel ^ 1];
-              residuals_wave<K>(mk, xy1, xy2, n, maxr, rt);
+              residuals_f4<K>(mk, xyf, n, maxr, rt);
               bool better = c > bn;
               double sum = 0.0;
+              if (pc && lane == 0) {
+                const uint64_t t1 = __builtin_amdgcn_s_memtime();
+                pc[1] += 1;
+                pc[5] += t1 - t0;
+                t0 = t1;
+              }
               if (!better) {  // tie on the inlier count: Compare the residual sums
                 sum = seq_inlier_sum(rt, n, maxr);
                 ensure_best_sum(s, res[best_sel], n, maxr);
                 better = sum < s.best_sum;
+                if (pc && lane == 0) {
+                  pc[2] += 1;
+                  pc[6] += __builtin_amdgcn_s_memtime() - t0;
+                }
               }
+              if (pc && lane == 0 && better) pc[3] += 1;
+              const uint64_t t_lo = pc ? __builtin_amdgcn_s_memtime() : 0;
               if (better) {
                 wsync();
                 if (lane == 0) {
@@ -1789,12 +2110,18 @@ __global__ __launch_bounds__(64) void rs_replay_kernel(
                 // Recursive local optimisation.
                 if (c > Tr::kmin && c >= Tr::kmin_local) {
                   for (int lt = 0; lt < 10; ++lt) {
-                    const int ni = gather_inliers(res[best_sel], n, maxr, xy1, xy2, xin1, xin2);
+                    if (pc && lane == 0) pc[4] += 1;
+                    uint64_t* pl = pc ? pc + 20 : nullptr;
+                    uint64_t tl0 = pl ? __builtin_amdgcn_s_memtime() : 0;
+                    const int ni = gather_inliers_f4(res[best_sel], n, maxr, xyf, xin);
+                    if (pl && lane == 0) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[0] += t - tl0; tl0 = t; pl[5] += ni; }
                     double lm[9];
-                    local_estimate_wave<K>(s, xin1, xin2, ni, lm);
+                    local_estimate_f4<K>(s, xin, ni, lm, pl);
+                    if (pl && lane == 0) tl0 = __builtin_amdgcn_s_memtime();
                     const int prev = s.best_n;
                     double* rl = res[best_sel ^ 1];
-                    const int lcn = residuals_wave<K>(lm, xy1, xy2, n, maxr, rl);
+                    const int lcn = residuals_f4<K>(lm, xyf, n, maxr, rl);
+                    if (pl && lane == 0) pl[4] += __builtin_amdgcn_s_memtime() - tl0;
                     bool lbetter = lcn > prev;
                     double lsum = 0.0;
                     if (lcn == prev) {
@@ -1821,6 +2148,7 @@ __global__ __launch_bounds__(64) void rs_replay_kernel(
                                    num_trials((uint64_t)s.best_n, (uint64_t)n, P.confidence,
                                               P.dyn_num_trials_multiplier, Tr::kmin));
               }
+              if (pc && lane == 0) pc[7] += __builtin_amdgcn_s_memtime() - t_lo;
             }
             if (tt >= dyn_max && tt >= P.min_num_trials) {
               abort = true;
@@ -1864,6 +2192,10 @@ __global__ __launch_bounds__(64) void rs_replay_kernel(
     if (lane == 0) rst[q] = st;
     if (st.done) rs_finish<K>(ps, st, masks, maxr);
     else if (lane == 0) act_next[atomicAdd(nact_next, 1)] = q;
+    if (pc && lane == 0) {
+      pc[8] += __builtin_amdgcn_s_memtime() - t_enter;
+      pc[9] += (uint64_t)Btot;
+    }
   }
 }
 
@@ -1921,26 +2253,27 @@ template <int K>
 hipError_t run_rounds(const VerifyPair* pairs, int npairs, const double* xy1, const double* xy2,
                       double* scratch, uint32_t* snaps, uint8_t* masks, VerifyOut* out,
                       const VerifyParams& P, const float4* xyf, const VerifyRoundBufs& rb,
-                      int max_chunks, int max_m, hipStream_t stream) {
+                      int max_chunks, int max_m, uint64_t* prof, hipStream_t stream) {
   const size_t lds = sizeof(VerifyLds);
-  const size_t lds_sample = lds + (size_t)((max_m + 7) / 8 * 8) * sizeof(uint16_t);
   const int max_trials = K == KIND_F ? P.max_trials_F : P.max_trials_H;
   const int gw = npairs < 4096 ? npairs : 4096;
   int covered = 0, W = 1, r = 0;
   while (covered < max_trials) {
     const int cur = r & 1, nxt = cur ^ 1;
-    hipLaunchKernelGGL(rs_sample_kernel<K>, dim3(gw), dim3(64), lds_sample, stream, pairs, scratch,
-                       snaps, out, rb.rst, rb.act[cur], rb.nact + cur, rb.nact + nxt, rb.samp,
-                       rb.cnts, rb.wsnap, W);
+    hipLaunchKernelGGL(rs_draw_kernel<K>, dim3(gw), dim3(64), lds, stream, pairs, scratch, snaps,
+                       out, rb.rst, rb.act[cur], rb.nact + cur, rb.nact + nxt, rb.samp, rb.cnts,
+                       rb.wsnap, W);
+    hipLaunchKernelGGL(rs_shuffle_kernel<K>, dim3((npairs + 63) / 64), dim3(64), 0, stream, pairs,
+                       scratch, snaps, out, rb.rst, rb.act[cur], rb.nact + cur, rb.samp);
     hipLaunchKernelGGL(rs_solve_kernel<K>, dim3(4096), dim3(64), 0, stream, pairs, xy1, xy2,
                        rb.rst, rb.act[cur], rb.nact + cur, rb.samp, rb.nmod, rb.fcon, rb.mods, W,
                        P.max_residual);
     hipLaunchKernelGGL(rs_score_kernel<K>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs, xyf,
                        rb.rst, rb.act[cur], rb.nact + cur, rb.nmod, rb.fcon, rb.mods, rb.cnts,
                        max_chunks, P.max_residual);
-    hipLaunchKernelGGL(rs_replay_kernel<K>, dim3(gw), dim3(64), lds, stream, pairs, xy1, xy2,
-                       scratch, snaps, out, masks, rb.rst, rb.act[cur], rb.nact + cur,
-                       rb.act[nxt], rb.nact + nxt, rb.nmod, rb.cnts, rb.mods, rb.wsnap, P);
+    hipLaunchKernelGGL(rs_replay_kernel<K>, dim3(gw), dim3(64), lds, stream, pairs, scratch, snaps, out, masks, rb.rst, rb.act[cur], rb.nact + cur,
+                       rb.act[nxt], rb.nact + nxt, rb.nmod, rb.cnts, rb.mods, rb.wsnap, P, prof,
+                       xyf);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     covered += W * kTrialBatch;
@@ -1962,8 +2295,8 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   if (!attr) {
     set_lds_attr(rs_begin_kernel<KIND_F>);
     set_lds_attr(rs_begin_kernel<KIND_H>);
-    set_lds_attr(rs_sample_kernel<KIND_F>);
-    set_lds_attr(rs_sample_kernel<KIND_H>);
+    set_lds_attr(rs_draw_kernel<KIND_F>);
+    set_lds_attr(rs_draw_kernel<KIND_H>);
     set_lds_attr(rs_replay_kernel<KIND_F>);
     set_lds_attr(rs_replay_kernel<KIND_H>);
     set_lds_attr(verify_final_kernel);
@@ -1978,14 +2311,14 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   hipLaunchKernelGGL(rs_begin_kernel<KIND_F>, dim3(gw), dim3(64), lds, stream, pairs, npairs,
                      scratch, snaps, out, masks, xyf, rb.rst, rb.act[0], rb.nact, params);
   if ((err = run_rounds<KIND_F>(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf,
-                                rb, max_chunks, max_m, stream)) != hipSuccess)
+                                rb, max_chunks, max_m, prof, stream)) != hipSuccess)
     return err;
   // H: LORANSAC<H, H> on the same PRNG streams.
   if ((err = hipMemsetAsync(rb.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
   hipLaunchKernelGGL(rs_begin_kernel<KIND_H>, dim3(gw), dim3(64), lds, stream, pairs, npairs,
                      scratch, snaps, out, masks, xyf, rb.rst, rb.act[0], rb.nact, params);
   if ((err = run_rounds<KIND_H>(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf,
-                                rb, max_chunks, max_m, stream)) != hipSuccess)
+                                rb, max_chunks, max_m, prof, stream)) != hipSuccess)
     return err;
   hipLaunchKernelGGL(verify_final_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
                      xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
