@@ -14,11 +14,15 @@ constexpr int kIter = 2048;
 #define MAXU(d, a) asm volatile("v_max_u32 %0, %1, %0" : "+v"(d) : "v"(a))
 #define LSHLOR(d, a, s) asm volatile("v_lshl_or_b32 %0, %1, 9, %2" : "=v"(d) : "v"(a), "s"(s))
 #define ADDU(d, a) asm volatile("v_add_u32 %0, %1, %0" : "+v"(d) : "v"(a))
+#define FMAF(d, a) asm volatile("v_fma_f32 %0, %1, %1, %0" : "+v"(d) : "v"(a))
+#define PKFMA(d, a) asm volatile("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(d) : "v"(a))
+#define FMA64(d, a) asm volatile("v_fma_f64 %0, %1, %1, %0" : "+v"(d) : "v"(a))
+#define CMPF(a, b) asm volatile("v_cmp_le_f32 vcc, %0, %1" : : "v"(a), "v"(b) : "vcc")
 
 // MODE: 0 max, 1 med3, 2 lshl_or, 3 add, 4 mfma only, 5 mfma + NV valu (epilogue mix) per mfma,
 //       6 mfma + NV valu, two independent chains
 template <int MODE, int NV>
-__global__ __launch_bounds__(512) void rate_kernel(uint32_t* out, long long* cyc, uint32_t seed) {
+__global__ __launch_bounds__(1024) void rate_kernel(uint32_t* out, long long* cyc, uint32_t seed) {
   extern __shared__ uint8_t lds[];
   uint32_t x[16];
   for (int i = 0; i < 16; ++i) x[i] = seed * (threadIdx.x + i);
@@ -42,6 +46,23 @@ __global__ __launch_bounds__(512) void rate_kernel(uint32_t* out, long long* cyc
     } else if (MODE == 3) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) ADDU(x[i], y);
+    } else if (MODE == 7) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) FMAF(x[i], y);
+    } else if (MODE == 8) {
+      typedef __attribute__((ext_vector_type(2))) float f2;
+      f2* xp = reinterpret_cast<f2*>(x);
+      f2 yy = {__uint_as_float(y), __uint_as_float(z)};
+#pragma unroll
+      for (int i = 0; i < 8; ++i) PKFMA(xp[i], yy);
+    } else if (MODE == 9) {
+      double* xd = reinterpret_cast<double*>(x);
+      double yd = (double)y;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) FMA64(xd[i], yd);
+    } else if (MODE == 10) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) CMPF(x[i], y);
     } else if (MODE == 4) {
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc0, 0, 0, 0);
     } else if (MODE == 5) {
@@ -93,7 +114,7 @@ void run(const char* name, int threads, double ops_per_iter) {
   double avg = 0;
   for (int i = 0; i < nw; ++i) avg += h[i];
   avg /= nw;
-  const int wps = threads / 256;  // waves per SIMD
+  const int wps = threads / 256;  // waves per SIMD (one workgroup per CU)
   printf("%-28s waves/SIMD %d  cycles/iter/wave %.1f  per-SIMD cycles per op %.2f  (%.3f ms)\n", name,
          wps, avg / kIter, avg / kIter / (ops_per_iter * wps), ms);
   delete[] h;
@@ -102,7 +123,11 @@ void run(const char* name, int threads, double ops_per_iter) {
 }
 
 int main() {
-  for (int threads : {256, 512}) {
+  for (int threads : {256, 512, 1024}) {
+    run<7, 0>("v_fma_f32 x16", threads, 16);
+    run<8, 0>("v_pk_fma_f32 x8", threads, 8);
+    run<9, 0>("v_fma_f64 x8", threads, 8);
+    run<10, 0>("v_cmp_le_f32 x16", threads, 16);
     run<0, 0>("v_max_u32 x16", threads, 16);
     run<1, 0>("v_med3_u32 x16", threads, 16);
     run<2, 0>("v_lshl_or_b32 x16", threads, 16);

@@ -94,7 +94,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
                          const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb,
                          hipStream_t stream);
 size_t verify_lds_bytes(int max_m);
-constexpr int kVerifyProfSlots = 80;
+constexpr int kVerifyProfSlots = 90;
 
 // Gathers the matched keypoint coordinates of each pair (float -> double,
 // FeatureKeypointsToPointsVector, sequential_matching.cc:91-92).

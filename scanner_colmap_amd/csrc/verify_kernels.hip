@@ -473,6 +473,7 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
                                              int n, int base, double maxr, int* nslow) {
   int cnt = 0;
   uint64_t any = 0;
+  uint64_t um[PCH];  // per point slot: lanes the filter left undecided
 #pragma unroll
   for (int q = 0; q < PCH / 2; ++q) {
     f32x2 diff, mg;
@@ -487,15 +488,26 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
       u1 &= ok1;
     }
     cnt += __popcll(i0) + __popcll(i1);
+    um[2 * q] = u0;
+    um[2 * q + 1] = u1;
     any |= u0 | u1;
   }
-  if (any) {  // rare: exact test of the undecided points, slot pair by slot pair
+  if (any) {  // rare: exact test of the undecided points only
     ++*nslow;
+    const uint64_t me = 1ull << threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < PCH / 2; ++q)
-      cnt += h_exact_pair(mk, f, s0[q], s1[q], d0[q], d1[q],
-                          FULL ? ~0ull : slot_mask(n, base, 2 * q),
-                          FULL ? ~0ull : slot_mask(n, base, 2 * q + 1), maxr);
+    for (int q = 0; q < PCH / 2; ++q) {
+      if (um[2 * q]) {
+        bool e = false;
+        if (um[2 * q] & me) e = h_exact_pt(mk, s0[q].x, s1[q].x, d0[q].x, d1[q].x, maxr);
+        cnt += __popcll(__ballot(e));
+      }
+      if (um[2 * q + 1]) {
+        bool e = false;
+        if (um[2 * q + 1] & me) e = h_exact_pt(mk, s0[q].y, s1[q].y, d0[q].y, d1[q].y, maxr);
+        cnt += __popcll(__ballot(e));
+      }
+    }
   }
   return cnt;
 }
@@ -631,6 +643,7 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
                                              int n, int base, double maxr, int* nslow) {
   int cnt = 0;
   uint64_t any = 0;
+  uint64_t um[PCH];  // per point slot: lanes the filter left undecided
 #pragma unroll
   for (int q = 0; q < PCH / 2; ++q) {
     f32x2 diff, mg;
@@ -645,15 +658,26 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
       u1 &= ok1;
     }
     cnt += __popcll(i0) + __popcll(i1);
+    um[2 * q] = u0;
+    um[2 * q + 1] = u1;
     any |= u0 | u1;
   }
-  if (any) {
+  if (any) {  // rare: exact test of the undecided points only
     ++*nslow;
+    const uint64_t me = 1ull << threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < PCH / 2; ++q)
-      cnt += f_exact_pair(mk, f, x0[q], x1[q], y0[q], y1[q],
-                          FULL ? ~0ull : slot_mask(n, base, 2 * q),
-                          FULL ? ~0ull : slot_mask(n, base, 2 * q + 1), maxr);
+    for (int q = 0; q < PCH / 2; ++q) {
+      if (um[2 * q]) {
+        bool e = false;
+        if (um[2 * q] & me) e = f_exact_pt(mk, x0[q].x, x1[q].x, y0[q].x, y1[q].x, maxr);
+        cnt += __popcll(__ballot(e));
+      }
+      if (um[2 * q + 1]) {
+        bool e = false;
+        if (um[2 * q + 1] & me) e = f_exact_pt(mk, x0[q].y, x1[q].y, y0[q].y, y1[q].y, maxr);
+        cnt += __popcll(__ballot(e));
+      }
+    }
   }
   return cnt;
 }
@@ -1919,7 +1943,7 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
 // the filter constants of one round at a time are broadcast from LDS and
 // lane t accumulates the count of hypothesis t of the round.
 constexpr int kScoreThreads = 64;
-constexpr int kScorePch = 16;  // points per lane
+constexpr int kScorePch = 8;  // points per lane
 constexpr int kScoreChunk = kScoreThreads * kScorePch;
 
 template <int K>
@@ -1928,7 +1952,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
     const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
     const float* __restrict__ fcon, const double* __restrict__ mods,
-    uint32_t* __restrict__ cnts, int max_chunks, double maxr) {
+    uint32_t* __restrict__ cnts, int max_chunks, double maxr, uint64_t* __restrict__ prof) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * 3][12];
@@ -1994,6 +2018,11 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
           else if (k == 1) c1 += add;
           else c2 += add;
         }
+      }
+      if (prof && lane == 0) {  // diagnostics: chunk-models scored, slow (exact) passes
+        uint64_t* pc = prof + (int64_t)q * kVerifyProfSlots + (K == KIND_F ? 80 : 84);
+        atomicAdd(reinterpret_cast<unsigned long long*>(pc), (unsigned long long)(B * MM));
+        atomicAdd(reinterpret_cast<unsigned long long*>(pc + 1), (unsigned long long)nslow);
       }
       uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3 + r0 * MM;
       if (lane < B) {
@@ -2270,7 +2299,7 @@ hipError_t run_rounds(const VerifyPair* pairs, int npairs, const double* xy1, co
                        P.max_residual);
     hipLaunchKernelGGL(rs_score_kernel<K>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs, xyf,
                        rb.rst, rb.act[cur], rb.nact + cur, rb.nmod, rb.fcon, rb.mods, rb.cnts,
-                       max_chunks, P.max_residual);
+                       max_chunks, P.max_residual, prof);
     hipLaunchKernelGGL(rs_replay_kernel<K>, dim3(gw), dim3(64), lds, stream, pairs, scratch, snaps, out, masks, rb.rst, rb.act[cur], rb.nact + cur,
                        rb.act[nxt], rb.nact + nxt, rb.nmod, rb.cnts, rb.mods, rb.wsnap, P, prof,
                        xyf);
