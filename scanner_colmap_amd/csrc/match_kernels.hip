@@ -43,7 +43,7 @@ typedef __attribute__((ext_vector_type(16))) float f32x16;
 
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t d;
-  asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
   return d;
 }
 
@@ -75,24 +75,45 @@ __device__ __forceinline__ f32x16 chain(const bf16x8 (&a)[8], const bf16x8 (&b)[
 // Keys of one finished sub-tile: row top-2 state update; returns the
 // sub-tile's column partial (best two keys of the lane's column, re-keyed
 // with the row inside the workgroup).
+// Top-2 of three unique keys: (max, median).
+__device__ __forceinline__ uint2 top2_of3(uint32_t a, uint32_t b, uint32_t c) {
+  return make_uint2(max(max(a, b), c), med3_u32(a, b, c));
+}
+
+// Merge of three top-2 pairs: best = max of the bests; second = max(median
+// of the bests, largest second) -- a second can only beat the median of the
+// bests when it belongs to the overall best's pair.
+__device__ __forceinline__ uint2 merge3(uint2 a, uint2 b, uint2 c) {
+  return make_uint2(max(max(a.x, b.x), c.x), max(med3_u32(a.x, b.x, c.x), max(max(a.y, b.y), c.y)));
+}
+
 template <bool CLAMP>
 __device__ __forceinline__ uint2 subtile_epilogue(const f32x16& acc, uint32_t tbits,
                                                   uint32_t (&b1r)[16], uint32_t (&b2r)[16],
                                                   uint32_t row_base) {
-  uint32_t b1c = 0u, b2c = 0u;
+  uint32_t key[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const uint32_t bits = __float_as_uint(acc[i]);
-    uint32_t key;
     if (CLAMP)
-      key = (min(bits, 0x4B040000u) << 13) | tbits | ((uint32_t)(15 - i) << 9);
+      key[i] = (min(bits, 0x4B040000u) << 13) | tbits | ((uint32_t)(15 - i) << 9);
     else
-      key = (bits << 9) | tbits;
-    b2r[i] = med3_u32(key, b1r[i], b2r[i]);
-    b1r[i] = max(b1r[i], key);
-    b2c = med3_u32(key, b1c, b2c);
-    b1c = max(b1c, key);
+      key[i] = (bits << 9) | tbits;
+    b2r[i] = med3_u32(key[i], b1r[i], b2r[i]);
+    b1r[i] = max(b1r[i], key[i]);
   }
+  // Column top-2 of the lane's 16 keys (unique: the row code differs) as a
+  // 3-input tree: 21 ops instead of 32 for the streaming update.
+  const uint2 p0 = top2_of3(key[0], key[1], key[2]);
+  const uint2 p1 = top2_of3(key[3], key[4], key[5]);
+  const uint2 p2 = top2_of3(key[6], key[7], key[8]);
+  const uint2 p3 = top2_of3(key[9], key[10], key[11]);
+  const uint2 p4 = top2_of3(key[12], key[13], key[14]);
+  const uint2 l0 = merge3(p0, p1, p2);
+  const uint2 l1 = make_uint2(max(max(p3.x, p4.x), key[15]),
+                              max(med3_u32(p3.x, p4.x, key[15]), max(p3.y, p4.y)));
+  const uint32_t b1c = max(l0.x, l1.x);
+  const uint32_t b2c = max(max(min(l0.x, l1.x), l0.y), l1.y);
   const uint32_t ii = 15u - ((b1c >> 9) & 15u);
   const uint32_t row_in_blk = row_base + (ii & 3u) + 8u * (ii >> 2);
   return make_uint2((b1c & ~kIdxMask) | (kIdxMask - row_in_blk), b2c & ~kIdxMask);
@@ -102,7 +123,7 @@ __device__ __forceinline__ uint2 subtile_epilogue(const f32x16& acc, uint32_t tb
 // rows, two 32-row MFMA sub-tiles per wave, A fragments register-resident)
 // swept against every column of every neighbour image of the job, 32 columns
 // per LDS tile.  Per element (fast variant): 1 v_lshl_or (key) + 2 row-state
-// ops + 2 column-state ops.
+// ops + ~1.3 column-state ops (3-input tree).
 //
 // Software pipeline (per wave, sub-tile granularity): the MFMA chain of
 // sub-tile (t, 1) runs while the epilogue of (t, 0) executes, and the chain of
