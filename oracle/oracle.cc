@@ -643,6 +643,12 @@ uint64_t oracle_num_trials(uint64_t num_inliers, uint64_t num_samples,
                                       multiplier, kmin);
 }
 
+// Least-squares null vector of a packed 9 x 9 normal matrix (45 entries) as
+// the LO estimators compute it (geom_solvers.h ata_null_vector).
+void oracle_ata_null_vector(const double* ata45, double* out9) {
+  scm::geom::ata_null_vector(ata45, out9);
+}
+
 int oracle_match_pair(const scm_matching_options* o, const uint8_t* d1,
                       int64_t n1, const uint8_t* d2, int64_t n2,
                       uint32_t* out, int64_t cap, int64_t* m) {

@@ -60,6 +60,8 @@ def lib() -> ctypes.CDLL:
                                    POINTER(POINTER(c_uint8)), POINTER(c_size_t)]
     L.oracle_num_trials.argtypes = [c_uint64, c_uint64, c_double, c_double, c_int32]
     L.oracle_num_trials.restype = c_uint64
+    L.oracle_ata_null_vector.argtypes = [c_void_p, c_void_p]
+    L.oracle_ata_null_vector.restype = None
     L.oracle_free.argtypes = [POINTER(c_uint8)]
     L.oracle_free.restype = None
     _lib = L
@@ -141,6 +143,14 @@ def loransac(kind, x1, x2, seed, opts=None):
 
 def num_trials(num_inliers, num_samples, confidence=0.999, multiplier=3.0, kmin=7) -> int:
     return int(lib().oracle_num_trials(num_inliers, num_samples, confidence, multiplier, kmin))
+
+
+def ata_null_vector(ata45) -> np.ndarray:
+    a = np.ascontiguousarray(ata45, np.float64)
+    assert a.shape == (45,)
+    out = np.zeros(9, np.float64)
+    lib().oracle_ata_null_vector(a.ctypes.data, out.ctypes.data)
+    return out
 
 
 def std_uniform(seed, lo, hi) -> np.ndarray:

@@ -225,3 +225,30 @@ def test_verify_pair_too_few_matches_is_empty_geometry():
     assert len(blob) == 292
     assert struct.unpack_from("<i", blob, 0)[0] == 0
     assert struct.unpack_from("<Q", blob, 284)[0] == 0
+
+
+# --- the 9 x 9 eigen solver of the local optimisation (parallel-order Jacobi) --
+def _pack45(a):
+    return np.array([a[p, q] for p in range(9) for q in range(p, 9)])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_ata_null_vector_matches_lapack(seed):
+    """geom_solvers.h jacobi9_par_eigen_min (4 disjoint rotations per round)
+    returns the eigenvector of the smallest eigenvalue of the normal matrix to
+    LAPACK accuracy, including near-singular systems (exact data + noise)."""
+    rng = np.random.default_rng(seed)
+    x = rng.normal(size=(400, 9))
+    x[:, 8] = 1.0
+    x[:, :8] *= rng.uniform(0.05, 3.0, 8)
+    if seed % 2:  # one direction almost in the null space
+        nvec = rng.normal(size=9)
+        nvec /= np.linalg.norm(nvec)
+        x -= np.outer(x @ nvec, nvec) * (1.0 - 1e-6)
+    a = x.T @ x
+    got = oracle.ata_null_vector(_pack45(a))
+    w, v = np.linalg.eigh(a)
+    ref = v[:, 0]
+    assert abs(np.linalg.norm(got) - 1.0) < 1e-12
+    assert min(np.abs(got - ref).max(), np.abs(got + ref).max()) < 1e-8 * max(1.0, w[-1] / (w[1] - w[0]) * 1e-8)
+    assert np.linalg.norm(a @ got - w[0] * got) <= 1e-9 * w[-1]
