@@ -1796,100 +1796,67 @@ __global__ __launch_bounds__(64) void rs_draw_kernel(
   }
 }
 
-// RandomSampler::Sample's Shuffle for every trial of the window, one thread
-// per pair (the swaps of one pair are a sequential chain; 64 pairs advance
-// together in a wavefront).  The targets drawn by rs_draw_kernel are read
-// from samp and replaced by the trial's sample.  The kmin hot positions live
-// in registers.  The loop is software-pipelined: the cold values of trial
-// b + 1 are loaded before trial b stores its own, and then corrected for any
-// position trial b wrote (forwarding), so one memory latency covers a trial.
+// RandomSampler::Sample's Shuffle for every trial of the window: the swap
+// chain of one pair is sequential, so each lane runs one pair's chain; the
+// pairs' sample-index vectors are staged in LDS (SCM_SHUFFLE_LDS_KB per
+// block) so that every swap costs one LDS round trip.  The targets drawn by
+// rs_draw_kernel are read from samp and replaced by the trial's sample.
 template <int K>
 __global__ __launch_bounds__(64) void rs_shuffle_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
     const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
-    const int32_t* __restrict__ nact, uint16_t* __restrict__ samp) {
-  using Tr = KindTraits<K>;
-  constexpr int KM = Tr::kmin;
+    const int32_t* __restrict__ nact, uint16_t* __restrict__ samp, int ppb, int stride) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  uint16_t* lsidx = reinterpret_cast<uint16_t*>(dyn_lds);
   const int na = *nact;
-  const int a = blockIdx.x * 64 + threadIdx.x;
-  if (a >= na) return;
-  const int q = act[a];
-  const PairSetup ps = pair_at(pairs, q, scratch, snaps, out);
-  uint16_t* sidx = pair_sidx(ps);
-  const int Btot = rst[q].B;
-  uint16_t* sq = samp + (int64_t)q * kWindowTrials * 8;
-  uint32_t R[KM];
-#pragma unroll
-  for (int i = 0; i < KM; ++i) R[i] = sidx[i];
-  uint32_t j[KM], v[KM], jb[KM];
-  auto load_targets = [&](int b, uint32_t (&t)[KM]) {
-    const uint4 raw = *reinterpret_cast<const uint4*>(sq + b * 8);
-    const uint32_t wv[4] = {raw.x, raw.y, raw.z, raw.w};
-#pragma unroll
-    for (int i = 0; i < KM; ++i) t[i] = (wv[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-  };
-  // Pipeline: targets two trials ahead, cold values one trial ahead.
-#pragma unroll
-  for (int i = 0; i < KM; ++i) j[i] = jb[i] = v[i] = 0u;
-  if (Btot > 0) {
-    load_targets(0, j);
-#pragma unroll
-    for (int i = 0; i < KM; ++i) v[i] = j[i] >= (uint32_t)KM ? sidx[j[i]] : 0u;
+  const int a0 = blockIdx.x * ppb;
+  if (a0 >= na) return;
+  const int np = min(ppb, na - a0);
+  // Stage the sample-index vectors of this block's ppb pairs in LDS (every
+  // thread helps), run one pair's swap chain per lane, write them back.
+  for (int l = 0; l < np; ++l) {
+    const PairSetup pl = pair_at(pairs, act[a0 + l], scratch, snaps, out);
+    const uint16_t* g = pair_sidx(pl);
+    for (int i = threadIdx.x; i < pl.n; i += 64) lsidx[l * stride + i] = g[i];
   }
-  if (Btot > 1) load_targets(1, jb);
-  for (int b = 0; b < Btot; ++b) {
-    uint32_t jc[KM], vn[KM];
+  __syncthreads();
+  if ((int)threadIdx.x < np) {
+    // The swap chain as the reference writes it (std::swap of positions i and
+    // j of the persistent vector, i = 0..kmin-1), on LDS: one LDS round trip
+    // per swap, no register bookkeeping.
+    constexpr int KM = KindTraits<K>::kmin;
+    const int q = act[a0 + threadIdx.x];
+    uint16_t* sid = lsidx + threadIdx.x * stride;
+    uint16_t* sq = samp + (int64_t)q * kWindowTrials * 8;
+    const int Btot = rst[q].B;
+    uint4 tn = Btot > 0 ? *reinterpret_cast<const uint4*>(sq) : make_uint4(0u, 0u, 0u, 0u);
+    for (int b = 0; b < Btot; ++b) {
+      const uint4 tc = tn;
+      if (b + 1 < Btot) tn = *reinterpret_cast<const uint4*>(sq + (b + 1) * 8);
+      const uint32_t wv[4] = {tc.x, tc.y, tc.z, tc.w};
 #pragma unroll
-    for (int i = 0; i < KM; ++i) jc[i] = vn[i] = 0u;
-    if (b + 2 < Btot) load_targets(b + 2, jc);
-    if (b + 1 < Btot) {
-#pragma unroll
-      for (int i = 0; i < KM; ++i) vn[i] = jb[i] >= (uint32_t)KM ? sidx[jb[i]] : 0u;
-    }
-    uint32_t w[KM];
-#pragma unroll
-    for (int i = 0; i < KM; ++i) {
-      w[i] = 0xFFFFFFFFu;
-      if (j[i] < (uint32_t)KM) {  // hot swap R[i] <-> R[j] (j >= i)
-        uint32_t rj = R[i];
-#pragma unroll
-        for (int t = 0; t < KM; ++t) rj = (t == (int)j[i]) ? R[t] : rj;
-#pragma unroll
-        for (int t = 0; t < KM; ++t) R[t] = (t == (int)j[i]) ? R[i] : R[t];
-        R[i] = rj;
-      } else {
-        uint32_t cur = v[i];
-#pragma unroll
-        for (int i2 = 0; i2 < i; ++i2) cur = (j[i2] == j[i]) ? w[i2] : cur;
-        w[i] = R[i];
-        sidx[j[i]] = (uint16_t)R[i];
-        R[i] = cur;
+      for (int i = 0; i < KM; ++i) {
+        const uint32_t jj = (wv[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
+        const uint16_t ti = sid[i];
+        const uint16_t tj = sid[jj];
+        sid[i] = tj;
+        sid[jj] = ti;
       }
-    }
-    uint32_t ow[4] = {0u, 0u, 0u, 0u};
+      uint32_t ow[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int i = 0; i < KM; ++i) ow[i >> 1] |= (R[i] & 0xFFFFu) << (16 * (i & 1));
-    *reinterpret_cast<uint4*>(sq + b * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-    // Forward this trial's cold writes into the next trial's loaded values
-    // (the last write to a position wins).
-#pragma unroll
-    for (int i = 0; i < KM; ++i) {
-      uint32_t val = vn[i];
-#pragma unroll
-      for (int i2 = 0; i2 < KM; ++i2) val = (w[i2] != 0xFFFFFFFFu && j[i2] == jb[i]) ? w[i2] : val;
-      vn[i] = val;
-    }
-#pragma unroll
-    for (int i = 0; i < KM; ++i) {
-      v[i] = vn[i];
-      j[i] = jb[i];
-      jb[i] = jc[i];
+      for (int i = 0; i < KM; ++i) ow[i >> 1] |= (uint32_t)sid[i] << (16 * (i & 1));
+      *reinterpret_cast<uint4*>(sq + b * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
     }
   }
-#pragma unroll
-  for (int i = 0; i < KM; ++i) sidx[i] = (uint16_t)R[i];
+  __syncthreads();
+  for (int l = 0; l < np; ++l) {
+    const PairSetup pl = pair_at(pairs, act[a0 + l], scratch, snaps, out);
+    uint16_t* g = pair_sidx(pl);
+    for (int i = threadIdx.x; i < pl.n; i += 64) g[i] = lsidx[l * stride + i];
+  }
 }
+
 
 // Minimal solvers, one thread per hypothesis of the window, plus the fp32
 // filter constants of every model.
@@ -2286,14 +2253,23 @@ hipError_t run_rounds(const VerifyPair* pairs, int npairs, const double* xy1, co
   const size_t lds = sizeof(VerifyLds);
   const int max_trials = K == KIND_F ? P.max_trials_F : P.max_trials_H;
   const int gw = npairs < 4096 ? npairs : 4096;
+#ifndef SCM_SHUFFLE_LDS_KB
+#define SCM_SHUFFLE_LDS_KB 16
+#endif
+  // Shuffle blocks: as many pairs per block as fit SCM_SHUFFLE_LDS_KB of LDS sample-index
+  // vectors (the swap chains are latency-bound; LDS instead of global memory
+  // shortens every step of them).
+  const int sh_stride = (max_m + 7) / 8 * 8;
+  const int sh_ppb = std::max(1, std::min(64, (SCM_SHUFFLE_LDS_KB * 1024) / (2 * sh_stride)));
   int covered = 0, W = 1, r = 0;
   while (covered < max_trials) {
     const int cur = r & 1, nxt = cur ^ 1;
     hipLaunchKernelGGL(rs_draw_kernel<K>, dim3(gw), dim3(64), lds, stream, pairs, scratch, snaps,
                        out, rb.rst, rb.act[cur], rb.nact + cur, rb.nact + nxt, rb.samp, rb.cnts,
                        rb.wsnap, W);
-    hipLaunchKernelGGL(rs_shuffle_kernel<K>, dim3((npairs + 63) / 64), dim3(64), 0, stream, pairs,
-                       scratch, snaps, out, rb.rst, rb.act[cur], rb.nact + cur, rb.samp);
+    hipLaunchKernelGGL(rs_shuffle_kernel<K>, dim3((npairs + sh_ppb - 1) / sh_ppb), dim3(64),
+                       (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch, snaps,
+                       out, rb.rst, rb.act[cur], rb.nact + cur, rb.samp, sh_ppb, sh_stride);
     hipLaunchKernelGGL(rs_solve_kernel<K>, dim3(4096), dim3(64), 0, stream, pairs, xy1, xy2,
                        rb.rst, rb.act[cur], rb.nact + cur, rb.samp, rb.nmod, rb.fcon, rb.mods, W,
                        P.max_residual);
@@ -2325,6 +2301,8 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     set_lds_attr(rs_begin_kernel<KIND_F>);
     set_lds_attr(rs_begin_kernel<KIND_H>);
     set_lds_attr(rs_draw_kernel<KIND_F>);
+    set_lds_attr(rs_shuffle_kernel<KIND_F>);
+    set_lds_attr(rs_shuffle_kernel<KIND_H>);
     set_lds_attr(rs_draw_kernel<KIND_H>);
     set_lds_attr(rs_replay_kernel<KIND_F>);
     set_lds_attr(rs_replay_kernel<KIND_H>);
