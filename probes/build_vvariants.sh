@@ -1,0 +1,19 @@
+#!/bin/bash
+# Builds libscm.so variants of the verifier (diagnostics): probes/build/libscm_<name>.so
+# usage: probes/build_vvariants.sh name:"-DFOO=1 -DBAR=0" ...
+set -e
+cd "$(dirname "$0")/.."
+mkdir -p probes/build
+make -C scanner_colmap_amd/csrc -s
+O=scanner_colmap_amd/lib/obj
+for spec in "$@"; do
+  name=${spec%%:*}; defs=${spec#*:}
+  /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC -ffp-contract=off --offload-arch=gfx950 $defs \
+    -c scanner_colmap_amd/csrc/verify_kernels.hip -o probes/build/verify_$name.o &
+done
+wait
+for spec in "$@"; do
+  name=${spec%%:*}
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o probes/build/libscm_$name.so \
+    $O/match_kernels.o probes/build/verify_$name.o $O/scm_runtime.o $O/scm_codec.o
+done

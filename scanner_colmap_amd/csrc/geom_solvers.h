@@ -309,9 +309,8 @@ SCM_UNROLL
 // Cyclic Jacobi eigen-decomposition of a symmetric N x N matrix (row-major).
 // On return the diagonal of a holds the eigenvalues and column j of v
 // (row-major, v[r*N+j]) the j-th eigenvector.  Returns the index of the
-// smallest eigenvalue (lowest index on ties).  Sweep structure (rotation
-// order, convergence test, zeroing of a_pq) is the definition the GPU's
-// lane-distributed 9x9 version (verify_kernels.hip) reproduces exactly.
+// smallest eigenvalue (lowest index on ties).  Used for the 3 x 3 rank-2
+// projection of the 8-point estimator (host and device run this same code).
 constexpr int kJacobiMaxSweeps = 64;
 
 SCM_HD inline void jacobi_params(double app, double aqq, double apq, double* c, double* s) {
@@ -599,91 +598,134 @@ SCM_HD inline int fundamental_7pt(const double* x1, const double* x2,
   return nm;
 }
 
-// Parallel-order Jacobi for the 9 x 9 normal equations.  Sweeps cover the
-// 36 index pairs in 9 rounds of 4 disjoint pairs (round-robin: round r
-// leaves index r idle and pairs (r + i) mod 9 with (r - i) mod 9, i = 1..4),
-// and the 4 rotations of a round are applied together: their parameters come
-// from the same matrix, then all column updates (B = A J), then all row
-// updates (A' = J^T B), then the rotated off-diagonal entries are zeroed.
-// Rotations of a round are independent, so a GPU wavefront evaluates the four
-// (expensive, latency-bound) parameter chains at once; the arithmetic of
-// every entry is fixed by this definition, so host and device agree bit for
-// bit.  A pair whose off-diagonal entry is zero uses (c, s) = (1, 0).
-SCM_HD inline void jacobi9_round_pairs(int r, int* P, int* Q) {
+// Least-squares null vector of the 9 x 9 normal equations of the local
+// estimators (the right singular vector of the smallest singular value that
+// the reference's Eigen JacobiSVD returns), by
+// repeated squaring of the inverse:
+//   M0 = (A + delta I)^-1, delta = 2^-40 trace(A)   (Gauss-Jordan, no pivoting:
+//        A + delta I is SPD, its pivots stay >= delta), symmetrised;
+//   M_{s+1} = M_s M_s / trace(M_s M_s)               (entry (i, j) summed over
+//        k = 0..8 in order: bitwise symmetric);
+// M_s -> v v^T at rate ((l1 + delta) / (l2 + delta))^(2^s).  Squaring stops
+// one step after the column j* of the largest diagonal passes the rank-one
+// test |1 - sum_i M_ij*^2 / M_j*j*| <= 2^-44 (at least 4, at most 16
+// squarings); v = column j* / its norm.  Every entry's arithmetic is fixed by
+// this definition, so the GPU's lane-per-entry version (verify_kernels.hip,
+// invsq9_null_wave) agrees bit for bit.  Accuracy is the eigenproblem's own
+// (tests/test_oracle_geometry.py pins it against LAPACK); a zero matrix
+// returns e_0.
+constexpr int kInvSqMin = 4, kInvSqMax = 16;
+constexpr double kInvSqTol = 0x1p-44;
+
+// One Gauss-Jordan step on pivot k: entry (i, j) of the new matrix from the
+// old one (every entry reads only row k, column k and itself).
+SCM_HD inline double gj9_entry(double mij, double mik, double mkj, double inv, int i, int j, int k) {
+  if (i == k && j == k) return inv;
+  if (i == k) return mkj * inv;
+  if (j == k) return -(mik * inv);
+  return mij - mik * (mkj * inv);
+}
+
+SCM_HD inline double sq9_entry(const double* m, int i, int j) {
+  double acc = m[i * 9 + 0] * m[0 * 9 + j];
 SCM_UNROLL
-  for (int i = 0; i < 4; ++i) {
-    const int a = (r + 1 + i) % 9, b = (r + 8 - i) % 9;
-    P[i] = a < b ? a : b;
-    Q[i] = a < b ? b : a;
-  }
+  for (int k = 1; k < 9; ++k) acc = acc + m[i * 9 + k] * m[k * 9 + j];
+  return acc;
 }
 
-SCM_HD inline int jacobi9_par_eigen_min(double* a, double* v) {
-  for (int r = 0; r < 9; ++r)
-    for (int c = 0; c < 9; ++c) v[r * 9 + c] = (r == c) ? 1.0 : 0.0;
-  for (int sweep = 0; sweep < kJacobiMaxSweeps; ++sweep) {
-    double off = 0.0, diag = 0.0;
-    for (int p = 0; p < 9; ++p) {
-      diag += a[p * 9 + p] * a[p * 9 + p];
-      for (int q = p + 1; q < 9; ++q) off += a[p * 9 + q] * a[p * 9 + q];
-    }
-    if (off <= 1e-36 * diag || off == 0.0) break;
-    for (int r = 0; r < 9; ++r) {
-      int P[4], Q[4];
-      double C[4], S[4];
-      jacobi9_round_pairs(r, P, Q);
-      for (int i = 0; i < 4; ++i) {
-        const double apq = a[P[i] * 9 + Q[i]];
-        if (apq == 0.0) {
-          C[i] = 1.0;
-          S[i] = 0.0;
-        } else {
-          jacobi_params(a[P[i] * 9 + P[i]], a[Q[i] * 9 + Q[i]], apq, &C[i], &S[i]);
-        }
-      }
-      for (int k = 0; k < 9; ++k)
-        for (int i = 0; i < 4; ++i) {
-          const double akp = a[k * 9 + P[i]], akq = a[k * 9 + Q[i]];
-          a[k * 9 + P[i]] = C[i] * akp - S[i] * akq;
-          a[k * 9 + Q[i]] = S[i] * akp + C[i] * akq;
-          const double vkp = v[k * 9 + P[i]], vkq = v[k * 9 + Q[i]];
-          v[k * 9 + P[i]] = C[i] * vkp - S[i] * vkq;
-          v[k * 9 + Q[i]] = S[i] * vkp + C[i] * vkq;
-        }
-      for (int i = 0; i < 4; ++i)
-        for (int k = 0; k < 9; ++k) {
-          const double bpk = a[P[i] * 9 + k], bqk = a[Q[i] * 9 + k];
-          a[P[i] * 9 + k] = C[i] * bpk - S[i] * bqk;
-          a[Q[i] * 9 + k] = S[i] * bpk + C[i] * bqk;
-        }
-      for (int i = 0; i < 4; ++i) {
-        a[P[i] * 9 + Q[i]] = 0.0;
-        a[Q[i] * 9 + P[i]] = 0.0;
-      }
-    }
-  }
-  int best = 0;
-  double bv = a[0];
-  for (int j = 1; j < 9; ++j)
-    if (a[j * 9 + j] < bv) {
-      bv = a[j * 9 + j];
-      best = j;
-    }
-  return best;
+// Trace-normalisation factor, column of the largest diagonal (lowest index on
+// ties) and the rank-one test of a squared iterate.
+SCM_HD inline double sq9_trace_inv(const double* m) {
+  double t = m[0];
+SCM_UNROLL
+  for (int i = 1; i < 9; ++i) t = t + m[i * 9 + i];
+  return 1.0 / t;
 }
 
-// Least-squares null vector of a packed A^T A (45 entries) via Jacobi.
+SCM_HD inline int sq9_argmax_diag(const double* m) {
+  int j = 0;
+  double d = m[0];
+SCM_UNROLL
+  for (int i = 1; i < 9; ++i)
+    if (m[i * 9 + i] > d) {
+      d = m[i * 9 + i];
+      j = i;
+    }
+  return j;
+}
+
+SCM_HD inline bool sq9_rank_one(const double* m, int j) {
+  double c = m[j] * m[j];
+SCM_UNROLL
+  for (int i = 1; i < 9; ++i) c = c + m[i * 9 + j] * m[i * 9 + j];
+  const double r = c / m[j * 9 + j];
+  return fabs(1.0 - r) <= kInvSqTol;
+}
+
+SCM_HD inline void sq9_column_unit(const double* m, int j, double* out9) {
+  double n2 = m[j] * m[j];
+SCM_UNROLL
+  for (int i = 1; i < 9; ++i) n2 = n2 + m[i * 9 + j] * m[i * 9 + j];
+  const double nrm = sqrt(n2);
+SCM_UNROLL
+  for (int i = 0; i < 9; ++i) out9[i] = m[i * 9 + j] / nrm;
+}
+
+SCM_HD inline double ata9_trace(const double* ata45) {
+  // diagonal entries of the packed upper triangle: offsets 0, 9, 17, ...
+  double t = ata45[0];
+  int k = 9;
+SCM_UNROLL
+  for (int p = 1; p < 9; ++p) {
+    t = t + ata45[k];
+    k += 9 - p;
+  }
+  return t;
+}
+
+#if defined(SCM_GEOM_ATA_HOOK) && !defined(__HIP_DEVICE_COMPILE__)
+void SCM_GEOM_ATA_HOOK(const double* ata45);  // diagnostics builds only (probes/)
+#endif
 SCM_HD inline void ata_null_vector(const double* ata45, double* out9) {
-  double a[81], v[81];
+#if defined(SCM_GEOM_ATA_HOOK) && !defined(__HIP_DEVICE_COMPILE__)
+  SCM_GEOM_ATA_HOOK(ata45);
+#endif
+  double a[81], b[81];
+  const double tr = ata9_trace(ata45);
+  if (!(tr > 0.0)) {
+    for (int i = 0; i < 9; ++i) out9[i] = i == 0 ? 1.0 : 0.0;
+    return;
+  }
+  const double delta = tr * 0x1p-40;
   int k = 0;
   for (int p = 0; p < 9; ++p)
     for (int q = p; q < 9; ++q) {
-      a[p * 9 + q] = ata45[k];
-      a[q * 9 + p] = ata45[k];
+      const double v = p == q ? ata45[k] + delta : ata45[k];
+      a[p * 9 + q] = v;
+      a[q * 9 + p] = v;
       ++k;
     }
-  const int jmin = jacobi9_par_eigen_min(a, v);
-  for (int i = 0; i < 9; ++i) out9[i] = v[i * 9 + jmin];
+  for (int kk = 0; kk < 9; ++kk) {
+    const double inv = 1.0 / a[kk * 9 + kk];
+    for (int e = 0; e < 81; ++e) {
+      const int i = e / 9, j = e % 9;
+      b[e] = gj9_entry(a[e], a[i * 9 + kk], a[kk * 9 + j], inv, i, j, kk);
+    }
+    for (int e = 0; e < 81; ++e) a[e] = b[e];
+  }
+  for (int e = 0; e < 81; ++e) b[e] = 0.5 * (a[e] + a[(e % 9) * 9 + e / 9]);
+  // b = symmetrised M0
+  int jstar = 0;
+  bool done = false;
+  for (int sq = 0; sq < kInvSqMax; ++sq) {
+    for (int e = 0; e < 81; ++e) a[e] = sq9_entry(b, e / 9, e % 9);
+    const double ti = sq9_trace_inv(a);
+    for (int e = 0; e < 81; ++e) b[e] = a[e] * ti;
+    jstar = sq9_argmax_diag(b);
+    if (done) break;
+    done = sq + 1 >= kInvSqMin && sq9_rank_one(b, jstar);
+  }
+  sq9_column_unit(b, jstar, out9);
 }
 
 // Final step of colmap::FundamentalMatrixEightPointEstimator::Estimate

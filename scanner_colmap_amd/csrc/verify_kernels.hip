@@ -492,6 +492,9 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
     um[2 * q + 1] = u1;
     any |= u0 | u1;
   }
+#ifdef SCM_DIAG_SCORE_NOSLOW
+  any = 0;  // diagnostics only: undecided points counted as outliers
+#endif
   if (any) {  // rare: exact test of the undecided points only
     ++*nslow;
     const uint64_t me = 1ull << threadIdx.x;
@@ -662,6 +665,9 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
     um[2 * q + 1] = u1;
     any |= u0 | u1;
   }
+#ifdef SCM_DIAG_SCORE_NOSLOW
+  any = 0;  // diagnostics only: undecided points counted as outliers
+#endif
   if (any) {  // rare: exact test of the undecided points only
     ++*nslow;
     const uint64_t me = 1ull << threadIdx.x;
@@ -813,92 +819,69 @@ __device__ int gather_inliers_f4(const double* res, int n, double maxr, const fl
   return base_out;
 }
 
-// Wavefront twin of jacobi9_par_eigen_min (geom_solvers.h) on LDS-resident
-// A and V (row-major 9 x 9).  Per round the four rotation parameter chains
-// are evaluated together (every lane, uniform values: the latency of one
-// chain instead of four), then lane (k, i) < 36 applies the column update of
-// pair i to row k of A and V, then lane (i, c) < 36 the row update of pair i
-// at column c, then the rotated off-diagonal entries are zeroed.  Same
-// operations, same order as the host version.  Returns the eigenvector of the
-// smallest eigenvalue in f (every lane).
-__device__ void jacobi9_par_wave(const double* ata45, double* A, double* V, double* f) {
+// Wavefront twin of ata_null_vector (geom_solvers.h): lane e (and e + 64)
+// owns entry e of the 9 x 9 iterate (row-major, LDS buffers A and B); each
+// Gauss-Jordan step and each squaring computes every entry from the previous
+// matrix with exactly the host's operations, so the result is bit-identical.
+// The uniform scalars (pivot reciprocal, trace factor, j*, rank-one test) are
+// evaluated by every lane from broadcast LDS reads.  Returns the unit null
+// vector in f (every lane).
+__device__ void invsq9_null_wave(const double* ata45, double* A, double* B, double* f) {
   const int lane = threadIdx.x;
-  if (lane < 9) {
+  const int e0 = lane, e1 = lane + 64;  // e1 valid for lane < 17
+  const bool has1 = e1 < 81;
+  const double tr = ata9_trace(ata45);
+  if (!(tr > 0.0)) {
 #pragma unroll
-    for (int c = 0; c < 9; ++c) {
-      const int p = lane < c ? lane : c, q = lane < c ? c : lane;
-      A[lane * 9 + c] = ata45[ata_index(p, q)];
-      V[lane * 9 + c] = (lane == c) ? 1.0 : 0.0;
-    }
+    for (int i = 0; i < 9; ++i) f[i] = i == 0 ? 1.0 : 0.0;
+    return;
+  }
+  const double delta = tr * 0x1p-40;
+  {
+    // packed upper-triangle index of (p, q), p <= q
+    auto load = [&](int e) {
+      const int i = e / 9, j = e - 9 * (e / 9);
+      const int p = i < j ? i : j, q = i < j ? j : i;
+      const double v = ata45[ata_index(p, q)];
+      A[e] = p == q ? v + delta : v;
+    };
+    load(e0);
+    if (has1) load(e1);
   }
   wsync();
-  for (int sweep = 0; sweep < kJacobiMaxSweeps; ++sweep) {
-    double off = 0.0, diag = 0.0;
-#pragma unroll
-    for (int p = 0; p < 9; ++p) {
-      diag += A[p * 9 + p] * A[p * 9 + p];
-#pragma unroll
-      for (int q = p + 1; q < 9; ++q) off += A[p * 9 + q] * A[p * 9 + q];
-    }
-    if (off <= 1e-36 * diag || off == 0.0) break;
+  const int i0 = e0 / 9, j0 = e0 - 9 * (e0 / 9);
+  const int i1 = e1 / 9, j1 = e1 - 9 * (e1 / 9);
 #pragma unroll 1
-    for (int r = 0; r < 9; ++r) {
-      int P[4], Q[4];
-      jacobi9_round_pairs(r, P, Q);
-      double C[4], S[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const double apq = A[P[i] * 9 + Q[i]];
-        double c, sn;
-        jacobi_params(A[P[i] * 9 + P[i]], A[Q[i] * 9 + Q[i]], apq == 0.0 ? 1.0 : apq, &c, &sn);
-        C[i] = apq == 0.0 ? 1.0 : c;
-        S[i] = apq == 0.0 ? 0.0 : sn;
-      }
-      wsync();
-      if (lane < 36) {  // B = A J, V = V J: row k, pair i
-        const int k = lane >> 2, i = lane & 3;
-        const int pi = P[0] * (i == 0) + P[1] * (i == 1) + P[2] * (i == 2) + P[3] * (i == 3);
-        const int qi = Q[0] * (i == 0) + Q[1] * (i == 1) + Q[2] * (i == 2) + Q[3] * (i == 3);
-        const double ci = i == 0 ? C[0] : (i == 1 ? C[1] : (i == 2 ? C[2] : C[3]));
-        const double si = i == 0 ? S[0] : (i == 1 ? S[1] : (i == 2 ? S[2] : S[3]));
-        const double akp = A[k * 9 + pi], akq = A[k * 9 + qi];
-        const double vkp = V[k * 9 + pi], vkq = V[k * 9 + qi];
-        A[k * 9 + pi] = ci * akp - si * akq;
-        A[k * 9 + qi] = si * akp + ci * akq;
-        V[k * 9 + pi] = ci * vkp - si * vkq;
-        V[k * 9 + qi] = si * vkp + ci * vkq;
-      }
-      wsync();
-      if (lane < 36) {  // A' = J^T B: pair i, column c
-        const int i = lane / 9, c = lane - 9 * (lane / 9);
-        const int pi = P[0] * (i == 0) + P[1] * (i == 1) + P[2] * (i == 2) + P[3] * (i == 3);
-        const int qi = Q[0] * (i == 0) + Q[1] * (i == 1) + Q[2] * (i == 2) + Q[3] * (i == 3);
-        const double ci = i == 0 ? C[0] : (i == 1 ? C[1] : (i == 2 ? C[2] : C[3]));
-        const double si = i == 0 ? S[0] : (i == 1 ? S[1] : (i == 2 ? S[2] : S[3]));
-        const double bpk = A[pi * 9 + c], bqk = A[qi * 9 + c];
-        A[pi * 9 + c] = ci * bpk - si * bqk;
-        A[qi * 9 + c] = si * bpk + ci * bqk;
-      }
-      wsync();
-      if (lane < 4) {
-        const int pi = P[0] * (lane == 0) + P[1] * (lane == 1) + P[2] * (lane == 2) + P[3] * (lane == 3);
-        const int qi = Q[0] * (lane == 0) + Q[1] * (lane == 1) + Q[2] * (lane == 2) + Q[3] * (lane == 3);
-        A[pi * 9 + qi] = 0.0;
-        A[qi * 9 + pi] = 0.0;
-      }
-      wsync();
-    }
+  for (int k = 0; k < 9; ++k) {
+    const double inv = 1.0 / A[k * 9 + k];
+    const double n0 = gj9_entry(A[e0], A[i0 * 9 + k], A[k * 9 + j0], inv, i0, j0, k);
+    const double n1 = has1 ? gj9_entry(A[e1], A[i1 * 9 + k], A[k * 9 + j1], inv, i1, j1, k) : 0.0;
+    wsync();
+    A[e0] = n0;
+    if (has1) A[e1] = n1;
+    wsync();
   }
-  int best = 0;
-  double bv = A[0];
-#pragma unroll
-  for (int j = 1; j < 9; ++j)
-    if (A[j * 9 + j] < bv) {
-      bv = A[j * 9 + j];
-      best = j;
-    }
-#pragma unroll
-  for (int i = 0; i < 9; ++i) f[i] = V[i * 9 + best];
+  B[e0] = 0.5 * (A[e0] + A[j0 * 9 + i0]);
+  if (has1) B[e1] = 0.5 * (A[e1] + A[j1 * 9 + i1]);
+  wsync();
+  int jstar = 0;
+  bool done = false;
+#pragma unroll 1
+  for (int sq = 0; sq < kInvSqMax; ++sq) {
+    const double q0 = sq9_entry(B, i0, j0);
+    const double q1 = has1 ? sq9_entry(B, i1, j1) : 0.0;
+    A[e0] = q0;  // A is free: B holds the iterate
+    if (has1) A[e1] = q1;
+    wsync();
+    const double ti = sq9_trace_inv(A);
+    B[e0] = q0 * ti;
+    if (has1) B[e1] = q1 * ti;
+    wsync();
+    jstar = sq9_argmax_diag(B);
+    if (done) break;
+    done = sq + 1 >= kInvSqMin && sq9_rank_one(B, jstar);
+  }
+  sq9_column_unit(B, jstar, f);
 }
 
 // normalize_transform (geom_solvers.h) of both point sets, canonical sums.
@@ -1008,7 +991,7 @@ __device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const doub
   ata_pass_wave<K, 2>(s, xin1, xin2, n, T1, T2);
   wsync();
   double f[9];
-  jacobi9_par_wave(s.ata, s.jA, s.jV, f);
+  invsq9_null_wave(s.ata, s.jA, s.jV, f);
   wsync();
   if (K == KIND_F) fundamental_8pt_finish(f, T1, T2, model);
   else homography_finish(f, T1, T2, model);
@@ -1120,7 +1103,7 @@ __device__ void local_estimate_f4(VerifyLds& s, const float4* xin, int n, double
   wsync();
   if (pl && threadIdx.x == 0) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[2] += t - t0; t0 = t; }
   double f[9];
-  jacobi9_par_wave(s.ata, s.jA, s.jV, f);
+  invsq9_null_wave(s.ata, s.jA, s.jV, f);
   wsync();
   if (pl && threadIdx.x == 0) pl[3] += __builtin_amdgcn_s_memtime() - t0;
   if (K == KIND_F) fundamental_8pt_finish(f, T1, T2, model);
