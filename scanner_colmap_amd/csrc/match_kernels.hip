@@ -213,13 +213,24 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
         const int t = t_begin + k;
         const uint4 nxt = src0[(int64_t)min(t + 2, tlast) * 32 * 16];
         const uint32_t tbits = (uint32_t)(kTilesPerSeg - 1 - k);
+#ifdef SCM_MATCH_BPREF
+        // B fragments of tile t + 1 (staged since the last barrier) requested
+        // a whole sub-tile ahead of their chain.
+        bf16x8 bnext[8];
+        load_bfrag(lds + ((k + 1) % kStages) * kTileBytes, r, h, bnext);
+#endif
         // chain (t, 1) || epilogue (t, 0)
         const f32x16 acc1 = chain(afrag[1], bfrag, cinit);
         const uint2 c0 = subtile_epilogue<CLAMP>(acc0, tbits, b1r[0], b2r[0], row_base0);
         // chain (t + 1, 0) || epilogue (t, 1).  The barrier keeps the next
         // B fragments from being loaded while the current ones are live.
         __builtin_amdgcn_sched_barrier(0);
+#ifdef SCM_MATCH_BPREF
+#pragma unroll
+        for (int q = 0; q < 8; ++q) bfrag[q] = bnext[q];
+#else
         load_bfrag(lds + ((k + 1) % kStages) * kTileBytes, r, h, bfrag);
+#endif
         acc0 = chain(afrag[0], bfrag, cinit);
         const uint2 c1 = subtile_epilogue<CLAMP>(acc1, tbits, b1r[1], b2r[1], row_base0 + 32u);
         // Column partial of this wave: merge the two sub-tiles and the halves.

@@ -1895,6 +1895,7 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
 constexpr int kScoreThreads = 64;
 constexpr int kScorePch = 8;  // points per lane
 constexpr int kScoreChunk = kScoreThreads * kScorePch;
+constexpr int kScoreTargetItems = 65536;  // work items per score launch (8 per wave slot)
 
 template <int K>
 __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
@@ -1902,7 +1903,8 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
     const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
     const float* __restrict__ fcon, const double* __restrict__ mods,
-    uint32_t* __restrict__ cnts, int max_chunks, double maxr, uint64_t* __restrict__ prof) {
+    uint32_t* __restrict__ cnts, int max_chunks, int W, double maxr,
+    uint64_t* __restrict__ prof) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * 3][12];
@@ -1910,14 +1912,25 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
   const int lane = threadIdx.x;
   const int na = *nact;
   const float maxrf = (float)maxr;
-  for (int w = blockIdx.x; w < na * max_chunks; w += gridDim.x) {
-    const int q = act[w / max_chunks];
-    const int chunk = w % max_chunks;
+  // Work item = (active pair, chunk, run of rpi rounds of the window): late
+  // windows (few far pairs left) split their rounds over separate items so
+  // that they still fill the GPU; busy windows keep long runs (points loaded
+  // once per run).
+  const int rpi = max(1, min(W, (int)(((int64_t)na * max_chunks * W) / kScoreTargetItems)));
+  const int nri = (W + rpi - 1) / rpi;
+  const int per_pair = max_chunks * nri;
+  for (int w = blockIdx.x; w < na * per_pair; w += gridDim.x) {
+    const int q = act[w / per_pair];
+    const int rem = w - (w / per_pair) * per_pair;
+    const int chunk = rem / nri, ri = rem - (rem / nri) * nri;
     const VerifyPair pp = pairs[q];
     const int n = pp.m;
     const int base = chunk * kScoreChunk;
     if (base >= n) continue;
-    const int Btot = rst[q].B;
+    const int Bpair = rst[q].B;
+    const int rbeg = ri * rpi * kTrialBatch;
+    const int rend = min(Bpair, rbeg + rpi * kTrialBatch);
+    if (rbeg >= rend) continue;
     const float4* xyf = xyf_all + pp.pts_off / 2;
     f32x2 x0[kScorePch / 2], x1[kScorePch / 2], y0[kScorePch / 2], y1[kScorePch / 2];
 #pragma unroll
@@ -1931,8 +1944,8 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
       y1[qq] = f32x2{v0.w, v1.w};
     }
     const bool full = base + kScoreChunk <= n;
-    for (int r0 = 0; r0 < Btot; r0 += kTrialBatch) {
-      const int B = min(kTrialBatch, Btot - r0);
+    for (int r0 = rbeg; r0 < rend; r0 += kTrialBatch) {
+      const int B = min(kTrialBatch, rend - r0);
       __syncthreads();
       if (lane < B) lnm[lane] = nmod[(int64_t)q * kWindowTrials + r0 + lane];
       {
@@ -2258,7 +2271,7 @@ hipError_t run_rounds(const VerifyPair* pairs, int npairs, const double* xy1, co
                        P.max_residual);
     hipLaunchKernelGGL(rs_score_kernel<K>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs, xyf,
                        rb.rst, rb.act[cur], rb.nact + cur, rb.nmod, rb.fcon, rb.mods, rb.cnts,
-                       max_chunks, P.max_residual, prof);
+                       max_chunks, W, P.max_residual, prof);
     hipLaunchKernelGGL(rs_replay_kernel<K>, dim3(gw), dim3(64), lds, stream, pairs, scratch, snaps, out, masks, rb.rst, rb.act[cur], rb.nact + cur,
                        rb.act[nxt], rb.nact + nxt, rb.nmod, rb.cnts, rb.mods, rb.wsnap, P, prof,
                        xyf);
