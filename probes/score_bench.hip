@@ -29,6 +29,13 @@ __global__ __launch_bounds__(64) void kern(const float4* pts, const float* cons,
       if (VAR == 2) {  // constants without LDS / readfirstlane
         for (int j = 0; j < 9; ++j) f.h[j] = 0.001f * (j + 1) + 1e-7f * m;
         f.a0 = 0.5f; f.a2 = 1e-4f; f.mr = 16.f;
+      } else if (VAR == 4) {  // constants stay in VGPRs (no readfirstlane)
+        const float4 c0 = reinterpret_cast<const float4*>(&lc[m][0])[0];
+        const float4 c1 = reinterpret_cast<const float4*>(&lc[m][0])[1];
+        const float4 c2 = reinterpret_cast<const float4*>(&lc[m][0])[2];
+        f.h[0] = c0.x; f.h[1] = c0.y; f.h[2] = c0.z; f.h[3] = c0.w;
+        f.h[4] = c1.x; f.h[5] = c1.y; f.h[6] = c1.z; f.h[7] = c1.w;
+        f.h[8] = c2.x; f.a0 = c2.y; f.a2 = c2.z; f.mr = 16.f;
       } else {
         const float4 c0 = reinterpret_cast<const float4*>(&lc[m][0])[0];
         const float4 c1 = reinterpret_cast<const float4*>(&lc[m][0])[1];
@@ -40,6 +47,25 @@ __global__ __launch_bounds__(64) void kern(const float4* pts, const float* cons,
       int cnt = 0;
       uint64_t any = 0;
       uint32_t vc = 0;
+      if (VAR == 3) {  // scalar fp32 (no packed math)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int hh = 0; hh < 2; ++hh) {
+            const float S0 = hh ? s0[q].y : s0[q].x, S1 = hh ? s1[q].y : s1[q].x;
+            const float D0 = hh ? d0[q].y : d0[q].x, D1 = hh ? d1[q].y : d1[q].x;
+            const float Q0 = __builtin_fmaf(f.h[0], S0, __builtin_fmaf(f.h[1], S1, f.h[2]));
+            const float Q1 = __builtin_fmaf(f.h[3], S0, __builtin_fmaf(f.h[4], S1, f.h[5]));
+            const float Q2 = __builtin_fmaf(f.h[6], S0, __builtin_fmaf(f.h[7], S1, f.h[8]));
+            const float W0 = __builtin_fmaf(D0, Q2, -Q0), W1 = __builtin_fmaf(D1, Q2, -Q1);
+            const float L = __builtin_fmaf(W0, W0, W1 * W1);
+            const float T = Q2 * Q2;
+            const float lo = __builtin_fmaf(T, f.mr, -f.a0), hi = __builtin_fmaf(T, f.a2, f.a0);
+            cnt += __popcll(__ballot(L <= lo));
+            any |= ~(__ballot(L <= lo) | __ballot(L > hi));
+          }
+        }
+      } else
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const f32x2 q0 = __builtin_elementwise_fma(f32x2(f.h[0]), s0[q], __builtin_elementwise_fma(f32x2(f.h[1]), s1[q], f32x2(f.h[2])));
@@ -89,5 +115,7 @@ int main() {
   run(kern<0>, "ballot+LDS consts");
   run(kern<1>, "VALU count");
   run(kern<2>, "no LDS consts");
+  run(kern<3>, "scalar fp32 lo/hi");
+  run(kern<4>, "VGPR consts");
   return 0;
 }

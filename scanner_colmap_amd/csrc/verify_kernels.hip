@@ -419,47 +419,27 @@ __device__ __attribute__((noinline)) bool h_exact_pt(const double* mk, float sx,
   return homography_sq(mk, (double)sx, (double)sy, (double)dx, (double)dy) <= maxr;
 }
 
-__device__ __forceinline__ int h_exact_pair(const double* mk, const HFilt& f, f32x2 s0, f32x2 s1,
-                                            f32x2 d0, f32x2 d1, uint64_t ok0, uint64_t ok1,
-                                            double maxr) {
-  f32x2 diff, mg;
-  h_filter_pair(f, s0, s1, d0, d1, &diff, &mg);
-  const bool u0 = fabsf(diff.x) <= mg.x, u1 = fabsf(diff.y) <= mg.y;
-  int cnt = 0;
-  if (__ballot(u0) & ok0) {
-    bool e = false;
-    if (u0) e = h_exact_pt(mk, s0.x, s1.x, d0.x, d1.x, maxr);
-    cnt += __popcll(__ballot(e) & ok0);
-  }
-  if (__ballot(u1) & ok1) {
-    bool e = false;
-    if (u1) e = h_exact_pt(mk, s0.y, s1.y, d0.y, d1.y, maxr);
-    cnt += __popcll(__ballot(e) & ok1);
-  }
-  return cnt;
-}
 
-__device__ __forceinline__ float uniform_f(float v) {
-  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
 
-// The hypothesis' constants (LDS, broadcast read) moved to scalar registers.
+// The hypothesis' constants (LDS, broadcast read), kept in vector registers:
+// no readfirstlane / SGPR copies per model (filter loop 20 % faster,
+// probes/score_bench.hip).
 __device__ __forceinline__ HFilt h_filter_load(const float* hc, float maxrf) {
   const float4 c0 = reinterpret_cast<const float4*>(hc)[0];
   const float4 c1 = reinterpret_cast<const float4*>(hc)[1];
   const float4 c2 = reinterpret_cast<const float4*>(hc)[2];
   HFilt f;
-  f.h0 = uniform_f(c0.x);
-  f.h1 = uniform_f(c0.y);
-  f.h2 = uniform_f(c0.z);
-  f.h3 = uniform_f(c0.w);
-  f.h4 = uniform_f(c1.x);
-  f.h5 = uniform_f(c1.y);
-  f.h6 = uniform_f(c1.z);
-  f.h7 = uniform_f(c1.w);
-  f.h8 = uniform_f(c2.x);
-  f.a0 = uniform_f(c2.y);
-  f.a2 = uniform_f(c2.z);
+  f.h0 = c0.x;
+  f.h1 = c0.y;
+  f.h2 = c0.z;
+  f.h3 = c0.w;
+  f.h4 = c1.x;
+  f.h5 = c1.y;
+  f.h6 = c1.z;
+  f.h7 = c1.w;
+  f.h8 = c2.x;
+  f.a0 = c2.y;
+  f.a2 = c2.z;
   f.mr = maxrf;
   return f;
 }
@@ -581,17 +561,17 @@ __device__ __forceinline__ FFilt f_filter_load(const float* fc, float maxrf) {
   const float4 c1 = reinterpret_cast<const float4*>(fc)[1];
   const float4 c2 = reinterpret_cast<const float4*>(fc)[2];
   FFilt f;
-  f.f0 = uniform_f(c0.x);
-  f.f1 = uniform_f(c0.y);
-  f.f2 = uniform_f(c0.z);
-  f.f3 = uniform_f(c0.w);
-  f.f4 = uniform_f(c1.x);
-  f.f5 = uniform_f(c1.y);
-  f.f6 = uniform_f(c1.z);
-  f.f7 = uniform_f(c1.w);
-  f.f8 = uniform_f(c2.x);
-  f.a0 = uniform_f(c2.y);
-  f.a1 = uniform_f(c2.z);
+  f.f0 = c0.x;
+  f.f1 = c0.y;
+  f.f2 = c0.z;
+  f.f3 = c0.w;
+  f.f4 = c1.x;
+  f.f5 = c1.y;
+  f.f6 = c1.z;
+  f.f7 = c1.w;
+  f.f8 = c2.x;
+  f.a0 = c2.y;
+  f.a1 = c2.z;
   f.mr = maxrf;
   return f;
 }
@@ -618,25 +598,6 @@ __device__ __attribute__((noinline)) bool f_exact_pt(const double* mk, float x0,
   return sampson_sq(mk, (double)x0, (double)x1, (double)y0, (double)y1) <= maxr;
 }
 
-__device__ __forceinline__ int f_exact_pair(const double* mk, const FFilt& f, f32x2 x0, f32x2 x1,
-                                            f32x2 y0, f32x2 y1, uint64_t ok0, uint64_t ok1,
-                                            double maxr) {
-  f32x2 diff, mg;
-  f_filter_pair(f, x0, x1, y0, y1, &diff, &mg);
-  const bool u0 = fabsf(diff.x) <= mg.x, u1 = fabsf(diff.y) <= mg.y;
-  int cnt = 0;
-  if (__ballot(u0) & ok0) {
-    bool e = false;
-    if (u0) e = f_exact_pt(mk, x0.x, x1.x, y0.x, y1.x, maxr);
-    cnt += __popcll(__ballot(e) & ok0);
-  }
-  if (__ballot(u1) & ok1) {
-    bool e = false;
-    if (u1) e = f_exact_pt(mk, x0.y, x1.y, y0.y, y1.y, maxr);
-    cnt += __popcll(__ballot(e) & ok1);
-  }
-  return cnt;
-}
 
 // Inlier count of one 7-point model (filter f; fp64 model mk in LDS, read
 // only for undecided points) over one chunk of points.
