@@ -1,7 +1,10 @@
 // io.cc byte formats (reference integration/op_cpp/io.cc) and the proto2
 // decoding of SequentialMatchingArgs (reference colmap.proto:6-65,
 // sequential_matching.cc:36-76) for the product library.
+#include <malloc.h>
+
 #include <cstdlib>
+#include <mutex>
 #include <string>
 
 #include "geom_solvers.h"
@@ -253,9 +256,45 @@ extern "C" uint32_t scm_pair_seed(uint32_t base, uint32_t id1, uint32_t id2) {
   return scm::geom::pair_seed(base, id1, id2);
 }
 
+// Recycled output buffers: a packed table-run result is hundreds of MB, and
+// the first touch of freshly mapped pages costs the host ~50 ms per step.
+// scm_blob_free parks up to two large blocks here and the next packed run
+// writes into one of them (its pages are already mapped).
+namespace scm {
+namespace {
+std::mutex g_pool_mu;
+void* g_pool[2] = {nullptr, nullptr};
+constexpr size_t kPoolMin = 16u << 20;
+}  // namespace
+
+void* pool_take(size_t* cap) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  int best = -1;
+  for (int i = 0; i < 2; ++i)
+    if (g_pool[i] && (best < 0 || malloc_usable_size(g_pool[i]) > malloc_usable_size(g_pool[best])))
+      best = i;
+  if (best < 0) return nullptr;
+  void* p = g_pool[best];
+  g_pool[best] = nullptr;
+  *cap = malloc_usable_size(p);
+  return p;
+}
+
+bool pool_give(void* p) {
+  if (!p || malloc_usable_size(p) < kPoolMin) return false;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  for (int i = 0; i < 2; ++i)
+    if (!g_pool[i]) {
+      g_pool[i] = p;
+      return true;
+    }
+  return false;
+}
+}  // namespace scm
+
 extern "C" void scm_blob_free(scm_blob* b) {
   if (!b) return;
-  std::free(b->data);
+  if (!scm::pool_give(b->data)) std::free(b->data);
   b->data = nullptr;
   b->size = 0;
 }

@@ -106,6 +106,10 @@ struct Tvg {
 
 void append_tvg(std::vector<uint8_t>* out, const Tvg& t);
 int make_blob(const std::vector<uint8_t>& bytes, scm_blob* out);
+// Large-output buffer recycling (scm_codec.cpp): take a parked block (its
+// usable size in *cap) or nullptr; give parks a block of >= 16 MiB.
+void* pool_take(size_t* cap);
+bool pool_give(void* p);
 std::vector<uint8_t> tvg_list_bytes(const std::vector<Tvg>& list);
 std::vector<uint8_t> id_list_bytes(const std::vector<uint32_t>& ids);
 

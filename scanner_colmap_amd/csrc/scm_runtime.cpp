@@ -731,6 +731,7 @@ struct Packed {
   size_t size = 0, cap = 0;
   std::vector<int64_t> row_off;  // [ids_r, tvgs_r] per row, then the end
   bool reserve(size_t need) {
+    if (!data) data = (uint8_t*)pool_take(&cap);  // recycled, already-mapped pages
     if (need <= cap) return true;
     const size_t want = std::max(need, cap + cap / 2);
     uint8_t* p = (uint8_t*)std::realloc(data, want);
@@ -1193,7 +1194,7 @@ int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t 
   Packed pk;
   const int rc = table_run_common(ctx, overlap, row_begin, row_end, &pk);
   if (rc != SCM_OK) {
-    std::free(pk.data);
+    if (!pool_give(pk.data)) std::free(pk.data);
     return rc;
   }
   const int64_t nrows = row_end - row_begin;
@@ -1208,7 +1209,7 @@ int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t 
         scm_blob_free(&pair_image_ids_out[q]);
         scm_blob_free(&tvgs_out[q]);
       }
-      std::free(pk.data);
+      if (!pool_give(pk.data)) std::free(pk.data);
       set_error("malloc failed");
       return SCM_E_NOMEM;
     }
@@ -1217,7 +1218,7 @@ int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t 
     pair_image_ids_out[r] = scm_blob{pa, (size_t)(b - a)};
     tvgs_out[r] = scm_blob{pb, (size_t)(c - b)};
   }
-  std::free(pk.data);
+  if (!pool_give(pk.data)) std::free(pk.data);
   return SCM_OK;
 }
 
