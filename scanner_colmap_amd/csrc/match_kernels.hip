@@ -72,6 +72,22 @@ __device__ __forceinline__ f32x16 chain(const bf16x8 (&a)[8], const bf16x8 (&b)[
   return acc;
 }
 
+// The same chain, refilling each B fragment with the next tile's as soon as
+// its last MFMA has been issued: the next tile's LDS reads are in flight for
+// the whole epilogue instead of stalling the next chain (no extra VGPRs).
+__device__ __forceinline__ f32x16 chain_refill(const bf16x8 (&a)[8], bf16x8 (&b)[8],
+                                               const f32x16& cinit, const uint8_t* bt_next,
+                                               int r, int h) {
+  f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], cinit, 0, 0, 0);
+  b[0] = *reinterpret_cast<const bf16x8*>(bt_next + r * 256 + (((h * 8 + 0) ^ (r & 15)) << 4));
+#pragma unroll
+  for (int q = 1; q < 8; ++q) {
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b[q], acc, 0, 0, 0);
+    b[q] = *reinterpret_cast<const bf16x8*>(bt_next + r * 256 + (((h * 8 + q) ^ (r & 15)) << 4));
+  }
+  return acc;
+}
+
 // Keys of one finished sub-tile: row top-2 state update; returns the
 // sub-tile's column partial (best two keys of the lane's column, re-keyed
 // with the row inside the workgroup).
@@ -91,6 +107,14 @@ template <bool CLAMP>
 __device__ __forceinline__ uint2 subtile_epilogue(const f32x16& acc, uint32_t tbits,
                                                   uint32_t (&b1r)[16], uint32_t (&b2r)[16],
                                                   uint32_t row_base) {
+#ifdef SCM_DIAG_MATCH_SKELETON
+  // diagnostics only: MFMA + LDS + staging skeleton, results discarded
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x ^= __float_as_uint(acc[i]);
+  b1r[0] ^= x;
+  return make_uint2(x, x);
+#endif
   uint32_t key[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -220,15 +244,20 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
         load_bfrag(lds + ((k + 1) % kStages) * kTileBytes, r, h, bnext);
 #endif
         // chain (t, 1) || epilogue (t, 0)
+#ifdef SCM_MATCH_REFILL
+        const f32x16 acc1 = chain_refill(afrag[1], bfrag, cinit,
+                                         lds + ((k + 1) % kStages) * kTileBytes, r, h);
+#else
         const f32x16 acc1 = chain(afrag[1], bfrag, cinit);
+#endif
         const uint2 c0 = subtile_epilogue<CLAMP>(acc0, tbits, b1r[0], b2r[0], row_base0);
         // chain (t + 1, 0) || epilogue (t, 1).  The barrier keeps the next
         // B fragments from being loaded while the current ones are live.
         __builtin_amdgcn_sched_barrier(0);
-#ifdef SCM_MATCH_BPREF
+#if defined(SCM_MATCH_BPREF)
 #pragma unroll
         for (int q = 0; q < 8; ++q) bfrag[q] = bnext[q];
-#else
+#elif !defined(SCM_MATCH_REFILL)
         load_bfrag(lds + ((k + 1) % kStages) * kTileBytes, r, h, bfrag);
 #endif
         acc0 = chain(afrag[0], bfrag, cinit);
@@ -243,7 +272,11 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
         *reinterpret_cast<uint4*>(lds + ((k + 2) % kStages) * kTileBytes + st_lds) = nxt;
         __syncthreads();
         // One wave merges the 8 wave partials of this tile and stores them.
+#ifdef SCM_DIAG_MATCH_NOCOLMERGE
+        if (false) {  // diagnostics only: column results dropped
+#else
         if (wave == (k & (kMatchWaves - 1)) && h == 0) {
+#endif
           uint2 m = colscratch[((k & 1) * kMatchWaves + 0) * 32 + r];
 #pragma unroll
           for (int w = 1; w < kMatchWaves; ++w) {

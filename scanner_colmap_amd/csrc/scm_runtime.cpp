@@ -40,6 +40,7 @@ namespace {
 
 constexpr int64_t kMaxPairsPerBatch = 16384;
 constexpr int64_t kDefaultPairsPerBatch = 8192;
+constexpr int64_t kDefaultEdgePairs = kDefaultPairsPerBatch;  // short edge batches: off (measured slower)
 
 struct ImageTable {
   int64_t n = 0;
@@ -148,6 +149,7 @@ struct scm_context {
   HostBuf h_stage;  // table upload staging
   int threads = 1;
   int64_t batch_pairs = kDefaultPairsPerBatch;  // SCM_BATCH_PAIRS overrides
+  int64_t edge_pairs = kDefaultEdgePairs;        // SCM_EDGE_PAIRS overrides
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
@@ -831,22 +833,50 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
   std::vector<Batch> batches;
   std::vector<uint32_t> ids(overlap);
   std::vector<int64_t> rows(overlap), sel;
-  Batch cur;
+  // Pair lists of every row first (the stencil dedup of execute()).
+  const int64_t nr = row_end - row_begin;
+  std::vector<std::vector<int64_t>> rsel(nr);
+  std::vector<std::vector<int64_t>> rrows(nr);
+  std::vector<std::vector<uint32_t>> rids(nr);
+  int64_t total_pairs = 0;
   for (int64_t r = row_begin; r < row_end; ++r) {
     for (int64_t s = 0; s < overlap; ++s) {
       rows[s] = std::min(r + s, t.n - 1);  // stencil clamped at the table end
       ids[s] = t.ids[rows[s]];
     }
     row_pairs(ids, &sel);
-    if (!cur.specs.empty() && (int64_t)(cur.specs.size() + sel.size()) > ctx->batch_pairs) {
+    rsel[r - row_begin] = sel;
+    rrows[r - row_begin] = rows;
+    rids[r - row_begin] = ids;
+    total_pairs += (int64_t)sel.size();
+  }
+  // Batches of whole rows, at most batch_pairs pairs each.  The first and
+  // the last batch are short (edge_pairs): the matcher runs alone until the
+  // first batch is matched and verification runs alone after the last one,
+  // so short edges shorten the pipeline's fill and drain.
+  const int64_t edge = (!ctx->serial && total_pairs > 2 * ctx->batch_pairs)
+                           ? std::min(ctx->batch_pairs, ctx->edge_pairs)
+                           : ctx->batch_pairs;
+  Batch cur;
+  int64_t remaining = total_pairs;  // pairs of rows i.. (this row included)
+  bool in_tail = false;
+  for (int64_t i = 0; i < nr; ++i) {
+    const int64_t np = (int64_t)rsel[i].size();
+    const int64_t limit = batches.empty() ? edge : ctx->batch_pairs;
+    const bool tail_starts =
+        edge < ctx->batch_pairs && !in_tail && !batches.empty() && remaining <= edge;
+    if (tail_starts) in_tail = true;
+    if (!cur.specs.empty() && ((int64_t)cur.specs.size() + np > limit || tail_starts)) {
       cur.pairs_begin.push_back((int64_t)cur.specs.size());
       batches.push_back(std::move(cur));
       cur = Batch();
     }
+    remaining -= np;
     cur.pairs_begin.push_back((int64_t)cur.specs.size());
-    for (int64_t s : sel) {
-      cur.specs.push_back({(int32_t)r, (int32_t)rows[s]});
-      cur.pair_ids.push_back(ids[s]);
+    const int64_t r = row_begin + i;
+    for (int64_t s : rsel[i]) {
+      cur.specs.push_back({(int32_t)r, (int32_t)rrows[i][s]});
+      cur.pair_ids.push_back(rids[i][s]);
     }
   }
   if (!cur.pairs_begin.empty()) {
@@ -957,6 +987,8 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   if (const char* e = std::getenv("SCM_SERIAL")) ctx->serial = e[0] == '1';
   if (const char* e = std::getenv("SCM_BATCH_PAIRS"))
     ctx->batch_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
+  if (const char* e = std::getenv("SCM_EDGE_PAIRS"))
+    ctx->edge_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
   if (hipSetDevice(device_index) != hipSuccess ||
       hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, stream_priority("SCM_MATCH_PRIO", false)) != hipSuccess ||
       hipStreamCreateWithPriority(&ctx->sets[0].vstream, hipStreamNonBlocking, stream_priority("SCM_VERIFY_PRIO", true)) != hipSuccess ||

@@ -456,6 +456,10 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
   uint64_t um[PCH];  // per point slot: lanes the filter left undecided
 #pragma unroll
   for (int q = 0; q < PCH / 2; ++q) {
+    if (!FULL && base + 128 * q >= n) {  // slot pair past the last point
+      um[2 * q] = um[2 * q + 1] = 0;
+      continue;
+    }
     f32x2 diff, mg;
     h_filter_pair(f, s0[q], s1[q], d0[q], d1[q], &diff, &mg);
     uint64_t i0 = __ballot(diff.x <= -mg.x), i1 = __ballot(diff.y <= -mg.y);
@@ -610,6 +614,10 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
   uint64_t um[PCH];  // per point slot: lanes the filter left undecided
 #pragma unroll
   for (int q = 0; q < PCH / 2; ++q) {
+    if (!FULL && base + 128 * q >= n) {  // slot pair past the last point
+      um[2 * q] = um[2 * q + 1] = 0;
+      continue;
+    }
     f32x2 diff, mg;
     f_filter_pair(f, x0[q], x1[q], y0[q], y1[q], &diff, &mg);
     uint64_t i0 = __ballot(diff.x < -mg.x), i1 = __ballot(diff.y < -mg.y);
