@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "image-pairs/s + Gdesc-dist/s, 8192×8192-kpt pairs, 1/2/4/8 GPU"
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (spec)
+I8_DENSE_PEAK_TOPS = 5000.0      # MI355X_MICROARCH.md matrix cores: i8 32x32x32 = 2x the bf16 rate
 DEFAULT_BATCH_PAIRS = 8192       # scm_runtime.cpp kDefaultPairsPerBatch (one matcher launch per batch)
 
 # BASELINE.json configs (synthetic stand-ins; no dataset is present).
@@ -104,7 +105,7 @@ def cpu_model() -> str:
     return "unknown"
 
 
-def pmc_traffic(workload: str, kpts: int, images: int):
+def pmc_traffic(workload: str, kpts: int, images: int, kernel: str):
     """HBM bytes per matcher launch from the committed rocprofv3 PMC summary
     of this workload (profiles/rNN_pmc_match.json, profiles/pmc_summary.py),
     or None when no summary matches the configuration being run."""
@@ -114,7 +115,8 @@ def pmc_traffic(workload: str, kpts: int, images: int):
         return None
     d = json.load(open(files[-1]))
     wl = WORKLOADS.get(workload, {})
-    if d.get("workload") != workload or kpts != wl.get("kpts") or images != wl.get("images"):
+    if (d.get("workload") != workload or kpts != wl.get("kpts") or images != wl.get("images")
+            or d.get("kernel") != kernel):
         return None
     return d, os.path.relpath(files[-1], ROOT)
 
@@ -220,8 +222,12 @@ def main():
         achieved_tf = flops_rank / (match_ms * 1e-3) / 1e12 if match_ms > 0 else None
         launches = max(1, -(-npairs // DEFAULT_BATCH_PAIRS))
         avg_n = float(np.mean(n_per_img)) if n_per_img else 0.0
-        alg_bytes_launch = npairs / launches * 2 * avg_n * 128 * 2  # bf16 descriptors of both images
-        pmc = pmc_traffic(args.workload, kpts, per_rank) if world == 1 else None
+        bf16 = os.environ.get("SCM_MATCH_BF16", "0") == "1"  # else the default i8 matcher
+        kernel = "match_tiles_kernel" if bf16 else "match_tiles_i8_kernel"
+        peak = BF16_DENSE_PEAK_TFLOPS if bf16 else I8_DENSE_PEAK_TOPS
+        # descriptors of both images, bf16 (2 B) or offset i8 (1 B) per element
+        alg_bytes_launch = npairs / launches * 2 * avg_n * 128 * (2 if bf16 else 1)
+        pmc = pmc_traffic(args.workload, kpts, per_rank, kernel) if world == 1 else None
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(corridor, args.cpu_baseline_pairs, overlap)
@@ -237,23 +243,28 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16 (exact u8 dot products) + f64 geometry",
+            "dtype": ("bf16 MFMA" if bf16 else "i8 MFMA on offset u8 descriptors, int32 accumulate")
+                     + " (exact u8 dot products) + f64 geometry",
             "data": "synthetic (seeded corridor scene, RootSIFT u8 descriptors; no dataset)",
             "config": {"workload": args.workload, "description": wl["desc"],
                        "images_per_rank": per_rank, "kpts": kpts, "overlap": overlap,
                        "pairs_per_step": int(total_pairs), "parallelism": f"pairs sharded x{world}"},
             "roofline": {
                 "bound": "mfma",
-                "kernel": "match_tiles_kernel",
+                "kernel": kernel,
                 "achieved": round(achieved_tf, 2) if achieved_tf else None,
-                "peak": BF16_DENSE_PEAK_TFLOPS,
+                "peak": peak,
                 "unit": "TFLOP/s",
-                "frac": round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4) if achieved_tf else None,
+                "frac": round(achieved_tf / peak, 4) if achieved_tf else None,
+                "frac_of_bf16_peak": (round(achieved_tf / BF16_DENSE_PEAK_TFLOPS, 4)
+                                      if achieved_tf else None),
                 "traffic": round(pmc[0]["traffic_bytes_per_launch"]) if pmc else None,
                 "traffic_source": (f"{pmc[1]}: FETCH_SIZE x2 + WRITE_SIZE per launch, "
                                    f"separate rocprofv3 --pmc passes") if pmc else None,
                 "algorithmic_bytes_per_launch": round(alg_bytes_launch),
-                "algorithmic": "2*N1*N2*128 flop per pair; per-launch time from HIP events",
+                "algorithmic": ("2*N1*N2*128 ops per pair (one multiply-add = 2 ops, i8 or bf16); "
+                                "per-launch time from HIP events; peak = dense MFMA peak of the "
+                                "kernel's dtype (i8 5.0 POP/s, bf16 2.5 PFLOP/s)"),
             },
             "stage_ms_per_step": {"match": round(match_ms / steps, 3),
                                   "finalize": round(final_ms / steps, 3),

@@ -9,8 +9,11 @@ namespace scm {
 constexpr int kMatchWaves = 8;                   // waves per workgroup
 constexpr int kMatchThreads = kMatchWaves * 64;  // 512
 constexpr int kRowsPerBlock = kMatchWaves * 64;  // pivot rows per workgroup
-constexpr int kTileBytes = 32 * 256;             // 32 bf16 descriptors
-constexpr int kTilesPerSeg = 256;                // 8 tile-index bits per key
+constexpr int kTileBytes = 32 * 256;             // bf16 kernel: 32 descriptors per LDS tile
+constexpr int kTile8Cols = 64;                   // i8 kernel: 64 descriptors per LDS tile
+constexpr int kTile8Bytes = kTile8Cols * 128;    // 8 KiB
+constexpr int kDescRowAlign = 64;                // descriptor rows of an image padded to this
+constexpr int kTilesPerSeg = 256;                // 8 tile-index bits per key (32-column units)
 constexpr int kColsPerSeg = kTilesPerSeg * 32;   // 8192 columns per segment
 constexpr int kIdxBits = 13;
 constexpr uint32_t kIdxMask = (1u << kIdxBits) - 1u;
@@ -40,10 +43,15 @@ struct PairDesc {
 hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int njobs,
                               const PairDesc* pairs, uint2* rowres, uint2* colpart,
                               bool clamp, hipStream_t stream);
+hipError_t launch_match_tiles_i8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
+                                 int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
+                                 bool clamp, hipStream_t stream);
 hipError_t launch_match_finalize(const PairDesc* pairs, int npairs, const uint2* rowres,
                                  const uint2* colpart, int32_t* m21, const float* lut,
                                  float max_ratio, float max_distance, int cross_check,
                                  uint2* matches, int32_t* counts, hipStream_t stream);
 hipError_t launch_u8_to_bf16(const uint8_t* in, uint16_t* out, int64_t n, hipStream_t stream);
+hipError_t launch_u8_to_i8(const uint8_t* in, uint8_t* out, int32_t* csum, int64_t nrows,
+                           hipStream_t stream);
 
 }  // namespace scm

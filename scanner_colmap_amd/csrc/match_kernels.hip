@@ -1,6 +1,6 @@
 // Kernel 1 of the sequential-matching stage: brute-force SIFT descriptor
-// similarity on bf16 MFMA with a fused, bit-exact two-way top-2 reduction,
-// plus the finalize kernel (ratio / distance tests, cross-check, ordered
+// similarity on MFMA with a fused, bit-exact two-way top-2 reduction, plus
+// the finalize kernel (ratio / distance tests, cross-check, ordered
 // compaction).
 //
 // Replaces colmap::MatchSiftFeaturesCPU as called from
@@ -9,24 +9,30 @@
 // ComputeSiftDistanceMatrix + FindBestMatchesOneWay x2 + FindBestMatches
 // (SURVEY.md §8a a5-a7).  The int32 N1 x N2 matrix is never materialised.
 //
+// Two matchers produce the same keys and partial results and share the
+// finalize kernel: match_tiles_i8_kernel (default: integer MFMA on offset
+// operands, see its section) and match_tiles_kernel (bf16 MFMA, selected by
+// SCM_MATCH_BF16=1).
+//
 // Exactness (SURVEY.md §8a "Exactness facts"):
-//  * u8 descriptors are exact in bf16; each MFMA chain starts from an
+//  * bf16: u8 descriptors are exact in bf16; each MFMA chain starts from an
 //    accumulator tuple holding 2^23, so every partial sum is an integer in
 //    [2^23, 2^24) — exact in f32 — and the f32 bit pattern of the result is
 //    0x4B000000 | dot (dot <= 128*255^2 < 2^23).  Verified on gfx950
-//    (probes/probe_mfma.hip, including all-255 operands).
+//    (probes/probe_mfma.hip, including all-255 operands).  i8: integer
+//    accumulation, exact by construction (see the i8 section).
 //  * Ordering keys are 32-bit: key = (dot << 13) | 13 index bits, where the
-//    index bits are [row code i (4 bits) | spare | tile index t (8 bits)].
-//    Fast variant: the pivot's bf16 operand is pre-scaled by 16 (exact) and
-//    the accumulator of register i starts at 2^23 + (15 - i), so the MFMA
-//    result bits are 0x4B000000 | dot << 4 | (15 - i) and ONE v_lshl_or_b32
-//    (acc << 9 | t-bits from an SGPR) forms the key.  This needs dot < 2^19
-//    for every pair of rows, which the host guarantees from exact squared
-//    norms (|a||b| < 2^19; RootSIFT u8 descriptors have |a|^2 ~ 2^18).
-//  * Otherwise the CLAMP variant (unscaled operand, accumulator 2^23) uses
-//    min(dot, 2^18), which changes no output: acosf(min(d * 2^-18, 1)) is 0
-//    for every d >= 2^18, so any (best, second) >= 2^18 fails the ratio test
-//    and a unique best above 2^18 keeps its index.
+//    index bits are [row code i (4 bits) | spare | tile index t (8 bits, in
+//    32-column units)].  Fast variant: the host guarantees dot < 2^19 for
+//    every pair of rows from exact squared norms (|a||b| < 2^19; RootSIFT u8
+//    descriptors have |a|^2 ~ 2^18) and the key is ONE v_lshl_or_b32.  (bf16:
+//    the pivot's operand is pre-scaled by 16 (exact) and the accumulator of
+//    register i starts at 2^23 + (15 - i), so the result bits are
+//    0x4B000000 | dot << 4 | (15 - i) and the key is acc << 9 | t-bits.)
+//  * Otherwise the CLAMP variant uses min(dot, 2^18), which changes no
+//    output: acosf(min(d * 2^-18, 1)) is 0 for every d >= 2^18, so any (best,
+//    second) >= 2^18 fails the ratio test and a unique best above 2^18 keeps
+//    its index.
 //  * max(key) = largest dot, lowest index among ties (FindBestMatchesOneWay
 //    keeps the first maximum; equal values fall to "second"); the running
 //    second is med3(key, best, second).  Both merges are associative, so the
@@ -40,6 +46,8 @@ namespace scm {
 
 typedef __attribute__((ext_vector_type(8))) short bf16x8;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(16))) int i32x16;
 
 __device__ __forceinline__ uint32_t med3_u32(uint32_t a, uint32_t b, uint32_t c) {
   uint32_t d;
@@ -53,6 +61,78 @@ __device__ __forceinline__ uint32_t merge_second(uint32_t b1a, uint32_t b2a,
   return max(max(b2a, b2b), lo);
 }
 
+// Top-2 of three unique keys: (max, median).
+__device__ __forceinline__ uint2 top2_of3(uint32_t a, uint32_t b, uint32_t c) {
+  return make_uint2(max(max(a, b), c), med3_u32(a, b, c));
+}
+
+// Merge of three top-2 pairs: best = max of the bests; second = max(median
+// of the bests, largest second) -- a second can only beat the median of the
+// bests when it belongs to the overall best's pair.
+__device__ __forceinline__ uint2 merge3(uint2 a, uint2 b, uint2 c) {
+  return make_uint2(max(max(a.x, b.x), c.x), max(med3_u32(a.x, b.x, c.x), max(max(a.y, b.y), c.y)));
+}
+
+// Column top-2 of one lane's 16 keys of a sub-tile (unique: the row code
+// differs) as a 3-input tree, 21 ops instead of 32 for the streaming update;
+// the best is re-keyed with its row inside the workgroup's 512-row block.
+__device__ __forceinline__ uint2 column_top2(const uint32_t (&key)[16], uint32_t row_base) {
+  const uint2 p0 = top2_of3(key[0], key[1], key[2]);
+  const uint2 p1 = top2_of3(key[3], key[4], key[5]);
+  const uint2 p2 = top2_of3(key[6], key[7], key[8]);
+  const uint2 p3 = top2_of3(key[9], key[10], key[11]);
+  const uint2 p4 = top2_of3(key[12], key[13], key[14]);
+  const uint2 l0 = merge3(p0, p1, p2);
+  const uint2 l1 = make_uint2(max(max(p3.x, p4.x), key[15]),
+                              max(med3_u32(p3.x, p4.x, key[15]), max(p3.y, p4.y)));
+  const uint32_t b1c = max(l0.x, l1.x);
+  const uint32_t b2c = max(max(min(l0.x, l1.x), l0.y), l1.y);
+  const uint32_t ii = 15u - ((b1c >> 9) & 15u);
+  const uint32_t row_in_blk = row_base + (ii & 3u) + 8u * (ii >> 2);
+  return make_uint2((b1c & ~kIdxMask) | (kIdxMask - row_in_blk), b2c & ~kIdxMask);
+}
+
+// Column partial of one 32-column sub-tile of a wave: merge the two row
+// sub-tiles and the two lane halves; lanes of half 0 store it for the
+// workgroup merge.
+__device__ __forceinline__ void wave_col_partial(uint2 c0, uint2 c1, uint2* dst, int h, int r) {
+  uint32_t B1 = max(c0.x, c1.x), B2 = merge_second(c0.x, c0.y, c1.x, c1.y);
+  const uint32_t o1 = __shfl_xor(B1, 32);
+  const uint32_t o2 = __shfl_xor(B2, 32);
+  B2 = merge_second(B1, B2, o1, o2);
+  B1 = max(B1, o1);
+  if (h == 0) dst[r] = make_uint2(B1, B2);
+}
+
+// Row flush at the end of a column segment: re-key each row's best with its
+// column inside the segment, reduce over the 32 lanes of each half, store.
+__device__ __forceinline__ void row_flush(const uint32_t (&b1r)[2][16], const uint32_t (&b2r)[2][16],
+                                          uint2* rr, int row0, int n1, int r, int h) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t k1 = b1r[s][i];
+      const uint32_t tl = (uint32_t)(kTilesPerSeg - 1) - (k1 & 255u);
+      const uint32_t col = tl * 32u + (uint32_t)r;
+      uint32_t B1 = (k1 & ~kIdxMask) | (kIdxMask - col);
+      uint32_t B2 = b2r[s][i] & ~kIdxMask;
+#pragma unroll
+      for (int x = 1; x < 32; x <<= 1) {
+        const uint32_t o1 = __shfl_xor(B1, x);
+        const uint32_t o2 = __shfl_xor(B2, x);
+        B2 = merge_second(B1, B2, o1, o2);
+        B1 = max(B1, o1);
+      }
+      const int row = row0 + 32 * s + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (r == i + 16 * s && row < n1) rr[row] = make_uint2(B1, B2);
+    }
+  }
+}
+
+// ===========================================================================
+// bf16 matcher (SCM_MATCH_BF16=1).
+// ===========================================================================
 constexpr int kStages = 3;
 
 __device__ __forceinline__ void load_bfrag(const uint8_t* bt, int r, int h, bf16x8 (&bfrag)[8]) {
@@ -72,37 +152,8 @@ __device__ __forceinline__ f32x16 chain(const bf16x8 (&a)[8], const bf16x8 (&b)[
   return acc;
 }
 
-// The same chain, refilling each B fragment with the next tile's as soon as
-// its last MFMA has been issued: the next tile's LDS reads are in flight for
-// the whole epilogue instead of stalling the next chain (no extra VGPRs).
-__device__ __forceinline__ f32x16 chain_refill(const bf16x8 (&a)[8], bf16x8 (&b)[8],
-                                               const f32x16& cinit, const uint8_t* bt_next,
-                                               int r, int h) {
-  f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[0], cinit, 0, 0, 0);
-  b[0] = *reinterpret_cast<const bf16x8*>(bt_next + r * 256 + (((h * 8 + 0) ^ (r & 15)) << 4));
-#pragma unroll
-  for (int q = 1; q < 8; ++q) {
-    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[q], b[q], acc, 0, 0, 0);
-    b[q] = *reinterpret_cast<const bf16x8*>(bt_next + r * 256 + (((h * 8 + q) ^ (r & 15)) << 4));
-  }
-  return acc;
-}
-
 // Keys of one finished sub-tile: row top-2 state update; returns the
-// sub-tile's column partial (best two keys of the lane's column, re-keyed
-// with the row inside the workgroup).
-// Top-2 of three unique keys: (max, median).
-__device__ __forceinline__ uint2 top2_of3(uint32_t a, uint32_t b, uint32_t c) {
-  return make_uint2(max(max(a, b), c), med3_u32(a, b, c));
-}
-
-// Merge of three top-2 pairs: best = max of the bests; second = max(median
-// of the bests, largest second) -- a second can only beat the median of the
-// bests when it belongs to the overall best's pair.
-__device__ __forceinline__ uint2 merge3(uint2 a, uint2 b, uint2 c) {
-  return make_uint2(max(max(a.x, b.x), c.x), max(med3_u32(a.x, b.x, c.x), max(max(a.y, b.y), c.y)));
-}
-
+// sub-tile's column partial.
 template <bool CLAMP>
 __device__ __forceinline__ uint2 subtile_epilogue(const f32x16& acc, uint32_t tbits,
                                                   uint32_t (&b1r)[16], uint32_t (&b2r)[16],
@@ -126,21 +177,7 @@ __device__ __forceinline__ uint2 subtile_epilogue(const f32x16& acc, uint32_t tb
     b2r[i] = med3_u32(key[i], b1r[i], b2r[i]);
     b1r[i] = max(b1r[i], key[i]);
   }
-  // Column top-2 of the lane's 16 keys (unique: the row code differs) as a
-  // 3-input tree: 21 ops instead of 32 for the streaming update.
-  const uint2 p0 = top2_of3(key[0], key[1], key[2]);
-  const uint2 p1 = top2_of3(key[3], key[4], key[5]);
-  const uint2 p2 = top2_of3(key[6], key[7], key[8]);
-  const uint2 p3 = top2_of3(key[9], key[10], key[11]);
-  const uint2 p4 = top2_of3(key[12], key[13], key[14]);
-  const uint2 l0 = merge3(p0, p1, p2);
-  const uint2 l1 = make_uint2(max(max(p3.x, p4.x), key[15]),
-                              max(med3_u32(p3.x, p4.x, key[15]), max(p3.y, p4.y)));
-  const uint32_t b1c = max(l0.x, l1.x);
-  const uint32_t b2c = max(max(min(l0.x, l1.x), l0.y), l1.y);
-  const uint32_t ii = 15u - ((b1c >> 9) & 15u);
-  const uint32_t row_in_blk = row_base + (ii & 3u) + 8u * (ii >> 2);
-  return make_uint2((b1c & ~kIdxMask) | (kIdxMask - row_in_blk), b2c & ~kIdxMask);
+  return column_top2(key, row_base);
 }
 
 // One workgroup = one MatchJob = 512 rows of the pivot image (8 waves x 64
@@ -151,11 +188,10 @@ __device__ __forceinline__ uint2 subtile_epilogue(const f32x16& acc, uint32_t tb
 //
 // Software pipeline (per wave, sub-tile granularity): the MFMA chain of
 // sub-tile (t, 1) runs while the epilogue of (t, 0) executes, and the chain of
-// (t + 1, 0) while the epilogue of (t, 1) executes, so the matrix core and
-// the vector ALU overlap inside every wave with only two accumulators.  B
-// tiles rotate through three LDS buffers (tile t+2 is staged while t+1 is
-// read); one barrier per tile.  The loop body is branch-free: past the last
-// tile of a segment the chain runs on a clamped tile and is discarded.
+// (t + 1, 0) while the epilogue of (t, 1) executes.  B tiles rotate through
+// three LDS buffers (tile t+2 is staged while t+1 is read); one barrier per
+// tile.  Past the last tile of a segment the chain runs on a clamped tile and
+// is discarded.
 template <bool CLAMP>
 __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
     const uint16_t* __restrict__ desc,        // bf16 table, [rows][128]
@@ -237,46 +273,20 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
         const int t = t_begin + k;
         const uint4 nxt = src0[(int64_t)min(t + 2, tlast) * 32 * 16];
         const uint32_t tbits = (uint32_t)(kTilesPerSeg - 1 - k);
-#ifdef SCM_MATCH_BPREF
-        // B fragments of tile t + 1 (staged since the last barrier) requested
-        // a whole sub-tile ahead of their chain.
-        bf16x8 bnext[8];
-        load_bfrag(lds + ((k + 1) % kStages) * kTileBytes, r, h, bnext);
-#endif
         // chain (t, 1) || epilogue (t, 0)
-#ifdef SCM_MATCH_REFILL
-        const f32x16 acc1 = chain_refill(afrag[1], bfrag, cinit,
-                                         lds + ((k + 1) % kStages) * kTileBytes, r, h);
-#else
         const f32x16 acc1 = chain(afrag[1], bfrag, cinit);
-#endif
         const uint2 c0 = subtile_epilogue<CLAMP>(acc0, tbits, b1r[0], b2r[0], row_base0);
         // chain (t + 1, 0) || epilogue (t, 1).  The barrier keeps the next
         // B fragments from being loaded while the current ones are live.
         __builtin_amdgcn_sched_barrier(0);
-#if defined(SCM_MATCH_BPREF)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) bfrag[q] = bnext[q];
-#elif !defined(SCM_MATCH_REFILL)
         load_bfrag(lds + ((k + 1) % kStages) * kTileBytes, r, h, bfrag);
-#endif
         acc0 = chain(afrag[0], bfrag, cinit);
         const uint2 c1 = subtile_epilogue<CLAMP>(acc1, tbits, b1r[1], b2r[1], row_base0 + 32u);
-        // Column partial of this wave: merge the two sub-tiles and the halves.
-        uint32_t B1 = max(c0.x, c1.x), B2 = merge_second(c0.x, c0.y, c1.x, c1.y);
-        const uint32_t o1 = __shfl_xor(B1, 32);
-        const uint32_t o2 = __shfl_xor(B2, 32);
-        B2 = merge_second(B1, B2, o1, o2);
-        B1 = max(B1, o1);
-        if (h == 0) colscratch[((k & 1) * kMatchWaves + wave) * 32 + r] = make_uint2(B1, B2);
+        wave_col_partial(c0, c1, colscratch + ((k & 1) * kMatchWaves + wave) * 32, h, r);
         *reinterpret_cast<uint4*>(lds + ((k + 2) % kStages) * kTileBytes + st_lds) = nxt;
         __syncthreads();
         // One wave merges the 8 wave partials of this tile and stores them.
-#ifdef SCM_DIAG_MATCH_NOCOLMERGE
-        if (false) {  // diagnostics only: column results dropped
-#else
         if (wave == (k & (kMatchWaves - 1)) && h == 0) {
-#endif
           uint2 m = colscratch[((k & 1) * kMatchWaves + 0) * 32 + r];
 #pragma unroll
           for (int w = 1; w < kMatchWaves; ++w) {
@@ -288,34 +298,229 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
         }
       }
       __syncthreads();  // every wave done with the LDS tiles before the next segment
-
-      // ---- Row flush for this segment: re-key with the column inside the
-      // segment, reduce over the 32 lanes of each half, store.
-      uint2* rr = rowres + pd.rowres_off + (int64_t)seg * pd.n1;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const uint32_t k1 = b1r[s][i];
-          const uint32_t tl = (uint32_t)(kTilesPerSeg - 1) - (k1 & 255u);
-          const uint32_t col = tl * 32u + (uint32_t)r;
-          uint32_t B1 = (k1 & ~kIdxMask) | (kIdxMask - col);
-          uint32_t B2 = b2r[s][i] & ~kIdxMask;
-#pragma unroll
-          for (int x = 1; x < 32; x <<= 1) {
-            const uint32_t o1 = __shfl_xor(B1, x);
-            const uint32_t o2 = __shfl_xor(B2, x);
-            B2 = merge_second(B1, B2, o1, o2);
-            B1 = max(B1, o1);
-          }
-          const int row = job.rb * kRowsPerBlock + wave * 64 + 32 * s + (i & 3) + 8 * (i >> 2) + 4 * h;
-          if (r == i + 16 * s && row < pd.n1) rr[row] = make_uint2(B1, B2);
-        }
-      }
+      row_flush(b1r, b2r, rowres + pd.rowres_off + (int64_t)seg * pd.n1,
+                job.rb * kRowsPerBlock + wave * 64, pd.n1, r, h);
     }
   }
 }
 
+// ===========================================================================
+// i8 matcher (default).
+//
+// v_mfma_i32_32x32x32_i8 covers K = 32 in the cycles the bf16 form needs for
+// K = 16 (MI355X_MICROARCH.md, matrix cores), so a 128-long dot is 4 MFMAs
+// instead of 8, and a descriptor is 128 B in HBM, L2 and LDS instead of 256.
+// u8 is not an i8 range, so the table holds a' = a - 128 (the byte a ^ 0x80)
+// and, per descriptor, cs = 128 * sum_d a_d (u8_to_i8_kernel); then exactly
+//   a.b = a'.b' + 128 (Sa + Sb) - 2^21,        |a'.b'| <= 2^21,
+// so a chain that starts from the accumulator ra_i + cb_j, with
+// ra_i = cs(a_i) - 2^21 (registers, per job) and cb_j = cs(b_j) (per tile),
+// ends at the exact int32 dot.  A pivot row past the image's count is a zero
+// descriptor (bytes 0x80, cs 0) and yields dots of 0, like the zero padding
+// of the table.  Keys, row state, column tree and the rowres / colpart
+// layouts are those of the bf16 kernel; an LDS tile holds 64 columns (two
+// 32-column sub-tiles) and the tile bits of a key still count 32-column
+// units.  Cost against bf16: one v_add per element (the accumulator init is
+// no longer a constant tuple) for half the MFMA cycles and half the bytes.
+// ===========================================================================
+constexpr int kStages8 = 4;                      // LDS ring: tile t+3 is fetched during tile t
+constexpr int kTiles8PerSeg = kTilesPerSeg / 2;  // 64-column tiles per 8192-column segment
+
+// Byte offset of 16-B chunk c (of 8) of column col in an i8 LDS tile.  The
+// XOR with (col >> 1) & 7 makes each 16-lane group of a ds_read_b128 (one
+// chunk, the 32 columns of one lane half) cover all 64 banks once
+// (MI355X_MICROARCH.md, LDS table).
+__device__ __forceinline__ int sw8(int col, int c) {
+  return col * 128 + ((c ^ ((col >> 1) & 7)) << 4);
+}
+
+// B fragments of column col: chunk 4h + q feeds MFMA q, as in the A fragment.
+__device__ __forceinline__ void load_bfrag8(const uint8_t* bt, int col, int h, i32x4 (&b)[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const i32x4*>(bt + sw8(col, 4 * h + q));
+}
+
+// One 32 x 32 sub-tile over K = 128: 4 MFMAs from the accumulator ra + cb.
+__device__ __forceinline__ i32x16 chain8(const i32x4 (&a)[4], const i32x4 (&b)[4],
+                                         const uint32_t (&ra)[16], uint32_t cb) {
+  i32x16 acc;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = (int)(ra[i] + cb);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[q], b[q], acc, 0, 0, 0);
+  return acc;
+}
+
+// Keys of a finished sub-tile (one v_lshl_or_b32 each: the 13 low bits are
+// wave-uniform), row top-2 update; returns the column partial.
+template <bool CLAMP>
+__device__ __forceinline__ uint2 subtile_epilogue8(const i32x16& acc, uint32_t tbits,
+                                                   uint32_t (&b1r)[16], uint32_t (&b2r)[16],
+                                                   uint32_t row_base) {
+#ifdef SCM_DIAG_MATCH_SKELETON
+  // diagnostics only: MFMA + LDS + staging skeleton, results discarded
+  uint32_t x = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) x ^= (uint32_t)acc[i];
+  b1r[0] ^= x;
+  return make_uint2(x, x);
+#endif
+  uint32_t key[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t d = (uint32_t)acc[i];
+    key[i] = ((CLAMP ? min(d, kLutMax) : d) << 13) | (((uint32_t)(15 - i) << 9) | tbits);
+    b2r[i] = med3_u32(key[i], b1r[i], b2r[i]);
+    b1r[i] = max(b1r[i], key[i]);
+  }
+  return column_top2(key, row_base);
+}
+
+// One workgroup = one MatchJob (512 pivot rows, 8 waves x 64) swept against
+// every column of its neighbour images, 64 columns per LDS tile.  Per wave
+// and tile: four 4-MFMA chains (row sub-tile s, column sub-tile c), software
+// pipelined so that each chain runs under the epilogue of the previous one:
+//   (s1,c0) || epi(s0,c0);  (s0,c1) || epi(s1,c0);  (s1,c1) || epi(s0,c1);
+//   (t+1: s0,c0) || epi(s1,c1).
+// Tiles rotate through a 4-stage LDS ring; one barrier per tile.
+template <bool CLAMP>
+__global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
+    const uint8_t* __restrict__ desc8,  // a ^ 0x80, [rows][128]
+    const int32_t* __restrict__ csum,   // 128 * sum_d a_d per row
+    const MatchJob* __restrict__ jobs, const PairDesc* __restrict__ pairs,
+    uint2* __restrict__ rowres,         // per pair [nseg][n1]
+    uint2* __restrict__ colpart) {      // per pair [nrb][n2pad]
+  __shared__ __attribute__((aligned(16))) uint8_t
+      lds[kStages8 * kTile8Bytes + 2 * 2 * kMatchWaves * 32 * 8];
+  // column partials: [tile parity][column sub-tile][wave][32]
+  uint2* colscratch = reinterpret_cast<uint2*>(lds + kStages8 * kTile8Bytes);
+
+  const MatchJob job = jobs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int row0 = job.rb * kRowsPerBlock + wave * 64;
+
+  // ---- A fragments (rows row0 + 32 s + r, chunks 4h + q) and the
+  // accumulator offsets of the rows this lane's results belong to.
+  i32x4 afrag[2][4];
+  uint32_t ra[2][16];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int row = row0 + 32 * s + r;
+    const bool ok = row < job.n1;
+    const i32x4* src =
+        reinterpret_cast<const i32x4*>(desc8 + (job.a_row + (ok ? row : 0)) * 128) + h * 4;
+    const int z = (int)0x80808080u;  // a = 0
+#pragma unroll
+    for (int q = 0; q < 4; ++q) afrag[s][q] = ok ? src[q] : i32x4{z, z, z, z};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int rw = row0 + 32 * s + 4 * h + (i & 3) + 8 * (i >> 2);
+      ra[s][i] = (rw < job.n1 ? (uint32_t)csum[job.a_row + rw] : 0u) - (1u << 21);
+    }
+  }
+  const uint32_t row_base0 = (uint32_t)wave * 64u + 4u * (uint32_t)h;
+
+  // Staging role of this thread: one 16-B chunk of the 8 KiB tile.
+  const int st_col = tid >> 3;   // 0..63
+  const int st_chunk = tid & 7;  // 0..7
+  const int st_lds = sw8(st_col, st_chunk);
+  constexpr int kTileChunks = kTile8Cols * 8;  // 16-B chunks per tile
+
+  for (int p = 0; p < job.npairs; ++p) {
+    const PairDesc pd = pairs[job.pair0 + p];
+    const int ntiles_total = (pd.n2 + kTile8Cols - 1) / kTile8Cols;
+    uint2* colp = colpart + pd.colpart_off + (int64_t)job.rb * pd.n2pad;
+    const int32_t* bsum = csum + pd.b_row;
+    const i32x4* src0 = reinterpret_cast<const i32x4*>(desc8 + (pd.b_row + st_col) * 128) + st_chunk;
+    for (int seg = 0; seg < pd.nseg; ++seg) {
+      const int t_begin = seg * kTiles8PerSeg;
+      const int t_end = min(ntiles_total, t_begin + kTiles8PerSeg);
+      const int tlast = t_end - 1;
+      uint32_t b1r[2][16], b2r[2][16];
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { b1r[s][i] = 0u; b2r[s][i] = 0u; }
+      // Prologue: stage tiles t_begin .. t_begin + 2, the column offsets of
+      // the first three, and the chain (t_begin: s0, c0).
+#pragma unroll
+      for (int j = 0; j < kStages8 - 1; ++j)
+        *reinterpret_cast<i32x4*>(lds + j * kTile8Bytes + st_lds) =
+            src0[(int64_t)min(t_begin + j, tlast) * kTileChunks];
+      const int t1 = min(t_begin + 1, tlast), t2 = min(t_begin + 2, tlast);
+      uint32_t cb0 = (uint32_t)bsum[t_begin * kTile8Cols + r];
+      uint32_t cb1 = (uint32_t)bsum[t_begin * kTile8Cols + 32 + r];
+      uint32_t cn0 = (uint32_t)bsum[t1 * kTile8Cols + r];
+      uint32_t cn1 = (uint32_t)bsum[t1 * kTile8Cols + 32 + r];
+      uint32_t cm0 = (uint32_t)bsum[t2 * kTile8Cols + r];
+      uint32_t cm1 = (uint32_t)bsum[t2 * kTile8Cols + 32 + r];
+      __syncthreads();
+      i32x4 bf0[4], bf1[4];
+      load_bfrag8(lds, r, h, bf0);
+      i32x16 acc = chain8(afrag[0], bf0, ra[0], cb0);
+
+      for (int k = 0; k < t_end - t_begin; ++k) {
+        const int t = t_begin + k;
+        const int t3 = min(t + 3, tlast);
+        const i32x4 nxt = src0[(int64_t)t3 * kTileChunks];
+        const uint32_t cf0 = (uint32_t)bsum[t3 * kTile8Cols + r];
+        const uint32_t cf1 = (uint32_t)bsum[t3 * kTile8Cols + 32 + r];
+        const uint32_t tb0 = (uint32_t)(kTilesPerSeg - 1 - 2 * k), tb1 = tb0 - 1u;
+        const uint8_t* cur = lds + (k % kStages8) * kTile8Bytes;
+        uint2* csc = colscratch + (k & 1) * 2 * kMatchWaves * 32;
+        // (s1, c0) || epilogue (s0, c0)
+        i32x16 acc2 = chain8(afrag[1], bf0, ra[1], cb0);
+        const uint2 e00 = subtile_epilogue8<CLAMP>(acc, tb0, b1r[0], b2r[0], row_base0);
+        __builtin_amdgcn_sched_barrier(0);
+        // (s0, c1) || epilogue (s1, c0)
+        load_bfrag8(cur, 32 + r, h, bf1);
+        acc = chain8(afrag[0], bf1, ra[0], cb1);
+        const uint2 e10 = subtile_epilogue8<CLAMP>(acc2, tb0, b1r[1], b2r[1], row_base0 + 32u);
+        wave_col_partial(e00, e10, csc + wave * 32, h, r);
+        __builtin_amdgcn_sched_barrier(0);
+        // (s1, c1) || epilogue (s0, c1)
+        acc2 = chain8(afrag[1], bf1, ra[1], cb1);
+        const uint2 e01 = subtile_epilogue8<CLAMP>(acc, tb1, b1r[0], b2r[0], row_base0);
+        __builtin_amdgcn_sched_barrier(0);
+        // (t + 1: s0, c0) || epilogue (s1, c1)
+        load_bfrag8(lds + ((k + 1) % kStages8) * kTile8Bytes, r, h, bf0);
+        acc = chain8(afrag[0], bf0, ra[0], cn0);
+        const uint2 e11 = subtile_epilogue8<CLAMP>(acc2, tb1, b1r[1], b2r[1], row_base0 + 32u);
+        wave_col_partial(e01, e11, csc + (kMatchWaves + wave) * 32, h, r);
+        *reinterpret_cast<i32x4*>(lds + ((k + 3) % kStages8) * kTile8Bytes + st_lds) = nxt;
+        cb0 = cn0;
+        cb1 = cn1;
+        cn0 = cm0;
+        cn1 = cm1;
+        cm0 = cf0;
+        cm1 = cf1;
+        __syncthreads();
+        // One wave merges the 8 wave partials of this tile's 64 columns.
+        if (wave == (k & (kMatchWaves - 1))) {
+          const uint2* src = csc + h * kMatchWaves * 32 + r;
+          uint2 m = src[0];
+#pragma unroll
+          for (int w = 1; w < kMatchWaves; ++w) {
+            const uint2 o = src[w * 32];
+            m.y = merge_second(m.x, m.y, o.x, o.y);
+            m.x = max(m.x, o.x);
+          }
+          colp[t * kTile8Cols + lane] = m;
+        }
+      }
+      __syncthreads();  // every wave done with the LDS tiles before the next segment
+      row_flush(b1r, b2r, rowres + pd.rowres_off + (int64_t)seg * pd.n1, row0, pd.n1, r, h);
+    }
+  }
+}
+
+// ===========================================================================
+// Finalize.
+// ===========================================================================
 // Upper bound, acosf LUT: lut[d] = acosf(min(d * 2^-18, 1.0f)), d in [0, 2^18],
 // built on the host with the host libm (the reference's own acosf).
 __device__ __forceinline__ float lut_at(const float* lut, uint32_t v) {
@@ -413,7 +618,10 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
   }
 }
 
-// u8 -> bf16 descriptor conversion at table load (exact: integers < 256).
+// ===========================================================================
+// Table conversion at load.
+// ===========================================================================
+// u8 -> bf16 (exact: integers < 256).
 __global__ void u8_to_bf16_kernel(const uint8_t* __restrict__ in,
                                   uint16_t* __restrict__ out, int64_t n) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -434,6 +642,28 @@ __global__ void u8_to_bf16_kernel(const uint8_t* __restrict__ in,
   }
 }
 
+// u8 -> i8 offset operands: a ^ 0x80 (= a - 128) per byte and
+// cs = 128 * sum_d a_d per 128-B descriptor (8 threads per descriptor).
+__global__ void u8_to_i8_kernel(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                int32_t* __restrict__ csum, int64_t nrows) {
+  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t row = g >> 3;
+  uint32_t s = 0;
+  if (row < nrows) {
+    const uint4 v = reinterpret_cast<const uint4*>(in)[g];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      s += (w[e] & 255u) + ((w[e] >> 8) & 255u) + ((w[e] >> 16) & 255u) + (w[e] >> 24);
+    reinterpret_cast<uint4*>(out)[g] = make_uint4(v.x ^ 0x80808080u, v.y ^ 0x80808080u,
+                                                  v.z ^ 0x80808080u, v.w ^ 0x80808080u);
+  }
+  s += __shfl_xor(s, 1);
+  s += __shfl_xor(s, 2);
+  s += __shfl_xor(s, 4);
+  if (row < nrows && (g & 7) == 0) csum[row] = (int32_t)(128u * s);
+}
+
 // ---------------------------------------------------------------------------
 // Host launchers.
 // ---------------------------------------------------------------------------
@@ -447,6 +677,19 @@ hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int nj
   else
     hipLaunchKernelGGL(match_tiles_kernel<false>, dim3(njobs), dim3(kMatchThreads), 0, stream,
                        desc, jobs, pairs, rowres, colpart);
+  return hipGetLastError();
+}
+
+hipError_t launch_match_tiles_i8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
+                                 int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
+                                 bool clamp, hipStream_t stream) {
+  if (njobs <= 0) return hipSuccess;
+  if (clamp)
+    hipLaunchKernelGGL(match_tiles_i8_kernel<true>, dim3(njobs), dim3(kMatchThreads), 0, stream,
+                       desc8, csum, jobs, pairs, rowres, colpart);
+  else
+    hipLaunchKernelGGL(match_tiles_i8_kernel<false>, dim3(njobs), dim3(kMatchThreads), 0, stream,
+                       desc8, csum, jobs, pairs, rowres, colpart);
   return hipGetLastError();
 }
 
@@ -466,6 +709,15 @@ hipError_t launch_u8_to_bf16(const uint8_t* in, uint16_t* out, int64_t n, hipStr
   const int64_t threads = (n + 7) / 8;
   hipLaunchKernelGGL(u8_to_bf16_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                      stream, in, out, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_u8_to_i8(const uint8_t* in, uint8_t* out, int32_t* csum, int64_t nrows,
+                           hipStream_t stream) {
+  if (nrows <= 0) return hipSuccess;
+  const int64_t threads = nrows * 8;
+  hipLaunchKernelGGL(u8_to_i8_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
+                     stream, in, out, csum, nrows);
   return hipGetLastError();
 }
 

@@ -50,11 +50,15 @@ struct ImageTable {
   std::vector<int64_t> kp_off;    // first float2 keypoint
   std::vector<uint64_t> max_norm2;
   int64_t total_rows = 0, total_kp = 0;
-  DevBuf desc;  // uint16 bf16 [total_rows][128]
-  DevBuf kpxy;  // float2 [total_kp]
-  DevBuf u8;    // upload staging
+  DevBuf desc;   // uint16 bf16 [total_rows][128] (bf16 matcher, SCM_MATCH_BF16=1)
+  DevBuf desc8;  // a ^ 0x80 [total_rows][128] (i8 matcher, default)
+  DevBuf csum;   // int32 128 * sum_d a_d [total_rows] (i8 matcher)
+  DevBuf kpxy;   // float2 [total_kp]
+  DevBuf u8;     // upload staging
   void release() {
     desc.release();
+    desc8.release();
+    csum.release();
     kpxy.release();
     u8.release();
   }
@@ -150,6 +154,7 @@ struct scm_context {
   int threads = 1;
   int64_t batch_pairs = kDefaultPairsPerBatch;  // SCM_BATCH_PAIRS overrides
   int64_t edge_pairs = kDefaultEdgePairs;        // SCM_EDGE_PAIRS overrides
+  bool match_bf16 = false;  // SCM_MATCH_BF16=1: bf16 MFMA matcher instead of i8
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
@@ -218,7 +223,7 @@ int upload_table(scm_context* ctx, ImageTable* t, const std::vector<RowView>& ro
     t->ndesc[i] = with_desc ? (int32_t)r.ndesc : 0;
     t->desc_row[i] = total_rows;
     t->kp_off[i] = total_kp;
-    if (with_desc) total_rows += (r.ndesc + 31) / 32 * 32;
+    if (with_desc) total_rows += (r.ndesc + kDescRowAlign - 1) / kDescRowAlign * kDescRowAlign;
     if (with_kp) total_kp += r.nkp;
   }
   t->total_rows = total_rows;
@@ -232,7 +237,7 @@ int upload_table(scm_context* ctx, ImageTable* t, const std::vector<RowView>& ro
       uint8_t* dst = h + (size_t)t->desc_row[i] * 128;
       const size_t nb = (size_t)r.ndesc * 128;
       std::memcpy(dst, r.desc, nb);
-      const size_t padded = (size_t)((r.ndesc + 31) / 32 * 32) * 128;
+      const size_t padded = (size_t)((r.ndesc + kDescRowAlign - 1) / kDescRowAlign * kDescRowAlign) * 128;
       std::memset(dst + nb, 0, padded - nb);
       uint64_t mx = 0;
       for (int64_t k = 0; k < r.ndesc; ++k) {
@@ -244,10 +249,17 @@ int upload_table(scm_context* ctx, ImageTable* t, const std::vector<RowView>& ro
       t->max_norm2[i] = mx;
     });
     SCM_TRY(t->u8.ensure(bytes));
-    SCM_TRY(t->desc.ensure(bytes * 2));
     SCM_HIP(hipMemcpyAsync(t->u8.ptr, h, bytes, hipMemcpyHostToDevice, ctx->stream));
-    SCM_HIP(launch_u8_to_bf16(t->u8.as<uint8_t>(), t->desc.as<uint16_t>(), (int64_t)bytes,
-                              ctx->stream));
+    if (ctx->match_bf16) {
+      SCM_TRY(t->desc.ensure(bytes * 2));
+      SCM_HIP(launch_u8_to_bf16(t->u8.as<uint8_t>(), t->desc.as<uint16_t>(), (int64_t)bytes,
+                                ctx->stream));
+    } else {
+      SCM_TRY(t->desc8.ensure(bytes));
+      SCM_TRY(t->csum.ensure((size_t)total_rows * sizeof(int32_t)));
+      SCM_HIP(launch_u8_to_i8(t->u8.as<uint8_t>(), t->desc8.as<uint8_t>(), t->csum.as<int32_t>(),
+                              total_rows, ctx->stream));
+    }
     SCM_HIP(hipStreamSynchronize(ctx->stream));
   }
   if (with_kp && total_kp > 0) {
@@ -375,7 +387,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
       std::memset(&pd, 0, sizeof(pd));
       pd.n1 = given ? 0 : t.ndesc[a];
       pd.n2 = given ? 0 : t.ndesc[b];
-      pd.n2pad = (pd.n2 + 31) / 32 * 32;
+      pd.n2pad = (pd.n2 + kTile8Cols - 1) / kTile8Cols * kTile8Cols;  // whole 64-column tiles
       pd.nseg = (pd.n2 + kColsPerSeg - 1) / kColsPerSeg;
       pd.nrb = (pd.n1 + kRowsPerBlock - 1) / kRowsPerBlock;
       pd.b_row = given ? 0 : t.desc_row[b];
@@ -469,14 +481,18 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
     }
   }
   SCM_HIP(hipEventRecord(bs.ev[0], sm));
-  if (!given) {
-    SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), bs.jobs.as<MatchJob>(), (int)nfast,
-                               bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
-                               bs.colpart.as<uint2>(), false, sm));
-    SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), bs.jobs.as<MatchJob>() + nfast,
-                               (int)(NJ - nfast), bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
-                               bs.colpart.as<uint2>(), true, sm));
-  }
+  if (!given)
+    for (int clamp = 0; clamp < 2; ++clamp) {
+      const MatchJob* jb = bs.jobs.as<MatchJob>() + (clamp ? nfast : 0);
+      const int nj = (int)(clamp ? NJ - nfast : nfast);
+      if (ctx->match_bf16)
+        SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), jb, nj, bs.pairs.as<PairDesc>(),
+                                   bs.rowres.as<uint2>(), bs.colpart.as<uint2>(), clamp, sm));
+      else
+        SCM_HIP(launch_match_tiles_i8(t.desc8.as<uint8_t>(), t.csum.as<int32_t>(), jb, nj,
+                                      bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
+                                      bs.colpart.as<uint2>(), clamp, sm));
+    }
   SCM_HIP(hipEventRecord(bs.ev[1], sm));
   if (!given)
     SCM_HIP(launch_match_finalize(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
@@ -989,6 +1005,7 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
     ctx->batch_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
   if (const char* e = std::getenv("SCM_EDGE_PAIRS"))
     ctx->edge_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
+  if (const char* e = std::getenv("SCM_MATCH_BF16")) ctx->match_bf16 = e[0] == '1';
   if (hipSetDevice(device_index) != hipSuccess ||
       hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, stream_priority("SCM_MATCH_PRIO", false)) != hipSuccess ||
       hipStreamCreateWithPriority(&ctx->sets[0].vstream, hipStreamNonBlocking, stream_priority("SCM_VERIFY_PRIO", true)) != hipSuccess ||

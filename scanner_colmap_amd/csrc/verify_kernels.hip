@@ -44,6 +44,9 @@ template <> struct KindTraits<KIND_T> { static constexpr int kmin = 1, kmin_loca
 // (uint16, one per match) lives in the pair's global scratch so that the LDS
 // footprint does not grow with the match count.
 struct __attribute__((aligned(16))) VerifyLds {
+  // Head: everything the windowed kernels (rs_begin / rs_draw / rs_replay)
+  // touch.  They allocate only kVerifyLdsHead bytes, so more of their
+  // wave-per-pair blocks fit on a CU.
   double best_model[9];
   double ata[45];
   double jA[81], jV[81];
@@ -52,6 +55,12 @@ struct __attribute__((aligned(16))) VerifyLds {
   uint32_t mt[624];
   uint32_t counts[kTrialBatch * 3];
   int32_t nmodels[kTrialBatch];
+  uint16_t jbuf[kTrialBatch * 7];  // Shuffle targets of one batch of samples
+  int32_t mt_idx;
+  int32_t best_n;
+  int32_t best_sum_valid;
+  int32_t pad_;
+  // Tail: the sequential LO-RANSAC of verify_final_kernel only.
   uint16_t samples[kTrialBatch][8];
   union {
     struct {
@@ -63,12 +72,11 @@ struct __attribute__((aligned(16))) VerifyLds {
       double fmod[kTrialBatchF * 3][9];  // the 7-point models (exact fallback)
     };
   };
-  uint16_t jbuf[kTrialBatch * 7];  // Shuffle targets of one batch of samples
-  int32_t mt_idx;
-  int32_t best_n;
-  int32_t best_sum_valid;
-  int32_t pad_;
 };
+#ifndef SCM_REPLAY_ATTR
+#define SCM_REPLAY_ATTR
+#endif
+constexpr size_t kVerifyLdsHead = __builtin_offsetof(VerifyLds, samples);
 
 // ---------------------------------------------------------------------------
 // Diagnostic phase timer (only when the launcher passes a profile buffer; no
@@ -462,7 +470,8 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
     }
     f32x2 diff, mg;
     h_filter_pair(f, s0[q], s1[q], d0[q], d1[q], &diff, &mg);
-    uint64_t i0 = __ballot(diff.x <= -mg.x), i1 = __ballot(diff.y <= -mg.y);
+    // strict: a point on the band's edge is undecided, never counted twice
+    uint64_t i0 = __ballot(diff.x < -mg.x), i1 = __ballot(diff.y < -mg.y);
     uint64_t u0 = __ballot(fabsf(diff.x) <= mg.x), u1 = __ballot(fabsf(diff.y) <= mg.y);
     if (!FULL) {
       const uint64_t ok0 = slot_mask(n, base, 2 * q), ok1 = slot_mask(n, base, 2 * q + 1);
@@ -1968,7 +1977,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
 
 // The sequential part of one window, in trial order, for every active pair.
 template <int K>
-__global__ __launch_bounds__(64) void rs_replay_kernel(
+__global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
     RansacState* __restrict__ rst, const int32_t* __restrict__ act,
@@ -2215,7 +2224,7 @@ hipError_t run_rounds(const VerifyPair* pairs, int npairs, const double* xy1, co
                       double* scratch, uint32_t* snaps, uint8_t* masks, VerifyOut* out,
                       const VerifyParams& P, const float4* xyf, const VerifyRoundBufs& rb,
                       int max_chunks, int max_m, uint64_t* prof, hipStream_t stream) {
-  const size_t lds = sizeof(VerifyLds);
+  const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
   const int max_trials = K == KIND_F ? P.max_trials_F : P.max_trials_H;
   const int gw = npairs < 4096 ? npairs : 4096;
 #ifndef SCM_SHUFFLE_LDS_KB
@@ -2280,14 +2289,14 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   hipError_t err;
   // F: LORANSAC<7-pt, 8-pt>, then the F inlier masks.
   if ((err = hipMemsetAsync(rb.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
-  hipLaunchKernelGGL(rs_begin_kernel<KIND_F>, dim3(gw), dim3(64), lds, stream, pairs, npairs,
+  hipLaunchKernelGGL(rs_begin_kernel<KIND_F>, dim3(gw), dim3(64), kVerifyLdsHead, stream, pairs, npairs,
                      scratch, snaps, out, masks, xyf, rb.rst, rb.act[0], rb.nact, params);
   if ((err = run_rounds<KIND_F>(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf,
                                 rb, max_chunks, max_m, prof, stream)) != hipSuccess)
     return err;
   // H: LORANSAC<H, H> on the same PRNG streams.
   if ((err = hipMemsetAsync(rb.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
-  hipLaunchKernelGGL(rs_begin_kernel<KIND_H>, dim3(gw), dim3(64), lds, stream, pairs, npairs,
+  hipLaunchKernelGGL(rs_begin_kernel<KIND_H>, dim3(gw), dim3(64), kVerifyLdsHead, stream, pairs, npairs,
                      scratch, snaps, out, masks, xyf, rb.rst, rb.act[0], rb.nact, params);
   if ((err = run_rounds<KIND_H>(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf,
                                 rb, max_chunks, max_m, prof, stream)) != hipSuccess)

@@ -74,3 +74,36 @@ def test_segmented_columns(gpu_ctx):
     b[8500:8800] = a
     b[100:200] = a[:100]
     _same(gpu_ctx, a, b)
+
+
+def test_high_bytes_fast_variant(gpu_ctx):
+    # Bytes >= 128 (outside the i8 range before the offset) with norms small
+    # enough for the fast keys: exercises the a - 128 correction terms.
+    rng = np.random.default_rng(12)
+    a = np.zeros((500, 128), np.uint8)
+    b = np.zeros((520, 128), np.uint8)
+    for m in (a, b):
+        idx = rng.integers(0, 128, size=(m.shape[0], 4))
+        np.put_along_axis(m, idx, rng.integers(128, 256, size=(m.shape[0], 4)).astype(np.uint8), 1)
+        m += rng.integers(0, 3, size=m.shape, dtype=np.uint8)
+    b[:150] = a[50:200]
+    _same(gpu_ctx, a, b)
+
+
+def test_bf16_matcher_parity(monkeypatch):
+    """SCM_MATCH_BF16=1 selects the bf16 MFMA matcher; it is bit-exact too."""
+    from scanner_colmap_amd import Context
+    monkeypatch.setenv("SCM_MATCH_BF16", "1")
+    ctx = Context(0)
+    try:
+        a, b = tie_stress_pair(1000, 777, 3)
+        _same(ctx, a, b)
+        imgs = Corridor(3, 1500, 3, seed=6).images()
+        _same(ctx, imgs[0][2], imgs[2][2])
+        rng = np.random.default_rng(10)
+        x = rng.integers(0, 256, size=(300, 128), dtype=np.uint8)
+        y = rng.integers(0, 256, size=(333, 128), dtype=np.uint8)
+        y[:100] = x[:100]
+        _same(ctx, x, y)
+    finally:
+        ctx.close()
