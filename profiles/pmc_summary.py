@@ -30,7 +30,7 @@ def main():
     ap.add_argument("fetch_csv")
     ap.add_argument("write_csv")
     ap.add_argument("out_json")
-    ap.add_argument("--kernel", default="match_tiles_kernel")
+    ap.add_argument("--kernel", default="match_tiles_i8_kernel")
     ap.add_argument("--workload", default="synth-1000x8192-k20")
     ap.add_argument("--pairs-per-step", type=int, default=18810)
     a = ap.parse_args()
