@@ -89,7 +89,7 @@ def match_pair(d1, d2, opts=None) -> np.ndarray:
     opts = opts or default_options()
     a = np.ascontiguousarray(d1, dtype=np.uint8).reshape(-1, 128)
     b = np.ascontiguousarray(d2, dtype=np.uint8).reshape(-1, 128)
-    cap = max(1, min(len(a), len(b)))
+    cap = max(1, len(a))  # one match per row at most (n1 without the cross-check)
     out = np.zeros((cap, 2), dtype=np.uint32)
     m = c_int64()
     rc = lib().oracle_match_pair(byref(opts), a.ctypes.data, len(a), b.ctypes.data, len(b),

@@ -228,7 +228,7 @@ class Context:
     def match_pair(self, desc1: np.ndarray, desc2: np.ndarray) -> np.ndarray:
         d1 = np.ascontiguousarray(desc1, dtype=np.uint8).reshape(-1, 128)
         d2 = np.ascontiguousarray(desc2, dtype=np.uint8).reshape(-1, 128)
-        cap = max(1, min(len(d1), len(d2)))
+        cap = max(1, len(d1))  # one match per row at most (n1 without the cross-check)
         out = np.zeros((cap, 2), dtype=np.uint32)
         n = c_int64()
         _check(self._lib.scm_match_pair(self._ptr, d1.ctypes.data, len(d1), d2.ctypes.data,

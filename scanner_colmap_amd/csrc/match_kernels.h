@@ -49,7 +49,8 @@ hipError_t launch_match_tiles_i8(const uint8_t* desc8, const int32_t* csum, cons
 hipError_t launch_match_finalize(const PairDesc* pairs, int npairs, const uint2* rowres,
                                  const uint2* colpart, int32_t* m21, const float* lut,
                                  float max_ratio, float max_distance, int cross_check,
-                                 uint2* matches, int32_t* counts, hipStream_t stream);
+                                 int colvals, uint2* matches, int32_t* counts,
+                                 hipStream_t stream);
 hipError_t launch_u8_to_bf16(const uint8_t* in, uint16_t* out, int64_t n, hipStream_t stream);
 hipError_t launch_u8_to_i8(const uint8_t* in, uint8_t* out, int32_t* csum, int64_t nrows,
                            hipStream_t stream);

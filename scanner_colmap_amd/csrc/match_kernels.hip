@@ -317,11 +317,24 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
 // ra_i = cs(a_i) - 2^21 (registers, per job) and cb_j = cs(b_j) (per tile),
 // ends at the exact int32 dot.  A pivot row past the image's count is a zero
 // descriptor (bytes 0x80, cs 0) and yields dots of 0, like the zero padding
-// of the table.  Keys, row state, column tree and the rowres / colpart
-// layouts are those of the bf16 kernel; an LDS tile holds 64 columns (two
-// 32-column sub-tiles) and the tile bits of a key still count 32-column
-// units.  Cost against bf16: one v_add per element (the accumulator init is
-// no longer a constant tuple) for half the MFMA cycles and half the bytes.
+// of the table.  An LDS tile holds 64 columns (two 32-column sub-tiles) and
+// the tile bits of a key still count 32-column units.
+//
+// Column side by VALUE (no index bits).  The chain starts from the per-row
+// registers ra_i = cs(a_i) + 2^21 as the MFMA's C operand (no VALU), so it
+// ends at x = dot - cb_j + 2^22, which lies in (0, 2^24) because cb_j <=
+// 128 * 128 * 255 < 2^22.  Within a column cb_j is a constant, so the top-2
+// values of the column are the top-2 of x plus (cb_j - 2^22), added once when
+// the workgroup's column partial is stored: the column tree runs on the raw
+// accumulators.  The column's best ROW is not tracked: with max_ratio <= 1 a
+// column whose best value is tied fails the ratio test (second == best), so
+// a passing column has a unique best row, and the cross-check "column j's
+// best row is i" reduces to "column j passes and its best value equals row
+// i's best value" (match_finalize_kernel, value mode).  The runtime selects
+// the bf16 kernel (column keys with the lowest-row tie rule) when max_ratio
+// > 1.  Row keys: one v_lshl_add_u32 per element, (x << 13) + ((cb_j << 13) |
+// t-bits), which is (dot << 13) | t-bits mod 2^32 (the 2^22 offset shifts out).
+// Per element: 1 (key) + 2 (row state) + ~1.3 (column tree) VALU ops.
 // ===========================================================================
 constexpr int kStages8 = 4;                      // LDS ring: tile t+3 is fetched during tile t
 constexpr int kTiles8PerSeg = kTilesPerSeg / 2;  // 64-column tiles per 8192-column segment
@@ -340,23 +353,55 @@ __device__ __forceinline__ void load_bfrag8(const uint8_t* bt, int col, int h, i
   for (int q = 0; q < 4; ++q) b[q] = *reinterpret_cast<const i32x4*>(bt + sw8(col, 4 * h + q));
 }
 
-// One 32 x 32 sub-tile over K = 128: 4 MFMAs from the accumulator ra + cb.
+// One 32 x 32 sub-tile over K = 128: 4 MFMAs, the first reading the per-row
+// offsets ra as its C operand.
 __device__ __forceinline__ i32x16 chain8(const i32x4 (&a)[4], const i32x4 (&b)[4],
-                                         const uint32_t (&ra)[16], uint32_t cb) {
-  i32x16 acc;
+                                         const i32x16& ra) {
+  i32x16 acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[0], b[0], ra, 0, 0, 0);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = (int)(ra[i] + cb);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[q], b[q], acc, 0, 0, 0);
+  for (int q = 1; q < 4; ++q) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[q], b[q], acc, 0, 0, 0);
   return acc;
 }
 
-// Keys of a finished sub-tile (one v_lshl_or_b32 each: the 13 low bits are
-// wave-uniform), row top-2 update; returns the column partial.
+// Top-2 VALUES (multiset: a tie puts the value in both) of one lane's 16
+// accumulators, as a 3-input tree (21 ops).
+__device__ __forceinline__ uint2 column_top2_values(const i32x16& acc) {
+  uint32_t v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = (uint32_t)acc[i];
+  const uint2 p0 = top2_of3(v[0], v[1], v[2]);
+  const uint2 p1 = top2_of3(v[3], v[4], v[5]);
+  const uint2 p2 = top2_of3(v[6], v[7], v[8]);
+  const uint2 p3 = top2_of3(v[9], v[10], v[11]);
+  const uint2 p4 = top2_of3(v[12], v[13], v[14]);
+  const uint2 l0 = merge3(p0, p1, p2);
+  const uint2 l1 = make_uint2(max(max(p3.x, p4.x), v[15]),
+                              max(med3_u32(p3.x, p4.x, v[15]), max(p3.y, p4.y)));
+  return make_uint2(max(l0.x, l1.x), max(max(min(l0.x, l1.x), l0.y), l1.y));
+}
+
+__device__ __forceinline__ uint32_t merge_second_values(uint32_t b1a, uint32_t b2a,
+                                                        uint32_t b1b, uint32_t b2b) {
+  return max(max(b2a, b2b), min(b1a, b1b));
+}
+
+// Column value partial of one 32-column sub-tile of a wave (both row
+// sub-tiles, both lane halves); lanes of half 0 store it for the workgroup merge.
+__device__ __forceinline__ void wave_col_partial_values(uint2 c0, uint2 c1, uint2* dst, int h, int r) {
+  uint32_t B1 = max(c0.x, c1.x), B2 = merge_second_values(c0.x, c0.y, c1.x, c1.y);
+  const uint32_t o1 = __shfl_xor(B1, 32);
+  const uint32_t o2 = __shfl_xor(B2, 32);
+  B2 = merge_second_values(B1, B2, o1, o2);
+  B1 = max(B1, o1);
+  if (h == 0) dst[r] = make_uint2(B1, B2);
+}
+
+// Row keys of a finished sub-tile and the row top-2 state update; returns the
+// column value partial.  kc = (cb_j << 13) | t-bits; cbm = cb_j - 2^22.
 template <bool CLAMP>
-__device__ __forceinline__ uint2 subtile_epilogue8(const i32x16& acc, uint32_t tbits,
-                                                   uint32_t (&b1r)[16], uint32_t (&b2r)[16],
-                                                   uint32_t row_base) {
+__device__ __forceinline__ uint2 subtile_epilogue8(const i32x16& acc, uint32_t kc, uint32_t cbm,
+                                                   uint32_t tbits, uint32_t (&b1r)[16],
+                                                   uint32_t (&b2r)[16]) {
 #ifdef SCM_DIAG_MATCH_SKELETON
   // diagnostics only: MFMA + LDS + staging skeleton, results discarded
   uint32_t x = 0;
@@ -365,15 +410,14 @@ __device__ __forceinline__ uint2 subtile_epilogue8(const i32x16& acc, uint32_t t
   b1r[0] ^= x;
   return make_uint2(x, x);
 #endif
-  uint32_t key[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
-    const uint32_t d = (uint32_t)acc[i];
-    key[i] = ((CLAMP ? min(d, kLutMax) : d) << 13) | (((uint32_t)(15 - i) << 9) | tbits);
-    b2r[i] = med3_u32(key[i], b1r[i], b2r[i]);
-    b1r[i] = max(b1r[i], key[i]);
+    const uint32_t x = (uint32_t)acc[i];
+    const uint32_t key = CLAMP ? (min(x + cbm, kLutMax) << 13) | tbits : (x << 13) + kc;
+    b2r[i] = med3_u32(key, b1r[i], b2r[i]);
+    b1r[i] = max(b1r[i], key);
   }
-  return column_top2(key, row_base);
+  return column_top2_values(acc);
 }
 
 // One workgroup = one MatchJob (512 pivot rows, 8 waves x 64) swept against
@@ -406,7 +450,7 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
   // ---- A fragments (rows row0 + 32 s + r, chunks 4h + q) and the
   // accumulator offsets of the rows this lane's results belong to.
   i32x4 afrag[2][4];
-  uint32_t ra[2][16];
+  i32x16 ra[2];
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     const int row = row0 + 32 * s + r;
@@ -419,10 +463,9 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int rw = row0 + 32 * s + 4 * h + (i & 3) + 8 * (i >> 2);
-      ra[s][i] = (rw < job.n1 ? (uint32_t)csum[job.a_row + rw] : 0u) - (1u << 21);
+      ra[s][i] = (int)((rw < job.n1 ? (uint32_t)csum[job.a_row + rw] : 0u) + (1u << 21));
     }
   }
-  const uint32_t row_base0 = (uint32_t)wave * 64u + 4u * (uint32_t)h;
 
   // Staging role of this thread: one 16-B chunk of the 8 KiB tile.
   const int st_col = tid >> 3;   // 0..63
@@ -461,7 +504,7 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
       __syncthreads();
       i32x4 bf0[4], bf1[4];
       load_bfrag8(lds, r, h, bf0);
-      i32x16 acc = chain8(afrag[0], bf0, ra[0], cb0);
+      i32x16 acc = chain8(afrag[0], bf0, ra[0]);
 
       for (int k = 0; k < t_end - t_begin; ++k) {
         const int t = t_begin + k;
@@ -472,26 +515,30 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
         const uint32_t tb0 = (uint32_t)(kTilesPerSeg - 1 - 2 * k), tb1 = tb0 - 1u;
         const uint8_t* cur = lds + (k % kStages8) * kTile8Bytes;
         uint2* csc = colscratch + (k & 1) * 2 * kMatchWaves * 32;
+        const uint32_t kc0 = (cb0 << 13) | tb0, kc1 = (cb1 << 13) | tb1;
+        const uint32_t cbm0 = cb0 - (1u << 22), cbm1 = cb1 - (1u << 22);
         // (s1, c0) || epilogue (s0, c0)
-        i32x16 acc2 = chain8(afrag[1], bf0, ra[1], cb0);
-        const uint2 e00 = subtile_epilogue8<CLAMP>(acc, tb0, b1r[0], b2r[0], row_base0);
+        i32x16 acc2 = chain8(afrag[1], bf0, ra[1]);
+        const uint2 e00 = subtile_epilogue8<CLAMP>(acc, kc0, cbm0, tb0, b1r[0], b2r[0]);
         __builtin_amdgcn_sched_barrier(0);
         // (s0, c1) || epilogue (s1, c0)
         load_bfrag8(cur, 32 + r, h, bf1);
-        acc = chain8(afrag[0], bf1, ra[0], cb1);
-        const uint2 e10 = subtile_epilogue8<CLAMP>(acc2, tb0, b1r[1], b2r[1], row_base0 + 32u);
-        wave_col_partial(e00, e10, csc + wave * 32, h, r);
+        acc = chain8(afrag[0], bf1, ra[0]);
+        const uint2 e10 = subtile_epilogue8<CLAMP>(acc2, kc0, cbm0, tb0, b1r[1], b2r[1]);
+        wave_col_partial_values(e00, e10, csc + wave * 32, h, r);
         __builtin_amdgcn_sched_barrier(0);
         // (s1, c1) || epilogue (s0, c1)
-        acc2 = chain8(afrag[1], bf1, ra[1], cb1);
-        const uint2 e01 = subtile_epilogue8<CLAMP>(acc, tb1, b1r[0], b2r[0], row_base0);
+        acc2 = chain8(afrag[1], bf1, ra[1]);
+        const uint2 e01 = subtile_epilogue8<CLAMP>(acc, kc1, cbm1, tb1, b1r[0], b2r[0]);
         __builtin_amdgcn_sched_barrier(0);
         // (t + 1: s0, c0) || epilogue (s1, c1)
         load_bfrag8(lds + ((k + 1) % kStages8) * kTile8Bytes, r, h, bf0);
-        acc = chain8(afrag[0], bf0, ra[0], cn0);
-        const uint2 e11 = subtile_epilogue8<CLAMP>(acc2, tb1, b1r[1], b2r[1], row_base0 + 32u);
-        wave_col_partial(e01, e11, csc + (kMatchWaves + wave) * 32, h, r);
+        acc = chain8(afrag[0], bf0, ra[0]);
+        const uint2 e11 = subtile_epilogue8<CLAMP>(acc2, kc1, cbm1, tb1, b1r[1], b2r[1]);
+        wave_col_partial_values(e01, e11, csc + (kMatchWaves + wave) * 32, h, r);
         *reinterpret_cast<i32x4*>(lds + ((k + 3) % kStages8) * kTile8Bytes + st_lds) = nxt;
+        // this lane's column in the merge below: 32 h + r of tile t
+        const uint32_t cbm_col = h ? cbm1 : cbm0;
         cb0 = cn0;
         cb1 = cn1;
         cn0 = cm0;
@@ -499,15 +546,22 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
         cm0 = cf0;
         cm1 = cf1;
         __syncthreads();
-        // One wave merges the 8 wave partials of this tile's 64 columns.
+        // One wave merges the 8 wave partials of this tile's 64 columns and
+        // stores the column's top-2 dot values.
         if (wave == (k & (kMatchWaves - 1))) {
           const uint2* src = csc + h * kMatchWaves * 32 + r;
           uint2 m = src[0];
 #pragma unroll
           for (int w = 1; w < kMatchWaves; ++w) {
             const uint2 o = src[w * 32];
-            m.y = merge_second(m.x, m.y, o.x, o.y);
+            m.y = merge_second_values(m.x, m.y, o.x, o.y);
             m.x = max(m.x, o.x);
+          }
+          m.x += cbm_col;
+          m.y += cbm_col;
+          if (CLAMP) {
+            m.x = min(m.x, kLutMax);
+            m.y = min(m.y, kLutMax);
           }
           colp[t * kTile8Cols + lane] = m;
         }
@@ -545,7 +599,7 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
     const PairDesc* __restrict__ pairs, const uint2* __restrict__ rowres,
     const uint2* __restrict__ colpart, int32_t* __restrict__ m21_scratch,
     const float* __restrict__ lut, float max_ratio, float max_distance,
-    int cross_check, uint2* __restrict__ matches, int32_t* __restrict__ counts) {
+    int cross_check, int colvals, uint2* __restrict__ matches, int32_t* __restrict__ counts) {
   __shared__ int32_t wave_tot[kFinThreads / 64];
   __shared__ int32_t wave_off[kFinThreads / 64];
   const PairDesc pd = pairs[blockIdx.x];
@@ -559,7 +613,20 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
   const uint2* cp = colpart + pd.colpart_off;
   const uint2* rr = rowres + pd.rowres_off;
 
-  if (cross_check) {
+  if (cross_check && colvals) {
+    // Column partials hold top-2 dot values (i8 kernel): m21[j] = the best
+    // value of a passing column (unique best row, max_ratio <= 1), else -1.
+    for (int j = tid; j < pd.n2; j += kFinThreads) {
+      uint2 m = cp[j];
+      for (int b = 1; b < pd.nrb; ++b) {
+        const uint2 o = cp[(int64_t)b * pd.n2pad + j];
+        m.y = max(max(m.y, o.y), min(m.x, o.x));
+        m.x = max(m.x, o.x);
+      }
+      m21[j] = passes(lut, m.x, m.y, max_ratio, max_distance) ? (int32_t)m.x : -1;
+    }
+    __syncthreads();
+  } else if (cross_check) {
     for (int j = tid; j < pd.n2; j += kFinThreads) {
       uint2 m = cp[j];
       int best_rb = 0;
@@ -609,7 +676,7 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
       const uint32_t best = m.x >> kIdxBits, second = m.y >> kIdxBits;
       const int32_t col = best_seg * (kTilesPerSeg * 32) + (int32_t)(kIdxMask - (m.x & kIdxMask));
       bool ok = passes(lut, best, second, max_ratio, max_distance);
-      if (ok && cross_check) ok = (m21[col] == i);
+      if (ok && cross_check) ok = m21[col] == (colvals ? (int32_t)best : i);
       if (ok) {
         if (pass == 0) ++cnt;
         else matches[pd.match_off + out++] = make_uint2((uint32_t)i, (uint32_t)col);
@@ -696,11 +763,12 @@ hipError_t launch_match_tiles_i8(const uint8_t* desc8, const int32_t* csum, cons
 hipError_t launch_match_finalize(const PairDesc* pairs, int npairs, const uint2* rowres,
                                  const uint2* colpart, int32_t* m21, const float* lut,
                                  float max_ratio, float max_distance, int cross_check,
-                                 uint2* matches, int32_t* counts, hipStream_t stream) {
+                                 int colvals, uint2* matches, int32_t* counts,
+                                 hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(match_finalize_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
-                     rowres, colpart, m21, lut, max_ratio, max_distance, cross_check, matches,
-                     counts);
+                     rowres, colpart, m21, lut, max_ratio, max_distance, cross_check, colvals,
+                     matches, counts);
   return hipGetLastError();
 }
 

@@ -499,6 +499,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
                                   bs.colpart.as<uint2>(), bs.m21.as<int32_t>(),
                                   ctx->lut.as<float>(), (float)ctx->opts.max_ratio,
                                   (float)ctx->opts.max_distance, ctx->opts.cross_check,
+                                  ctx->match_bf16 ? 0 : 1,
                                   bs.matches.as<uint2>(), bs.counts.as<int32_t>(), sm));
   SCM_HIP(hipEventRecord(bs.ev[2], sm));
   uint8_t* outh = reinterpret_cast<uint8_t*>(bs.out.host);
@@ -1006,6 +1007,11 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   if (const char* e = std::getenv("SCM_EDGE_PAIRS"))
     ctx->edge_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
   if (const char* e = std::getenv("SCM_MATCH_BF16")) ctx->match_bf16 = e[0] == '1';
+  // The i8 matcher tracks column top-2 by value only, which decides the
+  // cross-check exactly when a tied column best fails the ratio test, i.e.
+  // max_ratio <= 1 (match_kernels.hip, i8 section); otherwise the bf16 matcher
+  // keeps the lowest-row tie rule with column keys.
+  if ((float)o.max_ratio > 1.0f) ctx->match_bf16 = true;
   if (hipSetDevice(device_index) != hipSuccess ||
       hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, stream_priority("SCM_MATCH_PRIO", false)) != hipSuccess ||
       hipStreamCreateWithPriority(&ctx->sets[0].vstream, hipStreamNonBlocking, stream_priority("SCM_VERIFY_PRIO", true)) != hipSuccess ||

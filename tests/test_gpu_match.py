@@ -107,3 +107,42 @@ def test_bf16_matcher_parity(monkeypatch):
         _same(ctx, x, y)
     finally:
         ctx.close()
+
+
+def _opts_pair(**kw):
+    from scanner_colmap_amd import default_options
+    o_gpu, o_ref = default_options(), oracle.default_options()
+    for k, v in kw.items():
+        setattr(o_gpu, k, v)
+        setattr(o_ref, k, v)
+    return o_gpu, o_ref
+
+
+@pytest.mark.parametrize("kw", [dict(max_ratio=1.5, max_distance=3.0),
+                                dict(cross_check=0),
+                                dict(cross_check=0, max_ratio=1.2),
+                                dict(max_ratio=1.0)])
+def test_option_variants(kw):
+    """max_ratio > 1 lets tied bests pass the ratio test, so the lowest-index
+    tie rule decides the cross-check: the runtime switches to the bf16 matcher
+    (column keys).  max_ratio <= 1 and cross_check off stay on the i8 matcher
+    (column values).  All are bit-exact against the oracle."""
+    from scanner_colmap_amd import Context
+    o_gpu, o_ref = _opts_pair(**kw)
+    ctx = Context(0, o_gpu)
+    try:
+        cases = [tie_stress_pair(1000, 777, 3), tie_stress_pair(600, 900, 4)]
+        rng = np.random.default_rng(21)
+        x = rng.integers(0, 256, size=(300, 128), dtype=np.uint8)
+        y = rng.integers(0, 256, size=(333, 128), dtype=np.uint8)
+        y[:100] = x[:100]
+        y[100:150] = x[:50]  # duplicated columns: tied column bests
+        cases.append((x, y))
+        imgs = Corridor(3, 1200, 3, seed=8).images()
+        cases.append((imgs[0][2], imgs[1][2]))
+        for a, b in cases:
+            got = ctx.match_pair(a, b)
+            ref = oracle.match_pair(a, b, o_ref)
+            np.testing.assert_array_equal(got, ref)
+    finally:
+        ctx.close()
