@@ -1,0 +1,7 @@
+set -e
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/s26
+mkdir -p $O
+cd $R
+B=probes/build
+IMAGES=200 timeout -k 10 600 python3 probes/match_variants.py $B/libscm_base.so $B/libscm_w4.so > $O/mv.log 2>&1

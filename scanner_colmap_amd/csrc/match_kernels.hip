@@ -428,14 +428,14 @@ __device__ __forceinline__ uint2 subtile_epilogue8(const i32x16& acc, uint32_t k
 //   (t+1: s0,c0) || epi(s1,c1).
 // Tiles rotate through a 4-stage LDS ring; one barrier per tile.
 template <bool CLAMP>
-__global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
+__global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_tiles_i8_kernel(
     const uint8_t* __restrict__ desc8,  // a ^ 0x80, [rows][128]
     const int32_t* __restrict__ csum,   // 128 * sum_d a_d per row
     const MatchJob* __restrict__ jobs, const PairDesc* __restrict__ pairs,
     uint2* __restrict__ rowres,         // per pair [nseg][n1]
     uint2* __restrict__ colpart) {      // per pair [nrb][n2pad]
   __shared__ __attribute__((aligned(16))) uint8_t
-      lds[kStages8 * kTile8Bytes + 2 * 2 * kMatchWaves * 32 * 8];
+      lds[kStages8 * kTile8Bytes + 2 * 2 * kMatch8Waves * 32 * 8];
   // column partials: [tile parity][column sub-tile][wave][32]
   uint2* colscratch = reinterpret_cast<uint2*>(lds + kStages8 * kTile8Bytes);
 
@@ -445,7 +445,7 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
   const int wave = tid >> 6;
   const int r = lane & 31;
   const int h = lane >> 5;
-  const int row0 = job.rb * kRowsPerBlock + wave * 64;
+  const int row0 = job.rb * kRowsPerBlock8 + wave * 64;
 
   // ---- A fragments (rows row0 + 32 s + r, chunks 4h + q) and the
   // accumulator offsets of the rows this lane's results belong to.
@@ -467,18 +467,25 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
     }
   }
 
-  // Staging role of this thread: one 16-B chunk of the 8 KiB tile.
-  const int st_col = tid >> 3;   // 0..63
-  const int st_chunk = tid & 7;  // 0..7
-  const int st_lds = sw8(st_col, st_chunk);
+  // Staging role of this thread: kSt 16-B chunks of the 8 KiB tile (chunk
+  // tid + kMatch8Threads * u = 8 col + c).
   constexpr int kTileChunks = kTile8Cols * 8;  // 16-B chunks per tile
+  constexpr int kSt = kTileChunks / kMatch8Threads;
+  static_assert(kSt * kMatch8Threads == kTileChunks, "staging covers the tile");
+  int st_lds[kSt], st_off[kSt];
+#pragma unroll
+  for (int u = 0; u < kSt; ++u) {
+    const int ch = tid + kMatch8Threads * u;
+    st_lds[u] = sw8(ch >> 3, ch & 7);
+    st_off[u] = (ch >> 3) * 8 + (ch & 7);  // in 16-B chunks from the tile's first column
+  }
 
   for (int p = 0; p < job.npairs; ++p) {
     const PairDesc pd = pairs[job.pair0 + p];
     const int ntiles_total = (pd.n2 + kTile8Cols - 1) / kTile8Cols;
     uint2* colp = colpart + pd.colpart_off + (int64_t)job.rb * pd.n2pad;
     const int32_t* bsum = csum + pd.b_row;
-    const i32x4* src0 = reinterpret_cast<const i32x4*>(desc8 + (pd.b_row + st_col) * 128) + st_chunk;
+    const i32x4* src0 = reinterpret_cast<const i32x4*>(desc8 + pd.b_row * 128);
     for (int seg = 0; seg < pd.nseg; ++seg) {
       const int t_begin = seg * kTiles8PerSeg;
       const int t_end = min(ntiles_total, t_begin + kTiles8PerSeg);
@@ -492,8 +499,10 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
       // the first three, and the chain (t_begin: s0, c0).
 #pragma unroll
       for (int j = 0; j < kStages8 - 1; ++j)
-        *reinterpret_cast<i32x4*>(lds + j * kTile8Bytes + st_lds) =
-            src0[(int64_t)min(t_begin + j, tlast) * kTileChunks];
+#pragma unroll
+        for (int u = 0; u < kSt; ++u)
+          *reinterpret_cast<i32x4*>(lds + j * kTile8Bytes + st_lds[u]) =
+              src0[(int64_t)min(t_begin + j, tlast) * kTileChunks + st_off[u]];
       const int t1 = min(t_begin + 1, tlast), t2 = min(t_begin + 2, tlast);
       uint32_t cb0 = (uint32_t)bsum[t_begin * kTile8Cols + r];
       uint32_t cb1 = (uint32_t)bsum[t_begin * kTile8Cols + 32 + r];
@@ -509,12 +518,14 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
       for (int k = 0; k < t_end - t_begin; ++k) {
         const int t = t_begin + k;
         const int t3 = min(t + 3, tlast);
-        const i32x4 nxt = src0[(int64_t)t3 * kTileChunks];
+        i32x4 nxt[kSt];
+#pragma unroll
+        for (int u = 0; u < kSt; ++u) nxt[u] = src0[(int64_t)t3 * kTileChunks + st_off[u]];
         const uint32_t cf0 = (uint32_t)bsum[t3 * kTile8Cols + r];
         const uint32_t cf1 = (uint32_t)bsum[t3 * kTile8Cols + 32 + r];
         const uint32_t tb0 = (uint32_t)(kTilesPerSeg - 1 - 2 * k), tb1 = tb0 - 1u;
         const uint8_t* cur = lds + (k % kStages8) * kTile8Bytes;
-        uint2* csc = colscratch + (k & 1) * 2 * kMatchWaves * 32;
+        uint2* csc = colscratch + (k & 1) * 2 * kMatch8Waves * 32;
         const uint32_t kc0 = (cb0 << 13) | tb0, kc1 = (cb1 << 13) | tb1;
         const uint32_t cbm0 = cb0 - (1u << 22), cbm1 = cb1 - (1u << 22);
         // (s1, c0) || epilogue (s0, c0)
@@ -535,8 +546,10 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
         load_bfrag8(lds + ((k + 1) % kStages8) * kTile8Bytes, r, h, bf0);
         acc = chain8(afrag[0], bf0, ra[0]);
         const uint2 e11 = subtile_epilogue8<CLAMP>(acc2, kc1, cbm1, tb1, b1r[1], b2r[1]);
-        wave_col_partial_values(e01, e11, csc + (kMatchWaves + wave) * 32, h, r);
-        *reinterpret_cast<i32x4*>(lds + ((k + 3) % kStages8) * kTile8Bytes + st_lds) = nxt;
+        wave_col_partial_values(e01, e11, csc + (kMatch8Waves + wave) * 32, h, r);
+#pragma unroll
+        for (int u = 0; u < kSt; ++u)
+          *reinterpret_cast<i32x4*>(lds + ((k + 3) % kStages8) * kTile8Bytes + st_lds[u]) = nxt[u];
         // this lane's column in the merge below: 32 h + r of tile t
         const uint32_t cbm_col = h ? cbm1 : cbm0;
         cb0 = cn0;
@@ -548,11 +561,11 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_i8_kernel(
         __syncthreads();
         // One wave merges the 8 wave partials of this tile's 64 columns and
         // stores the column's top-2 dot values.
-        if (wave == (k & (kMatchWaves - 1))) {
-          const uint2* src = csc + h * kMatchWaves * 32 + r;
+        if (wave == (k & (kMatch8Waves - 1))) {
+          const uint2* src = csc + h * kMatch8Waves * 32 + r;
           uint2 m = src[0];
 #pragma unroll
-          for (int w = 1; w < kMatchWaves; ++w) {
+          for (int w = 1; w < kMatch8Waves; ++w) {
             const uint2 o = src[w * 32];
             m.y = merge_second_values(m.x, m.y, o.x, o.y);
             m.x = max(m.x, o.x);
@@ -752,10 +765,10 @@ hipError_t launch_match_tiles_i8(const uint8_t* desc8, const int32_t* csum, cons
                                  bool clamp, hipStream_t stream) {
   if (njobs <= 0) return hipSuccess;
   if (clamp)
-    hipLaunchKernelGGL(match_tiles_i8_kernel<true>, dim3(njobs), dim3(kMatchThreads), 0, stream,
+    hipLaunchKernelGGL(match_tiles_i8_kernel<true>, dim3(njobs), dim3(kMatch8Threads), 0, stream,
                        desc8, csum, jobs, pairs, rowres, colpart);
   else
-    hipLaunchKernelGGL(match_tiles_i8_kernel<false>, dim3(njobs), dim3(kMatchThreads), 0, stream,
+    hipLaunchKernelGGL(match_tiles_i8_kernel<false>, dim3(njobs), dim3(kMatch8Threads), 0, stream,
                        desc8, csum, jobs, pairs, rowres, colpart);
   return hipGetLastError();
 }

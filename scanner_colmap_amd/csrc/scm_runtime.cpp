@@ -374,6 +374,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   std::vector<MatchJob> jobs, jobs_clamp;
   bs.moff.resize(P);
   int64_t rr = 0, cp = 0, m21 = 0, mo = 0;
+  const int32_t rpb = ctx->match_bf16 ? kRowsPerBlock : kRowsPerBlock8;  // pivot rows per job
   for (int64_t i = 0; i < P;) {
     const int32_t a = specs[i].a;
     int64_t j = i;
@@ -389,7 +390,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
       pd.n2 = given ? 0 : t.ndesc[b];
       pd.n2pad = (pd.n2 + kTile8Cols - 1) / kTile8Cols * kTile8Cols;  // whole 64-column tiles
       pd.nseg = (pd.n2 + kColsPerSeg - 1) / kColsPerSeg;
-      pd.nrb = (pd.n1 + kRowsPerBlock - 1) / kRowsPerBlock;
+      pd.nrb = (pd.n1 + rpb - 1) / rpb;
       pd.b_row = given ? 0 : t.desc_row[b];
       pd.rowres_off = rr;
       pd.colpart_off = cp;
@@ -409,7 +410,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
     if (!given && t.ndesc[a] > 0) {
       // Jobs over runs of consecutive active pairs of this pivot.
       const int32_t n1 = t.ndesc[a];
-      const int32_t nrb = (n1 + kRowsPerBlock - 1) / kRowsPerBlock;
+      const int32_t nrb = (n1 + rpb - 1) / rpb;
       for (int64_t k = i; k < j;) {
         while (k < j && pds[k].n2 == 0) ++k;
         int64_t e = k;
