@@ -227,16 +227,18 @@ def test_verify_pair_too_few_matches_is_empty_geometry():
     assert struct.unpack_from("<Q", blob, 284)[0] == 0
 
 
-# --- the 9 x 9 eigen solver of the local optimisation (parallel-order Jacobi) --
+# --- the 9 x 9 null-vector solver of the local optimisation (inverse squaring) --
 def _pack45(a):
     return np.array([a[p, q] for p in range(9) for q in range(p, 9)])
 
 
 @pytest.mark.parametrize("seed", range(6))
 def test_ata_null_vector_matches_lapack(seed):
-    """geom_solvers.h jacobi9_par_eigen_min (4 disjoint rotations per round)
-    returns the eigenvector of the smallest eigenvalue of the normal matrix to
-    LAPACK accuracy, including near-singular systems (exact data + noise)."""
+    """geom_solvers.h's LO null vector (repeated squaring of (A + delta I)^-1,
+    the definition the GPU's lane-per-entry invsq9_null_wave follows bit for
+    bit) returns the eigenvector of the smallest eigenvalue of the normal
+    matrix to LAPACK accuracy, including near-singular systems (exact data +
+    noise)."""
     rng = np.random.default_rng(seed)
     x = rng.normal(size=(400, 9))
     x[:, 8] = 1.0
