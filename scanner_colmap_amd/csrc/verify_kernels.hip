@@ -395,25 +395,41 @@ __device__ __forceinline__ uint64_t slot_mask(int n, int base, int p) {
   return rem >= 64 ? ~0ull : (rem <= 0 ? 0ull : ((1ull << rem) - 1ull));
 }
 
+// Packed-fp32 FMA whose first and third operands are single dwords of
+// constant pairs broadcast to both halves by op_sel (the constants stay in the
+// registers their LDS loads landed in: no v_mov pairs per model).  SA / SC
+// pick the dword (0 = low, 1 = high) of a / c; b is a regular pair.
+// Bitwise the same as __builtin_elementwise_fma on splats (probes/opsel_probe.hip).
+#define SCM_PKFMA_BB(d, a, b, c, SA, SC)                                                 \
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[" #SA ",0," #SC "] op_sel_hi:[" #SA ",1," #SC "]" \
+      : "=v"(d) : "v"(a), "v"(b), "v"(c))
+#define SCM_PKFMA_BV(d, a, b, c, SA)                                                   \
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[" #SA ",0,0] op_sel_hi:[" #SA ",1,1]"      \
+      : "=v"(d) : "v"(a), "v"(b), "v"(c))
+
+// Filter constants as the register pairs of their LDS loads:
+// (h0,h1) (h2,h3) (h4,h5) (h6,h7) (h8,a0) (a2,-), and maxr splat.
 struct HFilt {
-  float h0, h1, h2, h3, h4, h5, h6, h7, h8, a0, a2, mr;
+  f32x2 p01, p23, p45, p67, p8a, pa2, mr;
 };
 
 // Filter quantities of one packed pair of points: surely inside iff
 // diff <= -mg, undecided iff |diff| <= mg, surely outside otherwise.
 __device__ __forceinline__ void h_filter_pair(const HFilt& f, f32x2 s0, f32x2 s1, f32x2 d0,
                                               f32x2 d1, f32x2* diff, f32x2* mg) {
-  const f32x2 q0 = __builtin_elementwise_fma(f32x2(f.h0), s0,
-                                             __builtin_elementwise_fma(f32x2(f.h1), s1, f32x2(f.h2)));
-  const f32x2 q1 = __builtin_elementwise_fma(f32x2(f.h3), s0,
-                                             __builtin_elementwise_fma(f32x2(f.h4), s1, f32x2(f.h5)));
-  const f32x2 q2 = __builtin_elementwise_fma(f32x2(f.h6), s0,
-                                             __builtin_elementwise_fma(f32x2(f.h7), s1, f32x2(f.h8)));
+  f32x2 t0, t1, t2, q0, q1, q2, m;
+  SCM_PKFMA_BB(t0, f.p01, s1, f.p23, 1, 0);  // h1 s1 + h2
+  SCM_PKFMA_BB(t1, f.p45, s1, f.p45, 0, 1);  // h4 s1 + h5
+  SCM_PKFMA_BB(t2, f.p67, s1, f.p8a, 1, 0);  // h7 s1 + h8
+  SCM_PKFMA_BV(q0, f.p01, s0, t0, 0);        // h0 s0 + (h1 s1 + h2)
+  SCM_PKFMA_BV(q1, f.p23, s0, t1, 1);        // h3 s0 + (h4 s1 + h5)
+  SCM_PKFMA_BV(q2, f.p67, s0, t2, 0);        // h6 s0 + (h7 s1 + h8)
   const f32x2 w0 = __builtin_elementwise_fma(d0, q2, -q0);
   const f32x2 w1 = __builtin_elementwise_fma(d1, q2, -q1);
   const f32x2 lhs = __builtin_elementwise_fma(w0, w0, w1 * w1);
-  const f32x2 rhs = f32x2(f.mr) * (q2 * q2);
-  *mg = __builtin_elementwise_fma(f32x2(f.a2), rhs, f32x2(f.a0));
+  const f32x2 rhs = f.mr * (q2 * q2);
+  SCM_PKFMA_BB(m, f.pa2, rhs, f.p8a, 0, 1);  // a2 rhs + a0
+  *mg = m;
   *diff = lhs - rhs;
 }
 
@@ -437,18 +453,13 @@ __device__ __forceinline__ HFilt h_filter_load(const float* hc, float maxrf) {
   const float4 c1 = reinterpret_cast<const float4*>(hc)[1];
   const float4 c2 = reinterpret_cast<const float4*>(hc)[2];
   HFilt f;
-  f.h0 = c0.x;
-  f.h1 = c0.y;
-  f.h2 = c0.z;
-  f.h3 = c0.w;
-  f.h4 = c1.x;
-  f.h5 = c1.y;
-  f.h6 = c1.z;
-  f.h7 = c1.w;
-  f.h8 = c2.x;
-  f.a0 = c2.y;
-  f.a2 = c2.z;
-  f.mr = maxrf;
+  f.p01 = f32x2{c0.x, c0.y};
+  f.p23 = f32x2{c0.z, c0.w};
+  f.p45 = f32x2{c1.x, c1.y};
+  f.p67 = f32x2{c1.z, c1.w};
+  f.p8a = f32x2{c2.x, c2.y};
+  f.pa2 = f32x2{c2.z, c2.w};
+  f.mr = f32x2(maxrf);
   return f;
 }
 
@@ -526,8 +537,9 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
 //   c1 = 2 g sqrt(maxr) + 4 d maxr, c0 = g^2 + 2 maxr d^2,
 //   a1 = 1.01 c1 / (2 tau maxr) + 5.1u, a0 = c1 tau / 2 + c0   (x 1.5).
 // ---------------------------------------------------------------------------
+// (f0,f1) (f2,f3) (f4,f5) (f6,f7) (f8,a0) (a1,-), and maxr splat (see HFilt).
 struct FFilt {
-  float f0, f1, f2, f3, f4, f5, f6, f7, f8, a0, a1, mr;
+  f32x2 p01, p23, p45, p67, p8a, pa1, mr;
 };
 
 __device__ __forceinline__ void f_filter_consts(const double* F, double S, double maxr,
@@ -574,18 +586,13 @@ __device__ __forceinline__ FFilt f_filter_load(const float* fc, float maxrf) {
   const float4 c1 = reinterpret_cast<const float4*>(fc)[1];
   const float4 c2 = reinterpret_cast<const float4*>(fc)[2];
   FFilt f;
-  f.f0 = c0.x;
-  f.f1 = c0.y;
-  f.f2 = c0.z;
-  f.f3 = c0.w;
-  f.f4 = c1.x;
-  f.f5 = c1.y;
-  f.f6 = c1.z;
-  f.f7 = c1.w;
-  f.f8 = c2.x;
-  f.a0 = c2.y;
-  f.a1 = c2.z;
-  f.mr = maxrf;
+  f.p01 = f32x2{c0.x, c0.y};
+  f.p23 = f32x2{c0.z, c0.w};
+  f.p45 = f32x2{c1.x, c1.y};
+  f.p67 = f32x2{c1.z, c1.w};
+  f.p8a = f32x2{c2.x, c2.y};
+  f.pa1 = f32x2{c2.z, c2.w};
+  f.mr = f32x2(maxrf);
   return f;
 }
 
@@ -593,16 +600,23 @@ __device__ __forceinline__ FFilt f_filter_load(const float* fc, float maxrf) {
 __device__ __forceinline__ void f_filter_pair(const FFilt& f, f32x2 x0, f32x2 x1, f32x2 y0,
                                               f32x2 y1, f32x2* diff, f32x2* mg) {
   typedef f32x2 V;
-  const V U0 = __builtin_elementwise_fma(V(f.f0), x0, __builtin_elementwise_fma(V(f.f1), x1, V(f.f2)));
-  const V U1 = __builtin_elementwise_fma(V(f.f3), x0, __builtin_elementwise_fma(V(f.f4), x1, V(f.f5)));
-  const V U2 = __builtin_elementwise_fma(V(f.f6), x0, __builtin_elementwise_fma(V(f.f7), x1, V(f.f8)));
-  const V V0 = __builtin_elementwise_fma(V(f.f0), y0, __builtin_elementwise_fma(V(f.f3), y1, V(f.f6)));
-  const V V1 = __builtin_elementwise_fma(V(f.f1), y0, __builtin_elementwise_fma(V(f.f4), y1, V(f.f7)));
+  V t, U0, U1, U2, V0, V1, m;
+  SCM_PKFMA_BB(t, f.p01, x1, f.p23, 1, 0);  // f1 x1 + f2
+  SCM_PKFMA_BV(U0, f.p01, x0, t, 0);        // f0 x0 + .
+  SCM_PKFMA_BB(t, f.p45, x1, f.p45, 0, 1);  // f4 x1 + f5
+  SCM_PKFMA_BV(U1, f.p23, x0, t, 1);        // f3 x0 + .
+  SCM_PKFMA_BB(t, f.p67, x1, f.p8a, 1, 0);  // f7 x1 + f8
+  SCM_PKFMA_BV(U2, f.p67, x0, t, 0);        // f6 x0 + .
+  SCM_PKFMA_BB(t, f.p23, y1, f.p67, 1, 0);  // f3 y1 + f6
+  SCM_PKFMA_BV(V0, f.p01, y0, t, 0);        // f0 y0 + .
+  SCM_PKFMA_BB(t, f.p45, y1, f.p67, 0, 1);  // f4 y1 + f7
+  SCM_PKFMA_BV(V1, f.p01, y0, t, 1);        // f1 y0 + .
   const V e = __builtin_elementwise_fma(y0, U0, __builtin_elementwise_fma(y1, U1, U2));
   const V den = __builtin_elementwise_fma(
       U0, U0, __builtin_elementwise_fma(U1, U1, __builtin_elementwise_fma(V0, V0, V1 * V1)));
-  const V rhs = V(f.mr) * den;
-  *mg = __builtin_elementwise_fma(V(f.a1), rhs, V(f.a0));
+  const V rhs = f.mr * den;
+  SCM_PKFMA_BB(m, f.pa1, rhs, f.p8a, 0, 1);  // a1 rhs + a0
+  *mg = m;
   *diff = __builtin_elementwise_fma(e, e, -rhs);
 }
 
