@@ -2046,7 +2046,28 @@ __global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay_kernel(
       for (int i = lane; i < B * MM; i += 64)
         s.counts[i] = cnts[(int64_t)q * kWindowTrials * 3 + r0 * MM + i];
       wsync();
-      for (int t = 0; t < B && !abort; ++t) {
+      // Trials of the round in order.  Only two kinds need the sequential
+      // step: a candidate (a model whose inlier count reaches the best) and
+      // the abort trial (tt >= dyn_max and >= min_num_trials); the lanes
+      // find the next such trial in one ballot (lane = trial of the round),
+      // and the trials in between -- no model to compare, no abort -- are
+      // skipped as the sequential scan would pass them.
+      int t = 0;
+      while (t < B && !abort) {
+        bool need = false;
+        if (lane < B && lane >= t) {
+          const int nml = s.nmodels[lane];
+          const int bnl = s.best_n;
+          bool cand = false;
+#pragma unroll
+          for (int k = 0; k < MM; ++k)
+            cand |= k < nml && (int)s.counts[lane * MM + k] >= bnl;
+          const int ttl = trial + r0 + lane;
+          need = cand || (ttl >= dyn_max && ttl >= P.min_num_trials);
+        }
+        const uint64_t needm = __ballot(need);
+        if (!needm) break;
+        t = (int)__builtin_ctzll(needm);
         const int tt = trial + r0 + t;
         const int nmt = s.nmodels[t];
         for (int k = 0; k < MM; ++k) {
@@ -2140,6 +2161,7 @@ __global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay_kernel(
             }
           }
         }
+        ++t;
       }
     }
     wsync();
