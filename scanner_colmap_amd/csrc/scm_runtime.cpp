@@ -156,6 +156,8 @@ struct scm_context {
   int64_t edge_pairs = kDefaultEdgePairs;        // SCM_EDGE_PAIRS overrides
   bool match_bf16 = false;  // SCM_MATCH_BF16=1: bf16 MFMA matcher instead of i8
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
+  bool balanced = false;  // SCM_BALANCED=1: equal batches (measured slower: verification
+                         // batches are latency-bound, a short last batch drains faster)
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
   bool profile = false;
@@ -872,19 +874,29 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
   // the last batch are short (edge_pairs): the matcher runs alone until the
   // first batch is matched and verification runs alone after the last one,
   // so short edges shorten the pipeline's fill and drain.
+  // Balanced batches: the fewest batches of at most batch_pairs, sized
+  // equally (an unbalanced split leaves a long first matcher launch before
+  // verification can start, and a short last batch).
+  const int64_t nbatch = std::max<int64_t>(1, (total_pairs + ctx->batch_pairs - 1) / ctx->batch_pairs);
+  const int64_t bsize = ctx->balanced ? (total_pairs + nbatch - 1) / nbatch : ctx->batch_pairs;
   const int64_t edge = (!ctx->serial && total_pairs > 2 * ctx->batch_pairs)
-                           ? std::min(ctx->batch_pairs, ctx->edge_pairs)
-                           : ctx->batch_pairs;
+                           ? std::min(bsize, ctx->edge_pairs)
+                           : bsize;
   Batch cur;
   int64_t remaining = total_pairs;  // pairs of rows i.. (this row included)
   bool in_tail = false;
   for (int64_t i = 0; i < nr; ++i) {
     const int64_t np = (int64_t)rsel[i].size();
-    const int64_t limit = batches.empty() ? edge : ctx->batch_pairs;
+    const int64_t limit = batches.empty() ? edge : bsize;
     const bool tail_starts =
-        edge < ctx->batch_pairs && !in_tail && !batches.empty() && remaining <= edge;
+        edge < bsize && !in_tail && !batches.empty() && remaining <= edge;
     if (tail_starts) in_tail = true;
-    if (!cur.specs.empty() && ((int64_t)cur.specs.size() + np > limit || tail_starts)) {
+    // A batch closes once it holds its share (balanced: at least bsize, so
+    // the rows' granularity adds no extra batch) or would pass the cap.
+    const int64_t have = (int64_t)cur.specs.size();
+    const bool full = ctx->balanced && limit == bsize ? have >= limit || have + np > ctx->batch_pairs
+                                                      : have + np > limit;
+    if (!cur.specs.empty() && (full || tail_starts)) {
       cur.pairs_begin.push_back((int64_t)cur.specs.size());
       batches.push_back(std::move(cur));
       cur = Batch();
@@ -1003,6 +1015,7 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::max(1, std::atoi(e));
   ctx->threads = std::max(1, std::min(16, hw));
   if (const char* e = std::getenv("SCM_SERIAL")) ctx->serial = e[0] == '1';
+  if (const char* e = std::getenv("SCM_BALANCED")) ctx->balanced = e[0] == '1';
   if (const char* e = std::getenv("SCM_BATCH_PAIRS"))
     ctx->batch_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
   if (const char* e = std::getenv("SCM_EDGE_PAIRS"))
