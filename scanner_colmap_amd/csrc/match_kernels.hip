@@ -336,6 +336,9 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
 // t-bits), which is (dot << 13) | t-bits mod 2^32 (the 2^22 offset shifts out).
 // Per element: 1 (key) + 2 (row state) + ~1.3 (column tree) VALU ops.
 // ===========================================================================
+#ifndef SCM_DIAG_MERGE
+#define SCM_DIAG_MERGE 1  // diagnostics: 0 drops the column merge (wrong results)
+#endif
 constexpr int kStages8 = 4;                      // LDS ring: tile t+3 is fetched during tile t
 constexpr int kTiles8PerSeg = kTilesPerSeg / 2;  // 64-column tiles per 8192-column segment
 
@@ -558,10 +561,14 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_ti
         cn1 = cm1;
         cm0 = cf0;
         cm1 = cf1;
+#ifndef SCM_DIAG_NOBARRIER  // diagnostics only: no barrier (races; timing of the barrier)
         __syncthreads();
+#endif
         // One wave merges the 8 wave partials of this tile's 64 columns and
-        // stores the column's top-2 dot values.
-        if (wave == (k & (kMatch8Waves - 1))) {
+        // stores the column's top-2 dot values.  (All waves sharing the merge,
+        // 8 columns each, measured 6 % slower: every wave then waits on LDS
+        // right after the barrier.)
+        if (SCM_DIAG_MERGE && wave == (k & (kMatch8Waves - 1))) {
           const uint2* src = csc + h * kMatch8Waves * 32 + r;
           uint2 m = src[0];
 #pragma unroll

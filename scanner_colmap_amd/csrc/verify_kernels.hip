@@ -1885,7 +1885,10 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
 // the filter constants of one round at a time are broadcast from LDS and
 // lane t accumulates the count of hypothesis t of the round.
 constexpr int kScoreThreads = 64;
-constexpr int kScorePch = 8;  // points per lane
+#ifndef SCM_SCORE_PCH
+#define SCM_SCORE_PCH 8
+#endif
+constexpr int kScorePch = SCM_SCORE_PCH;  // points per lane
 constexpr int kScoreChunk = kScoreThreads * kScorePch;
 constexpr int kScoreTargetItems = 65536;  // work items per score launch (8 per wave slot)
 
