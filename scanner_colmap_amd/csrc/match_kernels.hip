@@ -339,7 +339,20 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
 #ifndef SCM_DIAG_MERGE
 #define SCM_DIAG_MERGE 1  // diagnostics: 0 drops the column merge (wrong results)
 #endif
-constexpr int kStages8 = 4;                      // LDS ring: tile t+3 is fetched during tile t
+// LDS ring: tile t + 3 is staged at the end of tile t and first read in tile
+// t + 2 (the B-fragment prefetch).  One barrier per kBarTiles tiles (2: 2-3 %
+// faster than 1): waves may then be two tiles apart, so the ring holds 6 tiles
+// and the column partials 4 buffers; every staging write still has a barrier
+// before its first read.  (4 would need staging further ahead: with t + 3 a
+// group of 4 leaves writes and reads of a tile without a barrier between.)
+#ifndef SCM_I8_BAR_TILES
+#define SCM_I8_BAR_TILES 2
+#endif
+constexpr int kBarTiles = SCM_I8_BAR_TILES;
+static_assert(kBarTiles == 1 || kBarTiles == 2, "barrier group");
+constexpr int kStages8 = kBarTiles == 1 ? 4 : 6;
+constexpr int kCscBufs = 2 * kBarTiles;
+constexpr int kAhead8 = 3;
 constexpr int kTiles8PerSeg = kTilesPerSeg / 2;  // 64-column tiles per 8192-column segment
 
 // Byte offset of 16-B chunk c (of 8) of column col in an i8 LDS tile.  The
@@ -423,6 +436,28 @@ __device__ __forceinline__ uint2 subtile_epilogue8(const i32x16& acc, uint32_t k
   return column_top2_values(acc);
 }
 
+// Merge of the kMatch8Waves wave partials of tile k's 64 columns (one wave;
+// lane = column 32 h + r) and store of the columns' top-2 dot values.
+template <bool CLAMP>
+__device__ __forceinline__ void merge_cols8(const uint2* colscratch, int k, int h, int r, int lane,
+                                            uint32_t cbm_col, uint2* dst) {
+  const uint2* src = colscratch + (k % kCscBufs) * 2 * kMatch8Waves * 32 + h * kMatch8Waves * 32 + r;
+  uint2 m = src[0];
+#pragma unroll
+  for (int w = 1; w < kMatch8Waves; ++w) {
+    const uint2 o = src[w * 32];
+    m.y = merge_second_values(m.x, m.y, o.x, o.y);
+    m.x = max(m.x, o.x);
+  }
+  m.x += cbm_col;
+  m.y += cbm_col;
+  if (CLAMP) {
+    m.x = min(m.x, kLutMax);
+    m.y = min(m.y, kLutMax);
+  }
+  dst[lane] = m;
+}
+
 // One workgroup = one MatchJob (512 pivot rows, 8 waves x 64) swept against
 // every column of its neighbour images, 64 columns per LDS tile.  Per wave
 // and tile: four 4-MFMA chains (row sub-tile s, column sub-tile c), software
@@ -438,7 +473,7 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_ti
     uint2* __restrict__ rowres,         // per pair [nseg][n1]
     uint2* __restrict__ colpart) {      // per pair [nrb][n2pad]
   __shared__ __attribute__((aligned(16))) uint8_t
-      lds[kStages8 * kTile8Bytes + 2 * 2 * kMatch8Waves * 32 * 8];
+      lds[kStages8 * kTile8Bytes + kCscBufs * 2 * kMatch8Waves * 32 * 8];
   // column partials: [tile parity][column sub-tile][wave][32]
   uint2* colscratch = reinterpret_cast<uint2*>(lds + kStages8 * kTile8Bytes);
 
@@ -501,7 +536,7 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_ti
       // Prologue: stage tiles t_begin .. t_begin + 2, the column offsets of
       // the first three, and the chain (t_begin: s0, c0).
 #pragma unroll
-      for (int j = 0; j < kStages8 - 1; ++j)
+      for (int j = 0; j < kAhead8; ++j)
 #pragma unroll
         for (int u = 0; u < kSt; ++u)
           *reinterpret_cast<i32x4*>(lds + j * kTile8Bytes + st_lds[u]) =
@@ -528,7 +563,7 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_ti
         const uint32_t cf1 = (uint32_t)bsum[t3 * kTile8Cols + 32 + r];
         const uint32_t tb0 = (uint32_t)(kTilesPerSeg - 1 - 2 * k), tb1 = tb0 - 1u;
         const uint8_t* cur = lds + (k % kStages8) * kTile8Bytes;
-        uint2* csc = colscratch + (k & 1) * 2 * kMatch8Waves * 32;
+        uint2* csc = colscratch + (k % kCscBufs) * 2 * kMatch8Waves * 32;
         const uint32_t kc0 = (cb0 << 13) | tb0, kc1 = (cb1 << 13) | tb1;
         const uint32_t cbm0 = cb0 - (1u << 22), cbm1 = cb1 - (1u << 22);
         // (s1, c0) || epilogue (s0, c0)
@@ -561,30 +596,32 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_ti
         cn1 = cm1;
         cm0 = cf0;
         cm1 = cf1;
+        if ((k + 1) % kBarTiles == 0) {
 #ifndef SCM_DIAG_NOBARRIER  // diagnostics only: no barrier (races; timing of the barrier)
-        __syncthreads();
+          __syncthreads();
 #endif
-        // One wave merges the 8 wave partials of this tile's 64 columns and
-        // stores the column's top-2 dot values.  (All waves sharing the merge,
-        // 8 columns each, measured 6 % slower: every wave then waits on LDS
-        // right after the barrier.)
-        if (SCM_DIAG_MERGE && wave == (k & (kMatch8Waves - 1))) {
-          const uint2* src = csc + h * kMatch8Waves * 32 + r;
-          uint2 m = src[0];
+          // One wave merges the 8 wave partials of the last kBarTiles tiles'
+          // 64 columns each and stores the columns' top-2 dot values.  (All
+          // waves sharing the merge, 8 columns each, measured 6 % slower:
+          // every wave then waits on LDS right after the barrier.)
+          if (SCM_DIAG_MERGE && wave == ((k / kBarTiles) & (kMatch8Waves - 1))) {
 #pragma unroll
-          for (int w = 1; w < kMatch8Waves; ++w) {
-            const uint2 o = src[w * 32];
-            m.y = merge_second_values(m.x, m.y, o.x, o.y);
-            m.x = max(m.x, o.x);
+            for (int g = kBarTiles - 1; g > 0; --g)
+              merge_cols8<CLAMP>(colscratch, k - g, h, r, lane,
+                                 (uint32_t)bsum[(t - g) * kTile8Cols + lane] - (1u << 22),
+                                 colp + (t - g) * kTile8Cols);
+            merge_cols8<CLAMP>(colscratch, k, h, r, lane, cbm_col, colp + t * kTile8Cols);
           }
-          m.x += cbm_col;
-          m.y += cbm_col;
-          if (CLAMP) {
-            m.x = min(m.x, kLutMax);
-            m.y = min(m.y, kLutMax);
-          }
-          colp[t * kTile8Cols + lane] = m;
         }
+      }
+      if (const int rest = (t_end - t_begin) % kBarTiles) {  // tiles after the last barrier
+        __syncthreads();
+        const int kl = t_end - t_begin - 1;
+        if (SCM_DIAG_MERGE && wave == ((kl / kBarTiles) & (kMatch8Waves - 1)))
+          for (int g = rest - 1; g >= 0; --g)
+            merge_cols8<CLAMP>(colscratch, kl - g, h, r, lane,
+                               (uint32_t)bsum[(t_end - 1 - g) * kTile8Cols + lane] - (1u << 22),
+                               colp + (t_end - 1 - g) * kTile8Cols);
       }
       __syncthreads();  // every wave done with the LDS tiles before the next segment
       row_flush(b1r, b2r, rowres + pd.rowres_off + (int64_t)seg * pd.n1, row0, pd.n1, r, h);
