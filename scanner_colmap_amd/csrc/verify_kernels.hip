@@ -377,7 +377,7 @@ __device__ __forceinline__ void h_filter_consts(const double* H, double S, doubl
 #pragma unroll
   for (int j = 0; j < 9; ++j) c[j] = (float)H[j];
   c[9] = __double2float_ru(a0);
-  c[10] = __double2float_ru(a2);
+  c[10] = __double2float_ru(a2 * maxr);  // a2 maxr: mg = a2mr Q2^2 + a0 (h_filter_pair)
   c[11] = 0.0f;
   if (!(lmax < 1e36 && rmax < 1e36 && a2 < 1e30 && a0 < 1e36)) {
     // fp32 evaluation unsafe: Q = 0, mg = 1 marks every point undecided, so
@@ -427,10 +427,13 @@ __device__ __forceinline__ void h_filter_pair(const HFilt& f, f32x2 s0, f32x2 s1
   const f32x2 w0 = __builtin_elementwise_fma(d0, q2, -q0);
   const f32x2 w1 = __builtin_elementwise_fma(d1, q2, -q1);
   const f32x2 lhs = __builtin_elementwise_fma(w0, w0, w1 * w1);
-  const f32x2 rhs = f.mr * (q2 * q2);
-  SCM_PKFMA_BB(m, f.pa2, rhs, f.p8a, 0, 1);  // a2 rhs + a0
+  const f32x2 qq = q2 * q2;
+  // rhs = maxr Q2^2 enters fused (one rounding fewer than fl(maxr fl(Q2^2)),
+  // inside the bound), and the margin a2 rhs + a0 as (a2 maxr) Q2^2 + a0 with
+  // a2 maxr rounded up in h_filter_consts.
+  SCM_PKFMA_BB(m, f.pa2, qq, f.p8a, 0, 1);  // a2mr Q2^2 + a0
   *mg = m;
-  *diff = lhs - rhs;
+  *diff = __builtin_elementwise_fma(-f.mr, qq, lhs);
 }
 
 // Exact fp64 test (HomographyMatrixEstimator::Residuals) of the undecided
