@@ -469,10 +469,36 @@ __device__ __forceinline__ HFilt h_filter_load(const float* hc, float maxrf) {
 // Inlier count of one hypothesis (filter f, fp64 model mk in LDS) over the
 // points [base, base + 64 PCH) (point base + 64 p + lane in slot p; FULL:
 // every slot holds a point).
+// Deferred exact tests of the scoring kernel: the filter's undecided
+// (model, point) elements of a round are queued in LDS and tested after the
+// round's model loop, 64 at a time (every lane busy), instead of one or two
+// lanes at a time inside it.  A full queue falls back to the immediate test.
+constexpr int kDeferCap = 256;
+struct DeferQ {
+  uint32_t* q;  // LDS: model << 16 | point offset within the chunk
+  int n;        // entries queued (wave-uniform)
+};
+
+// Queue the undecided lanes um of point slot p for model m; false when the
+// queue is full (the caller then tests them at once).
+__device__ __forceinline__ bool defer_push(DeferQ* d, uint64_t um, int p, int m) {
+  const int c = __popcll(um);
+  if (d->n + c > kDeferCap) return false;
+  const uint32_t lane = threadIdx.x;
+  if (um & (1ull << lane)) {
+    const int pos = d->n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(um >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)um, 0u));
+    d->q[pos] = ((uint32_t)m << 16) | (uint32_t)(64 * p + lane);
+  }
+  d->n += c;
+  return true;
+}
+
 template <int PCH, bool FULL>
 __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, const f32x2* s0,
                                              const f32x2* s1, const f32x2* d0, const f32x2* d1,
-                                             int n, int base, double maxr, int* nslow) {
+                                             int n, int base, double maxr, int* nslow,
+                                             DeferQ* dq = nullptr, int dm = 0) {
   int cnt = 0;
   uint64_t any = 0;
   uint64_t um[PCH];  // per point slot: lanes the filter left undecided
@@ -502,8 +528,13 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
 #ifdef SCM_DIAG_SCORE_NOSLOW
   any = 0;  // diagnostics only: undecided points counted as outliers
 #endif
-  if (any) {  // rare: exact test of the undecided points only
+  if (any) {  // rare: exact test of the undecided points only (queued when dq)
     ++*nslow;
+    if (dq) {
+#pragma unroll
+      for (int p = 0; p < PCH; ++p)
+        if (um[p] && defer_push(dq, um[p], p, dm)) um[p] = 0;
+    }
     const uint64_t me = 1ull << threadIdx.x;
 #pragma unroll
     for (int q = 0; q < PCH / 2; ++q) {
@@ -634,7 +665,8 @@ __device__ __attribute__((noinline)) bool f_exact_pt(const double* mk, float x0,
 template <int PCH, bool FULL>
 __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, const f32x2* x0,
                                              const f32x2* x1, const f32x2* y0, const f32x2* y1,
-                                             int n, int base, double maxr, int* nslow) {
+                                             int n, int base, double maxr, int* nslow,
+                                             DeferQ* dq = nullptr, int dm = 0) {
   int cnt = 0;
   uint64_t any = 0;
   uint64_t um[PCH];  // per point slot: lanes the filter left undecided
@@ -663,8 +695,13 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
 #ifdef SCM_DIAG_SCORE_NOSLOW
   any = 0;  // diagnostics only: undecided points counted as outliers
 #endif
-  if (any) {  // rare: exact test of the undecided points only
+  if (any) {  // rare: exact test of the undecided points only (queued when dq)
     ++*nslow;
+    if (dq) {
+#pragma unroll
+      for (int p = 0; p < PCH; ++p)
+        if (um[p] && defer_push(dq, um[p], p, dm)) um[p] = 0;
+    }
     const uint64_t me = 1ull << threadIdx.x;
 #pragma unroll
     for (int q = 0; q < PCH / 2; ++q) {
@@ -1905,8 +1942,10 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     uint64_t* __restrict__ prof) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
-  __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * 3][12];
+  __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * MM][12];
   __shared__ int32_t lnm[kTrialBatch];
+  __shared__ uint32_t ldq[kDeferCap];         // deferred exact tests (defer_push)
+  __shared__ uint32_t ldc[kTrialBatch * MM];  // their inliers per model of the round
   const int lane = threadIdx.x;
   const int na = *nact;
   const float maxrf = (float)maxr;
@@ -1952,8 +1991,10 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
         float4* dst = reinterpret_cast<float4*>(&lc[0][0]);
         for (int i = lane; i < B * MM * 3; i += kScoreThreads) dst[i] = src[i];
       }
+      for (int i = lane; i < B * MM; i += kScoreThreads) ldc[i] = 0;
       __syncthreads();
       const double* mb = mods + ((int64_t)q * kWindowTrials * 3 + r0 * MM) * MS;
+      DeferQ dq{ldq, 0};
       int nslow = 0;
       uint32_t c0 = 0, c1 = 0, c2 = 0;  // lane t: counts of hypothesis t's models
       for (int t = 0; t < B; ++t) {
@@ -1964,15 +2005,15 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
           if (K == KIND_F) {
             const FFilt f = f_filter_load(&lc[m][0], maxrf);
             c = full ? score_f_chunk<kScorePch, true>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                      maxr, &nslow)
+                                                      maxr, &nslow, &dq, m)
                      : score_f_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                       maxr, &nslow);
+                                                       maxr, &nslow, &dq, m);
           } else {
             const HFilt f = h_filter_load(&lc[m][0], maxrf);
             c = full ? score_h_chunk<kScorePch, true>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                      maxr, &nslow)
+                                                      maxr, &nslow, &dq, m)
                      : score_h_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                       maxr, &nslow);
+                                                       maxr, &nslow, &dq, m);
           }
           const uint32_t add = (lane == t) ? (uint32_t)c : 0u;
           if (k == 0) c0 += add;
@@ -1984,6 +2025,20 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
         uint64_t* pc = prof + (int64_t)q * kVerifyProfSlots + (K == KIND_F ? 80 : 84);
         atomicAdd(reinterpret_cast<unsigned long long*>(pc), (unsigned long long)(B * MM));
         atomicAdd(reinterpret_cast<unsigned long long*>(pc + 1), (unsigned long long)nslow);
+      }
+      // The queued exact tests, 64 at a time.
+      for (int e = lane; e < dq.n; e += kScoreThreads) {
+        const uint32_t v = ldq[e];
+        const int m = (int)(v >> 16), off = (int)(v & 0xFFFFu);
+        const float4 pt = xyf[base + off];
+        const bool in = K == KIND_F ? f_exact_pt(mb + m * MS, pt.x, pt.y, pt.z, pt.w, maxr)
+                                    : h_exact_pt(mb + m * MS, pt.x, pt.y, pt.z, pt.w, maxr);
+        if (in) atomicAdd(&ldc[m], 1u);
+      }
+      if (dq.n && lane < B) {
+        c0 += ldc[lane * MM];
+        if (MM > 1) c1 += ldc[lane * MM + 1];
+        if (MM > 2) c2 += ldc[lane * MM + 2];
       }
       uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3 + r0 * MM;
       if (lane < B) {
