@@ -2025,6 +2025,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
         uint64_t* pc = prof + (int64_t)q * kVerifyProfSlots + (K == KIND_F ? 80 : 84);
         atomicAdd(reinterpret_cast<unsigned long long*>(pc), (unsigned long long)(B * MM));
         atomicAdd(reinterpret_cast<unsigned long long*>(pc + 1), (unsigned long long)nslow);
+        atomicAdd(reinterpret_cast<unsigned long long*>(pc + 2), (unsigned long long)dq.n);
       }
       // The queued exact tests, 64 at a time.
       for (int e = lane; e < dq.n; e += kScoreThreads) {
