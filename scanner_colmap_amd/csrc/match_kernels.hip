@@ -675,7 +675,18 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
     // value of a passing column (unique best row, max_ratio <= 1), else -1.
     for (int j = tid; j < pd.n2; j += kFinThreads) {
       uint2 m = cp[j];
-      for (int b = 1; b < pd.nrb; ++b) {
+      int b = 1;
+      for (; b + 4 <= pd.nrb; b += 4) {  // four row blocks' loads in flight
+        uint2 o[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = cp[(int64_t)(b + u) * pd.n2pad + j];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          m.y = max(max(m.y, o[u].y), min(m.x, o[u].x));
+          m.x = max(m.x, o[u].x);
+        }
+      }
+      for (; b < pd.nrb; ++b) {
         const uint2 o = cp[(int64_t)b * pd.n2pad + j];
         m.y = max(max(m.y, o.y), min(m.x, o.x));
         m.x = max(m.x, o.x);
