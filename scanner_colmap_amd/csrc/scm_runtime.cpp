@@ -40,7 +40,7 @@ namespace {
 
 constexpr int64_t kMaxPairsPerBatch = 16384;
 constexpr int64_t kDefaultPairsPerBatch = 8192;
-constexpr int64_t kDefaultEdgePairs = kDefaultPairsPerBatch;  // short edge batches: off (measured slower)
+constexpr int64_t kDefaultEdgePairs = 0;  // short edge batches (SCM_EDGE_PAIRS): off (measured slower)
 
 struct ImageTable {
   int64_t n = 0;
@@ -879,7 +879,7 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
   // verification can start, and a short last batch).
   const int64_t nbatch = std::max<int64_t>(1, (total_pairs + ctx->batch_pairs - 1) / ctx->batch_pairs);
   const int64_t bsize = ctx->balanced ? (total_pairs + nbatch - 1) / nbatch : ctx->batch_pairs;
-  const int64_t edge = (!ctx->serial && total_pairs > 2 * ctx->batch_pairs)
+  const int64_t edge = (!ctx->serial && ctx->edge_pairs > 0 && total_pairs > 2 * ctx->batch_pairs)
                            ? std::min(bsize, ctx->edge_pairs)
                            : bsize;
   Batch cur;
