@@ -19,7 +19,6 @@ import argparse
 import json
 import os
 import sys
-import threading
 import time
 
 import numpy as np
@@ -30,7 +29,6 @@ sys.path.insert(0, ROOT)
 METRIC = "image-pairs/s + Gdesc-dist/s, 8192×8192-kpt pairs, 1/2/4/8 GPU"
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (spec)
 I8_DENSE_PEAK_TOPS = 5000.0      # MI355X_MICROARCH.md matrix cores: i8 32x32x32 = 2x the bf16 rate
-DEFAULT_BATCH_PAIRS = 8192       # scm_runtime.cpp kDefaultPairsPerBatch (one matcher launch per batch)
 
 # BASELINE.json configs (synthetic stand-ins; no dataset is present).
 WORKLOADS = {
@@ -51,48 +49,113 @@ def parse():
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--workload", default="synth-1000x8192-k20", choices=sorted(WORKLOADS))
-    p.add_argument("--images", type=int, default=None, help="override images per rank")
+    p.add_argument("--images", type=int, default=None,
+                   help="override the workload's image count (per rank for weak scaling)")
+    p.add_argument("--scaling", choices=("weak", "strong"), default="weak",
+                   help="weak: every rank owns the workload's images (default); strong: the "
+                        "workload's images in total, pivot rows split over the ranks "
+                        "(BASELINE configs 4 and 5)")
     p.add_argument("--kpts", type=int, default=None, help="override keypoints per image")
     p.add_argument("--gen-workers", type=int, default=16)
-    p.add_argument("--cpu-baseline-pairs", type=int, default=16)
+    p.add_argument("--cpu-baseline-pairs", type=int, default=64)
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
 
 
-def cpu_baseline(corridor, npairs: int, overlap: int) -> dict:
+def cpu_threads() -> tuple[int, int, float | None]:
+    """(threads to use, CPUs in this process's affinity mask, cgroup CPU
+    quota).  On the GPU box the affinity mask shows the whole machine while
+    the job's cgroup quota is its real CPU share."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    use = aff if quota is None else max(1, min(aff, int(quota)))
+    return use, aff, quota
+
+
+def sample_pairs(n_per_img: list, overlap: int, npairs: int) -> list:
+    """The first `npairs` pairs of the stencil order (row 0's pairs, then row
+    1's, ...) — the pairs the CPU baseline times and the parity check reads."""
+    out = []
+    T = len(n_per_img)
+    for r in range(T):
+        for j in range(r + 1, min(r + overlap, T)):
+            out.append((r, j))
+            if len(out) == npairs:
+                return out
+    return out
+
+
+def cpu_baseline(imgs: dict, pairs: list) -> tuple[dict, dict]:
     """The CPU oracle (faithful restatement of the reference op's matcher +
-    TwoViewGeometry) timed on this host: one pair per thread,
-    pairs (0, 1..npairs) of the same workload.  Reported, not optimised."""
+    TwoViewGeometry, SURVEY.md §8d: scalar ColMajor-strided integer dot
+    matrix, two one-way scans, sequential LO-RANSAC F + H + watermark) timed
+    on this host, one worker thread per CPU of the job's share, each taking
+    whole pairs (a Scanner pipeline instance per core).  Reported, not
+    optimised.  Returns the baseline and the oracle's per-pair outputs (raw
+    matches, TVG bytes) for the parity check of the timed GPU run."""
+    from concurrent.futures import ThreadPoolExecutor
     from oracle import oracle
 
-    imgs = [corridor.image(i) for i in range(min(corridor.num_images, npairs + 1))]
-    pairs = [(0, j) for j in range(1, len(imgs)) if j < overlap][:npairs]
     if not pairs:
-        return None
+        return None, {}
     oracle.lib()
+    threads, aff, quota = cpu_threads()
+    lat = {}
+    res = {}
 
-    lat = [0.0] * len(pairs)
-
-    def work(k):
-        i, j = pairs[k]
+    def work(pr):
+        i, j = pr
         t = time.perf_counter()
         m = oracle.match_pair(imgs[i][2], imgs[j][2])
-        oracle.verify_pair(imgs[i][1], imgs[j][1], m, imgs[i][0], imgs[j][0])
-        lat[k] = time.perf_counter() - t
+        tvg = oracle.verify_pair(imgs[i][1], imgs[j][1], m, imgs[i][0], imgs[j][0])
+        lat[pr] = time.perf_counter() - t
+        res[pr] = (m, tvg)
 
-    threads = [threading.Thread(target=work, args=(k,)) for k in range(len(pairs))]
     t0 = time.perf_counter()
-    for t in threads:
-        t.start()
-    for t in threads:
-        t.join()
+    with ThreadPoolExecutor(max_workers=threads) as ex:
+        list(ex.map(work, pairs))
     dt = time.perf_counter() - t0
-    n1 = imgs[0][2].shape[0]
-    return {"value": len(pairs) / dt, "unit": "image-pairs/s", "cores": len(pairs),
-            "kind": "port", "cpu_model": cpu_model(),
-            "pair_latency_s": round(sum(lat) / len(lat), 2),
-            "sample": f"{len(pairs)} pairs (0,1..{len(pairs)}) of {n1}x{n1} kpts, one pair per "
-                      f"thread, {dt:.1f} s wall (oracle/oracle.cc, -O3 scalar restatement)"}
+    n1 = imgs[pairs[0][0]][2].shape[0]
+    base = {"value": len(pairs) / dt, "unit": "image-pairs/s", "cores": min(threads, len(pairs)),
+            "kind": "port", "cpu_model": cpu_model(), "nproc_affinity": aff,
+            "cgroup_cpu_quota": quota,
+            "pair_latency_s": round(sum(lat.values()) / len(lat), 2),
+            "sample": f"the first {len(pairs)} pairs of the stencil order (rows "
+                      f"{pairs[0][0]}..{pairs[-1][0]}) of {n1}x{n1} kpts, "
+                      f"{min(threads, len(pairs))} worker threads, {dt:.1f} s wall "
+                      "(oracle/oracle.cc, -O3 scalar restatement)"}
+    return base, res
+
+
+def parity_check(ctx, packed, row_lo: int, oracle_out: dict, pairs: list) -> dict:
+    """Compare the timed run's GPU outputs for `pairs` with the oracle's:
+    raw cross-checked matches bit-exact, io.cc TVG bytes equal."""
+    from scanner_colmap_amd.codecs import split_tvg_list
+
+    rows = {}
+    ok_m = ok_t = True
+    bad = []
+    for (i, j) in pairs:
+        if i not in rows:
+            rows[i] = split_tvg_list(packed.element(2 * (i - row_lo) + 1))
+        m_ref, tvg_ref = oracle_out[(i, j)]
+        m_gpu = ctx.table_matches(i, j - i, cap=max(1, len(m_ref) + 1))
+        same_m = m_gpu.shape == m_ref.shape and bool((m_gpu == m_ref).all())
+        same_t = rows[i][j - i - 1] == tvg_ref
+        ok_m &= same_m
+        ok_t &= same_t
+        if not (same_m and same_t):
+            bad.append([i, j])
+    return {"pairs": len(pairs), "matches_bit_exact": ok_m, "tvg_bytes_equal": ok_t,
+            "mismatched_pairs": bad[:8],
+            "checked_against": "oracle/oracle.cc (CPU restatement), same inputs and seeds",
+            "source": "GPU outputs of the last timed step (raw matches kept for these rows)"}
 
 
 def cpu_model() -> str:
@@ -129,10 +192,12 @@ def main():
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     wl = dict(WORKLOADS[args.workload])
-    per_rank = args.images or wl["images"]
     kpts = args.kpts or wl["kpts"]
     overlap = wl["overlap"]
-    total_images = per_rank * world
+    if args.scaling == "strong":  # the workload's images in total, split over the ranks
+        total_images = args.images or wl["images"]
+    else:                         # every rank owns the workload's images
+        total_images = (args.images or wl["images"]) * world
 
     from scanner_colmap_amd import distributed as sd
     from scanner_colmap_amd.codecs import table_rows
@@ -140,13 +205,21 @@ def main():
 
     row_b, row_e = sd.shard_rows(total_images, overlap, world, rank)
     tab_b, tab_e = sd.table_range(row_b, row_e, total_images, overlap)
-    corridor = Corridor(total_images, kpts, min(overlap, 20), seed=wl["seed"])
+    # Scene overlap = the stencil's (K = 50 and exhaustive runs included): every pair of a
+    # stencil shares scene points, so every pair is matched and verified.
+    corridor = Corridor(total_images, kpts, min(overlap, total_images), seed=wl["seed"])
     # Data generation happens before any GPU runtime call (forked workers).
     t0 = time.perf_counter()
     imgs = corridor.images(tab_b, tab_e, workers=args.gen_workers)
     gen_s = time.perf_counter() - t0
     ids, kps, descs = table_rows(imgs)
     n_per_img = [im[2].shape[0] for im in imgs]
+    # Pairs the CPU baseline times and the parity check compares (rank 0, N = 1).
+    check_pairs = (sample_pairs(n_per_img, overlap, args.cpu_baseline_pairs)
+                   if world == 1 and args.cpu_baseline_pairs > 0 else [])
+    keep_rows = sorted({i for p in check_pairs for i in p})
+    sample_imgs = {i: imgs[i] for i in keep_rows}
+    keep_hi = max([i for i, _ in check_pairs], default=-1) + 1
     del imgs
 
     import torch
@@ -176,10 +249,15 @@ def main():
             npairs += 1
             gdesc += float(n_per_img[r]) * n_per_img[j]
 
+    if keep_hi > 0:  # raw matches of the parity rows are kept in every step (bounded copy)
+        ctx.set_keep_matches_range(0, keep_hi)
+    last = {}
+
     def step():
         packed = ctx.table_run_packed(overlap, lr_b, lr_e)
         if world > 1:
             sd.gather_to_root(sd.pack_packed(packed.offsets, packed.data), device=device)
+        last["packed"] = packed
         return ctx.table_timings()
 
     for _ in range(args.warmup):
@@ -192,11 +270,13 @@ def main():
     match_ms = 0.0
     verify_ms = 0.0
     final_ms = 0.0
+    launches = 0
     for _ in range(args.steps):
         tm = step()
         match_ms += tm["match_ms"]
         verify_ms += tm["verify_ms"]
         final_ms += tm["finalize_ms"]
+        launches += tm["match_launches"]
     if world > 1:
         dist.barrier()
     if torch.cuda.is_available():
@@ -220,17 +300,29 @@ def main():
         value = total_pairs * steps / elapsed
         flops_rank = 2.0 * 128.0 * gdesc * steps
         achieved_tf = flops_rank / (match_ms * 1e-3) / 1e12 if match_ms > 0 else None
-        launches = max(1, -(-npairs // DEFAULT_BATCH_PAIRS))
+        launches = max(1, launches)  # matcher launches the library reported
         avg_n = float(np.mean(n_per_img)) if n_per_img else 0.0
         bf16 = os.environ.get("SCM_MATCH_BF16", "0") == "1"  # else the default i8 matcher
         kernel = "match_tiles_kernel" if bf16 else "match_tiles_i8_kernel"
         peak = BF16_DENSE_PEAK_TFLOPS if bf16 else I8_DENSE_PEAK_TOPS
         # descriptors of both images, bf16 (2 B) or offset i8 (1 B) per element
         alg_bytes_launch = npairs / launches * 2 * avg_n * 128 * (2 if bf16 else 1)
-        pmc = pmc_traffic(args.workload, kpts, per_rank, kernel) if world == 1 else None
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(corridor, args.cpu_baseline_pairs, overlap)
+        pmc = (pmc_traffic(args.workload, kpts, total_images, kernel)
+               if world == 1 and not args.images else None)
+        cpu = parity = None
+        if check_pairs:
+            if args.no_cpu_baseline:  # parity only, with the oracle's BLAS-dot matcher
+                from oracle import oracle
+                ref = {}
+                for (i, j) in check_pairs:
+                    m = oracle.match_pair_fast(sample_imgs[i][2], sample_imgs[j][2])
+                    ref[(i, j)] = (m, oracle.verify_pair(sample_imgs[i][1], sample_imgs[j][1], m,
+                                                         sample_imgs[i][0], sample_imgs[j][0]))
+            else:
+                cpu, ref = cpu_baseline(sample_imgs, check_pairs)
+            parity = parity_check(ctx, last["packed"], lr_b, ref, check_pairs)
+        # SURVEY.md §8d headline fraction: kernel-1 work over the whole step's wall time.
+        wall_tops = flops_rank / elapsed / 1e12
         out = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -241,13 +333,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / steps * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": ("bf16 MFMA" if bf16 else "i8 MFMA on offset u8 descriptors, int32 accumulate")
                      + " (exact u8 dot products) + f64 geometry",
             "data": "synthetic (seeded corridor scene, RootSIFT u8 descriptors; no dataset)",
             "config": {"workload": args.workload, "description": wl["desc"],
-                       "images_per_rank": per_rank, "kpts": kpts, "overlap": overlap,
+                       "images": total_images, "kpts": kpts, "overlap": overlap,
                        "pairs_per_step": int(total_pairs), "parallelism": f"pairs sharded x{world}"},
             "roofline": {
                 "bound": "mfma",
@@ -262,14 +354,20 @@ def main():
                 "traffic_source": (f"{pmc[1]}: FETCH_SIZE x2 + WRITE_SIZE per launch, "
                                    f"separate rocprofv3 --pmc passes") if pmc else None,
                 "algorithmic_bytes_per_launch": round(alg_bytes_launch),
+                "launches_per_step": round(launches / steps, 2),
+                "wall_achieved": round(wall_tops, 2),
+                "wall_frac": round(wall_tops / peak, 4),
+                "wall_frac_of_bf16_peak": round(wall_tops / BF16_DENSE_PEAK_TFLOPS, 4),
                 "algorithmic": ("2*N1*N2*128 ops per pair (one multiply-add = 2 ops, i8 or bf16); "
                                 "per-launch time from HIP events; peak = dense MFMA peak of the "
-                                "kernel's dtype (i8 5.0 POP/s, bf16 2.5 PFLOP/s)"),
+                                "kernel's dtype (i8 5.0 POP/s, bf16 2.5 PFLOP/s); wall_* = the "
+                                "same ops over the whole step's wall time (SURVEY.md §8d)"),
             },
             "stage_ms_per_step": {"match": round(match_ms / steps, 3),
                                   "finalize": round(final_ms / steps, 3),
                                   "verify": round(verify_ms / steps, 3)},
             "cpu_baseline": cpu,
+            "parity": parity,
             "table_load_ms": round(table_load_ms, 1),
             "pcie_inclusive_pairs_per_s": round(total_pairs / (elapsed / steps + table_load_ms * 1e-3), 2),
             "gen_s": round(gen_s, 1),

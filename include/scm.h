@@ -185,6 +185,11 @@ int scm_table_run_packed(scm_context* ctx, int64_t overlap, int64_t row_begin,
 /* Keep (keep != 0) the raw cross-checked matches of every pair of the
  * following table runs for scm_table_matches; off by default. */
 int scm_set_keep_matches(scm_context* ctx, int32_t keep);
+/* Keep the raw matches only of the pairs whose pivot row lies in
+ * [row_begin, row_end) (a bounded debug output for spot checks of long runs:
+ * the bench keeps a few rows of its timed run for the parity check);
+ * row_end == row_begin turns keeping off. */
+int scm_set_keep_matches_range(scm_context* ctx, int64_t row_begin, int64_t row_end);
 /* Raw cross-checked matches of the most recent scm_table_run for the pair
  * (row, row + offset), offset in [1, overlap); the debug `matches` output the
  * bit-exact checks read.  Requires scm_set_keep_matches. */
@@ -194,7 +199,8 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset,
 /* Per-stage device time of the most recent scm_table_run, milliseconds,
  * measured with HIP events on the context's stream:
  * t[0] = descriptor-distance + top-2 kernel, t[1] = match finalize,
- * t[2] = RANSAC hypothesis kernels, t[3] = whole run (wall). */
+ * t[2] = RANSAC hypothesis kernels, t[3] = whole run (wall),
+ * t[4] = number of descriptor-distance kernel launches of the run. */
 int scm_table_timings(scm_context* ctx, double* t, int32_t n);
 
 #ifdef __cplusplus

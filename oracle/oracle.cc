@@ -77,13 +77,25 @@ void compute_sift_distance_matrix(const uint8_t* d1, int64_t n1,
   }
 }
 
+// The distance / ratio decision of FindBestMatchesOneWay for one scanned row
+// (best_i2 == -1 is tested by the caller).  float kDistNorm = 1/(512*512),
+// float max_ratio and max_distance (the function takes float parameters
+// [upstream]).
+bool passes_ratio_test(int best_dist, int second_best_dist, float max_ratio,
+                       float max_distance) {
+  const float kDistNorm = 1.0f / (512.0f * 512.0f);
+  const float best_dist_normed = std::acos(std::min(kDistNorm * best_dist, 1.0f));
+  if (best_dist_normed > max_distance) return false;
+  const float second_best_dist_normed =
+      std::acos(std::min(kDistNorm * second_best_dist, 1.0f));
+  return !(best_dist_normed >= max_ratio * second_best_dist_normed);
+}
+
 // FindBestMatchesOneWay over a ColMajor rows x cols int matrix (element (r, c)
-// at c * rows + r).  float kDistNorm = 1/(512*512), float max_ratio and
-// max_distance (the function takes float parameters [upstream]).
+// at c * rows + r).
 size_t find_best_matches_one_way(const std::vector<int32_t>& colmajor,
                                  int64_t rows, int64_t cols, float max_ratio,
                                  float max_distance, std::vector<int>* matches) {
-  const float kDistNorm = 1.0f / (512.0f * 512.0f);
   size_t num_matches = 0;
   matches->assign((size_t)rows, -1);
   for (int64_t i1 = 0; i1 < rows; ++i1) {
@@ -101,12 +113,7 @@ size_t find_best_matches_one_way(const std::vector<int32_t>& colmajor,
       }
     }
     if (best_i2 == -1) continue;
-    const float best_dist_normed =
-        std::acos(std::min(kDistNorm * best_dist, 1.0f));
-    if (best_dist_normed > max_distance) continue;
-    const float second_best_dist_normed =
-        std::acos(std::min(kDistNorm * second_best_dist, 1.0f));
-    if (best_dist_normed >= max_ratio * second_best_dist_normed) continue;
+    if (!passes_ratio_test(best_dist, second_best_dist, max_ratio, max_distance)) continue;
     num_matches += 1;
     (*matches)[(size_t)i1] = best_i2;
   }
@@ -148,6 +155,55 @@ void match_sift_features_cpu(const scm_matching_options& o, const uint8_t* d1,
   } else {
     for (size_t i1 = 0; i1 < m12.size(); ++i1)
       if (m12[i1] != -1) out->push_back({(uint32_t)i1, (uint32_t)m12[i1]});
+  }
+}
+
+// FindBestMatches on a precomputed RowMajor dot matrix (test support: the
+// tests compute the exact integer dots with a float32 BLAS product, every
+// partial sum being an integer below 2^24).  The decisions are those of
+// find_best_matches_one_way on dists and on dists.transpose(); only the loop
+// order differs: the column scans of the transposed pass run as per-column
+// state updated row by row, so each column still visits i1 in ascending
+// order (same ties, same "second"), without the two 256 MiB copies.
+void match_from_rowmajor_dots(const scm_matching_options& o, const int32_t* d,
+                              int64_t n1, int64_t n2, std::vector<Match>* out) {
+  out->clear();
+  const float max_ratio = (float)o.max_ratio;
+  const float max_distance = (float)o.max_distance;
+  std::vector<int> m12((size_t)n1, -1), m21((size_t)n2, -1);
+  std::vector<int> cbest((size_t)n2, 0), csecond((size_t)n2, 0), cidx((size_t)n2, -1);
+  for (int64_t i1 = 0; i1 < n1; ++i1) {
+    const int32_t* row = d + (size_t)i1 * n2;
+    int best_i2 = -1, best_dist = 0, second_best_dist = 0;
+    for (int64_t i2 = 0; i2 < n2; ++i2) {
+      const int dist = row[i2];
+      if (dist > best_dist) {
+        best_i2 = (int)i2;
+        second_best_dist = best_dist;
+        best_dist = dist;
+      } else if (dist > second_best_dist) {
+        second_best_dist = dist;
+      }
+      if (dist > cbest[(size_t)i2]) {
+        cidx[(size_t)i2] = (int)i1;
+        csecond[(size_t)i2] = cbest[(size_t)i2];
+        cbest[(size_t)i2] = dist;
+      } else if (dist > csecond[(size_t)i2]) {
+        csecond[(size_t)i2] = dist;
+      }
+    }
+    if (best_i2 != -1 &&
+        passes_ratio_test(best_dist, second_best_dist, max_ratio, max_distance))
+      m12[(size_t)i1] = best_i2;
+  }
+  for (int64_t i2 = 0; i2 < n2; ++i2)
+    if (cidx[(size_t)i2] != -1 &&
+        passes_ratio_test(cbest[(size_t)i2], csecond[(size_t)i2], max_ratio, max_distance))
+      m21[(size_t)i2] = cidx[(size_t)i2];
+  for (size_t i1 = 0; i1 < m12.size(); ++i1) {
+    if (m12[i1] == -1) continue;
+    if (o.cross_check && m21[(size_t)m12[i1]] != (int)i1) continue;
+    out->push_back({(uint32_t)i1, (uint32_t)m12[i1]});
   }
 }
 
@@ -649,11 +705,40 @@ void oracle_ata_null_vector(const double* ata45, double* out9) {
   scm::geom::ata_null_vector(ata45, out9);
 }
 
+// The shared estimator arithmetic (geom_solvers.h, compiled into the product
+// and into this oracle) exposed for the independent numpy restatement of
+// COLMAP's SVD / companion-matrix formulation (tests/test_estimators_independent.py).
+int oracle_fundamental_7pt(const double* x1, const double* x2, double* models27) {
+  return scm::geom::fundamental_7pt(x1, x2, models27);
+}
+int oracle_fundamental_8pt(const double* x1, const double* x2, int32_t n, double* F9) {
+  return scm::geom::fundamental_8pt(x1, x2, n, F9);
+}
+int oracle_homography_dlt(const double* x1, const double* x2, int32_t n, double* H9) {
+  return scm::geom::homography_dlt(x1, x2, n, H9);
+}
+
 int oracle_match_pair(const scm_matching_options* o, const uint8_t* d1,
                       int64_t n1, const uint8_t* d2, int64_t n2,
                       uint32_t* out, int64_t cap, int64_t* m) {
   std::vector<Match> matches;
   match_sift_features_cpu(*o, d1, n1, d2, n2, &matches);
+  *m = (int64_t)matches.size();
+  if ((int64_t)matches.size() > cap) return SCM_E_CAPACITY;
+  for (size_t i = 0; i < matches.size(); ++i) {
+    out[2 * i] = matches[i].idx1;
+    out[2 * i + 1] = matches[i].idx2;
+  }
+  return SCM_OK;
+}
+
+// FindBestMatches on an exact RowMajor int32 dot matrix (test support, see
+// match_from_rowmajor_dots).
+int oracle_match_from_dots(const scm_matching_options* o, const int32_t* dots,
+                           int64_t n1, int64_t n2, uint32_t* out, int64_t cap,
+                           int64_t* m) {
+  std::vector<Match> matches;
+  match_from_rowmajor_dots(*o, dots, n1, n2, &matches);
   *m = (int64_t)matches.size();
   if ((int64_t)matches.size() > cap) return SCM_E_CAPACITY;
   for (size_t i = 0; i < matches.size(); ++i) {

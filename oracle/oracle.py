@@ -39,6 +39,8 @@ def lib() -> ctypes.CDLL:
     L.oracle_pair_seed.restype = c_uint32
     L.oracle_match_pair.argtypes = [POINTER(MatchingOptions), c_void_p, c_int64, c_void_p,
                                     c_int64, c_void_p, c_int64, POINTER(c_int64)]
+    L.oracle_match_from_dots.argtypes = [POINTER(MatchingOptions), c_void_p, c_int64, c_int64,
+                                         c_void_p, c_int64, POINTER(c_int64)]
     L.oracle_row_top2.argtypes = [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_void_p,
                                   c_void_p]
     L.oracle_acosf_normed.argtypes = [c_int32]
@@ -62,6 +64,10 @@ def lib() -> ctypes.CDLL:
     L.oracle_num_trials.restype = c_uint64
     L.oracle_ata_null_vector.argtypes = [c_void_p, c_void_p]
     L.oracle_ata_null_vector.restype = None
+    for name in ("oracle_fundamental_7pt",):
+        getattr(L, name).argtypes = [c_void_p, c_void_p, c_void_p]
+    for name in ("oracle_fundamental_8pt", "oracle_homography_dlt"):
+        getattr(L, name).argtypes = [c_void_p, c_void_p, c_int32, c_void_p]
     L.oracle_free.argtypes = [POINTER(c_uint8)]
     L.oracle_free.restype = None
     _lib = L
@@ -94,6 +100,40 @@ def match_pair(d1, d2, opts=None) -> np.ndarray:
     m = c_int64()
     rc = lib().oracle_match_pair(byref(opts), a.ctypes.data, len(a), b.ctypes.data, len(b),
                                  out.ctypes.data, cap, byref(m))
+    assert rc == 0, rc
+    return out[: m.value].copy()
+
+
+def exact_dots(d1, d2) -> np.ndarray:
+    """The int32 dot matrix of ComputeSiftDistanceMatrix
+    via a float32 BLAS product: every product is <= 255^2 and every partial
+    sum an integer <= 128 * 255^2 < 2^24, so each is exact in float32 in any
+    summation order (checked on a sample of entries against int64 dots)."""
+    a = np.ascontiguousarray(d1, dtype=np.uint8).reshape(-1, 128)
+    b = np.ascontiguousarray(d2, dtype=np.uint8).reshape(-1, 128)
+    dots = np.matmul(a.astype(np.float32), b.astype(np.float32).T)
+    out = dots.astype(np.int32)
+    if out.size:
+        rng = np.random.default_rng(len(a) * 7919 + len(b))
+        i = rng.integers(0, len(a), 64)
+        j = rng.integers(0, len(b), 64)
+        ref = (a[i].astype(np.int64) * b[j].astype(np.int64)).sum(axis=1)
+        assert (out[i, j] == ref).all()
+    return out
+
+
+def match_pair_fast(d1, d2, opts=None) -> np.ndarray:
+    """oracle_match_pair's result from exact BLAS dots + the oracle's
+    FindBestMatches scans (test checker for large pairs; the faithful scalar
+    matcher takes ~20 s at 8192 x 8192)."""
+    opts = opts or default_options()
+    dots = np.ascontiguousarray(exact_dots(d1, d2))
+    n1, n2 = dots.shape
+    cap = max(1, n1)
+    out = np.zeros((cap, 2), dtype=np.uint32)
+    m = c_int64()
+    rc = lib().oracle_match_from_dots(byref(opts), dots.ctypes.data, n1, n2, out.ctypes.data,
+                                      cap, byref(m))
     assert rc == 0, rc
     return out[: m.value].copy()
 
@@ -153,6 +193,31 @@ def ata_null_vector(ata45) -> np.ndarray:
     return out
 
 
+def fundamental_7pt(x1, x2) -> np.ndarray:
+    """geom_solvers.h fundamental_7pt on 7 point pairs: (k, 3, 3) models."""
+    a = np.ascontiguousarray(x1, np.float64).reshape(7, 2)
+    b = np.ascontiguousarray(x2, np.float64).reshape(7, 2)
+    out = np.zeros(27)
+    k = lib().oracle_fundamental_7pt(a.ctypes.data, b.ctypes.data, out.ctypes.data)
+    return out[: 9 * k].reshape(k, 3, 3)
+
+
+def fundamental_8pt(x1, x2) -> np.ndarray:
+    a = np.ascontiguousarray(x1, np.float64).reshape(-1, 2)
+    b = np.ascontiguousarray(x2, np.float64).reshape(-1, 2)
+    out = np.zeros(9)
+    lib().oracle_fundamental_8pt(a.ctypes.data, b.ctypes.data, len(a), out.ctypes.data)
+    return out.reshape(3, 3)
+
+
+def homography_dlt(x1, x2) -> np.ndarray:
+    a = np.ascontiguousarray(x1, np.float64).reshape(-1, 2)
+    b = np.ascontiguousarray(x2, np.float64).reshape(-1, 2)
+    out = np.zeros(9)
+    lib().oracle_homography_dlt(a.ctypes.data, b.ctypes.data, len(a), out.ctypes.data)
+    return out.reshape(3, 3)
+
+
 def std_uniform(seed, lo, hi) -> np.ndarray:
     lo = np.ascontiguousarray(lo, dtype=np.uint32)
     hi = np.ascontiguousarray(hi, dtype=np.uint32)
@@ -193,3 +258,48 @@ def table_run(ids, kps, descs, overlap, row_begin, row_end, opts=None):
                                 pa, na, pb, nb)
     assert rc == 0, rc
     return ([_take(pa[i], na[i]) for i in range(n)], [_take(pb[i], nb[i]) for i in range(n)])
+
+
+def table_run_fast(images, overlap, row_begin, row_end, opts=None, threads=8,
+                   matches_out=None):
+    """oracle_table_run's rows for decoded images [(id, kp N x 6, desc N x 128)]
+    with the matcher of match_pair_fast, pairs verified in a thread pool.
+    Restates the stencil loop of SequentialMatchingCPUKernel::execute
+    (sequential_matching.cc:125-146: pivot = stencil[0], skip the pivot's id
+    and ids already paired; the stencil is clamped at the table end) and the
+    io.cc row layouts (io.cc:151-162 id vector, io.cc:256-297 TVG list).
+    `matches_out` (a dict) receives each pair's raw matches by (row, stencil row)."""
+    import struct
+    from concurrent.futures import ThreadPoolExecutor
+
+    opts = opts or default_options()
+    n = len(images)
+    rows = []
+    for r in range(row_begin, row_end):
+        st = [min(r + s, n - 1) for s in range(overlap)]
+        seen, sel = [], []
+        for s in st[1:]:
+            i2 = images[s][0]
+            if i2 == images[st[0]][0] or i2 in seen:
+                continue
+            seen.append(i2)
+            sel.append(s)
+        rows.append((r, sel))
+
+    def one(job):
+        r, s = job
+        m = match_pair_fast(images[r][2], images[s][2], opts)
+        if matches_out is not None:
+            matches_out[job] = m
+        return verify_pair(images[r][1], images[s][1], m, images[r][0], images[s][0], opts)
+
+    jobs = [(r, s) for r, sel in rows for s in sel]
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        tvgs = dict(zip(jobs, ex.map(one, jobs)))
+    pa, pb = [], []
+    for r, sel in rows:
+        ids = [images[s][0] for s in sel]
+        pa.append(struct.pack("<Q", len(ids)) + np.array(ids, np.uint32).tobytes())
+        body = b"".join(tvgs[(r, s)] for s in sel)
+        pb.append(struct.pack("<Qi", 12 + len(body), len(sel)) + body)
+    return pa, pb

@@ -33,6 +33,7 @@ EXPORTS = (
     "scm_context_create", "scm_context_destroy", "scm_match_pair",
     "scm_verify_pair", "scm_execute_stencil", "scm_table_load",
     "scm_table_run", "scm_table_run_packed", "scm_set_keep_matches",
+    "scm_set_keep_matches_range",
     "scm_table_matches", "scm_table_timings",
 )
 
@@ -106,6 +107,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.scm_table_run_packed.argtypes = [c_void_p, c_int64, c_int64, c_int64,
                                          POINTER(Blob), c_void_p]
     lib.scm_set_keep_matches.argtypes = [c_void_p, c_int32]
+    lib.scm_set_keep_matches_range.argtypes = [c_void_p, c_int64, c_int64]
     lib.scm_table_matches.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64,
                                       POINTER(c_int64)]
     lib.scm_table_timings.argtypes = [c_void_p, POINTER(c_double), c_int32]
@@ -280,6 +282,9 @@ class Context:
     def set_keep_matches(self, keep: bool = True) -> None:
         _check(self._lib.scm_set_keep_matches(self._ptr, 1 if keep else 0))
 
+    def set_keep_matches_range(self, row_begin: int, row_end: int) -> None:
+        _check(self._lib.scm_set_keep_matches_range(self._ptr, row_begin, row_end))
+
     def table_matches(self, row: int, offset: int, cap: int = 1 << 16) -> np.ndarray:
         out = np.zeros((max(1, cap), 2), dtype=np.uint32)
         n = c_int64()
@@ -288,6 +293,7 @@ class Context:
         return out[: n.value].copy()
 
     def table_timings(self) -> dict:
-        t = (c_double * 4)()
-        _check(self._lib.scm_table_timings(self._ptr, t, 4))
-        return {"match_ms": t[0], "finalize_ms": t[1], "verify_ms": t[2], "wall_ms": t[3]}
+        t = (c_double * 5)()
+        _check(self._lib.scm_table_timings(self._ptr, t, 5))
+        return {"match_ms": t[0], "finalize_ms": t[1], "verify_ms": t[2], "wall_ms": t[3],
+                "match_launches": int(t[4])}

@@ -106,6 +106,22 @@ def decode_tvg_list(b: bytes) -> list[TwoViewGeometry]:
     return out
 
 
+def split_tvg_list(b: bytes) -> list[bytes]:
+    """The per-TVG byte ranges of a two_view_geometries element (io.cc:256-297):
+    each TVG is 292 B + 8 B per inlier match."""
+    total, count = struct.unpack_from("<Qi", b, 0)
+    assert total == len(b), (total, len(b))
+    off = 12
+    out = []
+    for _ in range(count):
+        (n,) = struct.unpack_from("<Q", b, off + TVG_HEADER.size)
+        end = off + TVG_HEADER.size + 8 + 8 * n
+        out.append(bytes(b[off:end]))
+        off = end
+    assert off == total
+    return out
+
+
 def encode_tvg_list(tvgs: list[TwoViewGeometry]) -> bytes:
     """create_two_view_geometries_buffer (io.cc:256-297)."""
     body = b""

@@ -159,12 +159,14 @@ struct scm_context {
   bool balanced = false;  // SCM_BALANCED=1: equal batches (measured slower: verification
                          // batches are latency-bound, a short last batch drains faster)
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
+  int64_t n_match_launches = 0;  // matcher kernel launches of the last table run
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
   bool profile = false;
   std::vector<uint64_t> prof_sum;
   int64_t prof_pairs = 0;
   // raw matches of the last table run (scm_set_keep_matches)
   bool keep_matches = false;
+  int64_t keep_begin = 0, keep_end = INT64_MAX;  // rows whose matches are kept
   int64_t last_begin = 0, last_end = 0;
   std::vector<std::vector<std::pair<int64_t, std::vector<Match>>>> last_matches;
 };
@@ -488,6 +490,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
     for (int clamp = 0; clamp < 2; ++clamp) {
       const MatchJob* jb = bs.jobs.as<MatchJob>() + (clamp ? nfast : 0);
       const int nj = (int)(clamp ? NJ - nfast : nfast);
+      if (nj > 0) ctx->n_match_launches += 1;
       if (ctx->match_bf16)
         SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), jb, nj, bs.pairs.as<PairDesc>(),
                                    bs.rowres.as<uint2>(), bs.colpart.as<uint2>(), clamp, sm));
@@ -925,6 +928,7 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
     if (ctx->keep_matches)
       for (int64_t p = 0; p < v.P; ++p) {
         const int64_t row = b.specs[p].a, o = v.offsets[p];
+        if (row < ctx->keep_begin || row >= ctx->keep_end) continue;
         ctx->last_matches[row - row_begin].push_back(
             {b.specs[p].b - row, std::vector<Match>(v.matches + o, v.matches + o + v.counts[p])});
       }
@@ -1247,6 +1251,7 @@ static int table_run_common(scm_context* ctx, int64_t overlap, int64_t row_begin
   }
   SCM_HIP(hipSetDevice(ctx->device));
   ctx->t_match = ctx->t_final = ctx->t_verify = 0.0;
+  ctx->n_match_launches = 0;
   const auto w0 = std::chrono::steady_clock::now();
   const int rc = run_table(ctx, overlap, row_begin, row_end, pk);
   if (rc != SCM_OK) drain(ctx);
@@ -1316,7 +1321,21 @@ int scm_set_keep_matches(scm_context* ctx, int32_t keep) {
     return SCM_E_INVALID;
   }
   ctx->keep_matches = keep != 0;
+  ctx->keep_begin = 0;
+  ctx->keep_end = INT64_MAX;
   if (!keep) ctx->last_matches.clear();
+  return SCM_OK;
+}
+
+int scm_set_keep_matches_range(scm_context* ctx, int64_t row_begin, int64_t row_end) {
+  if (!ctx || row_begin < 0 || row_end < row_begin) {
+    set_error("invalid arguments");
+    return SCM_E_INVALID;
+  }
+  ctx->keep_matches = row_end > row_begin;
+  ctx->keep_begin = row_begin;
+  ctx->keep_end = row_end;
+  if (!ctx->keep_matches) ctx->last_matches.clear();
   return SCM_OK;
 }
 
@@ -1330,7 +1349,8 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset, uint32_t* m
     set_error("call scm_set_keep_matches(ctx, 1) before scm_table_run");
     return SCM_E_STATE;
   }
-  if (row < ctx->last_begin || row >= ctx->last_end ||
+  if (row < ctx->last_begin || row >= ctx->last_end || row < ctx->keep_begin ||
+      row >= ctx->keep_end ||
       ctx->last_matches.size() != (size_t)(ctx->last_end - ctx->last_begin)) {
     set_error("row outside the last scm_table_run");
     return SCM_E_INVALID;
@@ -1360,8 +1380,9 @@ int scm_table_timings(scm_context* ctx, double* t, int32_t n) {
     set_error("invalid arguments");
     return SCM_E_INVALID;
   }
-  const double v[4] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall};
-  for (int32_t i = 0; i < n && i < 4; ++i) t[i] = v[i];
+  const double v[5] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall,
+                       (double)ctx->n_match_launches};
+  for (int32_t i = 0; i < n && i < 5; ++i) t[i] = v[i];
   return SCM_OK;
 }
 

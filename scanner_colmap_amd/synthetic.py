@@ -132,8 +132,13 @@ class Corridor:
         import multiprocessing as mp
         global _POOL_CORRIDOR
         _POOL_CORRIDOR = self
-        with mp.get_context("fork").Pool(workers) as pool:
-            return pool.map(_pool_image, range(start, stop), chunksize=4)
+        pool = mp.get_context("fork").Pool(workers)
+        try:
+            out = pool.map(_pool_image, range(start, stop), chunksize=4)
+        finally:
+            pool.close()  # let the workers exit on their own (no SIGTERM from terminate())
+            pool.join()
+        return out
 
 
 _POOL_CORRIDOR = None

@@ -1,0 +1,115 @@
+"""GPU parity at the BASELINE.json sizes, through the C
+ABI: 8192 x 8192-keypoint pairs (16 row blocks: the finalize kernel's 4-way
+column merge, the XCD job order, full 8192-column segments), the Gerrard Hall
+shape (100 images, overlap 10), a prefix of the 1000 x 8192 overlap-20 roofline
+workload, the South-Building shape (exhaustive) and the 10000 x 4096 overlap-50
+shape (prefix, several batches in flight).
+
+The oracle's matcher here is oracle.match_pair_fast: the exact integer dot
+matrix from a float32 BLAS product (every partial sum an integer < 2^24) fed to
+the oracle's own FindBestMatches scans; tests/test_oracle_match.py pins it to
+the faithful scalar matcher.  Keypoint counts below 8192 are reductions of the
+real datasets' sizes chosen so the oracle finishes in seconds; the synthetic
+scenes are the bench's generator (no dataset is available).  Images are
+generated in-process (no forked workers once the GPU runtime is up)."""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle
+from scanner_colmap_amd import Context
+from scanner_colmap_amd.codecs import decode_tvg, decode_tvg_list, table_rows
+from scanner_colmap_amd.synthetic import Corridor
+
+pytestmark = pytest.mark.gpu
+THREADS = 16
+
+
+def _check_table(ctx, imgs, overlap, rows=None):
+    rows = rows or (0, len(imgs))
+    ids, kps, descs = table_rows(imgs)
+    ref_m = {}
+    ref = oracle.table_run_fast(imgs, overlap, rows[0], rows[1], threads=THREADS,
+                                matches_out=ref_m)
+    ctx.table_load(ids, kps, descs)
+    ctx.set_keep_matches(True)
+    try:
+        got = ctx.table_run(overlap, rows[0], rows[1])
+        for (r, s), m in ref_m.items():
+            g = ctx.table_matches(r, s - r, cap=max(1, len(m) + 1))
+            assert g.shape == m.shape and (g == m).all(), (r, s)
+    finally:
+        ctx.set_keep_matches(False)
+    assert got[0] == ref[0]
+    for i, (a, b) in enumerate(zip(got[1], ref[1])):
+        assert a == b, i
+    configs = [t.config for row in got[1] for t in decode_tvg_list(row)]
+    return configs
+
+
+def test_pair_8192_bit_exact(gpu_ctx):
+    """Config 3's pair shape: 8192 x 8192 (n1 > 2048 -> 16 row blocks)."""
+    c = Corridor(20, 8192, 20, seed=20252)
+    im = {i: c.image(i) for i in (0, 1, 10, 19)}
+    for j in (1, 10, 19):
+        got = gpu_ctx.match_pair(im[0][2], im[j][2])
+        ref = oracle.match_pair_fast(im[0][2], im[j][2])
+        assert got.shape == ref.shape and (got == ref).all(), j
+        assert len(ref) > 100
+        tg = gpu_ctx.verify_pair(im[0][1], im[j][1], ref, im[0][0], im[j][0])
+        tr = oracle.verify_pair(im[0][1], im[j][1], ref, im[0][0], im[j][0])
+        assert tg == tr, j
+        assert decode_tvg(tr).config in (3, 6)
+
+
+def test_pair_8192_ragged_and_reversed(gpu_ctx):
+    """Ragged full-size pairs: 8192 x 5000 and 5000 x 8192 (partial last
+    row block / column tile), and the same image against itself (every row a
+    tie with its own column)."""
+    c = Corridor(3, 8192, 3, seed=77)
+    a, b = c.image(0)[2], c.image(1)[2][:5000]
+    for x, y in ((a, b), (b, a), (a, a)):
+        got = gpu_ctx.match_pair(x, y)
+        ref = oracle.match_pair_fast(x, y)
+        assert got.shape == ref.shape and (got == ref).all()
+
+
+def test_gerrard_hall_shape_table():
+    """Configs 1/2 shape: 100 images, overlap 10 (855 pairs), every output row
+    and every pair's raw matches bit-identical to the CPU op's."""
+    imgs = Corridor(100, 4096, 10, seed=20251).images()
+    with Context(0) as ctx:
+        configs = _check_table(ctx, imgs, 10)
+    assert len(configs) == 855
+
+
+def test_roofline_workload_prefix():
+    """Config 3 (1000 x 8192, overlap 20): its first 24 images at full size
+    (266 pairs)."""
+    imgs = Corridor(1000, 8192, 20, seed=20252).images(0, 24)
+    with Context(0) as ctx:
+        configs = _check_table(ctx, imgs, 20)
+    assert len(configs) == 266
+
+
+def test_exhaustive_shape():
+    """Config 4 shape (South-Building exhaustive: overlap = number of images):
+    40 images x 2048 (780 pairs)."""
+    imgs = Corridor(40, 2048, 40, seed=20253).images()
+    with Context(0) as ctx:
+        configs = _check_table(ctx, imgs, 40)
+    assert len(configs) == 780
+
+
+def test_k50_shape_many_batches():
+    """Config 5 shape (4096 kpts, overlap 50): 64 images (1,911 pairs) in
+    batches of 400 pairs, so several batches are in flight at once."""
+    imgs = Corridor(10000, 4096, 50, seed=20254).images(0, 64)
+    os.environ["SCM_BATCH_PAIRS"] = "400"
+    try:
+        with Context(0) as ctx:
+            configs = _check_table(ctx, imgs, 50)
+    finally:
+        del os.environ["SCM_BATCH_PAIRS"]
+    assert len(configs) == sum(min(49, 63 - i) for i in range(64))

@@ -202,3 +202,38 @@ def test_matches_sorted_and_one_to_one():
     m = oracle.match_pair(d1, d2)
     assert (np.diff(m[:, 0].astype(np.int64)) > 0).all()
     assert len(np.unique(m[:, 1])) == len(m)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_fast_matcher_equals_faithful(seed):
+    """oracle.match_pair_fast (exact BLAS dots + the oracle's scans in
+    row-major order, the checker of the full-size GPU tests) returns exactly
+    the faithful scalar matcher's list: random, tie-stress, corridor pairs and
+    every option variant the GPU tests use."""
+    from scanner_colmap_amd.synthetic import Corridor, random_descriptors, tie_stress_pair
+    cases = [tie_stress_pair(500, 430, seed), (random_descriptors(300, seed), random_descriptors(280, seed + 9))]
+    imgs = Corridor(3, 900, 3, seed=seed).images()
+    cases += [(imgs[0][2], imgs[1][2]), (imgs[0][2], imgs[0][2])]
+    rng = np.random.default_rng(seed)
+    x = rng.integers(0, 256, size=(200, 128), dtype=np.uint8)
+    y = rng.integers(0, 256, size=(210, 128), dtype=np.uint8)
+    y[:80] = x[:80]
+    y[80:120] = x[:40]
+    cases.append((x, y))
+    for kw in ({}, dict(max_ratio=1.5, max_distance=3.0), dict(cross_check=0), dict(max_ratio=1.0)):
+        o = oracle.default_options()
+        for k, v in kw.items():
+            setattr(o, k, v)
+        for a, b in cases:
+            ref = oracle.match_pair(a, b, o)
+            got = oracle.match_pair_fast(a, b, o)
+            assert got.shape == ref.shape and (got == ref).all(), kw
+
+
+def test_fast_table_run_equals_faithful():
+    from scanner_colmap_amd.codecs import table_rows
+    from scanner_colmap_amd.synthetic import Corridor
+    imgs = Corridor(7, 500, 4, seed=3).images()
+    ids, kps, descs = table_rows(imgs)
+    assert oracle.table_run_fast(imgs, 4, 0, 7) == oracle.table_run(ids, kps, descs, 4, 0, 7)
+    assert oracle.table_run_fast(imgs, 3, 2, 6) == oracle.table_run(ids, kps, descs, 3, 2, 6)
