@@ -490,8 +490,8 @@ bool detect_watermark(const scm_matching_options& o, const std::vector<double>& 
 }
 
 // verifyTwoViewGeometry (sequential_matching.cc:84-101) -> Estimate ->
-// EstimateUncalibrated (dummy cameras have no prior focal length), then the
-// op's post-filter (:173-178).
+// EstimateUncalibrated (dummy cameras have no prior focal length); the op's
+// post-filter is verify_pair_filtered below.
 TVG verify_pair(const scm_matching_options& o, const float* kp1, const float* kp2,
                 const std::vector<Match>& matches, uint32_t id1, uint32_t id2) {
   TVG tvg;
@@ -534,8 +534,15 @@ TVG verify_pair(const scm_matching_options& o, const float* kp1, const float* kp
         tvg.config = SCM_TVG_WATERMARK;
     }
   }
-  // Post-filter: too few inliers -> TwoViewGeometry() (config 0, zero models).
-  if (tvg.inlier_matches.size() < min_num_inliers) tvg = TVG();
+  return tvg;
+}
+
+// verify_pair followed by the op's post-filter (sequential_matching.cc:173-178):
+// too few inliers -> TwoViewGeometry() (config 0, zero models).
+TVG verify_pair_filtered(const scm_matching_options& o, const float* kp1, const float* kp2,
+                         const std::vector<Match>& matches, uint32_t id1, uint32_t id2) {
+  TVG tvg = verify_pair(o, kp1, kp2, matches, id1, id2);
+  if (tvg.inlier_matches.size() < (size_t)o.min_num_inliers) tvg = TVG();
   return tvg;
 }
 
@@ -638,7 +645,7 @@ bool execute_rows(const scm_matching_options& o, const std::vector<Row>& st,
     std::vector<Match> matches;
     match_sift_features_cpu(o, pivot.desc, pivot.ndesc, st[i].desc, st[i].ndesc,
                             &matches);
-    tvgs.push_back(verify_pair(o, pivot.kp, st[i].kp, matches, pivot.id, id2));
+    tvgs.push_back(verify_pair_filtered(o, pivot.kp, st[i].kp, matches, pivot.id, id2));
   }
   *ids_blob = id_list_blob(pair_ids);
   *tvg_blob = tvg_list_blob(tvgs);
@@ -785,11 +792,25 @@ int oracle_verify_pair(const scm_matching_options* o, const float* kp1,
   (void)n2;
   std::vector<Match> mm((size_t)m);
   for (int64_t i = 0; i < m; ++i) mm[(size_t)i] = {matches[2 * i], matches[2 * i + 1]};
-  const TVG t = verify_pair(*o, kp1, kp2, mm, id1, id2);
+  const TVG t = verify_pair_filtered(*o, kp1, kp2, mm, id1, id2);
   std::vector<uint8_t> b;
   put_tvg(&b, t);
   *blob = to_heap(b, size);
   return SCM_OK;
+}
+
+// The configuration EstimateUncalibrated / DetectWatermark decide BEFORE the
+// op's post-filter, and the number of F-inlier matches (test support: shows
+// which branch a scene takes even when the post-filter then empties the row,
+// e.g. DEGENERATE with >= 15 matches).
+int oracle_verify_pair_config(const scm_matching_options* o, const float* kp1,
+                              const float* kp2, const uint32_t* matches, int64_t m,
+                              uint32_t id1, uint32_t id2, int64_t* num_inliers) {
+  std::vector<Match> mm((size_t)m);
+  for (int64_t i = 0; i < m; ++i) mm[(size_t)i] = {matches[2 * i], matches[2 * i + 1]};
+  const TVG t = verify_pair(*o, kp1, kp2, mm, id1, id2);
+  *num_inliers = (int64_t)t.inlier_matches.size();
+  return t.config;
 }
 
 // One LO-RANSAC run (kind 0 = F, 1 = H, 2 = translation) on explicit points

@@ -68,6 +68,9 @@ def lib() -> ctypes.CDLL:
         getattr(L, name).argtypes = [c_void_p, c_void_p, c_void_p]
     for name in ("oracle_fundamental_8pt", "oracle_homography_dlt"):
         getattr(L, name).argtypes = [c_void_p, c_void_p, c_int32, c_void_p]
+    L.oracle_verify_pair_config.argtypes = [POINTER(MatchingOptions), c_void_p, c_void_p,
+                                            c_void_p, c_int64, c_uint32, c_uint32,
+                                            POINTER(c_int64)]
     L.oracle_free.argtypes = [POINTER(c_uint8)]
     L.oracle_free.restype = None
     _lib = L
@@ -164,6 +167,18 @@ def verify_pair(kp1, kp2, matches, id1, id2, opts=None) -> bytes:
                                   m.ctypes.data, len(m), id1, id2, byref(p), byref(n))
     assert rc == 0
     return _take(p, n.value)
+
+
+def verify_pair_config(kp1, kp2, matches, id1, id2, opts=None) -> tuple[int, int]:
+    """(configuration before the op's post-filter, F-inlier count)."""
+    opts = opts or default_options()
+    k1 = np.ascontiguousarray(kp1, dtype=np.float32).reshape(-1, 6)
+    k2 = np.ascontiguousarray(kp2, dtype=np.float32).reshape(-1, 6)
+    m = np.ascontiguousarray(matches, dtype=np.uint32).reshape(-1, 2)
+    ni = c_int64()
+    cfg = lib().oracle_verify_pair_config(byref(opts), k1.ctypes.data, k2.ctypes.data,
+                                          m.ctypes.data, len(m), id1, id2, byref(ni))
+    return int(cfg), int(ni.value)
 
 
 def loransac(kind, x1, x2, seed, opts=None):

@@ -40,7 +40,6 @@ namespace {
 
 constexpr int64_t kMaxPairsPerBatch = 16384;
 constexpr int64_t kDefaultPairsPerBatch = 8192;
-constexpr int64_t kDefaultEdgePairs = 0;  // short edge batches (SCM_EDGE_PAIRS): off (measured slower)
 
 struct ImageTable {
   int64_t n = 0;
@@ -153,11 +152,9 @@ struct scm_context {
   HostBuf h_stage;  // table upload staging
   int threads = 1;
   int64_t batch_pairs = kDefaultPairsPerBatch;  // SCM_BATCH_PAIRS overrides
-  int64_t edge_pairs = kDefaultEdgePairs;        // SCM_EDGE_PAIRS overrides
+  int64_t batch_bytes = 0;  // HBM budget of one batch set (SCM_BATCH_BYTES; 0 = from free HBM)
   bool match_bf16 = false;  // SCM_MATCH_BF16=1: bf16 MFMA matcher instead of i8
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
-  bool balanced = false;  // SCM_BALANCED=1: equal batches (measured slower: verification
-                         // batches are latency-bound, a short last batch drains faster)
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
   int64_t n_match_launches = 0;  // matcher kernel launches of the last table run
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
@@ -843,6 +840,43 @@ void row_pairs(const std::vector<uint32_t>& stencil_ids, std::vector<int64_t>* s
   }
 }
 
+// Upper bound of the device workspace one pair takes in a batch set: the
+// matcher's row / column partials and match slots (enqueue_match), and the
+// verifier's points, scratch, window buffers and compaction output with every
+// pivot keypoint matched (enqueue_verify).
+int64_t pair_workspace_bytes(int64_t n1, int64_t n2) {
+  const int32_t rpb = kRowsPerBlock8 < kRowsPerBlock ? kRowsPerBlock8 : kRowsPerBlock;
+  const int64_t nseg = (n2 + kColsPerSeg - 1) / kColsPerSeg;
+  const int64_t nrb = (n1 + rpb - 1) / rpb;
+  const int64_t n2pad = (n2 + kTile8Cols - 1) / kTile8Cols * kTile8Cols;
+  const int64_t slots = std::max<int64_t>(n1, 1);
+  const int64_t match = nseg * n1 * 8 + nrb * n2pad * 8 + n2 * 4 + slots * (8 + 1);
+  const int64_t verify_pts = slots * (16 + 16 + 16 + 8 + 1);  // xy1, xy2, xyf, dpack, dpmask
+  const int64_t verify_pair = verify_scratch_doubles(slots) * 8 + kVerifySnapWords * 4 +
+                              (int64_t)sizeof(RansacState) + (int64_t)sizeof(VerifyOut) +
+                              (int64_t)kWindowTrials * (8 * 2 + 4 + 3 * 12 * 4 + 3 * 9 * 8 + 3 * 4) +
+                              (int64_t)kMaxWindow * 640 * 4 + 256;
+  return match + verify_pts + verify_pair;
+}
+
+// Byte budget of one of the three batch sets: SCM_BATCH_BYTES, or a third of
+// the free HBM plus what the sets already hold (reused), less a 2 GiB margin.
+int64_t set_budget_bytes(scm_context* ctx) {
+  if (ctx->batch_bytes > 0) return ctx->batch_bytes;
+  size_t free_b = 0, total_b = 0;
+  if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return INT64_MAX;
+  int64_t held = 0;
+  for (const BatchSet& bs : ctx->sets)
+    for (const DevBuf* b : {&bs.jobs, &bs.pairs, &bs.rowres, &bs.colpart, &bs.m21, &bs.matches,
+                            &bs.counts, &bs.gpairs, &bs.vpairs, &bs.xy1, &bs.xy2, &bs.scratch,
+                            &bs.snaps, &bs.masks, &bs.offsets, &bs.match_off, &bs.prof, &bs.xyf,
+                            &bs.dvout, &bs.dpack, &bs.dpmask, &bs.rst, &bs.samp, &bs.nmod,
+                            &bs.fcon, &bs.cnts, &bs.act, &bs.nact, &bs.mods, &bs.wsnap})
+      held += (int64_t)b->bytes;
+  const int64_t avail = (int64_t)free_b + held - ((int64_t)2 << 30);
+  return std::max<int64_t>(avail / 3, (int64_t)64 << 20);
+}
+
 // Runs the sequential stencil over table rows [row_begin, row_end) through
 // the double-buffered batch pipeline into one packed output.
 int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
@@ -861,7 +895,6 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
   std::vector<std::vector<int64_t>> rsel(nr);
   std::vector<std::vector<int64_t>> rrows(nr);
   std::vector<std::vector<uint32_t>> rids(nr);
-  int64_t total_pairs = 0;
   for (int64_t r = row_begin; r < row_end; ++r) {
     for (int64_t s = 0; s < overlap; ++s) {
       rows[s] = std::min(r + s, t.n - 1);  // stencil clamped at the table end
@@ -871,42 +904,30 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
     rsel[r - row_begin] = sel;
     rrows[r - row_begin] = rows;
     rids[r - row_begin] = ids;
-    total_pairs += (int64_t)sel.size();
   }
-  // Batches of whole rows, at most batch_pairs pairs each.  The first and
-  // the last batch are short (edge_pairs): the matcher runs alone until the
-  // first batch is matched and verification runs alone after the last one,
-  // so short edges shorten the pipeline's fill and drain.
-  // Balanced batches: the fewest batches of at most batch_pairs, sized
-  // equally (an unbalanced split leaves a long first matcher launch before
-  // verification can start, and a short last batch).
-  const int64_t nbatch = std::max<int64_t>(1, (total_pairs + ctx->batch_pairs - 1) / ctx->batch_pairs);
-  const int64_t bsize = ctx->balanced ? (total_pairs + nbatch - 1) / nbatch : ctx->batch_pairs;
-  const int64_t edge = (!ctx->serial && ctx->edge_pairs > 0 && total_pairs > 2 * ctx->batch_pairs)
-                           ? std::min(bsize, ctx->edge_pairs)
-                           : bsize;
+  // Batches of whole rows, closed at batch_pairs pairs or when the next row
+  // would push the batch's device workspace past the per-set byte budget
+  // (three sets are live at once).  A single row larger than the budget still
+  // forms a batch of its own (its allocation fails loudly if HBM is short).
+  // Measured on the bench workload: equal-size batches, short first / last
+  // batches, and caps of 4,096-9,472 pairs were all slower than 8,192.
+  const int64_t budget = set_budget_bytes(ctx);
   Batch cur;
-  int64_t remaining = total_pairs;  // pairs of rows i.. (this row included)
-  bool in_tail = false;
+  int64_t cur_bytes = 0;
   for (int64_t i = 0; i < nr; ++i) {
     const int64_t np = (int64_t)rsel[i].size();
-    const int64_t limit = batches.empty() ? edge : bsize;
-    const bool tail_starts =
-        edge < bsize && !in_tail && !batches.empty() && remaining <= edge;
-    if (tail_starts) in_tail = true;
-    // A batch closes once it holds its share (balanced: at least bsize, so
-    // the rows' granularity adds no extra batch) or would pass the cap.
+    const int64_t r = row_begin + i;
+    int64_t row_bytes = 0;
+    for (int64_t s : rsel[i]) row_bytes += pair_workspace_bytes(t.ndesc[r], t.ndesc[rrows[i][s]]);
     const int64_t have = (int64_t)cur.specs.size();
-    const bool full = ctx->balanced && limit == bsize ? have >= limit || have + np > ctx->batch_pairs
-                                                      : have + np > limit;
-    if (!cur.specs.empty() && (full || tail_starts)) {
-      cur.pairs_begin.push_back((int64_t)cur.specs.size());
+    if (have > 0 && (have + np > ctx->batch_pairs || cur_bytes + row_bytes > budget)) {
+      cur.pairs_begin.push_back(have);
       batches.push_back(std::move(cur));
       cur = Batch();
+      cur_bytes = 0;
     }
-    remaining -= np;
+    cur_bytes += row_bytes;
     cur.pairs_begin.push_back((int64_t)cur.specs.size());
-    const int64_t r = row_begin + i;
     for (int64_t s : rsel[i]) {
       cur.specs.push_back({(int32_t)r, (int32_t)rrows[i][s]});
       cur.pair_ids.push_back(rids[i][s]);
@@ -1019,11 +1040,9 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::max(1, std::atoi(e));
   ctx->threads = std::max(1, std::min(16, hw));
   if (const char* e = std::getenv("SCM_SERIAL")) ctx->serial = e[0] == '1';
-  if (const char* e = std::getenv("SCM_BALANCED")) ctx->balanced = e[0] == '1';
   if (const char* e = std::getenv("SCM_BATCH_PAIRS"))
     ctx->batch_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
-  if (const char* e = std::getenv("SCM_EDGE_PAIRS"))
-    ctx->edge_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
+  if (const char* e = std::getenv("SCM_BATCH_BYTES")) ctx->batch_bytes = std::max<int64_t>(1, std::atoll(e));
   if (const char* e = std::getenv("SCM_MATCH_BF16")) ctx->match_bf16 = e[0] == '1';
   // The i8 matcher tracks column top-2 by value only, which decides the
   // cross-check exactly when a tied column best fails the ratio test, i.e.

@@ -169,3 +169,72 @@ def tie_stress_pair(n1: int, n2: int, seed: int):
     a[5, :] = 255                                        # saturated rows
     b[7, :] = 255
     return a, b
+
+
+def geometry_scene(kind: str, num_matches: int, seed: int, outlier_frac: float = 0.2,
+                   noise_px: float = 0.5):
+    """Keypoints of two images and a match list whose geometry drives
+    TwoViewGeometry::EstimateUncalibrated into a chosen branch (reference
+    sequential_matching.cc:98-99 and the post-filter :164-178):
+
+    * "general":     a 3-D scene seen by two cameras -> UNCALIBRATED (3);
+    * "planar":      every inlier on one plane (x2 = H x1)
+                     -> PLANAR_OR_PANORAMIC (6): H explains > 80 % of the F inliers;
+    * "translation": x2 = x1 + t for the inliers, which a 2-D translation
+                     explains -> WATERMARK (7) (DetectWatermark; the dummy cameras
+                     put every inlier "in the border", SURVEY.md §8a a14);
+    * "random":      no geometry at all: F and H both find < 15 inliers
+                     -> DEGENERATE (1), which the op's post-filter turns into
+                     TwoViewGeometry() (config 0).
+
+    Returns (kp1 N x 6, kp2 N x 6, matches M x 2 uint32); keypoint order is
+    shuffled so the match indices are not the identity."""
+    rng = np.random.default_rng(seed)
+    m = num_matches
+    x1 = np.stack([rng.uniform(0, 1920, m), rng.uniform(0, 1080, m)], axis=1)
+    if kind == "planar":
+        H = np.array([[0.92, 0.06, 41.0], [-0.03, 1.04, 18.5], [2.0e-5, -1.5e-5, 1.0]])
+        p = np.c_[x1, np.ones(m)] @ H.T
+        x2 = p[:, :2] / p[:, 2:3]
+    elif kind == "translation":
+        x2 = x1 + np.array([37.5, -12.25])
+    elif kind == "random":
+        x2 = np.stack([rng.uniform(0, 1920, m), rng.uniform(0, 1080, m)], axis=1)
+    elif kind == "general":
+        X = np.stack([rng.uniform(-4, 4, m), rng.uniform(-2.5, 2.5, m), rng.uniform(6, 20, m)], 1)
+        f = 1200.0
+
+        def proj(R, c):
+            Xc = (X - c) @ R.T
+            return np.stack([f * Xc[:, 0] / Xc[:, 2] + 960, f * Xc[:, 1] / Xc[:, 2] + 540], 1)
+        a = 0.12
+        R2 = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
+        x1 = proj(np.eye(3), np.zeros(3))
+        x2 = proj(R2, np.array([1.5, 0.2, 0.3]))
+    else:
+        raise ValueError(kind)
+    x2 = x2 + rng.normal(0, noise_px, x2.shape)
+    nout = int(round(outlier_frac * m))
+    if nout:
+        x2[:nout] = np.stack([rng.uniform(0, 1920, nout), rng.uniform(0, 1080, nout)], axis=1)
+    p1 = rng.permutation(m)
+    p2 = rng.permutation(m)
+    kp1 = np.zeros((m, 6), np.float32)
+    kp2 = np.zeros((m, 6), np.float32)
+    kp1[p1, :2] = x1
+    kp2[p2, :2] = x2
+    kp1[:, 2] = kp1[:, 5] = kp2[:, 2] = kp2[:, 5] = 1.0
+    matches = np.stack([p1, p2], axis=1).astype(np.uint32)
+    matches = matches[np.argsort(matches[:, 0], kind="stable")]  # idx1 ascending, as the matcher
+    return kp1, kp2, matches
+
+
+def descriptors_for_matches(matches: np.ndarray, n1: int, n2: int, seed: int):
+    """Descriptor pair whose cross-checked matches are exactly `matches`
+    (idx1 ascending, one-to-one): each matched column is a copy of its row's
+    RootSIFT descriptor, every other row and column is random.  Lets a
+    geometry_scene run through the matcher of the table path."""
+    d1 = random_descriptors(n1, seed)
+    d2 = random_descriptors(n2, seed + 1)
+    d2[matches[:, 1]] = d1[matches[:, 0]]
+    return d1, d2

@@ -18,7 +18,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 
 from oracle import oracle  # noqa: E402
 from scanner_colmap_amd.codecs import table_rows  # noqa: E402
-from scanner_colmap_amd.synthetic import Corridor, random_descriptors, tie_stress_pair  # noqa: E402
+from scanner_colmap_amd.synthetic import (Corridor, geometry_scene, random_descriptors,  # noqa: E402
+                                          tie_stress_pair)
+
+# Two-view-geometry outcome scenes (name, kind, matches, seed): one per branch of
+# EstimateUncalibrated / DetectWatermark / the op's post-filter.
+OUTCOME_CASES = (("general", "general", 300, 0), ("planar", "planar", 300, 1),
+                 ("watermark", "translation", 300, 2), ("degenerate", "random", 40, 3),
+                 ("few_inliers", "random", 300, 4), ("planar_big", "planar", 2000, 5),
+                 ("watermark_big", "translation", 2000, 6))
 
 
 def _blob_array(blobs):
@@ -67,6 +75,25 @@ def main():
     out["num_trials_F_cap"] = np.array([oracle.num_trials(25000, 100000, 0.999, 3.0, 7)])
     np.savez_compressed(os.path.join(HERE, "golden_v1.npz"), **out)
     print("wrote", os.path.join(HERE, "golden_v1.npz"))
+    outcomes()
+
+
+def outcomes():
+    """golden_outcomes.npz: per scene the keypoints, matches, image ids, the
+    oracle's configuration before the post-filter, its F-inlier count and the
+    io.cc TVG bytes after it."""
+    out = {}
+    for name, kind, m, seed in OUTCOME_CASES:
+        kp1, kp2, mt = geometry_scene(kind, m, seed)
+        ids = np.array([100 + seed, 200 + seed], np.uint32)
+        cfg, ninl = oracle.verify_pair_config(kp1, kp2, mt, int(ids[0]), int(ids[1]))
+        out[f"{name}_kp1"], out[f"{name}_kp2"], out[f"{name}_matches"] = kp1, kp2, mt
+        out[f"{name}_ids"] = ids
+        out[f"{name}_raw"] = np.array([cfg, ninl], np.int64)
+        out[f"{name}_tvg"] = np.frombuffer(
+            oracle.verify_pair(kp1, kp2, mt, int(ids[0]), int(ids[1])), np.uint8)
+    np.savez_compressed(os.path.join(HERE, "golden_outcomes.npz"), **out)
+    print("wrote", os.path.join(HERE, "golden_outcomes.npz"))
 
 
 if __name__ == "__main__":

@@ -23,3 +23,15 @@ def table(g):
     from scanner_colmap_amd.codecs import encode_image_id
     ids = [encode_image_id(int(i)) for i in g["table_ids"]]
     return ids, blobs(g, "table_kps"), blobs(g, "table_descs")
+
+
+OUTCOMES_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                             "golden_outcomes.npz")
+# name -> (configuration before the post-filter, configuration in the output row)
+OUTCOMES = {"general": (3, 3), "planar": (6, 6), "watermark": (7, 7), "degenerate": (1, 0),
+            "few_inliers": (3, 3), "planar_big": (6, 6), "watermark_big": (7, 7)}
+
+
+def load_outcomes():
+    with np.load(OUTCOMES_PATH, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}

@@ -59,21 +59,29 @@ def test_keep_matches(gpu_ctx):
         gpu_ctx.set_keep_matches(False)
 
 
-def test_many_batches_in_flight():
-    """Batches of 3 pairs: exercises the double-buffered enqueue/collect
-    alternation and per-batch serialisation against the oracle."""
+@pytest.mark.parametrize("env", [{"SCM_BATCH_PAIRS": "3"},
+                                 {"SCM_BATCH_PAIRS": "3", "SCM_SERIAL": "1"},
+                                 {"SCM_BATCH_BYTES": str(6 << 20)}])
+def test_many_batches_in_flight(env):
+    """Batches of 3 pairs (or cut by a 6 MiB workspace budget, ~4 pairs of
+    these images, scm_runtime.cpp set_budget_bytes): exercises the three
+    rotating batch sets, the enqueue / collect alternation, the serial
+    diagnostic schedule and per-batch serialisation against the oracle."""
     imgs, (ids, kps, descs) = _table(12, 400, 43)
     ref = oracle.table_run(ids, kps, descs, 4, 0, len(imgs))
-    os.environ["SCM_BATCH_PAIRS"] = "3"
+    os.environ.update(env)
     try:
         with Context(0) as ctx:
             ctx.table_load(ids, kps, descs)
             got = ctx.table_run(4, 0, len(imgs))
             got2 = ctx.table_run_packed(4, 0, len(imgs)).rows()
+            launches = ctx.table_timings()["match_launches"]
     finally:
-        del os.environ["SCM_BATCH_PAIRS"]
+        for k in env:
+            del os.environ[k]
     assert got == ref
     assert got2 == ref
+    assert launches >= 4  # the budget or the pair cap cut the table into several batches
 
 
 def test_ragged_table_with_empty_images(gpu_ctx):
