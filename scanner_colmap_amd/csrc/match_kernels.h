@@ -43,7 +43,9 @@ struct PairDesc {
   int64_t colpart_off;  // uint2 offset: [nrb][n2pad]
   int64_t m21_off;      // int32 offset: [n2]
   int64_t match_off;    // uint2 offset: [n1]
-  int32_t n1, n2, n2pad, nseg, nrb, pad_;
+  int64_t a_row;        // table row of the pivot's descriptor 0 (finalize recompute)
+  int32_t n1, n2, n2pad, nseg, nrb;
+  int32_t clamp;        // 1: the pivot run took the CLAMP matcher variant
 };
 
 hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int njobs,
@@ -52,6 +54,16 @@ hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int nj
 hipError_t launch_match_tiles_i8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
                                  int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
                                  bool clamp, hipStream_t stream);
+// Version-2 i8 matcher (LDS-DMA staging, best-only column partials) and its
+// finalize (exact recompute of the deciding column seconds).
+hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
+                           int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
+                           bool clamp, hipStream_t stream);
+hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* rowres,
+                                    uint2* colpart, const uint8_t* desc8, const int32_t* csum,
+                                    const float* lut, float max_ratio, float max_distance,
+                                    int cross_check, uint2* matches, int32_t* counts,
+                                    int max_groups, hipStream_t stream);
 hipError_t launch_match_finalize(const PairDesc* pairs, int npairs, const uint2* rowres,
                                  const uint2* colpart, int32_t* m21, const float* lut,
                                  float max_ratio, float max_distance, int cross_check,

@@ -478,6 +478,7 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_ti
   uint2* colscratch = reinterpret_cast<uint2*>(lds + kStages8 * kTile8Bytes);
 
   const MatchJob job = jobs[blockIdx.x];
+  if (job.npairs == 0 || job.n1 <= 0) return;  // padding job of the XCD order (whole block)
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
@@ -501,7 +502,9 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_ti
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int rw = row0 + 32 * s + 4 * h + (i & 3) + 8 * (i >> 2);
-      ra[s][i] = (int)((rw < job.n1 ? (uint32_t)csum[job.a_row + rw] : 0u) + (1u << 21));
+      // unconditional load (clamped row), then select: no branch / wait per element
+      const uint32_t cs = (uint32_t)csum[job.a_row + min(rw, job.n1 - 1)];
+      ra[s][i] = (int)((rw < job.n1 ? cs : 0u) + (1u << 21));
     }
   }
 
@@ -630,6 +633,360 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_ti
 }
 
 // ===========================================================================
+// i8 matcher, version 2 (default): LDS-DMA staging, best-only columns.
+//
+// Same MFMA chains, accumulator offsets and row keys as match_tiles_i8_kernel
+// (above), with two changes that target what bounds it (VALU issue and
+// wave stalls on the staging loads):
+//  * B tiles and their column sums reach LDS by global_load_lds_dwordx4
+//    (LDS-DMA: no staging VGPRs, no ds_write, no wave waiting for a load in
+//    the tile it is issued): each wave moves 1 KiB of the 8 KiB tile, the
+//    XOR-swizzled LDS image is produced by permuting the per-lane SOURCE
+//    addresses (the destination of one instruction is lane-linear), tiles are
+//    issued three ahead into a 4-stage ring, and one raw s_barrier per tile is
+//    preceded by a counted vmcnt that retires exactly the next tile.
+//  * Column side by BEST VALUE ONLY: per lane a max3 tree over its 16 raw
+//    accumulators (8 ops instead of the 21 of a top-2 tree), then the two
+//    row sub-tiles and the two lane halves (best of the wave's 64 rows); the
+//    workgroup merge keeps, per column, the best value B1, the largest best
+//    of the OTHER waves B2', and the wave of B1.  The column's true second is
+//    max(B2', second within that wave's 64 rows): match_finalize_kernel
+//    recomputes the 64 dots of that group exactly (sdot4 on the same offset
+//    operands) for the few columns whose cross-check outcome depends on it.
+// Per element: 1 (row key) + 2 (row state) + ~0.6 (column) VALU ops.
+// colpart entry (per row block, column): x = B1 (exact dot, clamped like the
+// row keys in the CLAMP variant), y = (B2' << 3) | wave of B1.
+// ===========================================================================
+constexpr int kG8T = 4;                                        // tiles per barrier group
+constexpr int kG8Q = 4;                                        // groups in the LDS ring
+constexpr int kG8Stages = kG8T * kG8Q;                         // 16 x 8 KiB of B tiles
+constexpr int kG8CscGroups = 3;                                // column partials of 3 groups
+constexpr int kG8CbOff = kG8Stages * kTile8Bytes;              // column sums, 64 int32 per stage
+constexpr int kG8MetaOff = kG8CbOff + kG8Stages * kTile8Cols * 4;  // colpart index per tile
+constexpr int kG8CscOff = kG8MetaOff + kG8Stages * 8;
+constexpr int kG8LdsBytes = kG8CscOff + kG8CscGroups * kG8T * kMatch8Waves * kTile8Cols * 4;
+static_assert(kMatch8Waves * 1024 == kTile8Bytes, "one 1 KiB LDS-DMA per wave per tile");
+static_assert(kG8LdsBytes <= 160 * 1024, "LDS");
+
+typedef __attribute__((address_space(3))) void lds_void;
+
+// LDS-DMA of tile t of a neighbour (descriptors from b8, column sums from bs)
+// into ring stage `stage`: wave w moves columns 8w .. 8w + 7; lane L writes
+// LDS byte 16 L of the wave's block, i.e. (column 8w + L / 8, position L % 8),
+// which holds logical chunk (L % 8) ^ ((column >> 1) & 7) (sw8).  The last
+// wave also moves the tile's 64 column sums (4 B per lane).
+__device__ __forceinline__ void g8_stage(const uint8_t* b8, const int32_t* bs, int t, int stage,
+                                         int wave, int lane, uint8_t* lds) {
+  const int col = wave * 8 + (lane >> 3);
+  const int c = (lane & 7) ^ ((col >> 1) & 7);
+  __builtin_amdgcn_global_load_lds(b8 + ((int64_t)t * kTile8Cols + col) * 128 + c * 16,
+                                   (lds_void*)(lds + stage * kTile8Bytes + wave * 1024), 16, 0, 0);
+  if (wave == kMatch8Waves - 1)
+    __builtin_amdgcn_global_load_lds(bs + (int64_t)t * kTile8Cols + lane,
+                                     (lds_void*)(lds + kG8CbOff + stage * kTile8Cols * 4), 4, 0, 0);
+}
+
+// s_waitcnt vmcnt(n) for a wave-uniform n (immediate operand): at most n of
+// this wave's vector-memory operations (loads, stores, LDS-DMA) outstanding.
+#define SCM_VM_CASE(n) \
+  case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
+__device__ __forceinline__ void g8_wait_vm(int n) {
+  switch (n) {
+    SCM_VM_CASE(1) SCM_VM_CASE(2) SCM_VM_CASE(3) SCM_VM_CASE(4) SCM_VM_CASE(5) SCM_VM_CASE(6)
+    SCM_VM_CASE(7) SCM_VM_CASE(8) SCM_VM_CASE(9) SCM_VM_CASE(10) SCM_VM_CASE(11)
+    SCM_VM_CASE(12) SCM_VM_CASE(13) SCM_VM_CASE(14) SCM_VM_CASE(15) SCM_VM_CASE(16)
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+#undef SCM_VM_CASE
+
+// The first sub-tile's B fragments and the two column sums of tile g (ring
+// stage g mod kG8Stages), read one step ahead of their use.
+__device__ __forceinline__ void g8_next(const uint8_t* lds, int g, int r, int h, i32x4 (&bf)[4],
+                                        uint32_t& cb0, uint32_t& cb1) {
+  const int stage = g & (kG8Stages - 1);
+  load_bfrag8(lds + stage * kTile8Bytes, r, h, bf);
+  const int32_t* cbs = reinterpret_cast<const int32_t*>(lds + kG8CbOff + stage * kTile8Cols * 4);
+  cb0 = (uint32_t)cbs[r];
+  cb1 = (uint32_t)cbs[32 + r];
+}
+
+// One 4-MFMA chain of the v2 kernel; SCM_G8_PRIO (diagnostics) raises the
+// wave's issue priority around it.
+__device__ __forceinline__ i32x16 g8_chain(const i32x4 (&a)[4], const i32x4 (&b)[4],
+                                           const i32x16& ra) {
+#ifdef SCM_G8_PRIO
+  __builtin_amdgcn_s_setprio(1);
+  const i32x16 r = chain8(a, b, ra);
+  __builtin_amdgcn_s_setprio(0);
+  return r;
+#else
+  return chain8(a, b, ra);
+#endif
+}
+
+// Row keys and row state of a finished sub-tile (as subtile_epilogue8) and
+// the largest raw accumulator of the lane's 16 rows (column side).
+template <bool CLAMP>
+__device__ __forceinline__ uint32_t g8_epilogue(const i32x16& acc, uint32_t kc, uint32_t cbm,
+                                                uint32_t tbits, uint32_t (&b1r)[16],
+                                                uint32_t (&b2r)[16]) {
+#ifdef SCM_DIAG_MATCH_SKELETON
+  // diagnostics only: MFMA + LDS + staging skeleton, results discarded
+  uint32_t xs = 0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) xs ^= (uint32_t)acc[i];
+  b1r[0] ^= xs;
+  return xs;
+#endif
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t x = (uint32_t)acc[i];
+    const uint32_t key = CLAMP ? (min(x + cbm, kLutMax) << 13) | tbits : (x << 13) + kc;
+    b2r[i] = med3_u32(key, b1r[i], b2r[i]);
+    b1r[i] = max(b1r[i], key);
+  }
+#ifdef SCM_DIAG_G8_TOP2
+  // diagnostics only: the cost of the exact column top-2 tree (result unchanged:
+  // the second's bit 31 is always clear)
+  {
+    const uint2 t2 = column_top2_values(acc);
+    return t2.x | (t2.y & 0x80000000u);
+  }
+#endif
+  uint32_t v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) v[i] = (uint32_t)acc[i];
+  const uint32_t m0 = max(max(v[0], v[1]), v[2]), m1 = max(max(v[3], v[4]), v[5]);
+  const uint32_t m2 = max(max(v[6], v[7]), v[8]), m3 = max(max(v[9], v[10]), v[11]);
+  const uint32_t m4 = max(max(v[12], v[13]), v[14]);
+  return max(max(max(m0, m1), m2), max(max(m3, m4), v[15]));
+}
+
+// Best raw value of a column over the wave's 64 rows (both row sub-tiles,
+// both lane halves); lanes of half 0 write it for the workgroup merge.
+__device__ __forceinline__ void g8_col_partial(uint32_t e0, uint32_t e1, uint32_t* dst, int h,
+                                               int r) {
+  const uint32_t m = max(e0, e1);
+  // v_permlane32_swap(m, m) gives each lane m and its partner (lane ^ 32) in
+  // the two results: a VALU exchange instead of an LDS ds_bpermute round trip.
+  const auto sw = __builtin_amdgcn_permlane32_swap(m, m, false, false);
+  if (h == 0) dst[r] = max((uint32_t)sw[0], (uint32_t)sw[1]);
+}
+
+// Workgroup merge of one column of a tile (lane = column): the best of the 8
+// wave bests B1, the largest of the other seven B2' (a tie puts B1 there), the
+// lowest wave holding B1.  Raw accumulator units (dot - cb + 2^22; the
+// finalize kernel converts with the column's sum).
+__device__ __forceinline__ void g8_merge(const uint32_t* src, uint2* dst) {
+  uint32_t b1 = src[0], b2 = 0u, gw = 0u;
+#pragma unroll
+  for (int w = 1; w < kMatch8Waves; ++w) {
+    const uint32_t v = src[w * kTile8Cols];
+    b2 = max(b2, min(b1, v));
+    gw = v > b1 ? (uint32_t)w : gw;
+    b1 = max(b1, v);
+  }
+  *dst = make_uint2(b1, (b2 << 3) | gw);
+}
+
+// One workgroup = one MatchJob (512 pivot rows, 8 waves x 64) swept against
+// every column of its neighbour images.  The tiles of the job's pairs form one
+// stream (tile g -> pair p, tile t of p).  Groups of kG8T = 4 tiles share one
+// barrier: at the barrier ending group m every wave has (a) waited for its
+// LDS-DMA of group m + 1, (b) finished reading group m - 1's stages, which
+// then receive group m + 3, and (c) written its column partials of group
+// m - 1 (the last tile's second half is written just after barrier m - 1), so
+// four waves merge group m - 1's tiles.  Between barriers waves drift freely,
+// so the two waves of a SIMD overlap one's MFMA chains with the other's
+// epilogue.  Per wave and tile four 4-MFMA chains, software pipelined (each
+// chain under the previous epilogue), the chain of the next tile's first
+// sub-tile issued before the current tile's last epilogue.
+template <bool CLAMP>
+__global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8_kernel(
+    const uint8_t* __restrict__ desc8,  // a ^ 0x80, [rows][128]
+    const int32_t* __restrict__ csum,   // 128 * sum_d a_d per row
+    const MatchJob* __restrict__ jobs, const PairDesc* __restrict__ pairs,
+    uint2* __restrict__ rowres,         // per pair [nseg][n1]
+    uint2* __restrict__ colpart) {      // per pair [nrb][n2pad]
+  // One array for every LDS use (a second __shared__ object can make the
+  // compiler drain the LDS-DMA queue before each ds_read).
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kG8LdsBytes];
+  uint32_t* csc = reinterpret_cast<uint32_t*>(lds + kG8CscOff);
+  int64_t* meta = reinterpret_cast<int64_t*>(lds + kG8MetaOff);
+
+  const MatchJob job = jobs[blockIdx.x];
+  if (job.npairs == 0 || job.n1 <= 0) return;  // padding job of the XCD order (whole block)
+  const PairDesc* __restrict__ P = pairs + job.pair0;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int r = lane & 31;
+  const int h = lane >> 5;
+  const int row0 = job.rb * kRowsPerBlock8 + wave * 64;
+
+  i32x4 afrag[2][4];
+  i32x16 ra[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int row = row0 + 32 * s + r;
+    const bool ok = row < job.n1;
+    const i32x4* src =
+        reinterpret_cast<const i32x4*>(desc8 + (job.a_row + (ok ? row : 0)) * 128) + h * 4;
+    const int z = (int)0x80808080u;  // a = 0
+#pragma unroll
+    for (int q = 0; q < 4; ++q) afrag[s][q] = ok ? src[q] : i32x4{z, z, z, z};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int rw = row0 + 32 * s + 4 * h + (i & 3) + 8 * (i >> 2);
+      // unconditional load (clamped row), then select: no branch / wait per element
+      const uint32_t cs = (uint32_t)csum[job.a_row + min(rw, job.n1 - 1)];
+      ra[s][i] = (int)((rw < job.n1 ? cs : 0u) + (1u << 21));
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // operands in registers before any LDS-DMA
+
+  int G = 0;
+  for (int p = 0; p < job.npairs; ++p) G += (P[p].n2 + kTile8Cols - 1) / kTile8Cols;
+  // LDS-DMA cursor (groups ahead of the compute cursor; past the last tile it
+  // re-stages the last one, so every wave issues the same number of
+  // operations per group and the vmcnt counts stay fixed).
+  int fp = 0, ft = 0;
+  int64_t fb = P[0].b_row;
+  int fn = (P[0].n2 + kTile8Cols - 1) / kTile8Cols;
+  const int gpt = wave == kMatch8Waves - 1 ? 2 : 1;  // LDS-DMA operations per tile
+  auto dma_group = [&](int grp) {
+#pragma unroll 1
+    for (int i = 0; i < kG8T; ++i) {
+      g8_stage(desc8 + fb * 128, csum + fb, ft, (grp * kG8T + i) & (kG8Stages - 1), wave, lane, lds);
+      if (++ft == fn) {
+        if (fp + 1 < job.npairs) {
+          ++fp;
+          ft = 0;
+          fb = P[fp].b_row;
+          fn = (P[fp].n2 + kTile8Cols - 1) / kTile8Cols;
+        } else {
+          ft = fn - 1;
+        }
+      }
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < kG8Q - 1; ++j) dma_group(j);
+  g8_wait_vm((kG8Q - 2) * kG8T * gpt);  // group 0 landed
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  // Compute cursor.
+  int p = 0, t = 0;
+  PairDesc pd = P[0];
+  int nt = (pd.n2 + kTile8Cols - 1) / kTile8Cols;
+  int64_t cpi = pd.colpart_off + (int64_t)job.rb * pd.n2pad;  // colpart index of tile 0 of pair p
+  int flushed = -8;  // iteration of the last row flush (its stores)
+
+  uint32_t b1r[2][16], b2r[2][16];
+#pragma unroll
+  for (int s = 0; s < 2; ++s)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { b1r[s][i] = 0u; b2r[s][i] = 0u; }
+
+  i32x4 bf0[4], bf1[4];
+#ifdef SCM_G8_STAGGER  // diagnostics: delay waves 4-7 (the second half of each SIMD pair)
+  if (wave >= 4) __builtin_amdgcn_s_sleep(SCM_G8_STAGGER);
+#endif
+  uint32_t cbn0, cbn1;
+  g8_next(lds, 0, r, h, bf0, cbn0, cbn1);
+  i32x16 acc = g8_chain(afrag[0], bf0, ra[0]);
+
+  for (int g = 0; g < G; ++g) {
+    const int stage = g & (kG8Stages - 1);
+    const uint8_t* cur = lds + stage * kTile8Bytes;
+    const uint32_t cb0 = cbn0, cb1 = cbn1;  // read with the tile's c0 fragments
+    if (tid == 0) meta[stage] = cpi + (int64_t)t * kTile8Cols;
+    const int k = t & (kTiles8PerSeg - 1);  // 64-column tile within the segment
+    const uint32_t tb0 = (uint32_t)(kTilesPerSeg - 1 - 2 * k), tb1 = tb0 - 1u;
+    const uint32_t kc0 = (cb0 << 13) | tb0, kc1 = (cb1 << 13) | tb1;
+    const uint32_t cbm0 = cb0 - (1u << 22), cbm1 = cb1 - (1u << 22);
+    const int m = g / kG8T;
+    uint32_t* cscw =
+        csc + (((m % kG8CscGroups) * kG8T + (g & (kG8T - 1))) * kMatch8Waves + wave) * kTile8Cols;
+    const bool group_end = (g & (kG8T - 1)) == kG8T - 1;
+    // (s1, c0) || epilogue (s0, c0); the c1 fragments load under the epilogue
+    i32x16 acc2 = g8_chain(afrag[1], bf0, ra[1]);
+    load_bfrag8(cur, 32 + r, h, bf1);
+    const uint32_t e00 = g8_epilogue<CLAMP>(acc, kc0, cbm0, tb0, b1r[0], b2r[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    // (s0, c1) || epilogue (s1, c0)
+    acc = g8_chain(afrag[0], bf1, ra[0]);
+    const uint32_t e10 = g8_epilogue<CLAMP>(acc2, kc0, cbm0, tb0, b1r[1], b2r[1]);
+    g8_col_partial(e00, e10, cscw, h, r);
+    __builtin_amdgcn_sched_barrier(0);
+    // (s1, c1) || epilogue (s0, c1); inside a group the next tile's c0
+    // fragments load under the epilogue (at a group end only after the barrier)
+    acc2 = g8_chain(afrag[1], bf1, ra[1]);
+    if (!group_end) g8_next(lds, g + 1, r, h, bf0, cbn0, cbn1);
+    const uint32_t e01 = g8_epilogue<CLAMP>(acc, kc1, cbm1, tb1, b1r[0], b2r[0]);
+    __builtin_amdgcn_sched_barrier(0);
+    if (group_end) {
+      // Barrier m.  This wave's DMA of group m + 1 (issued at barrier m - 2)
+      // must be done: younger are group m + 2's DMA and the merge stores of
+      // barriers m - 2 and m - 1 (wave w merges at barrier j when
+      // ((j - 1) & 1) == w / 4); after a row flush (many stores) drain.
+      const int half = wave >> 2;
+      const int st = (m >= 3 && (((m - 3) & 1) == half)) + (m >= 2 && (((m - 2) & 1) == half));
+#ifndef SCM_DIAG_NOBARRIER  // diagnostics only (races): timing without the group barrier
+      g8_wait_vm(g - flushed <= 2 * kG8T ? 0 : kG8T * gpt + st);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+#else
+      (void)st;
+#endif
+      dma_group(m + kG8Q - 1);
+      if (m >= 1 && (((m - 1) & 1) == half)) {  // merge tile (wave & 3) of group m - 1
+        const int tg = (m - 1) * kG8T + (wave & (kG8T - 1));
+        const uint32_t* src =
+            csc + (((m - 1) % kG8CscGroups) * kG8T + (wave & (kG8T - 1))) * kMatch8Waves * kTile8Cols;
+        g8_merge(src + lane, colpart + meta[tg & (kG8Stages - 1)] + lane);
+      }
+      g8_next(lds, g + 1, r, h, bf0, cbn0, cbn1);
+    }
+    // (g + 1: s0, c0) || epilogue (s1, c1)
+    acc = g8_chain(afrag[0], bf0, ra[0]);
+    const uint32_t e11 = g8_epilogue<CLAMP>(acc2, kc1, cbm1, tb1, b1r[1], b2r[1]);
+    g8_col_partial(e01, e11, cscw + 32, h, r);
+    // Row flush at the end of a segment (or of the pair).
+    if (k == kTiles8PerSeg - 1 || t + 1 == nt) {
+      row_flush(b1r, b2r, rowres + pd.rowres_off + (int64_t)(t / kTiles8PerSeg) * pd.n1, row0,
+                pd.n1, r, h);
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) { b1r[s][i] = 0u; b2r[s][i] = 0u; }
+      flushed = g;
+    }
+    if (++t == nt && p + 1 < job.npairs) {
+      ++p;
+      t = 0;
+      pd = P[p];
+      nt = (pd.n2 + kTile8Cols - 1) / kTile8Cols;
+      cpi = pd.colpart_off + (int64_t)job.rb * pd.n2pad;
+    }
+  }
+  // Merge of the tiles no barrier merged: groups merged so far are those
+  // before the last barrier's group (barrier m merges group m - 1).
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const int nbar = G / kG8T;                         // barriers 0 .. nbar - 1 ran
+  const int first = nbar >= 1 ? (nbar - 1) * kG8T : 0;  // first unmerged tile
+  const int tg = first + wave;
+  if (tg < G) {
+    const uint32_t* src = csc + (((tg / kG8T) % kG8CscGroups) * kG8T + (tg & (kG8T - 1))) *
+                                    kMatch8Waves * kTile8Cols;
+    g8_merge(src + lane, colpart + meta[tg & (kG8Stages - 1)] + lane);
+  }
+}
+
+// ===========================================================================
 // Finalize.
 // ===========================================================================
 // Upper bound, acosf LUT: lut[d] = acosf(min(d * 2^-18, 1.0f)), d in [0, 2^18],
@@ -753,6 +1110,216 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
   }
 }
 
+// Finalize of the version-2 i8 matcher (best-only column partials, value
+// mode: max_ratio <= 1 with the cross-check, or no cross-check).  One
+// workgroup per pair:
+//  1. columns: merge the row blocks' (B1, B2', wave) (raw accumulator units,
+//     converted here with the column's sum) into colpart row 0 as
+//     x = B1 | rb << 19, y = B2' << 3 | wave (B1, B2' < 2^19: fast variant
+//     dots are < 2^19, clamp-variant values <= 2^18);
+//  2. rows: merge the segments' row keys, ratio / distance tests; with the
+//     cross-check a row i with best column j stays a CANDIDATE only if
+//     B1(j) equals its best value, the 64-row group holding B1 is the one
+//     of row i (otherwise another row ties B1: the column's second equals its
+//     best and fails), and column j passes with second >= B2';
+//  3. candidates, per 64-row group (one wave, one lane per row, the group's
+//     descriptors register-resident): the 64 exact dots of column j
+//     (v_dot4 on the offset operands, the same integers as the MFMA path),
+//     their top-2 (multiset), and the final column test with second =
+//     max(B2', second within the group);
+//  4. ordered compaction of the accepted rows (idx1 ascending).
+// The per-row decisions live in rowres segment 0 between the phases.
+
+__global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
+    const PairDesc* __restrict__ pairs, uint2* __restrict__ rowres, uint2* __restrict__ colpart,
+    const uint8_t* __restrict__ desc8, const int32_t* __restrict__ csum,
+    const float* __restrict__ lut, float max_ratio, float max_distance, int cross_check,
+    uint2* __restrict__ matches, int32_t* __restrict__ counts, int phase) {
+  __shared__ int32_t wave_tot[kFinThreads / 64];
+  __shared__ int32_t wave_off[kFinThreads / 64];
+  const PairDesc pd = pairs[blockIdx.x];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  if (pd.n1 == 0 || pd.n2 == 0) {
+    if (tid == 0) counts[blockIdx.x] = 0;
+    return;
+  }
+  uint2* cp = colpart + pd.colpart_off;
+  uint2* rr = rowres + pd.rowres_off;
+  constexpr uint32_t kV = (1u << 19) - 1u;
+  const int per = (pd.n1 + kFinThreads - 1) / kFinThreads;
+  const int i0 = min(pd.n1, tid * per), i1 = min(pd.n1, i0 + per);
+  if (phase == 0) {
+  if (cross_check) {
+    for (int j = tid; j < pd.n2; j += kFinThreads) {
+      const uint2 m = cp[j];
+      uint32_t b1 = m.x, b2 = m.y >> 3, w = m.y & 7u, rbest = 0u;
+      int b = 1;
+      for (; b + 8 <= pd.nrb; b += 8) {  // eight row blocks' loads in flight
+        uint2 o[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) o[u] = cp[(int64_t)(b + u) * pd.n2pad + j];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const bool gt = o[u].x > b1;
+          b2 = gt ? max(o[u].y >> 3, b1) : max(b2, o[u].x);
+          w = gt ? (o[u].y & 7u) : w;
+          rbest = gt ? (uint32_t)(b + u) : rbest;
+          b1 = gt ? o[u].x : b1;
+        }
+      }
+      for (; b < pd.nrb; ++b) {
+        const uint2 o = cp[(int64_t)b * pd.n2pad + j];
+        const bool gt = o.x > b1;
+        b2 = gt ? max(o.y >> 3, b1) : max(b2, o.x);
+        w = gt ? (o.y & 7u) : w;
+        rbest = gt ? (uint32_t)b : rbest;
+        b1 = gt ? o.x : b1;
+      }
+      // raw accumulator units (dot - cb_j + 2^22) -> dot values of the column
+      const uint32_t cbm = (uint32_t)csum[pd.b_row + j] - (1u << 22);
+      b1 += cbm;
+      b2 += cbm;
+      if (pd.clamp) {
+        b1 = min(b1, kLutMax);
+        b2 = min(b2, kLutMax);
+      }
+      cp[j] = make_uint2(b1 | (rbest << 19), (b2 << 3) | w);
+    }
+    __syncthreads();
+  }
+  // Phase 2: per-row decisions, contiguous chunk per thread (phase 4 order).
+  for (int i = i0; i < i1; ++i) {
+    uint2 m = rr[i];
+    int best_seg = 0;
+    for (int sg = 1; sg < pd.nseg; ++sg) {
+      const uint2 o = rr[(int64_t)sg * pd.n1 + i];
+      m.y = merge_second(m.x, m.y, o.x, o.y);
+      if (o.x > m.x) { m.x = o.x; best_seg = sg; }
+    }
+    const uint32_t best = m.x >> kIdxBits, second = m.y >> kIdxBits;
+    const int32_t col = best_seg * (kTilesPerSeg * 32) + (int32_t)(kIdxMask - (m.x & kIdxMask));
+    uint32_t state = passes(lut, best, second, max_ratio, max_distance) ? 1u : 0u;
+    if (state && cross_check) {
+      const uint2 c = cp[col];
+      const uint32_t b1 = c.x & kV, rb = c.x >> 19, w = c.y & 7u, b2 = c.y >> 3;
+      const uint32_t grp = rb * (uint32_t)(kRowsPerBlock8 / 64) + w;
+      if (b1 != best || grp != (uint32_t)(i >> 6) || !passes(lut, b1, b2, max_ratio, max_distance))
+        state = 0u;
+      else
+        state = 2u;  // decided by the exact second within the group (phase 3)
+    }
+    rr[i] = make_uint2((uint32_t)col, state);
+  }
+  return;
+  }
+  // Phase 4: ordered compaction.
+  int cnt = 0;
+  for (int i = i0; i < i1; ++i) cnt += rr[i].y == 1u;
+  int x = cnt;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const int y = __shfl_up(x, d);
+    if (lane >= d) x += y;
+  }
+  if (lane == 63) wave_tot[wave] = x;
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int w = 0; w < kFinThreads / 64; ++w) { wave_off[w] = acc; acc += wave_tot[w]; }
+    counts[blockIdx.x] = acc;
+  }
+  __syncthreads();
+  int out = wave_off[wave] + x - cnt;
+  for (int i = i0; i < i1; ++i) {
+    const uint2 st = rr[i];
+    if (st.y == 1u) matches[pd.match_off + out++] = make_uint2((uint32_t)i, st.x);
+  }
+}
+
+// Phase 3 of the version-2 finalize: one wave per 64-row group of a pair
+// (grid: x = groups of 4, y = pair).  The group's 64 rows are the A operand
+// of the matcher's own MFMA (i8 32x32x32, the same offset operands and
+// fragment layout), up to 32 candidate columns per pass the B operand; each
+// lane's 16-row top-2 tree, the row sub-tiles and the lane halves give every
+// candidate column the exact top-2 of the group's 64 dots.  With it, the
+// column's second is max(B2', second within the group) and the cross-check
+// decision of the candidate row is final.
+__global__ __launch_bounds__(256) void match_recheck_g8_kernel(
+    const PairDesc* __restrict__ pairs, uint2* __restrict__ rowres, uint2* __restrict__ colpart,
+    const uint8_t* __restrict__ desc8, const int32_t* __restrict__ csum,
+    const float* __restrict__ lut, float max_ratio, float max_distance) {
+  __shared__ int32_t cand_lane[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = lane & 31, h = lane >> 5;
+  const PairDesc pd = pairs[blockIdx.y];
+  const int grp = blockIdx.x * 4 + wave;
+  if (pd.n1 == 0 || pd.n2 == 0 || grp * 64 >= pd.n1) return;
+  uint2* cp = colpart + pd.colpart_off;
+  uint2* rr = rowres + pd.rowres_off;
+  constexpr uint32_t kV = (1u << 19) - 1u;
+  const int row = grp * 64 + lane;
+  const uint2 st = row < pd.n1 ? rr[row] : make_uint2(0u, 0u);
+  const uint64_t cand = __ballot(st.y == 2u);
+  if (!cand) return;
+  // Candidate k of the group (ascending lane) -> its lane.
+  const int k = __builtin_amdgcn_mbcnt_hi((uint32_t)(cand >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)cand, 0u));
+  if (st.y == 2u) cand_lane[wave][k] = lane;
+  const int ncand = __popcll(cand);
+  // A fragments: rows grp*64 + 32 s + r, chunks 4h + q; accumulator offsets
+  // cs(a) of the rows this lane's results belong to (zero rows past n1).
+  const int row0 = grp * 64;
+  i32x4 afrag[2][4];
+  i32x16 ra[2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int rw = row0 + 32 * s + r;
+    const bool ok = rw < pd.n1;
+    const i32x4* src =
+        reinterpret_cast<const i32x4*>(desc8 + (pd.a_row + (ok ? rw : 0)) * 128) + h * 4;
+    const int z = (int)0x80808080u;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) afrag[s][q] = ok ? src[q] : i32x4{z, z, z, z};
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int ri = row0 + 32 * s + 4 * h + (i & 3) + 8 * (i >> 2);
+      const uint32_t cs = (uint32_t)csum[pd.a_row + min(ri, pd.n1 - 1)];
+      ra[s][i] = (int)(ri < pd.n1 ? cs : 0u);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  for (int base = 0; base < ncand; base += 32) {
+    const int c = base + r;  // this lane's candidate column slot
+    const bool valid = c < ncand;
+    const int L = valid ? cand_lane[wave][c] : 0;
+    const int jc = __shfl((int)st.x, L);
+    const int jv = valid ? jc : 0;
+    i32x4 bfr[4];
+    const i32x4* bsrc = reinterpret_cast<const i32x4*>(desc8 + (pd.b_row + jv) * 128) + h * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bfr[q] = bsrc[q];
+    const uint32_t cbj = (uint32_t)csum[pd.b_row + jv];
+    const uint2 cpc = cp[jv];
+    const i32x16 acc0 = chain8(afrag[0], bfr, ra[0]);
+    const i32x16 acc1 = chain8(afrag[1], bfr, ra[1]);
+    const uint2 p0 = column_top2_values(acc0), p1 = column_top2_values(acc1);
+    const uint32_t t1 = max(p0.x, p1.x);
+    uint32_t t2 = merge_second_values(p0.x, p0.y, p1.x, p1.y);
+    const auto s1 = __builtin_amdgcn_permlane32_swap(t1, t1, false, false);
+    const auto s2 = __builtin_amdgcn_permlane32_swap(t2, t2, false, false);
+    // lanes of half 0: the partner's (half 1's) values are the second results
+    t2 = merge_second_values(t1, t2, (uint32_t)s1[1], (uint32_t)s2[1]);
+    if (h == 0 && valid) {
+      uint32_t d2 = t2 + cbj - (1u << 21);  // a'.b' + 128(Sa + Sb) - 2^21
+      if (pd.clamp) d2 = min(d2, kLutMax);
+      const uint32_t b1 = cpc.x & kV, b2 = max(cpc.y >> 3, d2);
+      rr[row0 + L] =
+          make_uint2((uint32_t)jc, passes(lut, b1, b2, max_ratio, max_distance) ? 1u : 0u);
+    }
+  }
+}
+
 // ===========================================================================
 // Table conversion at load.
 // ===========================================================================
@@ -825,6 +1392,38 @@ hipError_t launch_match_tiles_i8(const uint8_t* desc8, const int32_t* csum, cons
   else
     hipLaunchKernelGGL(match_tiles_i8_kernel<false>, dim3(njobs), dim3(kMatch8Threads), 0, stream,
                        desc8, csum, jobs, pairs, rowres, colpart);
+  return hipGetLastError();
+}
+
+hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
+                           int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
+                           bool clamp, hipStream_t stream) {
+  if (njobs <= 0) return hipSuccess;
+  if (clamp)
+    hipLaunchKernelGGL(match_g8_kernel<true>, dim3(njobs), dim3(kMatch8Threads), 0, stream, desc8,
+                       csum, jobs, pairs, rowres, colpart);
+  else
+    hipLaunchKernelGGL(match_g8_kernel<false>, dim3(njobs), dim3(kMatch8Threads), 0, stream, desc8,
+                       csum, jobs, pairs, rowres, colpart);
+  return hipGetLastError();
+}
+
+hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* rowres,
+                                    uint2* colpart, const uint8_t* desc8, const int32_t* csum,
+                                    const float* lut, float max_ratio, float max_distance,
+                                    int cross_check, uint2* matches, int32_t* counts,
+                                    int max_groups, hipStream_t stream) {
+  if (npairs <= 0) return hipSuccess;
+  hipLaunchKernelGGL(match_finalize_g8_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
+                     rowres, colpart, desc8, csum, lut, max_ratio, max_distance, cross_check,
+                     matches, counts, 0);
+  if (cross_check && max_groups > 0)
+    hipLaunchKernelGGL(match_recheck_g8_kernel, dim3((unsigned)((max_groups + 3) / 4), npairs),
+                       dim3(256), 0, stream, pairs, rowres, colpart, desc8, csum, lut, max_ratio,
+                       max_distance);
+  hipLaunchKernelGGL(match_finalize_g8_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
+                     rowres, colpart, desc8, csum, lut, max_ratio, max_distance, cross_check,
+                     matches, counts, 1);
   return hipGetLastError();
 }
 

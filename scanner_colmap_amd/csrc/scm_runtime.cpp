@@ -154,6 +154,8 @@ struct scm_context {
   int64_t batch_pairs = kDefaultPairsPerBatch;  // SCM_BATCH_PAIRS overrides
   int64_t batch_bytes = 0;  // HBM budget of one batch set (SCM_BATCH_BYTES; 0 = from free HBM)
   bool match_bf16 = false;  // SCM_MATCH_BF16=1: bf16 MFMA matcher instead of i8
+  bool match_i8v1 = false;  // SCM_MATCH_I8V1=1: the first i8 matcher (register staging,
+                            // top-2 column partials) instead of match_g8_kernel
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
   int64_t n_match_launches = 0;  // matcher kernel launches of the last table run
@@ -393,6 +395,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
       pd.nseg = (pd.n2 + kColsPerSeg - 1) / kColsPerSeg;
       pd.nrb = (pd.n1 + rpb - 1) / rpb;
       pd.b_row = given ? 0 : t.desc_row[b];
+      pd.a_row = given ? 0 : t.desc_row[a];
       pd.rowres_off = rr;
       pd.colpart_off = cp;
       pd.m21_off = m21;
@@ -408,6 +411,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
         if (prod >= ((unsigned __int128)1 << 38)) clamp = true;
       }
     }
+    for (int64_t k = i; k < j; ++k) pds[k].clamp = clamp ? 1 : 0;
     if (!given && t.ndesc[a] > 0) {
       // Jobs over runs of consecutive active pairs of this pivot.
       const int32_t n1 = t.ndesc[a];
@@ -465,6 +469,9 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   if (NJ) std::memcpy(st, jobs.data(), NJ * sizeof(MatchJob));
   std::memcpy(st + s_pairs, pds.data(), P * sizeof(PairDesc));
   std::memcpy(st + s_mo, bs.moff.data(), P * sizeof(int64_t));
+  // 64-row groups of the largest pivot (grid of match_recheck_g8_kernel)
+  int max_groups = 0;
+  for (int64_t k = 0; k < P; ++k) max_groups = std::max(max_groups, (pds[k].n1 + 63) / 64);
   hipStream_t sm = ctx->stream;
   if (NJ)
     SCM_HIP(hipMemcpyAsync(bs.jobs.ptr, st, NJ * sizeof(MatchJob), hipMemcpyHostToDevice, sm));
@@ -491,13 +498,24 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
       if (ctx->match_bf16)
         SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), jb, nj, bs.pairs.as<PairDesc>(),
                                    bs.rowres.as<uint2>(), bs.colpart.as<uint2>(), clamp, sm));
+      else if (!ctx->match_i8v1)
+        SCM_HIP(launch_match_g8(t.desc8.as<uint8_t>(), t.csum.as<int32_t>(), jb, nj,
+                                bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
+                                bs.colpart.as<uint2>(), clamp, sm));
       else
         SCM_HIP(launch_match_tiles_i8(t.desc8.as<uint8_t>(), t.csum.as<int32_t>(), jb, nj,
                                       bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
                                       bs.colpart.as<uint2>(), clamp, sm));
     }
   SCM_HIP(hipEventRecord(bs.ev[1], sm));
-  if (!given)
+  if (!given && !ctx->match_bf16 && !ctx->match_i8v1)
+    SCM_HIP(launch_match_finalize_g8(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
+                                     bs.colpart.as<uint2>(), t.desc8.as<uint8_t>(),
+                                     t.csum.as<int32_t>(), ctx->lut.as<float>(),
+                                     (float)ctx->opts.max_ratio, (float)ctx->opts.max_distance,
+                                     ctx->opts.cross_check, bs.matches.as<uint2>(),
+                                     bs.counts.as<int32_t>(), max_groups, sm));
+  else if (!given)
     SCM_HIP(launch_match_finalize(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
                                   bs.colpart.as<uint2>(), bs.m21.as<int32_t>(),
                                   ctx->lut.as<float>(), (float)ctx->opts.max_ratio,
@@ -1044,6 +1062,7 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
     ctx->batch_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
   if (const char* e = std::getenv("SCM_BATCH_BYTES")) ctx->batch_bytes = std::max<int64_t>(1, std::atoll(e));
   if (const char* e = std::getenv("SCM_MATCH_BF16")) ctx->match_bf16 = e[0] == '1';
+  if (const char* e = std::getenv("SCM_MATCH_I8V1")) ctx->match_i8v1 = e[0] == '1';
   // The i8 matcher tracks column top-2 by value only, which decides the
   // cross-check exactly when a tied column best fails the ratio test, i.e.
   // max_ratio <= 1 (match_kernels.hip, i8 section); otherwise the bf16 matcher
