@@ -59,6 +59,11 @@ def parse():
     p.add_argument("--gen-workers", type=int, default=16)
     p.add_argument("--cpu-baseline-pairs", type=int, default=64)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--stencil-rows", type=int, default=128,
+                   help="rows of the Scanner drop-in path (scm_execute_batch) timed after the "
+                        "table run, rank 0 at N = 1 (0 = skip)")
+    p.add_argument("--stencil-batches", default="1,64",
+                   help="Scanner batch sizes (stencils per execute() call) to time")
     return p.parse_args()
 
 
@@ -158,6 +163,41 @@ def parity_check(ctx, packed, row_lo: int, oracle_out: dict, pairs: list) -> dic
             "source": "GPU outputs of the last timed step (raw matches kept for these rows)"}
 
 
+def stencil_bench(ctx, src, overlap: int, rows: int, batches: list) -> dict:
+    """The Scanner drop-in path (scm_execute_batch, what the op's execute()
+    calls; sequential_matching.cc:103-185): output rows 0..rows-1 of the same
+    table in consecutive calls of `b` stencils each, inputs as host io.cc
+    elements (so every new image crosses PCIe inside the timed region), the
+    HBM image cache carried across calls.  One untimed call warms it up."""
+    ids, kps, descs = src
+    n = len(ids)
+    rows = min(rows, n)
+
+    def stencils(r0, r1):
+        out = []
+        for r in range(r0, r1):
+            sel = [min(r + s, n - 1) for s in range(overlap)]
+            out.append(([ids[i] for i in sel], [kps[i] for i in sel], [descs[i] for i in sel]))
+        return out
+
+    res = {"rows": rows, "stencil": overlap, "inputs": "host io.cc elements (PCIe inside the timed region)"}
+    for b in batches:
+        calls = [stencils(r0, min(rows, r0 + b)) for r0 in range(0, rows, b)]
+        ctx.execute_batch(calls[0])  # warm-up (buffers, cache)
+        r0_, u0_ = ctx.stencil_stats()
+        t0 = time.perf_counter()
+        npairs = 0
+        for c in calls:
+            a, _ = ctx.execute_batch(c)
+            npairs += sum(int(np.frombuffer(x[:8], np.uint64)[0]) for x in a)
+        dt = time.perf_counter() - t0
+        r1_, u1_ = ctx.stencil_stats()
+        res[f"batch{b}"] = {"pairs_per_s": round(npairs / dt, 1), "ms_per_call": round(dt / len(calls) * 1e3, 2),
+                            "calls": len(calls), "pairs": npairs,
+                            "images_uploaded": u1_ - u0_, "images_reused": r1_ - r0_}
+    return res
+
+
 def cpu_model() -> str:
     try:
         for line in open("/proc/cpuinfo"):
@@ -194,17 +234,14 @@ def main():
     wl = dict(WORKLOADS[args.workload])
     kpts = args.kpts or wl["kpts"]
     overlap = wl["overlap"]
-    if args.scaling == "strong":  # the workload's images in total, split over the ranks
-        total_images = args.images or wl["images"]
-    else:                         # every rank owns the workload's images
-        total_images = (args.images or wl["images"]) * world
-
     from scanner_colmap_amd import distributed as sd
     from scanner_colmap_amd.codecs import table_rows
     from scanner_colmap_amd.synthetic import Corridor
 
-    row_b, row_e = sd.shard_rows(total_images, overlap, world, rank)
-    tab_b, tab_e = sd.table_range(row_b, row_e, total_images, overlap)
+    plan = sd.ShardPlan(args.images or wl["images"], overlap, world, rank, args.scaling)
+    total_images = plan.total_images
+    row_b, row_e = plan.row_begin, plan.row_end
+    tab_b, tab_e = plan.table_begin, plan.table_end
     # Scene overlap = the stencil's (K = 50 and exhaustive runs included): every pair of a
     # stencil shares scene points, so every pair is matched and verified.
     corridor = Corridor(total_images, kpts, min(overlap, total_images), seed=wl["seed"])
@@ -237,8 +274,10 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     table_load_ms = (time.perf_counter() - t_load) * 1e3
+    srows = args.stencil_rows if world == 1 else 0
+    stencil_src = (ids[:srows + overlap], kps[:srows + overlap], descs[:srows + overlap]) if srows else None
     del ids, kps, descs
-    lr_b, lr_e = row_b - tab_b, row_e - tab_b
+    lr_b, lr_e = plan.local_rows
 
     # Pair count and algorithmic work of this rank's shard.
     npairs = 0
@@ -254,9 +293,7 @@ def main():
     last = {}
 
     def step():
-        packed = ctx.table_run_packed(overlap, lr_b, lr_e)
-        if world > 1:
-            sd.gather_to_root(sd.pack_packed(packed.offsets, packed.data), device=device)
+        packed, _ = plan.step(ctx, device=device)
         last["packed"] = packed
         return ctx.table_timings()
 
@@ -303,10 +340,12 @@ def main():
         launches = max(1, launches)  # matcher launches the library reported
         avg_n = float(np.mean(n_per_img)) if n_per_img else 0.0
         bf16 = os.environ.get("SCM_MATCH_BF16", "0") == "1"  # else the default i8 matcher
-        kernel = "match_tiles_kernel" if bf16 else "match_tiles_i8_kernel"
+        kernel = ("match_tiles_kernel" if bf16 else
+                  "match_tiles_i8_kernel" if os.environ.get("SCM_MATCH_I8V1", "0") == "1"
+                  else "match_g8_kernel")
         peak = BF16_DENSE_PEAK_TFLOPS if bf16 else I8_DENSE_PEAK_TOPS
         # descriptors of both images, bf16 (2 B) or offset i8 (1 B) per element
-        alg_bytes_launch = npairs / launches * 2 * avg_n * 128 * (2 if bf16 else 1)
+        alg_bytes_launch = npairs * steps / launches * 2 * avg_n * 128 * (2 if bf16 else 1)
         pmc = (pmc_traffic(args.workload, kpts, total_images, kernel)
                if world == 1 and not args.images else None)
         cpu = parity = None
@@ -321,6 +360,8 @@ def main():
             else:
                 cpu, ref = cpu_baseline(sample_imgs, check_pairs)
             parity = parity_check(ctx, last["packed"], lr_b, ref, check_pairs)
+        drop_in = stencil_bench(ctx, stencil_src, overlap, srows,
+                                [int(x) for x in args.stencil_batches.split(",") if x]) if srows else None
         # SURVEY.md §8d headline fraction: kernel-1 work over the whole step's wall time.
         wall_tops = flops_rank / elapsed / 1e12
         out = {
@@ -368,6 +409,7 @@ def main():
                                   "verify": round(verify_ms / steps, 3)},
             "cpu_baseline": cpu,
             "parity": parity,
+            "drop_in": drop_in,
             "table_load_ms": round(table_load_ms, 1),
             "pcie_inclusive_pairs_per_s": round(total_pairs / (elapsed / steps + table_load_ms * 1e-3), 2),
             "gen_s": round(gen_s, 1),

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SCM_ABI_VERSION 2
+#define SCM_ABI_VERSION 3
 
 enum {
   SCM_OK = 0,
@@ -158,6 +158,25 @@ int scm_execute_stencil(scm_context* ctx, int64_t stencil_size,
                         const scm_element* keypoints,
                         const scm_element* descriptors,
                         scm_blob* pair_image_ids_out, scm_blob* tvgs_out);
+
+/* The same for a Scanner batch of `batch` stencils (a `.batch()` kernel's
+ * StenciledBatchedElements, sequential_matching.cc:189-191 registers the
+ * kernel with .batch()): element (b, s) of each column at index
+ * b * stencil_size + s; writes `batch` output elements to each of
+ * pair_image_ids_out[] / tvgs_out[] (caller arrays).  Every output row is
+ * byte-identical to scm_execute_stencil on that stencil alone.  The
+ * reference's execute() reads only batch element 0 (:106-108) and emits one
+ * row; this entry point handles every element.  Images stay resident in HBM
+ * from one call to the next (keyed by image id; an id whose feature counts
+ * changed is uploaded again), so consecutive stencils upload only their new
+ * images, and all pairs of the call run through the pipelined batch path. */
+int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
+                      const scm_element* image_ids,
+                      const scm_element* keypoints,
+                      const scm_element* descriptors,
+                      scm_blob* pair_image_ids_out, scm_blob* tvgs_out);
+/* Images the execute() cache reused / uploaded so far (cumulative). */
+int scm_stencil_stats(scm_context* ctx, int64_t* reused, int64_t* uploaded);
 
 /* ---- table granularity (HBM-resident batch path) ---------------------- */
 /* Decode and upload num_rows rows of the `extraction` table (columns

@@ -3,7 +3,8 @@ SequentialMatchingCPU Scanner op of garyjyzhang/scanner-colmap).
 
 Public surface:
   * ``Context`` / ``MatchingOptions`` — the C ABI (include/scm.h) over ctypes;
-  * ``SequentialMatchingGPU`` — the Scanner op/kernel mirror (op.py);
+  * ``scanner_op/`` — the Scanner op/kernel shim over the C ABI (C++);
+  * ``feature_matching`` — the job-script mirror of feature_matching.py;
   * ``codecs`` — the io.cc element formats;
   * ``synthetic`` — deterministic synthetic `extraction` tables.
 """

@@ -31,7 +31,8 @@ EXPORTS = (
     "scm_abi_version", "scm_last_error", "scm_default_options",
     "scm_parse_args", "scm_pair_seed", "scm_blob_free",
     "scm_context_create", "scm_context_destroy", "scm_match_pair",
-    "scm_verify_pair", "scm_execute_stencil", "scm_table_load",
+    "scm_verify_pair", "scm_execute_stencil", "scm_execute_batch", "scm_stencil_stats",
+    "scm_table_load",
     "scm_table_run", "scm_table_run_packed", "scm_set_keep_matches",
     "scm_set_keep_matches_range",
     "scm_table_matches", "scm_table_timings",
@@ -100,6 +101,10 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.scm_execute_stencil.argtypes = [c_void_p, c_int64, POINTER(Element),
                                         POINTER(Element), POINTER(Element),
                                         POINTER(Blob), POINTER(Blob)]
+    lib.scm_execute_batch.argtypes = [c_void_p, c_int64, c_int64, POINTER(Element),
+                                      POINTER(Element), POINTER(Element),
+                                      POINTER(Blob), POINTER(Blob)]
+    lib.scm_stencil_stats.argtypes = [c_void_p, POINTER(c_int64), POINTER(c_int64)]
     lib.scm_table_load.argtypes = [c_void_p, c_int64, POINTER(Element),
                                    POINTER(Element), POINTER(Element)]
     lib.scm_table_run.argtypes = [c_void_p, c_int64, c_int64, c_int64,
@@ -256,6 +261,30 @@ class Context:
         _check(self._lib.scm_execute_stencil(self._ptr, len(ids), e_ids, e_kps, e_desc,
                                              byref(a), byref(b)))
         return _blob_bytes(a), _blob_bytes(b)
+
+    def execute_batch(self, stencils) -> tuple[list[bytes], list[bytes]]:
+        """scm_execute_batch over a list of stencils, each (ids, kps, descs)
+        lists of equal length K: one (pair_image_ids, tvgs) element per
+        stencil."""
+        B = len(stencils)
+        if B == 0:
+            return [], []
+        K = len(stencils[0][0])
+        if any(len(st[0]) != K or len(st[1]) != K or len(st[2]) != K for st in stencils):
+            raise ValueError("every stencil of a batch has the same size")
+        e_ids, k1 = _elements([x for st in stencils for x in st[0]])
+        e_kps, k2 = _elements([x for st in stencils for x in st[1]])
+        e_desc, k3 = _elements([x for st in stencils for x in st[2]])
+        a = (Blob * B)()
+        b = (Blob * B)()
+        _check(self._lib.scm_execute_batch(self._ptr, B, K, e_ids, e_kps, e_desc, a, b))
+        return [_blob_bytes(a[i]) for i in range(B)], [_blob_bytes(b[i]) for i in range(B)]
+
+    def stencil_stats(self) -> tuple[int, int]:
+        """(images reused from HBM, images uploaded) by execute calls so far."""
+        r, u = c_int64(), c_int64()
+        _check(self._lib.scm_stencil_stats(self._ptr, byref(r), byref(u)))
+        return r.value, u.value
 
     # --- table granularity ------------------------------------------------
     def table_load(self, ids, kps, descs) -> None:

@@ -25,6 +25,7 @@
 #include <cstdlib>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "geom_solvers.h"
@@ -148,6 +149,13 @@ struct scm_context {
   DevBuf lut;
   ImageTable table, scratch_table;
   bool table_loaded = false;
+  // execute() image cache: the images of the previous call stay in HBM
+  // (call_tab[call_cur], id -> table index in call_map); the next call's
+  // table reuses them by device-to-device copy and uploads only new images.
+  ImageTable call_tab[2];
+  std::unordered_map<uint32_t, int32_t> call_map[2];
+  int call_cur = -1;
+  int64_t call_reused = 0, call_uploaded = 0;  // images, cumulative (scm_stencil_stats)
   BatchSet sets[3];
   HostBuf h_stage;  // table upload staging
   int threads = 1;
@@ -278,6 +286,160 @@ int upload_table(scm_context* ctx, ImageTable* t, const std::vector<RowView>& ro
     SCM_HIP(hipMemcpyAsync(t->kpxy.ptr, h, bytes, hipMemcpyHostToDevice, ctx->stream));
     SCM_HIP(hipStreamSynchronize(ctx->stream));
   }
+  return SCM_OK;
+}
+
+// Table of one execute() call over the call's unique images `rows`:
+// images already resident in the previous call's table (same id and feature
+// counts) are copied device-to-device, the rest are staged, uploaded and
+// converted in one tail range.  Layout: reused images first (in their old
+// order, so consecutive ones coalesce into single copies), then new ones.
+// (*idx)[i] = table index of rows[i].
+int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows, std::vector<int32_t>* idx) {
+  const int nxt = ctx->call_cur < 0 ? 0 : 1 - ctx->call_cur;
+  const ImageTable* old = ctx->call_cur < 0 ? nullptr : &ctx->call_tab[ctx->call_cur];
+  const std::unordered_map<uint32_t, int32_t>* omap =
+      ctx->call_cur < 0 ? nullptr : &ctx->call_map[ctx->call_cur];
+  ImageTable* t = &ctx->call_tab[nxt];
+  std::unordered_map<uint32_t, int32_t>& nmap = ctx->call_map[nxt];
+  nmap.clear();
+  const int64_t n = (int64_t)rows.size();
+  std::vector<int32_t> from(n, -1);  // old table index, or -1 (upload)
+  std::vector<int64_t> reuse, fresh;
+  for (int64_t i = 0; i < n; ++i) {
+    const RowView& r = rows[i];
+    if (r.ndesc > INT32_MAX || r.nkp > INT32_MAX) {
+      set_error("image has too many features");
+      return SCM_E_INVALID;
+    }
+    if (omap) {
+      auto it = omap->find(r.id);
+      if (it != omap->end() && old->nkp[it->second] == r.nkp && old->ndesc[it->second] == r.ndesc)
+        from[i] = it->second;
+    }
+    (from[i] >= 0 ? reuse : fresh).push_back(i);
+  }
+  std::stable_sort(reuse.begin(), reuse.end(),
+                   [&](int64_t a, int64_t b) { return from[a] < from[b]; });
+  std::vector<int64_t> order = reuse;
+  order.insert(order.end(), fresh.begin(), fresh.end());
+  t->n = n;
+  t->ids.resize(n);
+  t->nkp.resize(n);
+  t->ndesc.resize(n);
+  t->desc_row.resize(n);
+  t->kp_off.resize(n);
+  t->max_norm2.assign(n, 0);
+  idx->assign(n, 0);
+  int64_t total_rows = 0, total_kp = 0, tail_row = 0, tail_kp = 0;
+  for (int64_t k = 0; k < n; ++k) {
+    const int64_t i = order[k];
+    const RowView& r = rows[i];
+    if (k == (int64_t)reuse.size()) {
+      tail_row = total_rows;
+      tail_kp = total_kp;
+    }
+    (*idx)[i] = (int32_t)k;
+    nmap[r.id] = (int32_t)k;
+    t->ids[k] = r.id;
+    t->nkp[k] = (int32_t)r.nkp;
+    t->ndesc[k] = (int32_t)r.ndesc;
+    t->desc_row[k] = total_rows;
+    t->kp_off[k] = total_kp;
+    if (from[i] >= 0) t->max_norm2[k] = old->max_norm2[from[i]];
+    total_rows += (r.ndesc + kDescRowAlign - 1) / kDescRowAlign * kDescRowAlign;
+    total_kp += r.nkp;
+  }
+  if (fresh.empty()) {
+    tail_row = total_rows;
+    tail_kp = total_kp;
+  }
+  t->total_rows = total_rows;
+  t->total_kp = total_kp;
+  const bool bf = ctx->match_bf16;
+  if (total_rows > 0) {
+    if (bf) SCM_TRY(t->desc.ensure((size_t)total_rows * 256));
+    else {
+      SCM_TRY(t->desc8.ensure((size_t)total_rows * 128));
+      SCM_TRY(t->csum.ensure((size_t)total_rows * sizeof(int32_t)));
+    }
+  }
+  if (total_kp > 0) SCM_TRY(t->kpxy.ensure((size_t)total_kp * sizeof(float2)));
+  hipStream_t st = ctx->stream;
+  // Reused images: coalesced device-to-device copies.
+  for (size_t k = 0; k < reuse.size();) {
+    size_t e = k + 1;
+    while (e < reuse.size() && from[reuse[e]] == from[reuse[e - 1]] + 1) ++e;
+    const int32_t o0 = from[reuse[k]], o1 = from[reuse[e - 1]];
+    const int64_t orow = old->desc_row[o0];
+    const int64_t nrow = old->desc_row[o1] - orow +
+                         (old->ndesc[o1] + kDescRowAlign - 1) / kDescRowAlign * kDescRowAlign;
+    const int64_t drow = t->desc_row[(size_t)k];
+    if (nrow > 0) {
+      if (bf)
+        SCM_HIP(hipMemcpyAsync(t->desc.as<uint8_t>() + drow * 256, old->desc.as<uint8_t>() + orow * 256,
+                               (size_t)nrow * 256, hipMemcpyDeviceToDevice, st));
+      else {
+        SCM_HIP(hipMemcpyAsync(t->desc8.as<uint8_t>() + drow * 128,
+                               old->desc8.as<uint8_t>() + orow * 128, (size_t)nrow * 128,
+                               hipMemcpyDeviceToDevice, st));
+        SCM_HIP(hipMemcpyAsync(t->csum.as<int32_t>() + drow, old->csum.as<int32_t>() + orow,
+                               (size_t)nrow * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+      }
+    }
+    const int64_t okp = old->kp_off[o0], nkp = old->kp_off[o1] + old->nkp[o1] - okp;
+    if (nkp > 0)
+      SCM_HIP(hipMemcpyAsync(t->kpxy.as<float2>() + t->kp_off[(size_t)k], old->kpxy.as<float2>() + okp,
+                             (size_t)nkp * sizeof(float2), hipMemcpyDeviceToDevice, st));
+    k = e;
+  }
+  // New images: one staged upload of the tail range (descriptors, then
+  // keypoint xy), converted on the GPU like scm_table_load.
+  const int64_t frows = total_rows - tail_row, fkp = total_kp - tail_kp;
+  if (frows > 0 || fkp > 0) {
+    const size_t dbytes = (size_t)frows * 128, kbytes = (size_t)fkp * sizeof(float2);
+    const size_t koff = (dbytes + 255) / 256 * 256;
+    SCM_TRY(ctx->h_stage.ensure(koff + kbytes));
+    uint8_t* h = ctx->h_stage.as<uint8_t>();
+    float2* hk = reinterpret_cast<float2*>(h + koff);
+    const size_t nfresh = fresh.size(), k0 = reuse.size();
+    parallel_for(ctx->threads, (int64_t)nfresh, [&](int64_t f) {
+      const int64_t k = (int64_t)(k0 + f);
+      const RowView& r = rows[order[k]];
+      uint8_t* dst = h + (size_t)(t->desc_row[k] - tail_row) * 128;
+      const size_t nb = (size_t)r.ndesc * 128;
+      if (nb) std::memcpy(dst, r.desc, nb);
+      const size_t padded =
+          (size_t)((r.ndesc + kDescRowAlign - 1) / kDescRowAlign * kDescRowAlign) * 128;
+      std::memset(dst + nb, 0, padded - nb);
+      uint64_t mx = 0;
+      for (int64_t q = 0; q < r.ndesc; ++q) {
+        const uint8_t* d = r.desc + q * 128;
+        uint32_t sq = 0;
+        for (int j = 0; j < 128; ++j) sq += (uint32_t)d[j] * d[j];
+        mx = std::max<uint64_t>(mx, sq);
+      }
+      t->max_norm2[k] = mx;
+      float2* kd = hk + (t->kp_off[k] - tail_kp);
+      for (int64_t q = 0; q < r.nkp; ++q) kd[q] = make_float2(r.kp[6 * q], r.kp[6 * q + 1]);
+    });
+    SCM_TRY(t->u8.ensure(koff + kbytes));
+    SCM_HIP(hipMemcpyAsync(t->u8.ptr, h, koff + kbytes, hipMemcpyHostToDevice, st));
+    if (frows > 0) {
+      if (bf)
+        SCM_HIP(launch_u8_to_bf16(t->u8.as<uint8_t>(), t->desc.as<uint16_t>() + tail_row * 128,
+                                  (int64_t)dbytes, st));
+      else
+        SCM_HIP(launch_u8_to_i8(t->u8.as<uint8_t>(), t->desc8.as<uint8_t>() + tail_row * 128,
+                                t->csum.as<int32_t>() + tail_row, frows, st));
+    }
+    if (fkp > 0)
+      SCM_HIP(hipMemcpyAsync(t->kpxy.as<float2>() + tail_kp, t->u8.as<uint8_t>() + koff, kbytes,
+                             hipMemcpyDeviceToDevice, st));
+  }
+  ctx->call_reused += (int64_t)reuse.size();
+  ctx->call_uploaded += (int64_t)fresh.size();
+  ctx->call_cur = nxt;  // the matching stream orders these copies before the call's kernels
   return SCM_OK;
 }
 
@@ -895,34 +1057,59 @@ int64_t set_budget_bytes(scm_context* ctx) {
   return std::max<int64_t>(avail / 3, (int64_t)64 << 20);
 }
 
+// One output row of a run: the pivot's table index and the table indices /
+// image ids of the stencil entries it is paired with (execute()'s loop after
+// the dedup, sequential_matching.cc:139-146).
+struct RowPlan {
+  int32_t pivot = 0;
+  std::vector<int32_t> nb;
+  std::vector<uint32_t> nb_ids;
+};
+
+// Runs output rows `plan` (pair lists over table t) through the pipelined
+// batch machinery into one packed output.  keep_row0 >= 0 (table path):
+// plan[i] is table row keep_row0 + i and the raw matches of the kept rows are
+// recorded for scm_table_matches.
+int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& plan,
+             int64_t keep_row0, Packed* out);
+
 // Runs the sequential stencil over table rows [row_begin, row_end) through
-// the double-buffered batch pipeline into one packed output.
+// the pipelined batch machinery into one packed output.
 int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
               Packed* out) {
   const ImageTable& t = ctx->table;
-  struct Batch {
-    std::vector<PairSpec> specs;
-    std::vector<uint32_t> pair_ids;
-    std::vector<int64_t> pairs_begin;
-  };
-  std::vector<Batch> batches;
   std::vector<uint32_t> ids(overlap);
   std::vector<int64_t> rows(overlap), sel;
   // Pair lists of every row first (the stencil dedup of execute()).
   const int64_t nr = row_end - row_begin;
-  std::vector<std::vector<int64_t>> rsel(nr);
-  std::vector<std::vector<int64_t>> rrows(nr);
-  std::vector<std::vector<uint32_t>> rids(nr);
+  std::vector<RowPlan> plan(nr);
   for (int64_t r = row_begin; r < row_end; ++r) {
     for (int64_t s = 0; s < overlap; ++s) {
       rows[s] = std::min(r + s, t.n - 1);  // stencil clamped at the table end
       ids[s] = t.ids[rows[s]];
     }
     row_pairs(ids, &sel);
-    rsel[r - row_begin] = sel;
-    rrows[r - row_begin] = rows;
-    rids[r - row_begin] = ids;
+    RowPlan& rp = plan[r - row_begin];
+    rp.pivot = (int32_t)r;
+    for (int64_t s : sel) {
+      rp.nb.push_back((int32_t)rows[s]);
+      rp.nb_ids.push_back(ids[s]);
+    }
   }
+  return run_rows(ctx, t, plan, row_begin, out);
+}
+
+int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& plan,
+             int64_t keep_row0, Packed* out) {
+  struct Batch {
+    std::vector<PairSpec> specs;
+    std::vector<uint32_t> pair_ids;
+    std::vector<int64_t> pairs_begin;
+  };
+  std::vector<Batch> batches;
+  const int64_t nr = (int64_t)plan.size();
+  const bool keep = keep_row0 >= 0 && ctx->keep_matches;
+  const int64_t row_begin = keep_row0, row_end = keep_row0 + nr;
   // Batches of whole rows, closed at batch_pairs pairs or when the next row
   // would push the batch's device workspace past the per-set byte budget
   // (three sets are live at once).  A single row larger than the budget still
@@ -933,10 +1120,10 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
   Batch cur;
   int64_t cur_bytes = 0;
   for (int64_t i = 0; i < nr; ++i) {
-    const int64_t np = (int64_t)rsel[i].size();
-    const int64_t r = row_begin + i;
+    const RowPlan& rp = plan[i];
+    const int64_t np = (int64_t)rp.nb.size();
     int64_t row_bytes = 0;
-    for (int64_t s : rsel[i]) row_bytes += pair_workspace_bytes(t.ndesc[r], t.ndesc[rrows[i][s]]);
+    for (int32_t b : rp.nb) row_bytes += pair_workspace_bytes(t.ndesc[rp.pivot], t.ndesc[b]);
     const int64_t have = (int64_t)cur.specs.size();
     if (have > 0 && (have + np > ctx->batch_pairs || cur_bytes + row_bytes > budget)) {
       cur.pairs_begin.push_back(have);
@@ -946,16 +1133,16 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
     }
     cur_bytes += row_bytes;
     cur.pairs_begin.push_back((int64_t)cur.specs.size());
-    for (int64_t s : rsel[i]) {
-      cur.specs.push_back({(int32_t)r, (int32_t)rrows[i][s]});
-      cur.pair_ids.push_back(rids[i][s]);
+    for (size_t k = 0; k < rp.nb.size(); ++k) {
+      cur.specs.push_back({rp.pivot, rp.nb[k]});
+      cur.pair_ids.push_back(rp.nb_ids[k]);
     }
   }
   if (!cur.pairs_begin.empty()) {
     cur.pairs_begin.push_back((int64_t)cur.specs.size());
     batches.push_back(std::move(cur));
   }
-  if (ctx->keep_matches) {
+  if (keep) {
     ctx->last_begin = row_begin;
     ctx->last_end = row_end;
     ctx->last_matches.assign(row_end - row_begin, {});
@@ -964,7 +1151,7 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
     BatchView v;
     SCM_TRY(collect_batch(ctx, bs, &v));
     SCM_TRY(serialize_rows(ctx, v, b.pair_ids, b.pairs_begin, out));
-    if (ctx->keep_matches)
+    if (keep)
       for (int64_t p = 0; p < v.P; ++p) {
         const int64_t row = b.specs[p].a, o = v.offsets[p];
         if (row < ctx->keep_begin || row >= ctx->keep_end) continue;
@@ -973,7 +1160,7 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
       }
     return SCM_OK;
   };
-  out->row_off.reserve(2 * (row_end - row_begin) + 1);
+  out->row_off.reserve(2 * nr + 1);
   // Three buffer sets: at step k the GPU holds match(k) on the matching
   // stream and verify(k-1) (+ verify(k-2)) on the verification stream while
   // the host serialises batch k-3.
@@ -1124,6 +1311,8 @@ void scm_context_destroy(scm_context* ctx) {
   }
   ctx->table.release();
   ctx->scratch_table.release();
+  ctx->call_tab[0].release();
+  ctx->call_tab[1].release();
   ctx->lut.release();
   for (BatchSet& bs : ctx->sets) bs.release();
   ctx->h_stage.release();
@@ -1210,55 +1399,102 @@ int scm_verify_pair(scm_context* ctx, const float* kp1, int64_t n1, const float*
   return make_blob(bytes, tvg_out);
 }
 
-int scm_execute_stencil(scm_context* ctx, int64_t stencil_size, const scm_element* image_ids,
-                        const scm_element* keypoints, const scm_element* descriptors,
-                        scm_blob* pair_image_ids_out, scm_blob* tvgs_out) {
-  if (!ctx || stencil_size < 1 || !pair_image_ids_out || !tvgs_out) {
+int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
+                      const scm_element* image_ids, const scm_element* keypoints,
+                      const scm_element* descriptors, scm_blob* pair_image_ids_out,
+                      scm_blob* tvgs_out) {
+  if (!ctx || batch < 0 || stencil_size < 1 || (batch > 0 && (!pair_image_ids_out || !tvgs_out))) {
     set_error("invalid arguments");
     return SCM_E_INVALID;
   }
+  if (batch == 0) return SCM_OK;
   SCM_HIP(hipSetDevice(ctx->device));
+  const int64_t ne = batch * stencil_size;
   std::vector<RowView> rows;
-  SCM_TRY(decode_rows(stencil_size, image_ids, keypoints, descriptors, &rows));
-  std::vector<uint32_t> ids(stencil_size);
-  for (int64_t i = 0; i < stencil_size; ++i) ids[i] = rows[i].id;
-  std::vector<int64_t> sel;
-  row_pairs(ids, &sel);
-  SCM_TRY(upload_table(ctx, &ctx->scratch_table, rows, true, true));
-  std::vector<PairSpec> specs;
-  std::vector<uint32_t> pair_ids;
-  for (int64_t s : sel) {
-    specs.push_back({0, (int32_t)s});
-    pair_ids.push_back(ids[s]);
+  SCM_TRY(decode_rows(ne, image_ids, keypoints, descriptors, &rows));
+  // Unique images of the call (by id: the `extraction` table's image_id is
+  // its key); an id that arrives with different feature counts is an error.
+  std::unordered_map<uint32_t, int32_t> uid;
+  std::vector<RowView> uniq;
+  std::vector<int32_t> elem_u(ne);
+  for (int64_t e = 0; e < ne; ++e) {
+    auto it = uid.find(rows[e].id);
+    if (it == uid.end()) {
+      it = uid.emplace(rows[e].id, (int32_t)uniq.size()).first;
+      uniq.push_back(rows[e]);
+    } else if (uniq[it->second].nkp != rows[e].nkp || uniq[it->second].ndesc != rows[e].ndesc) {
+      set_error("image id " + std::to_string(rows[e].id) + " arrives with different features");
+      return SCM_E_INVALID;
+    }
+    elem_u[e] = it->second;
   }
-  BatchSet& bs = ctx->sets[0];
-  BatchView v;
-  int rc = run_batch(ctx, bs, ctx->scratch_table, specs, true, nullptr, 0, &v);
+  std::vector<int32_t> uidx;
+  int rc = upload_call_table(ctx, uniq, &uidx);
   if (rc != SCM_OK) {
+    ctx->call_cur = -1;  // the cache may be half written
     drain(ctx);
     return rc;
   }
+  const ImageTable& t = ctx->call_tab[ctx->call_cur];
+  std::vector<RowPlan> plan(batch);
+  std::vector<uint32_t> ids(stencil_size);
+  std::vector<int64_t> sel;
+  for (int64_t b = 0; b < batch; ++b) {
+    for (int64_t s = 0; s < stencil_size; ++s) ids[s] = rows[b * stencil_size + s].id;
+    row_pairs(ids, &sel);
+    plan[b].pivot = uidx[elem_u[b * stencil_size]];
+    for (int64_t s : sel) {
+      plan[b].nb.push_back(uidx[elem_u[b * stencil_size + s]]);
+      plan[b].nb_ids.push_back(ids[s]);
+    }
+  }
+  ctx->t_match = ctx->t_final = ctx->t_verify = 0.0;
+  ctx->n_match_launches = 0;
   Packed pk;
-  rc = serialize_rows(ctx, v, pair_ids, {0, (int64_t)specs.size()}, &pk);
+  rc = run_rows(ctx, t, plan, -1, &pk);
   if (rc != SCM_OK) {
-    std::free(pk.data);
+    drain(ctx);
+    if (!pool_give(pk.data)) std::free(pk.data);
     return rc;
   }
-  const size_t split = (size_t)pk.row_off[1];
-  scm_blob a{(uint8_t*)std::malloc(split), split};
-  scm_blob b{(uint8_t*)std::malloc(pk.size - split), pk.size - split};
-  if (!a.data || !b.data) {
-    std::free(a.data);
-    std::free(b.data);
-    std::free(pk.data);
-    set_error("malloc failed");
-    return SCM_E_NOMEM;
+  for (int64_t r = 0; r < batch; ++r) {
+    const int64_t a = pk.row_off[2 * r], b = pk.row_off[2 * r + 1], c = pk.row_off[2 * r + 2];
+    uint8_t* pa = (uint8_t*)std::malloc((size_t)std::max<int64_t>(b - a, 1));
+    uint8_t* pb = (uint8_t*)std::malloc((size_t)std::max<int64_t>(c - b, 1));
+    if (!pa || !pb) {
+      std::free(pa);
+      std::free(pb);
+      for (int64_t q = 0; q < r; ++q) {
+        scm_blob_free(&pair_image_ids_out[q]);
+        scm_blob_free(&tvgs_out[q]);
+      }
+      if (!pool_give(pk.data)) std::free(pk.data);
+      set_error("malloc failed");
+      return SCM_E_NOMEM;
+    }
+    std::memcpy(pa, pk.data + a, (size_t)(b - a));
+    std::memcpy(pb, pk.data + b, (size_t)(c - b));
+    pair_image_ids_out[r] = scm_blob{pa, (size_t)(b - a)};
+    tvgs_out[r] = scm_blob{pb, (size_t)(c - b)};
   }
-  std::memcpy(a.data, pk.data, split);
-  std::memcpy(b.data, pk.data + split, pk.size - split);
-  std::free(pk.data);
-  *pair_image_ids_out = a;
-  *tvgs_out = b;
+  if (!pool_give(pk.data)) std::free(pk.data);
+  return SCM_OK;
+}
+
+int scm_execute_stencil(scm_context* ctx, int64_t stencil_size, const scm_element* image_ids,
+                        const scm_element* keypoints, const scm_element* descriptors,
+                        scm_blob* pair_image_ids_out, scm_blob* tvgs_out) {
+  return scm_execute_batch(ctx, 1, stencil_size, image_ids, keypoints, descriptors,
+                           pair_image_ids_out, tvgs_out);
+}
+
+int scm_stencil_stats(scm_context* ctx, int64_t* reused, int64_t* uploaded) {
+  if (!ctx || !reused || !uploaded) {
+    set_error("invalid arguments");
+    return SCM_E_INVALID;
+  }
+  *reused = ctx->call_reused;
+  *uploaded = ctx->call_uploaded;
   return SCM_OK;
 }
 

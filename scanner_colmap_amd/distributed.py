@@ -93,27 +93,88 @@ def gather_to_root(payload, device=None) -> list[bytes] | None:
     """Gather every rank's byte payload (bytes or a uint8 numpy array) to
     rank 0 (None elsewhere).
 
-    Sizes are exchanged with an all_gather of one int64 per rank, then each
-    rank ships its payload (padded to the largest) with dist.gather — on the
-    `nccl` (RCCL) backend every peer sends over its own xGMI link."""
+    Sizes are exchanged with an all_gather of one int64 per rank; then every
+    rank r > 0 sends exactly its payload to rank 0 point-to-point (isend /
+    irecv, no padding) -- on the `nccl` (RCCL) backend each peer's bytes
+    travel over its own xGMI link to GPU 0, all receives in flight at once."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size()
     rank = dist.get_rank()
     dev = device if device is not None else torch.device("cpu")
-    n = torch.tensor([len(payload)], dtype=torch.int64, device=dev)
+    src = (np.frombuffer(payload, dtype=np.uint8) if isinstance(payload, (bytes, bytearray))
+           else np.ascontiguousarray(payload, dtype=np.uint8).reshape(-1))
+    n = torch.tensor([src.size], dtype=torch.int64, device=dev)
     sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
     dist.all_gather(sizes, n)
     sizes = [int(s.item()) for s in sizes]
-    mx = max(1, max(sizes))
-    t = torch.zeros(mx, dtype=torch.uint8, device=dev)
-    if len(payload):
-        src = (np.frombuffer(payload, dtype=np.uint8) if isinstance(payload, (bytes, bytearray))
-               else np.ascontiguousarray(payload, dtype=np.uint8).reshape(-1))
-        t[: len(payload)] = torch.from_numpy(src.copy() if not src.flags.writeable else src).to(dev)
-    bufs = [torch.zeros(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
-    dist.gather(t, gather_list=bufs, dst=0)
     if rank != 0:
+        if sizes[rank]:
+            t = torch.from_numpy(src.copy() if not src.flags.writeable else src).to(dev)
+            dist.send(t, dst=0)
         return None
-    return [bytes(b[:s].cpu().numpy().tobytes()) for b, s in zip(bufs, sizes)]
+    bufs = {r: torch.empty(sizes[r], dtype=torch.uint8, device=dev)
+            for r in range(1, world) if sizes[r]}
+    reqs = [dist.irecv(b, src=r) for r, b in bufs.items()]
+    for q in reqs:
+        q.wait()
+    out = [src.tobytes()]
+    for r in range(1, world):
+        out.append(bufs[r].cpu().numpy().tobytes() if r in bufs else b"")
+    return out
+
+
+class ShardPlan:
+    """One rank's share of a sequential-matching job (bench.py and the job
+    script use this; tests/test_distributed.py drives it over gloo).
+
+    weak scaling: every rank owns `images` pivot rows of one long sequence
+    (total = images * world); strong: `images` rows in total, split over the
+    ranks (BASELINE configs 4 and 5).  Rows are balanced by pair count and a
+    rank loads its rows plus the overlap-1 halo."""
+
+    def __init__(self, images: int, overlap: int, world: int, rank: int, scaling: str = "weak"):
+        if scaling not in ("weak", "strong"):
+            raise ValueError(f"scaling must be weak or strong, got {scaling!r}")
+        self.overlap = overlap
+        self.world = world
+        self.rank = rank
+        self.total_images = images if scaling == "strong" else images * world
+        self.row_begin, self.row_end = shard_rows(self.total_images, overlap, world, rank)
+        self.table_begin, self.table_end = table_range(self.row_begin, self.row_end,
+                                                       self.total_images, overlap)
+
+    @property
+    def local_rows(self) -> tuple[int, int]:
+        """The rank's output rows as indices into its loaded table slice."""
+        return self.row_begin - self.table_begin, self.row_end - self.table_begin
+
+    def pairs(self) -> int:
+        return int(pairs_per_row(self.total_images, self.overlap)[self.row_begin:self.row_end].sum())
+
+    def step(self, runner, device=None):
+        """One pass of the op over this rank's rows: `runner.table_run_packed`
+        (the scm_table_run_packed binding, or a stand-in with the same
+        result shape), then for world > 1 the gather of the packed io.cc rows
+        to rank 0.  Returns (this rank's packed rows, the gathered per-rank
+        payloads on rank 0 / None)."""
+        lb, le = self.local_rows
+        packed = runner.table_run_packed(self.overlap, lb, le)
+        gathered = None
+        if self.world > 1:
+            gathered = gather_to_root(pack_packed(packed.offsets, packed.data), device=device)
+        return packed, gathered
+
+
+def merge_gathered(payloads: list) -> tuple[list[bytes], list[bytes]]:
+    """Rank 0: concatenate the gathered per-rank packed rows in rank order
+    (= pivot-row order) into (pair_image_ids rows, two_view_geometries rows)."""
+    rows_a, rows_b = [], []
+    for p in payloads:
+        if len(p) == 0:
+            continue
+        a, b = unpack_packed(p)
+        rows_a += a
+        rows_b += b
+    return rows_a, rows_b

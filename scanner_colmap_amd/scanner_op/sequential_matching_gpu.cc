@@ -46,25 +46,38 @@ class SequentialMatchingGPUKernel : public scanner::StenciledBatchedKernel,
   ~SequentialMatchingGPUKernel() override { scm_context_destroy(ctx_); }
 
   // Reference execute (sequential_matching.cc:103-185): column c, batch
-  // element 0, stencil offset s -> input_cols[c][0][s].
+  // element b, stencil offset s -> input_cols[c][b][s].  The reference reads
+  // only b = 0 and emits one row (:106-108); every element of the batch is
+  // matched here (one scm_execute_batch call, one output row per element),
+  // so `batch=` on the op call amortises the GPU pipeline over many rows.
   void execute(const scanner::StenciledBatchedElements& input_cols,
                scanner::BatchedElements& output_cols) override {
-    const auto& ids = input_cols[0][0];
-    const auto& kps = input_cols[1][0];
-    const auto& descs = input_cols[2][0];
-    const size_t k = ids.size();
-    std::vector<scm_element> e_ids(k), e_kps(k), e_descs(k);
-    for (size_t s = 0; s < k; ++s) {
-      e_ids[s] = {ids[s].buffer, ids[s].size};
-      e_kps[s] = {kps[s].buffer, kps[s].size};
-      e_descs[s] = {descs[s].buffer, descs[s].size};
+    const size_t nb = input_cols[0].size();
+    if (nb == 0) return;
+    const size_t k = input_cols[0][0].size();
+    std::vector<scm_element> e_ids(nb * k), e_kps(nb * k), e_descs(nb * k);
+    for (size_t b = 0; b < nb; ++b) {
+      const auto& ids = input_cols[0][b];
+      const auto& kps = input_cols[1][b];
+      const auto& descs = input_cols[2][b];
+      if (ids.size() != k || kps.size() != k || descs.size() != k) {
+        std::fprintf(stderr, "SequentialMatchingGPU: ragged stencils in one batch\n");
+        std::abort();
+      }
+      for (size_t s = 0; s < k; ++s) {
+        e_ids[b * k + s] = {ids[s].buffer, ids[s].size};
+        e_kps[b * k + s] = {kps[s].buffer, kps[s].size};
+        e_descs[b * k + s] = {descs[s].buffer, descs[s].size};
+      }
     }
-    scm_blob pair_ids{nullptr, 0}, tvgs{nullptr, 0};
-    scm_check(scm_execute_stencil(ctx_, (int64_t)k, e_ids.data(), e_kps.data(), e_descs.data(),
-                                  &pair_ids, &tvgs),
-              "scm_execute_stencil");
-    emit(output_cols[0], &pair_ids);
-    emit(output_cols[1], &tvgs);
+    std::vector<scm_blob> pair_ids(nb, scm_blob{nullptr, 0}), tvgs(nb, scm_blob{nullptr, 0});
+    scm_check(scm_execute_batch(ctx_, (int64_t)nb, (int64_t)k, e_ids.data(), e_kps.data(),
+                                e_descs.data(), pair_ids.data(), tvgs.data()),
+              "scm_execute_batch");
+    for (size_t b = 0; b < nb; ++b) {
+      emit(output_cols[0], &pair_ids[b]);
+      emit(output_cols[1], &tvgs[b]);
+    }
   }
 
  private:

@@ -1,10 +1,16 @@
 // Test driver (see tests/scanner_stub/README.md): instantiates a registered
-// kernel by op name, as a Scanner worker would, and runs execute() on one
-// stencil read from files:  drive_op OP DIR K [DEVICE]
+// kernel by op name, as a Scanner worker would, and runs execute() on
+// stencils read from files.
+//   drive_op OP DIR K [DEVICE]: one stencil;
+//     DIR/in_<c>_<s>: element s of input column c (c = 0 ids, 1 keypoints, 2 descriptors)
+//     writes DIR/out_<c> for every output column.
+//   drive_op OP DIR K DEVICE NROWS BATCH: a table of NROWS rows (DIR/in_<c>_<r>)
+//     run as Scanner runs a stencil range(0, K) op with batch BATCH: output rows
+//     0..NROWS-1 in consecutive execute() calls of up to BATCH stencils, the
+//     stencil of row r being rows min(r + s, NROWS - 1); writes DIR/out_<c>_<r>.
 //   DIR/args (optional): serialised op arguments
-//   DIR/in_<c>_<s>: element s of input column c (c = 0 ids, 1 keypoints, 2 descriptors)
-//   writes DIR/out_<c> for every output column.
 #include <cstdio>
+#include <algorithm>
 #include <cstdlib>
 #include <fstream>
 #include <iterator>
@@ -39,33 +45,50 @@ int main(int argc, char** argv) {
   config.devices.push_back({it->second.device, device});
   read_file(dir + "/args", &config.args);
 
+  const int nrows = argc > 5 ? std::atoi(argv[5]) : 0;
+  const int batch = argc > 6 ? std::max(1, std::atoi(argv[6])) : 1;
+  const bool table = nrows > 0;
+  const int nfiles = table ? nrows : k;
   std::vector<std::vector<std::vector<scanner::u8>>> store(info.inputs.size());
-  scanner::StenciledBatchedElements in(info.inputs.size());
   for (size_t c = 0; c < info.inputs.size(); ++c) {
-    store[c].resize(k);
-    in[c].resize(1);
-    for (int s = 0; s < k; ++s) {
+    store[c].resize(nfiles);
+    for (int s = 0; s < nfiles; ++s)
       if (!read_file(dir + "/in_" + std::to_string(c) + "_" + std::to_string(s), &store[c][s])) {
         std::fprintf(stderr, "missing input %zu/%d\n", c, s);
         return 2;
       }
-      scanner::Element e;
-      e.buffer = store[c][s].data();
-      e.size = store[c][s].size();
-      in[c][0].push_back(e);
-    }
   }
-  scanner::BatchedElements out(info.outputs.size());
   scanner::StenciledBatchedKernel* kernel = it->second.make(config);
-  kernel->execute(in, out);
-  for (size_t c = 0; c < out.size(); ++c) {
-    if (out[c].size() != 1) {
-      std::fprintf(stderr, "column %zu: %zu elements\n", c, out[c].size());
-      return 1;
+  const int rows_out = table ? nrows : 1;
+  for (int r0 = 0; r0 < rows_out; r0 += batch) {
+    const int nb = table ? std::min(batch, rows_out - r0) : 1;
+    scanner::StenciledBatchedElements in(info.inputs.size());
+    for (size_t c = 0; c < info.inputs.size(); ++c) {
+      in[c].resize(nb);
+      for (int b = 0; b < nb; ++b)
+        for (int s = 0; s < k; ++s) {
+          const int row = table ? std::min(r0 + b + s, nrows - 1) : s;
+          scanner::Element e;
+          e.buffer = store[c][row].data();
+          e.size = store[c][row].size();
+          in[c][b].push_back(e);
+        }
     }
-    std::ofstream f(dir + "/out_" + std::to_string(c), std::ios::binary);
-    f.write(reinterpret_cast<const char*>(out[c][0].buffer), (std::streamsize)out[c][0].size);
-    scanner::delete_buffer(scanner::CPU_DEVICE, out[c][0].buffer);
+    scanner::BatchedElements out(info.outputs.size());
+    kernel->execute(in, out);
+    for (size_t c = 0; c < out.size(); ++c) {
+      if (out[c].size() != (size_t)nb) {
+        std::fprintf(stderr, "column %zu: %zu elements for %d stencils\n", c, out[c].size(), nb);
+        return 1;
+      }
+      for (int b = 0; b < nb; ++b) {
+        const std::string name = table ? "/out_" + std::to_string(c) + "_" + std::to_string(r0 + b)
+                                       : "/out_" + std::to_string(c);
+        std::ofstream f(dir + name, std::ios::binary);
+        f.write(reinterpret_cast<const char*>(out[c][b].buffer), (std::streamsize)out[c][b].size);
+        scanner::delete_buffer(scanner::CPU_DEVICE, out[c][b].buffer);
+      }
+    }
   }
   delete kernel;
   return 0;

@@ -46,7 +46,27 @@ def _free_port():
     return p
 
 
-def _rank_main(rank, world, port, n, K, q):
+class _OracleRunner:
+    """Stand-in for the GPU context in the CPU test: the same
+    table_run_packed result shape (offsets + packed element bytes), computed
+    by the CPU oracle over the rank's loaded table slice."""
+
+    def __init__(self, ids, kps, descs):
+        self.table = (ids, kps, descs)
+
+    def table_run_packed(self, overlap, row_begin, row_end):
+        from oracle import oracle
+        pa, pb = oracle.table_run(*self.table, overlap, row_begin, row_end)
+        elems = [x for pair in zip(pa, pb) for x in pair]
+
+        class _P:
+            offsets = np.cumsum([0] + [len(x) for x in elems]).astype(np.int64)
+            data = (np.frombuffer(b"".join(elems), np.uint8) if elems
+                    else np.zeros(0, np.uint8))
+        return _P()
+
+
+def _rank_main(rank, world, port, n, K, scaling, q):
     import torch.distributed as dist
 
     from oracle import oracle
@@ -56,40 +76,45 @@ def _rank_main(rank, world, port, n, K, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        c = Corridor(n, 400, K, seed=53)
-        a, b = sd.shard_rows(n, K, world, rank)
-        ta, tb = sd.table_range(a, b, n, K)
-        ids, kps, descs = table_rows(c.images(ta, tb))
-        pa, pb = oracle.table_run(ids, kps, descs, K, a - ta, b - ta)
-        # same layout scm_table_run_packed returns
-        elems = [x for pair in zip(pa, pb) for x in pair]
-        offs = np.cumsum([0] + [len(x) for x in elems]).astype(np.int64)
-        data = np.frombuffer(b"".join(elems), np.uint8) if elems else np.zeros(0, np.uint8)
-        got = sd.gather_to_root(sd.pack_packed(offs, data))
+        # bench.py's own sharding and step: ShardPlan -> table slice with the
+        # halo -> runner.table_run_packed over the local rows -> P2P gather
+        plan = sd.ShardPlan(n, K, world, rank, scaling)
+        c = Corridor(plan.total_images, 400, K, seed=53)
+        runner = _OracleRunner(*table_rows(c.images(plan.table_begin, plan.table_end)))
+        _, got = plan.step(runner)
         if rank == 0:
-            rows_a, rows_b = [], []
-            for payload in got:
-                x, y = sd.unpack_packed(payload)
-                rows_a += x
-                rows_b += y
+            rows_a, rows_b = sd.merge_gathered(got)
             ids, kps, descs = table_rows(c.images())
-            ref = oracle.table_run(ids, kps, descs, K, 0, n)
-            q.put((rows_a == ref[0], rows_b == ref[1], len(rows_a)))
+            ref = oracle.table_run(ids, kps, descs, K, 0, plan.total_images)
+            q.put((rows_a == ref[0], rows_b == ref[1], len(rows_a), plan.total_images))
     finally:
         dist.destroy_process_group()
 
 
-def test_gloo_gather_world2():
-    n, K, world = 9, 4, 2
+@pytest.mark.parametrize("n,K,scaling", [(9, 4, "strong"), (5, 3, "weak"), (2, 5, "strong")])
+def test_gloo_shard_step_world2(n, K, scaling):
+    world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, K, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, K, scaling, q))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=240)
     codes = [p.exitcode for p in procs]
     assert codes == [0, 0], codes
-    ok_a, ok_b, nrows = q.get(timeout=5)
-    assert ok_a and ok_b and nrows == n
+    ok_a, ok_b, nrows, total = q.get(timeout=5)
+    assert ok_a and ok_b and nrows == total
+    assert total == (n if scaling == "strong" else n * world)
+
+
+def test_shard_plan_scaling():
+    weak = [sd.ShardPlan(1000, 20, 8, r, "weak") for r in range(8)]
+    strong = [sd.ShardPlan(10000, 50, 8, r, "strong") for r in range(8)]
+    assert weak[0].total_images == 8000 and strong[0].total_images == 10000
+    assert sum(p.pairs() for p in strong) == 488775  # BASELINE config 5
+    assert sum(p.pairs() for p in [sd.ShardPlan(128, 128, 8, r, "strong") for r in range(8)]) == 8128
+    with pytest.raises(ValueError):
+        sd.ShardPlan(10, 3, 2, 0, "both")

@@ -100,3 +100,30 @@ def test_op_parses_scanner_args(tmp_path):
     ref_ids, ref_tvgs = oracle.execute_stencil(ids, kps, descs, opts)
     assert (d / "out_0").read_bytes() == ref_ids
     assert (d / "out_1").read_bytes() == ref_tvgs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 5])
+def test_op_batched_rows_match_table_oracle(tmp_path, batch):
+    """A Scanner job over a 12-row table (stencil range(0, 4)) through the op:
+    consecutive execute() calls of `batch` stencils each (the reference's
+    default batch of 1, and a 5-stencil `.batch()` call with a short last
+    call), stencils clamped at the table end as Scanner does; every output
+    row equals the oracle's, and the HBM image cache is exercised across
+    calls."""
+    from oracle import oracle
+    from scanner_colmap_amd.codecs import table_rows
+    from scanner_colmap_amd.synthetic import Corridor
+    exe = _build_driver(tmp_path)
+    n, K = 12, 4
+    ids, kps, descs = table_rows(Corridor(n, 600, K, seed=45).images())
+    d = tmp_path / "io"
+    d.mkdir()
+    _write_stencil(d, ids, kps, descs)
+    r = subprocess.run([str(exe), "SequentialMatchingGPU", str(d), str(K), "0", str(n), str(batch)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    ref_ids, ref_tvgs = oracle.table_run(ids, kps, descs, K, 0, n)
+    for row in range(n):
+        assert (d / f"out_0_{row}").read_bytes() == ref_ids[row], row
+        assert (d / f"out_1_{row}").read_bytes() == ref_tvgs[row], row
