@@ -25,8 +25,10 @@
 // threshold of SURVEY.md §8a (d = 200,499), exact synthetic geometry, and the
 // libstdc++ std::mt19937 + std::uniform_int_distribution draw sequence.
 //
-// The RANSAC PRNG is std::mt19937 seeded per pair with scm_pair_seed() (the
-// reference's is time-seeded).  The fp64 estimator
+// The RANSAC PRNGs are std::mt19937 seeded per pair: F with scm_pair_seed(),
+// H and the watermark RANSAC with the second stream's seed (geom_solvers.h
+// pair_seed_h); the reference's single generator is time-seeded, SURVEY.md §0
+// fact 4.  The fp64 estimator
 // primitives are the shared header geom_solvers.h so that the GPU path can be
 // checked bit-for-bit; they are pinned separately by known-answer tests.
 #include <algorithm>
@@ -495,7 +497,11 @@ bool detect_watermark(const scm_matching_options& o, const std::vector<double>& 
 TVG verify_pair(const scm_matching_options& o, const float* kp1, const float* kp2,
                 const std::vector<Match>& matches, uint32_t id1, uint32_t id2) {
   TVG tvg;
+  // Two PRNG streams per pair: F from pair_seed, H (then the watermark
+  // RANSAC) from pair_seed_h (geom_solvers.h; the reference's single
+  // thread-local generator is time-seeded, so either is a realisation of it).
   std::mt19937 prng(oracle_pair_seed(o.ransac_seed, id1, id2));
+  std::mt19937 prng_h(oracle_pair_seed(o.ransac_seed ^ 0x6A09E667u, id1, id2));
   const size_t min_num_inliers = (size_t)o.min_num_inliers;
   if (matches.size() < min_num_inliers) {
     tvg.config = SCM_TVG_DEGENERATE;
@@ -511,7 +517,7 @@ TVG verify_pair(const scm_matching_options& o, const float* kp1, const float* kp
     const RansacOptions ro = ransac_options(o);
     const Report F_report = loransac(0, ro, p1, p2, &prng);
     if (!F_report.model.empty()) std::copy(F_report.model.begin(), F_report.model.end(), tvg.F);
-    const Report H_report = loransac(1, ro, p1, p2, &prng);
+    const Report H_report = loransac(1, ro, p1, p2, &prng_h);
     if (!H_report.model.empty()) std::copy(H_report.model.begin(), H_report.model.end(), tvg.H);
     if ((!F_report.success && !H_report.success) ||
         (F_report.support.num_inliers < min_num_inliers &&
@@ -530,7 +536,7 @@ TVG verify_pair(const scm_matching_options& o, const float* kp1, const float* kp
           if (F_report.inlier_mask[i]) tvg.inlier_matches.push_back(matches[i]);
       if (o.detect_watermark && F_report.success &&
           detect_watermark(o, p1, p2, F_report.support.num_inliers,
-                           F_report.inlier_mask, &prng))
+                           F_report.inlier_mask, &prng_h))
         tvg.config = SCM_TVG_WATERMARK;
     }
   }

@@ -138,6 +138,15 @@ SCM_HD inline uint32_t pair_seed(uint32_t base, uint32_t id1, uint32_t id2) {
   return h;
 }
 
+// Seed of the pair's second stream: the homography LO-RANSAC (and the
+// watermark RANSAC after it) draw from std::mt19937(pair_seed_h(...)), so
+// that the F and H estimations are independent and run concurrently.  (In
+// the reference both continue one thread-local, time-seeded generator; any
+// seeding is an equally valid realisation of it.)
+SCM_HD inline uint32_t pair_seed_h(uint32_t base, uint32_t id1, uint32_t id2) {
+  return pair_seed(base ^ 0x6A09E667u, id1, id2);
+}
+
 // ---------------------------------------------------------------------------
 // Residuals.  Term order follows the reference formulas exactly.
 // ---------------------------------------------------------------------------

@@ -26,6 +26,7 @@ constexpr uint32_t kIdxMask = (1u << kIdxBits) - 1u;
 constexpr uint32_t kLutMax = 1u << 18;           // acosf LUT covers [0, 2^18]
 constexpr int kFinThreads = 1024;
 constexpr int kXcds = 8;                         // MI355X: 8 XCDs, round-robin dispatch
+constexpr int kNumCUs = 256;                     // MI355X: 32 CUs per XCD
 
 // One workgroup of match_tiles_kernel: 512 rows of a pivot image against
 // every column of `npairs` neighbour images (pairs[pair0 .. pair0+npairs)).

@@ -96,6 +96,8 @@ struct BatchSet {
   DevBuf jobs, pairs, rowres, colpart, m21, matches, counts, gpairs, vpairs, xy1, xy2, scratch,
       snaps, masks, offsets, match_off, prof, xyf, dvout, dpack, dpmask, rst, samp, nmod, fcon,
       cnts, act, nact, mods, wsnap;
+  // round buffers of the H LO-RANSAC (advanced beside F's, own PRNG stream)
+  DevBuf h_rst, h_samp, h_nmod, h_fcon, h_cnts, h_act, h_nact, h_mods, h_wsnap;
   HostBuf stage, vstage;
   PinnedOut out;
   size_t off_counts = 0, off_offsets = 0, off_vout = 0, off_matches = 0, off_masks = 0;
@@ -115,7 +117,8 @@ struct BatchSet {
     for (DevBuf* b : {&jobs, &pairs, &rowres, &colpart, &m21, &matches, &counts, &gpairs, &vpairs,
                       &xy1, &xy2, &scratch, &snaps, &masks, &offsets, &match_off, &prof, &xyf, &dvout,
                       &dpack, &dpmask, &rst, &samp, &nmod, &fcon, &cnts, &act, &nact,
-                      &mods, &wsnap})
+                      &mods, &wsnap, &h_rst, &h_samp, &h_nmod, &h_fcon, &h_cnts, &h_act, &h_nact,
+                      &h_mods, &h_wsnap})
       b->release();
     stage.release();
     vstage.release();
@@ -537,6 +540,11 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   if (P == 0) return SCM_OK;
   std::vector<PairDesc> pds(P);
   std::vector<MatchJob> jobs, jobs_clamp;
+  struct Run {
+    int32_t a, pair0, npairs;
+    bool clamp;
+  };
+  std::vector<Run> runs;
   bs.moff.resize(P);
   int64_t rr = 0, cp = 0, m21 = 0, mo = 0;
   const int32_t rpb = ctx->match_bf16 ? kRowsPerBlock : kRowsPerBlock8;  // pivot rows per job
@@ -575,27 +583,47 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
     }
     for (int64_t k = i; k < j; ++k) pds[k].clamp = clamp ? 1 : 0;
     if (!given && t.ndesc[a] > 0) {
-      // Jobs over runs of consecutive active pairs of this pivot.
-      const int32_t n1 = t.ndesc[a];
-      const int32_t nrb = (n1 + rpb - 1) / rpb;
+      // Runs of consecutive active pairs of this pivot (jobs are cut below).
       for (int64_t k = i; k < j;) {
         while (k < j && pds[k].n2 == 0) ++k;
         int64_t e = k;
         while (e < j && pds[e].n2 > 0) ++e;
-        if (e > k)
-          for (int32_t rb = 0; rb < nrb; ++rb) {
-            MatchJob jb;
-            jb.a_row = t.desc_row[a];
-            jb.rb = rb;
-            jb.n1 = n1;
-            jb.pair0 = (int32_t)k;
-            jb.npairs = (int32_t)(e - k);
-            (clamp ? jobs_clamp : jobs).push_back(jb);
-          }
+        if (e > k) runs.push_back({a, (int32_t)k, (int32_t)(e - k), clamp});
         k = e;
       }
     }
     i = j;
+  }
+  // One job = one 512-row block of a pivot swept over a run of its pairs.  A
+  // small batch (a single execute() stencil: K-1 pairs of one pivot = 16 row
+  // blocks) would leave most of the 256 CUs idle, so runs are cut into
+  // shorter runs until the batch has ~4 jobs per CU (a job over fewer pairs
+  // re-reads nothing: every pair's columns are swept once per row block).
+  {
+    int64_t base_jobs = 0;
+    for (const Run& r : runs) base_jobs += (t.ndesc[r.a] + rpb - 1) / rpb;
+    const int64_t want = 4 * kNumCUs;
+    for (const Run& r : runs) {
+      const int32_t n1 = t.ndesc[r.a];
+      const int32_t nrb = (n1 + rpb - 1) / rpb;
+      int32_t parts = 1;
+      if (base_jobs > 0 && base_jobs < want)
+        parts = (int32_t)std::min<int64_t>(r.npairs, (want + base_jobs - 1) / base_jobs);
+      for (int32_t q = 0; q < parts; ++q) {
+        const int32_t p0 = r.pair0 + (int32_t)((int64_t)r.npairs * q / parts);
+        const int32_t p1 = r.pair0 + (int32_t)((int64_t)r.npairs * (q + 1) / parts);
+        if (p1 <= p0) continue;
+        for (int32_t rb = 0; rb < nrb; ++rb) {
+          MatchJob jb;
+          jb.a_row = t.desc_row[r.a];
+          jb.rb = rb;
+          jb.n1 = n1;
+          jb.pair0 = p0;
+          jb.npairs = p1 - p0;
+          (r.clamp ? jobs_clamp : jobs).push_back(jb);
+        }
+      }
+    }
   }
   bs.slots = mo;
   xcd_order(jobs, pds);
@@ -790,30 +818,41 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
     }
     bs.nprof = V;
     SCM_HIP(hipEventRecord(bs.ev[4], sv));
-    SCM_TRY(bs.rst.ensure(V * sizeof(RansacState)));
-    SCM_TRY(bs.samp.ensure(V * kWindowTrials * 8 * sizeof(uint16_t)));
-    SCM_TRY(bs.nmod.ensure(V * kWindowTrials * sizeof(int32_t)));
-    SCM_TRY(bs.fcon.ensure(V * kWindowTrials * 3 * 12 * sizeof(float)));
-    SCM_TRY(bs.mods.ensure(V * kWindowTrials * 3 * 9 * sizeof(double)));
-    SCM_TRY(bs.cnts.ensure(V * kWindowTrials * 3 * sizeof(uint32_t)));
-    SCM_TRY(bs.wsnap.ensure(V * kMaxWindow * 640 * sizeof(uint32_t)));
-    SCM_TRY(bs.act.ensure(2 * V * sizeof(int32_t)));
-    SCM_TRY(bs.nact.ensure(2 * sizeof(int32_t)));
-    VerifyRoundBufs rb;
-    rb.rst = bs.rst.as<RansacState>();
-    rb.samp = bs.samp.as<uint16_t>();
-    rb.nmod = bs.nmod.as<int32_t>();
-    rb.fcon = bs.fcon.as<float>();
-    rb.mods = bs.mods.as<double>();
-    rb.cnts = bs.cnts.as<uint32_t>();
-    rb.wsnap = bs.wsnap.as<uint32_t>();
-    rb.act[0] = bs.act.as<int32_t>();
-    rb.act[1] = bs.act.as<int32_t>() + V;
-    rb.nact = bs.nact.as<int32_t>();
+    // Round buffers per kind (H: one model per hypothesis).
+    auto round_bufs = [&](DevBuf& rst, DevBuf& samp, DevBuf& nmod, DevBuf& fcon, DevBuf& mods,
+                          DevBuf& cnts, DevBuf& wsnap, DevBuf& act, DevBuf& nact,
+                          VerifyRoundBufs* rb) -> int {
+      SCM_TRY(rst.ensure(V * sizeof(RansacState)));
+      SCM_TRY(samp.ensure(V * kWindowTrials * 8 * sizeof(uint16_t)));
+      SCM_TRY(nmod.ensure(V * kWindowTrials * sizeof(int32_t)));
+      SCM_TRY(fcon.ensure(V * kWindowTrials * 3 * 12 * sizeof(float)));
+      SCM_TRY(mods.ensure(V * kWindowTrials * 3 * 9 * sizeof(double)));
+      SCM_TRY(cnts.ensure(V * kWindowTrials * 3 * sizeof(uint32_t)));
+      SCM_TRY(wsnap.ensure(V * kMaxWindow * 640 * sizeof(uint32_t)));
+      SCM_TRY(act.ensure(2 * V * sizeof(int32_t)));
+      SCM_TRY(nact.ensure(2 * sizeof(int32_t)));
+      rb->rst = rst.as<RansacState>();
+      rb->samp = samp.as<uint16_t>();
+      rb->nmod = nmod.as<int32_t>();
+      rb->fcon = fcon.as<float>();
+      rb->mods = mods.as<double>();
+      rb->cnts = cnts.as<uint32_t>();
+      rb->wsnap = wsnap.as<uint32_t>();
+      rb->act[0] = act.as<int32_t>();
+      rb->act[1] = act.as<int32_t>() + V;
+      rb->nact = nact.as<int32_t>();
+      return SCM_OK;
+    };
+    VerifyRoundBufs rbf, rbh;
+    SCM_TRY(round_bufs(bs.rst, bs.samp, bs.nmod, bs.fcon, bs.mods, bs.cnts, bs.wsnap, bs.act,
+                       bs.nact, &rbf));
+    SCM_TRY(round_bufs(bs.h_rst, bs.h_samp, bs.h_nmod, bs.h_fcon, bs.h_mods, bs.h_cnts,
+                       bs.h_wsnap, bs.h_act, bs.h_nact, &rbh));
     SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
                           bs.xy2.as<double>(), bs.scratch.as<double>(), bs.snaps.as<uint32_t>(),
                           bs.masks.as<uint8_t>(), bs.dvout.as<VerifyOut>(),
-                          make_params(ctx->opts), prof, nullptr, bs.xyf.as<float4>(), rb, sv));
+                          make_params(ctx->opts), prof, nullptr, bs.xyf.as<float4>(), rbf, rbh,
+                          sv));
   }
   SCM_HIP(hipEventRecord(bs.ev[5], sv));
   // Compact matches + F-inlier masks in HBM, then DMA the results into the
@@ -1034,8 +1073,8 @@ int64_t pair_workspace_bytes(int64_t n1, int64_t n2) {
   const int64_t verify_pts = slots * (16 + 16 + 16 + 8 + 1);  // xy1, xy2, xyf, dpack, dpmask
   const int64_t verify_pair = verify_scratch_doubles(slots) * 8 + kVerifySnapWords * 4 +
                               (int64_t)sizeof(RansacState) + (int64_t)sizeof(VerifyOut) +
-                              (int64_t)kWindowTrials * (8 * 2 + 4 + 3 * 12 * 4 + 3 * 9 * 8 + 3 * 4) +
-                              (int64_t)kMaxWindow * 640 * 4 + 256;
+                              2 * ((int64_t)kWindowTrials * (8 * 2 + 4 + 3 * 12 * 4 + 3 * 9 * 8 + 3 * 4) +
+                                   (int64_t)kMaxWindow * 640 * 4) + 256;  // F and H round buffers
   return match + verify_pts + verify_pair;
 }
 
@@ -1051,7 +1090,9 @@ int64_t set_budget_bytes(scm_context* ctx) {
                             &bs.counts, &bs.gpairs, &bs.vpairs, &bs.xy1, &bs.xy2, &bs.scratch,
                             &bs.snaps, &bs.masks, &bs.offsets, &bs.match_off, &bs.prof, &bs.xyf,
                             &bs.dvout, &bs.dpack, &bs.dpmask, &bs.rst, &bs.samp, &bs.nmod,
-                            &bs.fcon, &bs.cnts, &bs.act, &bs.nact, &bs.mods, &bs.wsnap})
+                            &bs.fcon, &bs.cnts, &bs.act, &bs.nact, &bs.mods, &bs.wsnap,
+                            &bs.h_rst, &bs.h_samp, &bs.h_nmod, &bs.h_fcon, &bs.h_cnts, &bs.h_act,
+                            &bs.h_nact, &bs.h_mods, &bs.h_wsnap})
       held += (int64_t)b->bytes;
   const int64_t avail = (int64_t)free_b + held - ((int64_t)2 << 30);
   return std::max<int64_t>(avail / 3, (int64_t)64 << 20);

@@ -9,12 +9,18 @@ constexpr int kVerifyThreads = 64;    // one wavefront per pair
 constexpr int kTrialBatch = 64;       // hypotheses solved in parallel per round (one per lane)
 constexpr int kMaxVerifyMatches = 65535;  // uint16 sample indices in LDS
 constexpr int kVerifyModelDoubles = kTrialBatch * 27;  // per-pair model buffer
-constexpr int kVerifySnapWords = 1280;
-// Per-pair scratch (doubles): residuals / inlier gathers (10 m), the model
-// buffer, then the uint16 sample-index vector.
-inline int64_t verify_scratch_doubles(int64_t m) {
+// PRNG words per pair: for each of the two streams (F; H then watermark) the
+// handed-on mt19937 state (640) and the abort-rewind snapshot (640).
+constexpr int kVerifyStreamWords = 1280;
+constexpr int kVerifySnapWords = 2 * kVerifyStreamWords;
+// Per-pair scratch of one RANSAC kind (doubles): residuals / inlier gathers
+// (10 m), the model buffer, then the uint16 sample-index vector.  F and H run
+// concurrently, each in its own area (H's follows F's; the watermark RANSAC
+// reuses F's after both finished).
+__host__ __device__ inline int64_t verify_kind_scratch_doubles(int64_t m) {
   return 10 * m + kVerifyModelDoubles + (m + 3) / 4 + 1;
-}  // per pair: handed-on PRNG state + batch snapshot
+}
+inline int64_t verify_scratch_doubles(int64_t m) { return 2 * verify_kind_scratch_doubles(m); }
 
 // Scalar options of TwoViewGeometry::EstimateUncalibrated (SURVEY.md §8a a2,
 // a9-a14) after the op's parseConfigs (sequential_matching.cc:64-75).
@@ -89,13 +95,16 @@ struct VerifyRoundBufs {
   int32_t* nact;
 };
 
-// snaps: kVerifySnapWords uint32 per pair (PRNG state between the F, H and
-// watermark kernels + the per-round snapshot for the abort rewind).
+// snaps: kVerifySnapWords uint32 per pair (PRNG states handed between the
+// windowed kernels + the per-round snapshots for the abort rewind).  The F
+// LO-RANSAC (round buffers rb_f) and the H LO-RANSAC (rb_h, its own PRNG
+// stream) advance together in one launch sequence on `stream`; the
+// configuration, watermark and post-filter kernel follows.
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
-                         const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb,
-                         hipStream_t stream);
+                         const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb_f,
+                         const VerifyRoundBufs& rb_h, hipStream_t stream);
 size_t verify_lds_bytes(int max_m);
 constexpr int kVerifyProfSlots = 90;
 

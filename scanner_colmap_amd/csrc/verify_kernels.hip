@@ -1533,8 +1533,9 @@ __device__ __forceinline__ PairSetup pair_setup(const VerifyPair* pairs, double*
   PairSetup ps;
   ps.pp = pairs[blockIdx.x];
   ps.n = ps.pp.cidx >= 0 ? counts[ps.pp.cidx] : ps.pp.m;
-  ps.state = snaps + (int64_t)blockIdx.x * kVerifySnapWords;
-  ps.snap = ps.state + kVerifySnapWords / 2;
+  // the watermark RANSAC continues the H stream; F's scratch area is free
+  ps.state = snaps + (int64_t)blockIdx.x * kVerifySnapWords + kVerifyStreamWords;
+  ps.snap = ps.state + kVerifyStreamWords / 2;
   ps.base = scratch + ps.pp.scr_off;
   ps.o = out + ps.pp.out_idx;
   return ps;
@@ -1659,14 +1660,17 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
 // algorithm never draws them; the expensive scoring runs as a wide, regular
 // kernel and the sequential parts cost one short kernel per window.
 // ---------------------------------------------------------------------------
+// Kind K's PRNG stream words and scratch area of pair q (F and H run
+// concurrently, each on its own).
+template <int K>
 __device__ __forceinline__ PairSetup pair_at(const VerifyPair* pairs, int q, double* scratch,
                                              uint32_t* snaps, VerifyOut* out) {
   PairSetup ps;
   ps.pp = pairs[q];
   ps.n = ps.pp.m;
-  ps.state = snaps + (int64_t)q * kVerifySnapWords;
-  ps.snap = ps.state + kVerifySnapWords / 2;
-  ps.base = scratch + ps.pp.scr_off;
+  ps.state = snaps + (int64_t)q * kVerifySnapWords + (K == KIND_H ? kVerifyStreamWords : 0);
+  ps.snap = ps.state + kVerifyStreamWords / 2;
+  ps.base = scratch + ps.pp.scr_off + (K == KIND_H ? verify_kind_scratch_doubles(ps.n) : 0);
   ps.o = out + ps.pp.out_idx;
   return ps;
 }
@@ -1701,21 +1705,21 @@ __device__ void rs_finish(const PairSetup& ps, const RansacState& st, uint8_t* m
   }
 }
 
-// Start of a RANSAC for every pair: state, sample-index vector, F seeds the
-// pair's PRNG (H continues the stream F left).  Pairs with fewer points than
+// Start of a RANSAC for every pair: state, sample-index vector, the kind's
+// PRNG stream seeded (F: pair_seed, H: pair_seed_h).  Pairs with fewer points than
 // the minimal sample finish at once (LORANSAC returns an empty report).
 template <int K>
-__global__ __launch_bounds__(64) void rs_begin_kernel(
+__device__ __attribute__((always_inline)) void rs_begin_body(
     const VerifyPair* __restrict__ pairs, int npairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
     const float4* __restrict__ xyf_all, RansacState* __restrict__ rst,
-    int32_t* __restrict__ act, int32_t* __restrict__ nact, VerifyParams P) {
+    int32_t* __restrict__ act, int32_t* __restrict__ nact, VerifyParams P, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
   const int lane = threadIdx.x;
-  for (int q = blockIdx.x; q < npairs; q += gridDim.x) {
-    const PairSetup ps = pair_at(pairs, q, scratch, snaps, out);
+  for (int q = bid; q < npairs; q += nblk) {
+    const PairSetup ps = pair_at<K>(pairs, q, scratch, snaps, out);
     const int n = ps.n;
     const float4* xyf = xyf_all + ps.pp.pts_off / 2;
     float smax = 0.0f;
@@ -1725,12 +1729,12 @@ __global__ __launch_bounds__(64) void rs_begin_kernel(
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) smax = fmaxf(smax, __shfl_xor(smax, d));
-    if (K == KIND_F) {
-      wsync();
-      if (lane == 0) mt_seed(s, pair_seed(P.base_seed, ps.pp.id1, ps.pp.id2));
-      wsync();
-      mt_save(s, ps.state);
-    }
+    wsync();
+    if (lane == 0)
+      mt_seed(s, K == KIND_F ? pair_seed(P.base_seed, ps.pp.id1, ps.pp.id2)
+                             : pair_seed_h(P.base_seed, ps.pp.id1, ps.pp.id2));
+    wsync();
+    mt_save(s, ps.state);
     uint16_t* sidx = pair_sidx(ps);
     for (int i = lane; i < n; i += 64) sidx[i] = (uint16_t)i;
     if (lane == 0) {
@@ -1761,21 +1765,21 @@ __global__ __launch_bounds__(64) void rs_begin_kernel(
 // indices (RandomSampler::Sample); the PRNG state before each round of 64 is
 // kept in wsnap for the abort rewind, the state after the window in snaps.
 template <int K>
-__global__ __launch_bounds__(64) void rs_draw_kernel(
+__device__ __attribute__((always_inline)) void rs_draw_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, RansacState* __restrict__ rst,
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
     int32_t* __restrict__ nact_next, uint16_t* __restrict__ samp, uint32_t* __restrict__ cnts,
-    uint32_t* __restrict__ wsnap, int W) {
+    uint32_t* __restrict__ wsnap, int W, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
   const int lane = threadIdx.x;
-  if (blockIdx.x == 0 && lane == 0) *nact_next = 0;
+  if (bid == 0 && lane == 0) *nact_next = 0;
   const int na = *nact;
-  for (int a = blockIdx.x; a < na; a += gridDim.x) {
+  for (int a = bid; a < na; a += nblk) {
     const int q = act[a];
-    const PairSetup ps = pair_at(pairs, q, scratch, snaps, out);
+    const PairSetup ps = pair_at<K>(pairs, q, scratch, snaps, out);
     const int n = ps.n;
     const int Btot = min(kTrialBatch * W, rst[q].max_trials - rst[q].trial);
     wsync();
@@ -1817,21 +1821,21 @@ __global__ __launch_bounds__(64) void rs_draw_kernel(
 // block) so that every swap costs one LDS round trip.  The targets drawn by
 // rs_draw_kernel are read from samp and replaced by the trial's sample.
 template <int K>
-__global__ __launch_bounds__(64) void rs_shuffle_kernel(
+__device__ __attribute__((always_inline)) void rs_shuffle_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
     const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
-    const int32_t* __restrict__ nact, uint16_t* __restrict__ samp, int ppb, int stride) {
+    const int32_t* __restrict__ nact, uint16_t* __restrict__ samp, int ppb, int stride, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   uint16_t* lsidx = reinterpret_cast<uint16_t*>(dyn_lds);
   const int na = *nact;
-  const int a0 = blockIdx.x * ppb;
+  const int a0 = bid * ppb;
   if (a0 >= na) return;
   const int np = min(ppb, na - a0);
   // Stage the sample-index vectors of this block's ppb pairs in LDS (every
   // thread helps), run one pair's swap chain per lane, write them back.
   for (int l = 0; l < np; ++l) {
-    const PairSetup pl = pair_at(pairs, act[a0 + l], scratch, snaps, out);
+    const PairSetup pl = pair_at<K>(pairs, act[a0 + l], scratch, snaps, out);
     const uint16_t* g = pair_sidx(pl);
     for (int i = threadIdx.x; i < pl.n; i += 64) lsidx[l * stride + i] = g[i];
   }
@@ -1866,7 +1870,7 @@ __global__ __launch_bounds__(64) void rs_shuffle_kernel(
   }
   __syncthreads();
   for (int l = 0; l < np; ++l) {
-    const PairSetup pl = pair_at(pairs, act[a0 + l], scratch, snaps, out);
+    const PairSetup pl = pair_at<K>(pairs, act[a0 + l], scratch, snaps, out);
     uint16_t* g = pair_sidx(pl);
     for (int i = threadIdx.x; i < pl.n; i += 64) g[i] = lsidx[l * stride + i];
   }
@@ -2053,7 +2057,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
 
 // The sequential part of one window, in trial order, for every active pair.
 template <int K>
-__global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay_kernel(
+__device__ __attribute__((always_inline)) void rs_replay_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
     RansacState* __restrict__ rst, const int32_t* __restrict__ act,
@@ -2061,7 +2065,7 @@ __global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay_kernel(
     int32_t* __restrict__ nact_next, const int32_t* __restrict__ nmod,
     const uint32_t* __restrict__ cnts, const double* __restrict__ mods,
     const uint32_t* __restrict__ wsnap, VerifyParams P, uint64_t* __restrict__ prof,
-    const float4* __restrict__ xyf_all) {
+    const float4* __restrict__ xyf_all, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
@@ -2069,7 +2073,7 @@ __global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay_kernel(
   const int lane = threadIdx.x;
   const double maxr = P.max_residual;
   const int na = *nact;
-  for (int a = blockIdx.x; a < na; a += gridDim.x) {
+  for (int a = bid; a < na; a += nblk) {
     const int q = act[a];
     // Diagnostic counters (SCM_PROFILE=1 only): windows, candidates, ties,
     // new bests, LO iterations; cycles in candidate residuals, tie sums, LO,
@@ -2077,7 +2081,7 @@ __global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay_kernel(
     uint64_t* pc = prof ? prof + (int64_t)q * kVerifyProfSlots + (K == KIND_F ? 20 : 30) : nullptr;
     const uint64_t t_enter = pc ? __builtin_amdgcn_s_memtime() : 0;
     if (pc && lane == 0) pc[0] += 1;
-    const PairSetup ps = pair_at(pairs, q, scratch, snaps, out);
+    const PairSetup ps = pair_at<K>(pairs, q, scratch, snaps, out);
     const int n = ps.n;
     double* base = ps.base;
     double* res[2] = {base, base + n};
@@ -2267,6 +2271,66 @@ __global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// Window kernels over both RANSAC kinds at once: blocks [0, split) run the F
+// LO-RANSAC of every active pair, blocks [split, grid) the H LO-RANSAC (its
+// own PRNG stream, pair_seed_h), so one launch sequence advances both and the
+// latency-bound per-pair kernels carry twice the pairs.  split == grid: F
+// only (H has run out of windows).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(64) void rs_begin2_kernel(
+    const VerifyPair* __restrict__ pairs, int npairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
+    const float4* __restrict__ xyf, VerifyRoundBufs rf, VerifyRoundBufs rh, VerifyParams P,
+    int split) {
+  if ((int)blockIdx.x < split)
+    rs_begin_body<KIND_F>(pairs, npairs, scratch, snaps, out, masks, xyf, rf.rst, rf.act[0],
+                          rf.nact, P, blockIdx.x, split);
+  else
+    rs_begin_body<KIND_H>(pairs, npairs, scratch, snaps, out, masks, xyf, rh.rst, rh.act[0],
+                          rh.nact, P, blockIdx.x - split, gridDim.x - split);
+}
+
+__global__ __launch_bounds__(64) void rs_draw2_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
+    VerifyRoundBufs rh, int cur, int W, int split) {
+  if ((int)blockIdx.x < split)
+    rs_draw_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[cur], rf.nact + cur,
+                         rf.nact + (cur ^ 1), rf.samp, rf.cnts, rf.wsnap, W, blockIdx.x, split);
+  else
+    rs_draw_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[cur], rh.nact + cur,
+                         rh.nact + (cur ^ 1), rh.samp, rh.cnts, rh.wsnap, W, blockIdx.x - split,
+                         gridDim.x - split);
+}
+
+__global__ __launch_bounds__(64) void rs_shuffle2_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
+    VerifyRoundBufs rh, int cur, int ppb, int stride, int split) {
+  if ((int)blockIdx.x < split)
+    rs_shuffle_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[cur], rf.nact + cur,
+                            rf.samp, ppb, stride, blockIdx.x, split);
+  else
+    rs_shuffle_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[cur], rh.nact + cur,
+                            rh.samp, ppb, stride, blockIdx.x - split, gridDim.x - split);
+}
+
+__global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay2_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
+    VerifyRoundBufs rf, VerifyRoundBufs rh, int cur, VerifyParams P, uint64_t* __restrict__ prof,
+    const float4* __restrict__ xyf, int split) {
+  if ((int)blockIdx.x < split)
+    rs_replay_body<KIND_F>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[cur], rf.nact + cur,
+                           rf.act[cur ^ 1], rf.nact + (cur ^ 1), rf.nmod, rf.cnts, rf.mods,
+                           rf.wsnap, P, prof, xyf, blockIdx.x, split);
+  else
+    rs_replay_body<KIND_H>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[cur], rh.nact + cur,
+                           rh.act[cur ^ 1], rh.nact + (cur ^ 1), rh.nmod, rh.cnts, rh.mods,
+                           rh.wsnap, P, prof, xyf, blockIdx.x - split, gridDim.x - split);
+}
+
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
                               const float2* __restrict__ kpxy, double* __restrict__ xy1,
                               double* __restrict__ xy2, const int32_t* __restrict__ counts,
@@ -2315,15 +2379,16 @@ void set_lds_attr(F f) {
                             160 * 1024);
 }
 
-// Windows of one RANSAC kind (W = 1, 2, 4, ..., kMaxWindow rounds) until the
-// trial cap; kernels of windows with no active pair exit at once.
-template <int K>
-hipError_t run_rounds(const VerifyPair* pairs, int npairs, const double* xy1, const double* xy2,
-                      double* scratch, uint32_t* snaps, uint8_t* masks, VerifyOut* out,
-                      const VerifyParams& P, const float4* xyf, const VerifyRoundBufs& rb,
-                      int max_chunks, int max_m, uint64_t* prof, hipStream_t stream) {
+// Windows of both RANSAC kinds (W = 1, 2, 4, ..., kMaxWindow rounds) until
+// each kind's trial cap: draw / shuffle / replay as dual-kind launches, the
+// wide solve and score kernels per kind.  Kernels of windows with no active
+// pair exit at once.
+hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, const double* xy2,
+                       double* scratch, uint32_t* snaps, uint8_t* masks, VerifyOut* out,
+                       const VerifyParams& P, const float4* xyf, const VerifyRoundBufs& rf,
+                       const VerifyRoundBufs& rh, int max_chunks, int max_m, uint64_t* prof,
+                       hipStream_t stream) {
   const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
-  const int max_trials = K == KIND_F ? P.max_trials_F : P.max_trials_H;
   const int gw = npairs < 4096 ? npairs : 4096;
 #ifndef SCM_SHUFFLE_LDS_KB
 #define SCM_SHUFFLE_LDS_KB 16
@@ -2333,24 +2398,36 @@ hipError_t run_rounds(const VerifyPair* pairs, int npairs, const double* xy1, co
   // shortens every step of them).
   const int sh_stride = (max_m + 7) / 8 * 8;
   const int sh_ppb = std::max(1, std::min(64, (SCM_SHUFFLE_LDS_KB * 1024) / (2 * sh_stride)));
+  const int sh_blocks = (npairs + sh_ppb - 1) / sh_ppb;
   int covered = 0, W = 1, r = 0;
-  while (covered < max_trials) {
-    const int cur = r & 1, nxt = cur ^ 1;
-    hipLaunchKernelGGL(rs_draw_kernel<K>, dim3(gw), dim3(64), lds, stream, pairs, scratch, snaps,
-                       out, rb.rst, rb.act[cur], rb.nact + cur, rb.nact + nxt, rb.samp, rb.cnts,
-                       rb.wsnap, W);
-    hipLaunchKernelGGL(rs_shuffle_kernel<K>, dim3((npairs + sh_ppb - 1) / sh_ppb), dim3(64),
+  while (covered < P.max_trials_F || covered < P.max_trials_H) {
+    const int cur = r & 1;
+    const bool f = covered < P.max_trials_F, h = covered < P.max_trials_H;
+    const int g1 = (f ? gw : 0) + (h ? gw : 0), s1 = f ? gw : 0;
+    const int g2 = (f ? sh_blocks : 0) + (h ? sh_blocks : 0), s2 = f ? sh_blocks : 0;
+    hipLaunchKernelGGL(rs_draw2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
+                       out, rf, rh, cur, W, s1);
+    hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
                        (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch, snaps,
-                       out, rb.rst, rb.act[cur], rb.nact + cur, rb.samp, sh_ppb, sh_stride);
-    hipLaunchKernelGGL(rs_solve_kernel<K>, dim3(4096), dim3(64), 0, stream, pairs, xy1, xy2,
-                       rb.rst, rb.act[cur], rb.nact + cur, rb.samp, rb.nmod, rb.fcon, rb.mods, W,
-                       P.max_residual);
-    hipLaunchKernelGGL(rs_score_kernel<K>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs, xyf,
-                       rb.rst, rb.act[cur], rb.nact + cur, rb.nmod, rb.fcon, rb.mods, rb.cnts,
-                       max_chunks, W, P.max_residual, prof);
-    hipLaunchKernelGGL(rs_replay_kernel<K>, dim3(gw), dim3(64), lds, stream, pairs, scratch, snaps, out, masks, rb.rst, rb.act[cur], rb.nact + cur,
-                       rb.act[nxt], rb.nact + nxt, rb.nmod, rb.cnts, rb.mods, rb.wsnap, P, prof,
-                       xyf);
+                       out, rf, rh, cur, sh_ppb, sh_stride, s2);
+    if (f)
+      hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(4096), dim3(64), 0, stream, pairs, xy1, xy2,
+                         rf.rst, rf.act[cur], rf.nact + cur, rf.samp, rf.nmod, rf.fcon, rf.mods,
+                         W, P.max_residual);
+    if (h)
+      hipLaunchKernelGGL(rs_solve_kernel<KIND_H>, dim3(4096), dim3(64), 0, stream, pairs, xy1, xy2,
+                         rh.rst, rh.act[cur], rh.nact + cur, rh.samp, rh.nmod, rh.fcon, rh.mods,
+                         W, P.max_residual);
+    if (f)
+      hipLaunchKernelGGL(rs_score_kernel<KIND_F>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs,
+                         xyf, rf.rst, rf.act[cur], rf.nact + cur, rf.nmod, rf.fcon, rf.mods,
+                         rf.cnts, max_chunks, W, P.max_residual, prof);
+    if (h)
+      hipLaunchKernelGGL(rs_score_kernel<KIND_H>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs,
+                         xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon, rh.mods,
+                         rh.cnts, max_chunks, W, P.max_residual, prof);
+    hipLaunchKernelGGL(rs_replay2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
+                       out, masks, rf, rh, cur, P, prof, xyf, s1);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     covered += W * kTrialBatch;
@@ -2365,19 +2442,15 @@ hipError_t run_rounds(const VerifyPair* pairs, int npairs, const double* xy1, co
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
-                         const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb,
-                         hipStream_t stream) {
+                         const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb_f,
+                         const VerifyRoundBufs& rb_h, hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(rs_begin_kernel<KIND_F>);
-    set_lds_attr(rs_begin_kernel<KIND_H>);
-    set_lds_attr(rs_draw_kernel<KIND_F>);
-    set_lds_attr(rs_shuffle_kernel<KIND_F>);
-    set_lds_attr(rs_shuffle_kernel<KIND_H>);
-    set_lds_attr(rs_draw_kernel<KIND_H>);
-    set_lds_attr(rs_replay_kernel<KIND_F>);
-    set_lds_attr(rs_replay_kernel<KIND_H>);
+    set_lds_attr(rs_begin2_kernel);
+    set_lds_attr(rs_draw2_kernel);
+    set_lds_attr(rs_shuffle2_kernel);
+    set_lds_attr(rs_replay2_kernel);
     set_lds_attr(verify_final_kernel);
     attr = true;
   }
@@ -2385,19 +2458,14 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   const int gw = npairs < 4096 ? npairs : 4096;
   const int max_chunks = (max_m + kScoreChunk - 1) / kScoreChunk;
   hipError_t err;
-  // F: LORANSAC<7-pt, 8-pt>, then the F inlier masks.
-  if ((err = hipMemsetAsync(rb.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
-  hipLaunchKernelGGL(rs_begin_kernel<KIND_F>, dim3(gw), dim3(64), kVerifyLdsHead, stream, pairs, npairs,
-                     scratch, snaps, out, masks, xyf, rb.rst, rb.act[0], rb.nact, params);
-  if ((err = run_rounds<KIND_F>(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf,
-                                rb, max_chunks, max_m, prof, stream)) != hipSuccess)
-    return err;
-  // H: LORANSAC<H, H> on the same PRNG streams.
-  if ((err = hipMemsetAsync(rb.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
-  hipLaunchKernelGGL(rs_begin_kernel<KIND_H>, dim3(gw), dim3(64), kVerifyLdsHead, stream, pairs, npairs,
-                     scratch, snaps, out, masks, xyf, rb.rst, rb.act[0], rb.nact, params);
-  if ((err = run_rounds<KIND_H>(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf,
-                                rb, max_chunks, max_m, prof, stream)) != hipSuccess)
+  // LORANSAC<7-pt, 8-pt> (F, then its inlier masks) and LORANSAC<H, H>, each
+  // on its own PRNG stream, advanced together window by window.
+  if ((err = hipMemsetAsync(rb_f.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  if ((err = hipMemsetAsync(rb_h.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  hipLaunchKernelGGL(rs_begin2_kernel, dim3(2 * gw), dim3(64), kVerifyLdsHead, stream, pairs,
+                     npairs, scratch, snaps, out, masks, xyf, rb_f, rb_h, params, gw);
+  if ((err = run_windows(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf, rb_f,
+                         rb_h, max_chunks, max_m, prof, stream)) != hipSuccess)
     return err;
   hipLaunchKernelGGL(verify_final_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
                      xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
