@@ -45,6 +45,8 @@ struct PairDesc {
   int64_t m21_off;      // int32 offset: [n2]
   int64_t match_off;    // uint2 offset: [n1]
   int64_t a_row;        // table row of the pivot's descriptor 0 (finalize recompute)
+  int64_t aux_off;      // uint2 offset: [n1] row (best, second lower bound) (v2 finalize)
+  int64_t rlist_off;    // int32 offset: [33 + n1] row-recheck buckets (v2 finalize)
   int32_t n1, n2, n2pad, nseg, nrb;
   int32_t clamp;        // 1: the pivot run took the CLAMP matcher variant
 };
@@ -61,7 +63,8 @@ hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const Matc
                            int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
                            bool clamp, hipStream_t stream);
 hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* rowres,
-                                    uint2* colpart, const uint8_t* desc8, const int32_t* csum,
+                                    uint2* colpart, uint2* rowaux, int32_t* rlist,
+                                    const uint8_t* desc8, const int32_t* csum,
                                     const float* lut, float max_ratio, float max_distance,
                                     int cross_check, uint2* matches, int32_t* counts,
                                     int max_groups, hipStream_t stream);

@@ -40,6 +40,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <climits>
+
 #include "match_kernels.h"
 
 namespace scm {
@@ -117,6 +119,36 @@ __device__ __forceinline__ void row_flush(const uint32_t (&b1r)[2][16], const ui
       const uint32_t col = tl * 32u + (uint32_t)r;
       uint32_t B1 = (k1 & ~kIdxMask) | (kIdxMask - col);
       uint32_t B2 = b2r[s][i] & ~kIdxMask;
+#pragma unroll
+      for (int x = 1; x < 32; x <<= 1) {
+        const uint32_t o1 = __shfl_xor(B1, x);
+        const uint32_t o2 = __shfl_xor(B2, x);
+        B2 = merge_second(B1, B2, o1, o2);
+        B1 = max(B1, o1);
+      }
+      const int row = row0 + 32 * s + (i & 3) + 8 * (i >> 2) + 4 * h;
+      if (r == i + 16 * s && row < n1) rr[row] = make_uint2(B1, B2);
+    }
+  }
+}
+
+// Row flush of the v2 matcher (best-only row state): each lane holds, per
+// row, the best key over ITS columns only (column = lane + 32 t); re-keyed
+// with the column and reduced over the 32 lanes this gives the row's exact
+// best and, as second, the best of the OTHER lanes: a lower bound of the
+// row's second that misses only the second within the winning lane
+// (recomputed exactly by match_rowcheck_g8_kernel where it matters).
+__device__ __forceinline__ void row_flush_best(const uint32_t (&b1r)[2][16], uint2* rr, int row0,
+                                               int n1, int r, int h) {
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t k1 = b1r[s][i];
+      const uint32_t tl = (uint32_t)(kTilesPerSeg - 1) - (k1 & 255u);
+      const uint32_t col = tl * 32u + (uint32_t)r;
+      uint32_t B1 = (k1 & ~kIdxMask) | (kIdxMask - col);
+      uint32_t B2 = 0u;
 #pragma unroll
       for (int x = 1; x < 32; x <<= 1) {
         const uint32_t o1 = __shfl_xor(B1, x);
@@ -729,8 +761,7 @@ __device__ __forceinline__ i32x16 g8_chain(const i32x4 (&a)[4], const i32x4 (&b)
 // the largest raw accumulator of the lane's 16 rows (column side).
 template <bool CLAMP>
 __device__ __forceinline__ uint32_t g8_epilogue(const i32x16& acc, uint32_t kc, uint32_t cbm,
-                                                uint32_t tbits, uint32_t (&b1r)[16],
-                                                uint32_t (&b2r)[16]) {
+                                                uint32_t tbits, uint32_t (&b1r)[16]) {
 #ifdef SCM_DIAG_MATCH_SKELETON
   // diagnostics only: MFMA + LDS + staging skeleton, results discarded
   uint32_t xs = 0;
@@ -743,7 +774,6 @@ __device__ __forceinline__ uint32_t g8_epilogue(const i32x16& acc, uint32_t kc, 
   for (int i = 0; i < 16; ++i) {
     const uint32_t x = (uint32_t)acc[i];
     const uint32_t key = CLAMP ? (min(x + cbm, kLutMax) << 13) | tbits : (x << 13) + kc;
-    b2r[i] = med3_u32(key, b1r[i], b2r[i]);
     b1r[i] = max(b1r[i], key);
   }
 #ifdef SCM_DIAG_G8_TOP2
@@ -884,11 +914,11 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
   int64_t cpi = pd.colpart_off + (int64_t)job.rb * pd.n2pad;  // colpart index of tile 0 of pair p
   int flushed = -8;  // iteration of the last row flush (its stores)
 
-  uint32_t b1r[2][16], b2r[2][16];
+  uint32_t b1r[2][16];  // per lane and row: best key over this lane's columns
 #pragma unroll
   for (int s = 0; s < 2; ++s)
 #pragma unroll
-    for (int i = 0; i < 16; ++i) { b1r[s][i] = 0u; b2r[s][i] = 0u; }
+    for (int i = 0; i < 16; ++i) b1r[s][i] = 0u;
 
   i32x4 bf0[4], bf1[4];
 #ifdef SCM_G8_STAGGER  // diagnostics: delay waves 4-7 (the second half of each SIMD pair)
@@ -914,18 +944,18 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
     // (s1, c0) || epilogue (s0, c0); the c1 fragments load under the epilogue
     i32x16 acc2 = g8_chain(afrag[1], bf0, ra[1]);
     load_bfrag8(cur, 32 + r, h, bf1);
-    const uint32_t e00 = g8_epilogue<CLAMP>(acc, kc0, cbm0, tb0, b1r[0], b2r[0]);
+    const uint32_t e00 = g8_epilogue<CLAMP>(acc, kc0, cbm0, tb0, b1r[0]);
     __builtin_amdgcn_sched_barrier(0);
     // (s0, c1) || epilogue (s1, c0)
     acc = g8_chain(afrag[0], bf1, ra[0]);
-    const uint32_t e10 = g8_epilogue<CLAMP>(acc2, kc0, cbm0, tb0, b1r[1], b2r[1]);
+    const uint32_t e10 = g8_epilogue<CLAMP>(acc2, kc0, cbm0, tb0, b1r[1]);
     g8_col_partial(e00, e10, cscw, h, r);
     __builtin_amdgcn_sched_barrier(0);
     // (s1, c1) || epilogue (s0, c1); inside a group the next tile's c0
     // fragments load under the epilogue (at a group end only after the barrier)
     acc2 = g8_chain(afrag[1], bf1, ra[1]);
     if (!group_end) g8_next(lds, g + 1, r, h, bf0, cbn0, cbn1);
-    const uint32_t e01 = g8_epilogue<CLAMP>(acc, kc1, cbm1, tb1, b1r[0], b2r[0]);
+    const uint32_t e01 = g8_epilogue<CLAMP>(acc, kc1, cbm1, tb1, b1r[0]);
     __builtin_amdgcn_sched_barrier(0);
     if (group_end) {
       // Barrier m.  This wave's DMA of group m + 1 (issued at barrier m - 2)
@@ -952,16 +982,16 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
     }
     // (g + 1: s0, c0) || epilogue (s1, c1)
     acc = g8_chain(afrag[0], bf0, ra[0]);
-    const uint32_t e11 = g8_epilogue<CLAMP>(acc2, kc1, cbm1, tb1, b1r[1], b2r[1]);
+    const uint32_t e11 = g8_epilogue<CLAMP>(acc2, kc1, cbm1, tb1, b1r[1]);
     g8_col_partial(e01, e11, cscw + 32, h, r);
     // Row flush at the end of a segment (or of the pair).
     if (k == kTiles8PerSeg - 1 || t + 1 == nt) {
-      row_flush(b1r, b2r, rowres + pd.rowres_off + (int64_t)(t / kTiles8PerSeg) * pd.n1, row0,
+      row_flush_best(b1r, rowres + pd.rowres_off + (int64_t)(t / kTiles8PerSeg) * pd.n1, row0,
                 pd.n1, r, h);
 #pragma unroll
       for (int s = 0; s < 2; ++s)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) { b1r[s][i] = 0u; b2r[s][i] = 0u; }
+        for (int i = 0; i < 16; ++i) b1r[s][i] = 0u;
       flushed = g;
     }
     if (++t == nt && p + 1 < job.npairs) {
@@ -1132,11 +1162,13 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
 
 __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     const PairDesc* __restrict__ pairs, uint2* __restrict__ rowres, uint2* __restrict__ colpart,
+    uint2* __restrict__ rowaux, int32_t* __restrict__ rlist,
     const uint8_t* __restrict__ desc8, const int32_t* __restrict__ csum,
     const float* __restrict__ lut, float max_ratio, float max_distance, int cross_check,
     uint2* __restrict__ matches, int32_t* __restrict__ counts, int phase) {
   __shared__ int32_t wave_tot[kFinThreads / 64];
   __shared__ int32_t wave_off[kFinThreads / 64];
+  __shared__ int32_t bcnt[32], bcur[32];
   const PairDesc pd = pairs[blockIdx.x];
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -1189,6 +1221,15 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     __syncthreads();
   }
   // Phase 2: per-row decisions, contiguous chunk per thread (phase 4 order).
+  // The rows' seconds are lower bounds (best of the other lanes, see
+  // row_flush_best): a row that fails with it fails; a row that passes (and,
+  // with the cross-check, can still be its column's match) is queued for the
+  // exact second in the bucket of its best column's lane residue (state 3,
+  // match_rowcheck_g8_kernel).
+  int32_t* rl = rlist + pd.rlist_off;
+  uint2* ax = rowaux + pd.aux_off;
+  if (tid < 32) bcnt[tid] = 0;
+  __syncthreads();
   for (int i = i0; i < i1; ++i) {
     uint2 m = rr[i];
     int best_seg = 0;
@@ -1199,17 +1240,34 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     }
     const uint32_t best = m.x >> kIdxBits, second = m.y >> kIdxBits;
     const int32_t col = best_seg * (kTilesPerSeg * 32) + (int32_t)(kIdxMask - (m.x & kIdxMask));
-    uint32_t state = passes(lut, best, second, max_ratio, max_distance) ? 1u : 0u;
+    uint32_t state = passes(lut, best, second, max_ratio, max_distance) ? 3u : 0u;
     if (state && cross_check) {
       const uint2 c = cp[col];
       const uint32_t b1 = c.x & kV, rb = c.x >> 19, w = c.y & 7u, b2 = c.y >> 3;
       const uint32_t grp = rb * (uint32_t)(kRowsPerBlock8 / 64) + w;
       if (b1 != best || grp != (uint32_t)(i >> 6) || !passes(lut, b1, b2, max_ratio, max_distance))
         state = 0u;
-      else
-        state = 2u;  // decided by the exact second within the group (phase 3)
     }
     rr[i] = make_uint2((uint32_t)col, state);
+    if (state == 3u) {
+      ax[i] = make_uint2(best, second);
+      atomicAdd(&bcnt[col & 31], 1);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int acc = 0;
+    for (int b = 0; b < 32; ++b) {
+      rl[b] = acc;
+      bcur[b] = acc;
+      acc += bcnt[b];
+    }
+    rl[32] = acc;
+  }
+  __syncthreads();
+  for (int i = i0; i < i1; ++i) {
+    const uint2 st = rr[i];
+    if (st.y == 3u) rl[33 + atomicAdd(&bcur[st.x & 31u], 1)] = i;
   }
   return;
   }
@@ -1234,6 +1292,96 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
   for (int i = i0; i < i1; ++i) {
     const uint2 st = rr[i];
     if (st.y == 1u) matches[pd.match_off + out++] = make_uint2((uint32_t)i, st.x);
+  }
+}
+
+// Exact row seconds of the version-2 finalize (phase 2b).  The matcher keeps
+// per lane only the best key of each row over that lane's columns (j = lane +
+// 32 t), so the row's second is known up to the second within the winning
+// lane.  One workgroup per (pair, lane residue b): the queued rows whose best
+// column is ≡ b (mod 32) against every column ≡ b (mod 32) of the neighbour
+// (staged in LDS, 256 at a time), on the matcher's own MFMA with the same
+// offset operands: A = those columns (C operand = their sums), B = the rows;
+// per row the exact top-2 (multiset) over the residue class.  With it the
+// row's second is exact (max of the lower bound and the in-class second) and
+// the ratio / distance test final: the row becomes a candidate of the
+// column check (2, cross-check) or a match (1).
+constexpr int kRcThreads = 256;
+constexpr int kRcChunk = 256;  // columns of one residue class staged per pass (32 KiB)
+
+__global__ __launch_bounds__(kRcThreads) void match_rowcheck_g8_kernel(
+    const PairDesc* __restrict__ pairs, uint2* __restrict__ rowres,
+    const uint2* __restrict__ rowaux, const int32_t* __restrict__ rlist,
+    const uint8_t* __restrict__ desc8, const int32_t* __restrict__ csum,
+    const float* __restrict__ lut, float max_ratio, float max_distance, int cross_check) {
+  __shared__ __attribute__((aligned(16))) uint8_t lcol[kRcChunk * 128];
+  __shared__ int32_t lcs[kRcChunk + 32];
+  const PairDesc pd = pairs[blockIdx.y];
+  const int b = blockIdx.x;
+  if (pd.n1 == 0 || pd.n2 <= b) return;
+  const int32_t* rl = rlist + pd.rlist_off;
+  const int q0 = rl[b], R = rl[b + 1] - q0;
+  if (R <= 0) return;
+  const int32_t* rows = rl + 33 + q0;
+  const int Cb = (pd.n2 - b + 31) / 32;  // columns b, b + 32, ... < n2
+  const int nchunks = (Cb + kRcChunk - 1) / kRcChunk;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r = lane & 31, h = lane >> 5;
+  uint2* rr = rowres + pd.rowres_off;
+  const uint2* ax = rowaux + pd.aux_off;
+  for (int g0 = 0; g0 < R; g0 += 4 * 32) {  // row groups: 4 waves x 32 rows
+    const int k = g0 + wave * 32 + r;
+    const bool rv = k < R;
+    const int row = rows[rv ? k : 0];
+    i32x4 bfr[4];
+    {
+      const i32x4* src = reinterpret_cast<const i32x4*>(desc8 + (pd.a_row + row) * 128) + 4 * h;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bfr[q] = src[q];
+    }
+    int t1 = INT_MIN, t2 = INT_MIN;  // this lane's top-2 (multiset) over its columns
+    for (int c = 0; c < nchunks; ++c) {
+      const int cbeg = c * kRcChunk, cn = min(kRcChunk, Cb - cbeg);
+      if (nchunks > 1 || g0 == 0) {
+        __syncthreads();
+        for (int e = tid; e < cn * 8; e += kRcThreads) {
+          const int x = e >> 3, ch = e & 7;
+          const int64_t j = b + 32 * (int64_t)(cbeg + x);
+          *reinterpret_cast<i32x4*>(lcol + sw8(x, ch)) =
+              *reinterpret_cast<const i32x4*>(desc8 + (pd.b_row + j) * 128 + ch * 16);
+        }
+        for (int x = tid; x < cn; x += kRcThreads) lcs[x] = csum[pd.b_row + b + 32 * (int64_t)(cbeg + x)];
+        __syncthreads();
+      }
+      for (int ct = 0; ct * 32 < cn; ++ct) {
+        i32x4 afr[4];
+        load_bfrag8(lcol, ct * 32 + r, h, afr);  // column ct*32 + r, chunk 4h + q
+        i32x16 cinit;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) cinit[i] = lcs[ct * 32 + 4 * h + (i & 3) + 8 * (i >> 2)];
+        const i32x16 acc = chain8(afr, bfr, cinit);  // a'.b' + cs(column): dot - cs(row) + 2^21
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int x = ct * 32 + 4 * h + (i & 3) + 8 * (i >> 2);
+          const int v = x < cn ? acc[i] : INT_MIN;
+          t2 = max(t2, min(t1, v));
+          t1 = max(t1, v);
+        }
+      }
+    }
+    // The two lane halves hold the class's columns 4h + (i & 3) + 8 (i >> 2) of
+    // each 32-column tile: merge them (symmetric in the two halves).
+    const auto e1 = __builtin_amdgcn_permlane32_swap(t1, t1, false, false);
+    const auto e2 = __builtin_amdgcn_permlane32_swap(t2, t2, false, false);
+    if (h == 0 && rv) {
+      const int s2 = max(max((int)e2[0], (int)e2[1]), min((int)e1[0], (int)e1[1]));
+      const uint2 a = ax[row];
+      const int32_t rowsum = csum[pd.a_row + row] - (1 << 21);
+      uint32_t d2 = s2 == INT_MIN ? 0u : (uint32_t)(s2 + rowsum);  // one column only: second 0
+      if (pd.clamp) d2 = min(d2, kLutMax);
+      const uint32_t second = max(a.y, d2);
+      const bool ok = passes(lut, a.x, second, max_ratio, max_distance);
+      rr[row] = make_uint2(rr[row].x, ok ? (cross_check ? 2u : 1u) : 0u);
+    }
   }
 }
 
@@ -1409,21 +1557,25 @@ hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const Matc
 }
 
 hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* rowres,
-                                    uint2* colpart, const uint8_t* desc8, const int32_t* csum,
+                                    uint2* colpart, uint2* rowaux, int32_t* rlist,
+                                    const uint8_t* desc8, const int32_t* csum,
                                     const float* lut, float max_ratio, float max_distance,
                                     int cross_check, uint2* matches, int32_t* counts,
                                     int max_groups, hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
   hipLaunchKernelGGL(match_finalize_g8_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
-                     rowres, colpart, desc8, csum, lut, max_ratio, max_distance, cross_check,
-                     matches, counts, 0);
+                     rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
+                     cross_check, matches, counts, 0);
+  hipLaunchKernelGGL(match_rowcheck_g8_kernel, dim3(32, npairs), dim3(kRcThreads), 0, stream,
+                     pairs, rowres, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
+                     cross_check);
   if (cross_check && max_groups > 0)
     hipLaunchKernelGGL(match_recheck_g8_kernel, dim3((unsigned)((max_groups + 3) / 4), npairs),
                        dim3(256), 0, stream, pairs, rowres, colpart, desc8, csum, lut, max_ratio,
                        max_distance);
   hipLaunchKernelGGL(match_finalize_g8_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
-                     rowres, colpart, desc8, csum, lut, max_ratio, max_distance, cross_check,
-                     matches, counts, 1);
+                     rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
+                     cross_check, matches, counts, 1);
   return hipGetLastError();
 }
 

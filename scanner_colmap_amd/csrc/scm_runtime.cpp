@@ -93,6 +93,7 @@ struct PinnedOut {
 
 // One in-flight batch: device workspace, descriptor staging, results.
 struct BatchSet {
+  DevBuf rowaux, rlist;  // v2 finalize: row (best, second bound), row-recheck buckets
   DevBuf jobs, pairs, rowres, colpart, m21, matches, counts, gpairs, vpairs, xy1, xy2, scratch,
       snaps, masks, offsets, match_off, prof, xyf, dvout, dpack, dpmask, rst, samp, nmod, fcon,
       cnts, act, nact, mods, wsnap;
@@ -114,7 +115,7 @@ struct BatchSet {
   bool posted = false;   // stage 2 enqueued
   bool matched = false;
   void release() {
-    for (DevBuf* b : {&jobs, &pairs, &rowres, &colpart, &m21, &matches, &counts, &gpairs, &vpairs,
+    for (DevBuf* b : {&rowaux, &rlist, &jobs, &pairs, &rowres, &colpart, &m21, &matches, &counts, &gpairs, &vpairs,
                       &xy1, &xy2, &scratch, &snaps, &masks, &offsets, &match_off, &prof, &xyf, &dvout,
                       &dpack, &dpmask, &rst, &samp, &nmod, &fcon, &cnts, &act, &nact,
                       &mods, &wsnap, &h_rst, &h_samp, &h_nmod, &h_fcon, &h_cnts, &h_act, &h_nact,
@@ -546,7 +547,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   };
   std::vector<Run> runs;
   bs.moff.resize(P);
-  int64_t rr = 0, cp = 0, m21 = 0, mo = 0;
+  int64_t rr = 0, cp = 0, m21 = 0, mo = 0, ax = 0, rlo = 0;
   const int32_t rpb = ctx->match_bf16 ? kRowsPerBlock : kRowsPerBlock8;  // pivot rows per job
   for (int64_t i = 0; i < P;) {
     const int32_t a = specs[i].a;
@@ -570,6 +571,10 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
       pd.colpart_off = cp;
       pd.m21_off = m21;
       pd.match_off = mo;
+      pd.aux_off = ax;
+      pd.rlist_off = rlo;
+      ax += pd.n1;
+      rlo += 33 + (int64_t)pd.n1;
       bs.moff[k] = mo;
       rr += (int64_t)pd.nseg * pd.n1;
       cp += (int64_t)pd.nrb * pd.n2pad;
@@ -637,6 +642,8 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   SCM_TRY(bs.rowres.ensure(std::max<int64_t>(rr, 1) * sizeof(uint2)));
   SCM_TRY(bs.colpart.ensure(std::max<int64_t>(cp, 1) * sizeof(uint2)));
   SCM_TRY(bs.m21.ensure(std::max<int64_t>(m21, 1) * sizeof(int32_t)));
+  SCM_TRY(bs.rowaux.ensure(std::max<int64_t>(ax, 1) * sizeof(uint2)));
+  SCM_TRY(bs.rlist.ensure(std::max<int64_t>(rlo, 1) * sizeof(int32_t)));
   SCM_TRY(bs.matches.ensure(std::max<int64_t>(mo, 1) * sizeof(uint2)));
   SCM_TRY(bs.masks.ensure(std::max<int64_t>(mo, 1)));
   SCM_TRY(bs.counts.ensure(P * sizeof(int32_t)));
@@ -700,7 +707,8 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   SCM_HIP(hipEventRecord(bs.ev[1], sm));
   if (!given && !ctx->match_bf16 && !ctx->match_i8v1)
     SCM_HIP(launch_match_finalize_g8(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
-                                     bs.colpart.as<uint2>(), t.desc8.as<uint8_t>(),
+                                     bs.colpart.as<uint2>(), bs.rowaux.as<uint2>(),
+                                     bs.rlist.as<int32_t>(), t.desc8.as<uint8_t>(),
                                      t.csum.as<int32_t>(), ctx->lut.as<float>(),
                                      (float)ctx->opts.max_ratio, (float)ctx->opts.max_distance,
                                      ctx->opts.cross_check, bs.matches.as<uint2>(),
@@ -1069,7 +1077,8 @@ int64_t pair_workspace_bytes(int64_t n1, int64_t n2) {
   const int64_t nrb = (n1 + rpb - 1) / rpb;
   const int64_t n2pad = (n2 + kTile8Cols - 1) / kTile8Cols * kTile8Cols;
   const int64_t slots = std::max<int64_t>(n1, 1);
-  const int64_t match = nseg * n1 * 8 + nrb * n2pad * 8 + n2 * 4 + slots * (8 + 1);
+  const int64_t match = nseg * n1 * 8 + nrb * n2pad * 8 + n2 * 4 + slots * (8 + 1) +
+                        n1 * 8 + (33 + n1) * 4;  // + v2 row aux and recheck buckets
   const int64_t verify_pts = slots * (16 + 16 + 16 + 8 + 1);  // xy1, xy2, xyf, dpack, dpmask
   const int64_t verify_pair = verify_scratch_doubles(slots) * 8 + kVerifySnapWords * 4 +
                               (int64_t)sizeof(RansacState) + (int64_t)sizeof(VerifyOut) +
@@ -1086,7 +1095,7 @@ int64_t set_budget_bytes(scm_context* ctx) {
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return INT64_MAX;
   int64_t held = 0;
   for (const BatchSet& bs : ctx->sets)
-    for (const DevBuf* b : {&bs.jobs, &bs.pairs, &bs.rowres, &bs.colpart, &bs.m21, &bs.matches,
+    for (const DevBuf* b : {&bs.rowaux, &bs.rlist, &bs.jobs, &bs.pairs, &bs.rowres, &bs.colpart, &bs.m21, &bs.matches,
                             &bs.counts, &bs.gpairs, &bs.vpairs, &bs.xy1, &bs.xy2, &bs.scratch,
                             &bs.snaps, &bs.masks, &bs.offsets, &bs.match_off, &bs.prof, &bs.xyf,
                             &bs.dvout, &bs.dpack, &bs.dpmask, &bs.rst, &bs.samp, &bs.nmod,
