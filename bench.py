@@ -29,6 +29,12 @@ sys.path.insert(0, ROOT)
 METRIC = "image-pairs/s + Gdesc-dist/s, 8192×8192-kpt pairs, 1/2/4/8 GPU"
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (spec)
 I8_DENSE_PEAK_TOPS = 5000.0      # MI355X_MICROARCH.md matrix cores: i8 32x32x32 = 2x the bf16 rate
+FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector, packed)
+# Reference residual arithmetic (upstream COLMAP estimators): ComputeSquaredSampsonError
+# (F x1, F^T x2, x2^T F x1, e^2 / (4 squares)) and HomographyMatrixEstimator::Residuals
+# (H s, one division, two differences, two squares).
+SAMPSON_FLOPS = 33
+TRANSFER_FLOPS = 20
 
 # BASELINE.json configs (synthetic stand-ins; no dataset is present).
 WORKLOADS = {
@@ -307,12 +313,17 @@ def main():
     match_ms = 0.0
     verify_ms = 0.0
     final_ms = 0.0
+    score_ms = 0.0
+    evals_f = evals_h = 0
     launches = 0
     for _ in range(args.steps):
         tm = step()
         match_ms += tm["match_ms"]
         verify_ms += tm["verify_ms"]
         final_ms += tm["finalize_ms"]
+        score_ms += tm["score_ms"]
+        evals_f += tm["evals_f"]
+        evals_h += tm["evals_h"]
         launches += tm["match_launches"]
     if world > 1:
         dist.barrier()
@@ -362,6 +373,7 @@ def main():
             parity = parity_check(ctx, last["packed"], lr_b, ref, check_pairs)
         drop_in = stencil_bench(ctx, stencil_src, overlap, srows,
                                 [int(x) for x in args.stencil_batches.split(",") if x]) if srows else None
+        score_flops = (SAMPSON_FLOPS + 1) * evals_f + (TRANSFER_FLOPS + 1) * evals_h
         # SURVEY.md §8d headline fraction: kernel-1 work over the whole step's wall time.
         wall_tops = flops_rank / elapsed / 1e12
         out = {
@@ -403,6 +415,24 @@ def main():
                                 "per-launch time from HIP events; peak = dense MFMA peak of the "
                                 "kernel's dtype (i8 5.0 POP/s, bf16 2.5 PFLOP/s); wall_* = the "
                                 "same ops over the whole step's wall time (SURVEY.md §8d)"),
+            },
+            "roofline_verify": {
+                "bound": "valu",
+                "kernel": "rs_score_kernel<F> + rs_score_kernel<H>",
+                "achieved": round(score_flops / (score_ms * 1e-3) / 1e12, 2) if score_ms > 0 else None,
+                "peak": FP32_VECTOR_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": (round(score_flops / (score_ms * 1e-3) / 1e12 / FP32_VECTOR_PEAK_TFLOPS, 4)
+                         if score_ms > 0 else None),
+                "evals_per_step": {"F": evals_f // steps, "H": evals_h // steps},
+                "score_ms_per_step": round(score_ms / steps, 3),
+                "algorithmic": ("reference residual arithmetic per (model, point): Sampson error "
+                                f"{SAMPSON_FLOPS} flops (F), transfer error {TRANSFER_FLOPS} flops (H), "
+                                "each + 1 compare, counted over the trials the sequential "
+                                "LO-RANSAC scores up to its stop; time = HIP events around "
+                                "each window's scoring kernels; peak = FP32 vector (packed) "
+                                "157.3 TF (MI355X_MICROARCH.md): the kernels evaluate packed "
+                                "fp32 filters with fp64 exact tests for undecided points"),
             },
             "stage_ms_per_step": {"match": round(match_ms / steps, 3),
                                   "finalize": round(final_ms / steps, 3),

@@ -219,7 +219,9 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset,
  * measured with HIP events on the context's stream:
  * t[0] = descriptor-distance + top-2 kernel, t[1] = match finalize,
  * t[2] = RANSAC hypothesis kernels, t[3] = whole run (wall),
- * t[4] = number of descriptor-distance kernel launches of the run. */
+ * t[4] = number of descriptor-distance kernel launches of the run,
+ * t[5] = inlier-scoring kernels (F + H), t[6] / t[7] = F / H (model, point)
+ * residual evaluations of the sequential LO-RANSAC up to its stop. */
 int scm_table_timings(scm_context* ctx, double* t, int32_t n);
 
 #ifdef __cplusplus

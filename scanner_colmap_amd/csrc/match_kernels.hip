@@ -752,6 +752,12 @@ __device__ __forceinline__ i32x16 g8_chain(const i32x4 (&a)[4], const i32x4 (&b)
   const i32x16 r = chain8(a, b, ra);
   __builtin_amdgcn_s_setprio(0);
   return r;
+#elif defined(SCM_DIAG_G9_TIMING)
+  // diagnostics only: a fifth MFMA per chain (the digit block), B from the
+  // first chunk's registers as a stand-in for its LDS fragment
+  i32x16 acc = chain8(a, b, ra);
+  const i32x4 c127 = {0x7F7F7F7F, 0x7F7F7F7F, 0x7F7F7F7F, 0x7F7F7F7F};
+  return __builtin_amdgcn_mfma_i32_32x32x32_i8(c127, b[0], acc, 0, 0, 0);
 #else
   return chain8(a, b, ra);
 #endif
@@ -770,12 +776,19 @@ __device__ __forceinline__ uint32_t g8_epilogue(const i32x16& acc, uint32_t kc, 
   b1r[0] ^= xs;
   return xs;
 #endif
+#ifdef SCM_DIAG_G9_TIMING
+  // diagnostics only (wrong results): the row state as a raw max, as the
+  // digit-MFMA design would keep it
+#pragma unroll
+  for (int i = 0; i < 16; ++i) b1r[i] = max(b1r[i], (uint32_t)acc[i]);
+#else
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
     const uint32_t x = (uint32_t)acc[i];
     const uint32_t key = CLAMP ? (min(x + cbm, kLutMax) << 13) | tbits : (x << 13) + kc;
     b1r[i] = max(b1r[i], key);
   }
+#endif
 #ifdef SCM_DIAG_G8_TOP2
   // diagnostics only: the cost of the exact column top-2 tree (result unchanged:
   // the second's bit 31 is always clear)

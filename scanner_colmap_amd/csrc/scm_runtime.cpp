@@ -105,6 +105,8 @@ struct BatchSet {
   // 0 match start, 1 tiles done, 2 finalize done, 3 counts on host (match
   // stream); 4 verify start, 5 verify done, 6 compaction done (verify stream)
   hipEvent_t ev[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t sev[2 * kMaxVerifyWindows] = {};  // around each window's scoring kernels
+  int nwin = 0;                                // windows of the last verification
   hipStream_t vstream = nullptr;  // verification stream of this set
   const ImageTable* table = nullptr;
   std::vector<PairSpec> specs;
@@ -125,6 +127,10 @@ struct BatchSet {
     vstage.release();
     out.release();
     for (auto& e : ev) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+    for (auto& e : sev) {
       if (e) (void)hipEventDestroy(e);
       e = nullptr;
     }
@@ -170,6 +176,8 @@ struct scm_context {
                             // top-2 column partials) instead of match_g8_kernel
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
+  double t_score = 0;                  // scoring kernels (F + H) of the last run
+  int64_t evals_f = 0, evals_h = 0;    // their (model, point) evaluations
   int64_t n_match_launches = 0;  // matcher kernel launches of the last table run
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
   bool profile = false;
@@ -856,11 +864,13 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
                        bs.nact, &rbf));
     SCM_TRY(round_bufs(bs.h_rst, bs.h_samp, bs.h_nmod, bs.h_fcon, bs.h_mods, bs.h_cnts,
                        bs.h_wsnap, bs.h_act, bs.h_nact, &rbh));
+    if (!bs.sev[0])
+      for (auto& e : bs.sev) SCM_HIP(hipEventCreate(&e));
     SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
                           bs.xy2.as<double>(), bs.scratch.as<double>(), bs.snaps.as<uint32_t>(),
                           bs.masks.as<uint8_t>(), bs.dvout.as<VerifyOut>(),
                           make_params(ctx->opts), prof, nullptr, bs.xyf.as<float4>(), rbf, rbh,
-                          sv));
+                          sv, bs.sev, &bs.nwin));
   }
   SCM_HIP(hipEventRecord(bs.ev[5], sv));
   // Compact matches + F-inlier masks in HBM, then DMA the results into the
@@ -901,12 +911,21 @@ int collect_batch(scm_context* ctx, BatchSet& bs, BatchView* v) {
     ctx->t_final += event_ms(bs.ev[1], bs.ev[2]);
   }
   if (bs.verify) ctx->t_verify += event_ms(bs.ev[4], bs.ev[5]);
+  if (bs.verify) {
+    for (int w = 0; w < bs.nwin; ++w) ctx->t_score += event_ms(bs.sev[2 * w], bs.sev[2 * w + 1]);
+    bs.nwin = 0;
+  }
   const uint8_t* o = reinterpret_cast<const uint8_t*>(bs.out.host);
   v->counts = reinterpret_cast<const int32_t*>(o + bs.off_counts);
   v->offsets = reinterpret_cast<const int64_t*>(o + bs.off_offsets);
   v->vout = bs.verify ? reinterpret_cast<const VerifyOut*>(o + bs.off_vout) : nullptr;
   v->matches = reinterpret_cast<const Match*>(o + bs.off_matches);
   v->masks = o + bs.off_masks;
+  if (v->vout)
+    for (int64_t p = 0; p < bs.P; ++p) {
+      ctx->evals_f += v->vout[p].f_evals;
+      ctx->evals_h += v->vout[p].h_evals;
+    }
   if (ctx->profile && bs.verify && bs.nprof > 0) {
     std::vector<uint64_t> pr(bs.nprof * kVerifyProfSlots);
     SCM_HIP(hipMemcpy(pr.data(), bs.prof.ptr, pr.size() * sizeof(uint64_t),
@@ -1498,7 +1517,8 @@ int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
       plan[b].nb_ids.push_back(ids[s]);
     }
   }
-  ctx->t_match = ctx->t_final = ctx->t_verify = 0.0;
+  ctx->t_match = ctx->t_final = ctx->t_verify = ctx->t_score = 0.0;
+  ctx->evals_f = ctx->evals_h = 0;
   ctx->n_match_launches = 0;
   Packed pk;
   rc = run_rows(ctx, t, plan, -1, &pk);
@@ -1574,7 +1594,8 @@ static int table_run_common(scm_context* ctx, int64_t overlap, int64_t row_begin
     return SCM_E_INVALID;
   }
   SCM_HIP(hipSetDevice(ctx->device));
-  ctx->t_match = ctx->t_final = ctx->t_verify = 0.0;
+  ctx->t_match = ctx->t_final = ctx->t_verify = ctx->t_score = 0.0;
+  ctx->evals_f = ctx->evals_h = 0;
   ctx->n_match_launches = 0;
   const auto w0 = std::chrono::steady_clock::now();
   const int rc = run_table(ctx, overlap, row_begin, row_end, pk);
@@ -1704,9 +1725,10 @@ int scm_table_timings(scm_context* ctx, double* t, int32_t n) {
     set_error("invalid arguments");
     return SCM_E_INVALID;
   }
-  const double v[5] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall,
-                       (double)ctx->n_match_launches};
-  for (int32_t i = 0; i < n && i < 5; ++i) t[i] = v[i];
+  const double v[8] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall,
+                       (double)ctx->n_match_launches, ctx->t_score, (double)ctx->evals_f,
+                       (double)ctx->evals_h};
+  for (int32_t i = 0; i < n && i < 8; ++i) t[i] = v[i];
   return SCM_OK;
 }
 

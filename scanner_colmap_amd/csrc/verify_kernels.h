@@ -60,6 +60,10 @@ struct VerifyOut {
   int32_t watermark, pad_;
   double F[9];
   double H[9];
+  // (model, point) residual evaluations the sequential LO-RANSAC scores up to
+  // its stop (speculative trials past the abort excluded): the scoring
+  // kernels' algorithmic work (bench.py roofline_verify)
+  int64_t f_evals, h_evals;
 };
 
 // Per-pair state of the round-synchronous LO-RANSAC (verify_kernels.hip).
@@ -67,6 +71,7 @@ struct RansacState {
   int32_t n, done, trial, dyn_max;
   int32_t max_trials, best_n, best_sum_valid, res_sel;
   int32_t B, num_trials, pad_, pad2_;
+  int64_t evals;  // (model, point) evaluations of the trials up to the stop
   double best_sum;
   double S;  // max |coordinate| of the pair's points (fp32 filter bound)
   double best_model[9];
@@ -100,11 +105,15 @@ struct VerifyRoundBufs {
 // LO-RANSAC (round buffers rb_f) and the H LO-RANSAC (rb_h, its own PRNG
 // stream) advance together in one launch sequence on `stream`; the
 // configuration, watermark and post-filter kernel follows.
+// score_ev (optional, 2 * kMaxVerifyWindows events): recorded around each
+// window's scoring kernels; *nwin receives the number of windows launched.
+constexpr int kMaxVerifyWindows = 64;
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
                          const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb_f,
-                         const VerifyRoundBufs& rb_h, hipStream_t stream);
+                         const VerifyRoundBufs& rb_h, hipStream_t stream,
+                         hipEvent_t* score_ev = nullptr, int* nwin = nullptr);
 size_t verify_lds_bytes(int max_m);
 constexpr int kVerifyProfSlots = 90;
 

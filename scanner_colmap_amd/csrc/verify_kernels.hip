@@ -1695,12 +1695,14 @@ __device__ void rs_finish(const PairSetup& ps, const RansacState& st, uint8_t* m
     if (lane == 0) {
       ps.o->f_trials = st.num_trials;
       ps.o->f_inliers_raw = st.best_n;
+      ps.o->f_evals = st.evals;
     }
   } else {
     if (lane < 9) ps.o->H[lane] = st.best_model[lane];
     if (lane == 0) {
       ps.o->h_trials = st.num_trials;
       ps.o->h_inliers_raw = st.best_n;
+      ps.o->h_evals = st.evals;
     }
   }
 }
@@ -1748,6 +1750,7 @@ __device__ __attribute__((always_inline)) void rs_begin_body(
       st.res_sel = 0;
       st.B = 0;
       st.num_trials = 0;
+      st.evals = 0;
       st.done = (n < Tr::kmin || st.max_trials <= 0) ? 1 : 0;
       st.pad_ = 0;
       st.best_sum = 1.7976931348623157e308;  // Support() default: DBL_MAX
@@ -2105,6 +2108,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     const int Btot = st.B;
     bool abort = false;
     int abort_trial = -1;
+    int64_t evals = st.evals;
     for (int r0 = 0; r0 < Btot && !abort; r0 += kTrialBatch) {
       const int B = min(kTrialBatch, Btot - r0);
       wsync();
@@ -2229,6 +2233,12 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
         }
         ++t;
       }
+      // models scored by the trials of this round up to the stop
+      {
+        const int lastt = abort ? abort_trial - (trial + r0) : B - 1;
+        const int nm = lane <= lastt && lane < B ? s.nmodels[lane] : 0;
+        evals += (int64_t)wave_sum_i(nm) * n;
+      }
     }
     wsync();
     if (abort) {
@@ -2254,6 +2264,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
       if (st.trial >= st.max_trials) st.done = 1;
     }
     st.dyn_max = dyn_max;
+    st.evals = evals;
     st.res_sel = best_sel;
     st.best_n = s.best_n;
     st.best_sum = s.best_sum;
@@ -2387,7 +2398,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                        double* scratch, uint32_t* snaps, uint8_t* masks, VerifyOut* out,
                        const VerifyParams& P, const float4* xyf, const VerifyRoundBufs& rf,
                        const VerifyRoundBufs& rh, int max_chunks, int max_m, uint64_t* prof,
-                       hipStream_t stream) {
+                       hipStream_t stream, hipEvent_t* score_ev, int* nwin) {
   const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
   const int gw = npairs < 4096 ? npairs : 4096;
 #ifndef SCM_SHUFFLE_LDS_KB
@@ -2418,6 +2429,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       hipLaunchKernelGGL(rs_solve_kernel<KIND_H>, dim3(4096), dim3(64), 0, stream, pairs, xy1, xy2,
                          rh.rst, rh.act[cur], rh.nact + cur, rh.samp, rh.nmod, rh.fcon, rh.mods,
                          W, P.max_residual);
+    if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r], stream);
     if (f)
       hipLaunchKernelGGL(rs_score_kernel<KIND_F>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs,
                          xyf, rf.rst, rf.act[cur], rf.nact + cur, rf.nmod, rf.fcon, rf.mods,
@@ -2426,6 +2438,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       hipLaunchKernelGGL(rs_score_kernel<KIND_H>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs,
                          xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon, rh.mods,
                          rh.cnts, max_chunks, W, P.max_residual, prof);
+    if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r + 1], stream);
     hipLaunchKernelGGL(rs_replay2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
                        out, masks, rf, rh, cur, P, prof, xyf, s1);
     const hipError_t err = hipGetLastError();
@@ -2434,6 +2447,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     W = W * 2 > kMaxWindow ? kMaxWindow : W * 2;
     ++r;
   }
+  if (nwin) *nwin = r < kMaxVerifyWindows ? r : kMaxVerifyWindows;
   return hipSuccess;
 }
 
@@ -2443,7 +2457,8 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
                          const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb_f,
-                         const VerifyRoundBufs& rb_h, hipStream_t stream) {
+                         const VerifyRoundBufs& rb_h, hipStream_t stream, hipEvent_t* score_ev,
+                         int* nwin) {
   if (npairs <= 0) return hipSuccess;
   static bool attr = false;
   if (!attr) {
@@ -2465,7 +2480,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   hipLaunchKernelGGL(rs_begin2_kernel, dim3(2 * gw), dim3(64), kVerifyLdsHead, stream, pairs,
                      npairs, scratch, snaps, out, masks, xyf, rb_f, rb_h, params, gw);
   if ((err = run_windows(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf, rb_f,
-                         rb_h, max_chunks, max_m, prof, stream)) != hipSuccess)
+                         rb_h, max_chunks, max_m, prof, stream, score_ev, nwin)) != hipSuccess)
     return err;
   hipLaunchKernelGGL(verify_final_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
                      xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
