@@ -95,6 +95,7 @@ struct VerifyRoundBufs {
   float* fcon;
   double* mods;
   uint32_t* cnts;
+  uint32_t* ucnt;  // split scoring: undecided points per model [V][3T]
   uint32_t* wsnap;
   int32_t* act[2];
   int32_t* nact;

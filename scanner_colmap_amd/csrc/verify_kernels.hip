@@ -494,11 +494,16 @@ __device__ __forceinline__ bool defer_push(DeferQ* d, uint64_t um, int p, int m)
   return true;
 }
 
-template <int PCH, bool FULL>
+// UND: no exact tests -- return the sure inliers and write the number of
+// undecided points to *nund (the exact pass, rs_exact_kernel, tests them
+// only for models that can still reach the pair's best count).  Otherwise
+// the sure count goes to *nsure (when given) before the exact tests.
+template <int PCH, bool FULL, bool UND = false>
 __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, const f32x2* s0,
                                              const f32x2* s1, const f32x2* d0, const f32x2* d1,
                                              int n, int base, double maxr, int* nslow,
-                                             DeferQ* dq = nullptr, int dm = 0) {
+                                             DeferQ* dq = nullptr, int dm = 0,
+                                             int* nund = nullptr, int* nsure = nullptr) {
   int cnt = 0;
   uint64_t any = 0;
   uint64_t um[PCH];  // per point slot: lanes the filter left undecided
@@ -528,6 +533,14 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
 #ifdef SCM_DIAG_SCORE_NOSLOW
   any = 0;  // diagnostics only: undecided points counted as outliers
 #endif
+  if (UND) {
+    int u = 0;
+#pragma unroll
+    for (int p = 0; p < PCH; ++p) u += __popcll(um[p]);
+    *nund = u;
+    return cnt;
+  }
+  if (nsure) *nsure = cnt;
   if (any) {  // rare: exact test of the undecided points only (queued when dq)
     ++*nslow;
     if (dq) {
@@ -662,11 +675,16 @@ __device__ __attribute__((noinline)) bool f_exact_pt(const double* mk, float x0,
 
 // Inlier count of one 7-point model (filter f; fp64 model mk in LDS, read
 // only for undecided points) over one chunk of points.
-template <int PCH, bool FULL>
+// UND: no exact tests -- return the sure inliers and write the number of
+// undecided points to *nund (the exact pass, rs_exact_kernel, tests them
+// only for models that can still reach the pair's best count).  Otherwise
+// the sure count goes to *nsure (when given) before the exact tests.
+template <int PCH, bool FULL, bool UND = false>
 __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, const f32x2* x0,
                                              const f32x2* x1, const f32x2* y0, const f32x2* y1,
                                              int n, int base, double maxr, int* nslow,
-                                             DeferQ* dq = nullptr, int dm = 0) {
+                                             DeferQ* dq = nullptr, int dm = 0,
+                                             int* nund = nullptr, int* nsure = nullptr) {
   int cnt = 0;
   uint64_t any = 0;
   uint64_t um[PCH];  // per point slot: lanes the filter left undecided
@@ -695,6 +713,14 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
 #ifdef SCM_DIAG_SCORE_NOSLOW
   any = 0;  // diagnostics only: undecided points counted as outliers
 #endif
+  if (UND) {
+    int u = 0;
+#pragma unroll
+    for (int p = 0; p < PCH; ++p) u += __popcll(um[p]);
+    *nund = u;
+    return cnt;
+  }
+  if (nsure) *nsure = cnt;
   if (any) {  // rare: exact test of the undecided points only (queued when dq)
     ++*nslow;
     if (dq) {
@@ -1773,7 +1799,7 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, RansacState* __restrict__ rst,
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
     int32_t* __restrict__ nact_next, uint16_t* __restrict__ samp, uint32_t* __restrict__ cnts,
-    uint32_t* __restrict__ wsnap, int W, int bid, int nblk) {
+    uint32_t* __restrict__ ucnt, uint32_t* __restrict__ wsnap, int W, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
@@ -1814,6 +1840,10 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     mt_save(s, ps.state);
     uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3;
     for (int i = lane; i < Btot * 3; i += 64) cq[i] = 0u;
+    if (ucnt) {
+      uint32_t* uq = ucnt + (int64_t)q * kWindowTrials * 3;
+      for (int i = lane; i < Btot * 3; i += 64) uq[i] = 0u;
+    }
     if (lane == 0) rst[q].B = Btot;
   }
 }
@@ -1939,20 +1969,20 @@ constexpr int kScorePch = SCM_SCORE_PCH;  // points per lane
 constexpr int kScoreChunk = kScoreThreads * kScorePch;
 constexpr int kScoreTargetItems = 65536;  // work items per score launch (8 per wave slot)
 
-template <int K>
+template <int K, bool SPLIT>
 __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     const VerifyPair* __restrict__ pairs, const float4* __restrict__ xyf_all,
     const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
     const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
     const float* __restrict__ fcon, const double* __restrict__ mods,
-    uint32_t* __restrict__ cnts, int max_chunks, int W, double maxr,
+    uint32_t* __restrict__ cnts, uint32_t* __restrict__ ucnt, int max_chunks, int W, double maxr,
     uint64_t* __restrict__ prof) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * MM][12];
   __shared__ int32_t lnm[kTrialBatch];
-  __shared__ uint32_t ldq[kDeferCap];         // deferred exact tests (defer_push)
-  __shared__ uint32_t ldc[kTrialBatch * MM];  // their inliers per model of the round
+  __shared__ uint32_t ldq[SPLIT ? 1 : kDeferCap];         // deferred exact tests (defer_push)
+  __shared__ uint32_t ldc[SPLIT ? 1 : kTrialBatch * MM];  // their inliers per model of the round
   const int lane = threadIdx.x;
   const int na = *nact;
   const float maxrf = (float)maxr;
@@ -1998,34 +2028,41 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
         float4* dst = reinterpret_cast<float4*>(&lc[0][0]);
         for (int i = lane; i < B * MM * 3; i += kScoreThreads) dst[i] = src[i];
       }
-      for (int i = lane; i < B * MM; i += kScoreThreads) ldc[i] = 0;
+      if (!SPLIT)
+        for (int i = lane; i < B * MM; i += kScoreThreads) ldc[i] = 0;
       __syncthreads();
       const double* mb = mods + ((int64_t)q * kWindowTrials * 3 + r0 * MM) * MS;
       DeferQ dq{ldq, 0};
       int nslow = 0;
       uint32_t c0 = 0, c1 = 0, c2 = 0;  // lane t: counts of hypothesis t's models
+      uint32_t u0 = 0, u1 = 0, u2 = 0;  // SPLIT: lane t: their undecided points
       for (int t = 0; t < B; ++t) {
         const int nmt = K == KIND_F ? __builtin_amdgcn_readfirstlane(lnm[t]) : 1;
         for (int k = 0; k < nmt; ++k) {
           const int m = t * MM + k;
-          int c;
+          int c, u = 0;
           if (K == KIND_F) {
             const FFilt f = f_filter_load(&lc[m][0], maxrf);
-            c = full ? score_f_chunk<kScorePch, true>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                      maxr, &nslow, &dq, m)
-                     : score_f_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                       maxr, &nslow, &dq, m);
+            c = full ? score_f_chunk<kScorePch, true, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
+                                                             base, maxr, &nslow,
+                                                             SPLIT ? nullptr : &dq, m, &u)
+                     : score_f_chunk<kScorePch, false, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
+                                                              base, maxr, &nslow,
+                                                              SPLIT ? nullptr : &dq, m, &u);
           } else {
             const HFilt f = h_filter_load(&lc[m][0], maxrf);
-            c = full ? score_h_chunk<kScorePch, true>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                      maxr, &nslow, &dq, m)
-                     : score_h_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                       maxr, &nslow, &dq, m);
+            c = full ? score_h_chunk<kScorePch, true, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
+                                                             base, maxr, &nslow,
+                                                             SPLIT ? nullptr : &dq, m, &u)
+                     : score_h_chunk<kScorePch, false, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
+                                                              base, maxr, &nslow,
+                                                              SPLIT ? nullptr : &dq, m, &u);
           }
           const uint32_t add = (lane == t) ? (uint32_t)c : 0u;
-          if (k == 0) c0 += add;
-          else if (k == 1) c1 += add;
-          else c2 += add;
+          const uint32_t uadd = (lane == t) ? (uint32_t)u : 0u;
+          if (k == 0) { c0 += add; u0 += uadd; }
+          else if (k == 1) { c1 += add; u1 += uadd; }
+          else { c2 += add; u2 += uadd; }
         }
       }
       if (prof && lane == 0) {  // diagnostics: chunk-models scored, slow (exact) passes
@@ -2034,25 +2071,133 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
         atomicAdd(reinterpret_cast<unsigned long long*>(pc + 1), (unsigned long long)nslow);
         atomicAdd(reinterpret_cast<unsigned long long*>(pc + 2), (unsigned long long)dq.n);
       }
-      // The queued exact tests, 64 at a time.
-      for (int e = lane; e < dq.n; e += kScoreThreads) {
-        const uint32_t v = ldq[e];
-        const int m = (int)(v >> 16), off = (int)(v & 0xFFFFu);
-        const float4 pt = xyf[base + off];
-        const bool in = K == KIND_F ? f_exact_pt(mb + m * MS, pt.x, pt.y, pt.z, pt.w, maxr)
-                                    : h_exact_pt(mb + m * MS, pt.x, pt.y, pt.z, pt.w, maxr);
-        if (in) atomicAdd(&ldc[m], 1u);
-      }
-      if (dq.n && lane < B) {
-        c0 += ldc[lane * MM];
-        if (MM > 1) c1 += ldc[lane * MM + 1];
-        if (MM > 2) c2 += ldc[lane * MM + 2];
+      if (!SPLIT) {
+        // The queued exact tests, 64 at a time.
+        for (int e = lane; e < dq.n; e += kScoreThreads) {
+          const uint32_t v = ldq[e];
+          const int m = (int)(v >> 16), off = (int)(v & 0xFFFFu);
+          const float4 pt = xyf[base + off];
+          const bool in = K == KIND_F ? f_exact_pt(mb + m * MS, pt.x, pt.y, pt.z, pt.w, maxr)
+                                      : h_exact_pt(mb + m * MS, pt.x, pt.y, pt.z, pt.w, maxr);
+          if (in) atomicAdd(&ldc[m], 1u);
+        }
+        if (dq.n && lane < B) {
+          c0 += ldc[lane * MM];
+          if (MM > 1) c1 += ldc[lane * MM + 1];
+          if (MM > 2) c2 += ldc[lane * MM + 2];
+        }
       }
       uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3 + r0 * MM;
       if (lane < B) {
         if (c0) atomicAdd(&cq[lane * MM], c0);
         if (MM > 1 && c1) atomicAdd(&cq[lane * MM + 1], c1);
         if (MM > 2 && c2) atomicAdd(&cq[lane * MM + 2], c2);
+      }
+      if (SPLIT && lane < B) {
+        uint32_t* uq = ucnt + (int64_t)q * kWindowTrials * 3 + r0 * MM;
+        if (u0) atomicAdd(&uq[lane * MM], u0);
+        if (MM > 1 && u1) atomicAdd(&uq[lane * MM + 1], u1);
+        if (MM > 2 && u2) atomicAdd(&uq[lane * MM + 2], u2);
+      }
+    }
+  }
+}
+
+// Exact pass of the split scoring (after rs_score_kernel<K, true>): a model's
+// count is needed exactly only if it can be a candidate of the sequential
+// replay, i.e. reach the pair's best count -- and the best only grows, so a
+// model whose sure + undecided inliers stay below the best at the start of
+// the window (rst.best_n) can never be one; its count stays the sure count
+// (a lower bound below the best, which the replay reads exactly as it would
+// read the exact count).  For the others the undecided points of every chunk
+// take the exact fp64 test here.  Same work items as the scoring kernel;
+// items with no such model exit without loading their points.
+template <int K>
+__global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
+    const VerifyPair* __restrict__ pairs, const float4* __restrict__ xyf_all,
+    const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
+    const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
+    const float* __restrict__ fcon, const double* __restrict__ mods,
+    uint32_t* __restrict__ cnts, const uint32_t* __restrict__ ucnt, int max_chunks, int W,
+    double maxr) {
+  using Tr = KindTraits<K>;
+  constexpr int MM = Tr::mm, MS = Tr::ms;
+  const int lane = threadIdx.x;
+  const int na = *nact;
+  const float maxrf = (float)maxr;
+  const int rpi = max(1, min(W, (int)(((int64_t)na * max_chunks * W) / kScoreTargetItems)));
+  const int nri = (W + rpi - 1) / rpi;
+  const int per_pair = max_chunks * nri;
+  for (int w = blockIdx.x; w < na * per_pair; w += gridDim.x) {
+    const int q = act[w / per_pair];
+    const int rem = w - (w / per_pair) * per_pair;
+    const int chunk = rem / nri, ri = rem - (rem / nri) * nri;
+    const VerifyPair pp = pairs[q];
+    const int n = pp.m;
+    const int base = chunk * kScoreChunk;
+    if (base >= n) continue;
+    const int Bpair = rst[q].B;
+    const uint32_t best0 = (uint32_t)rst[q].best_n;
+    const int rbeg = ri * rpi * kTrialBatch;
+    const int rend = min(Bpair, rbeg + rpi * kTrialBatch);
+    if (rbeg >= rend) continue;
+    const float4* xyf = xyf_all + pp.pts_off / 2;
+    f32x2 x0[kScorePch / 2], x1[kScorePch / 2], y0[kScorePch / 2], y1[kScorePch / 2];
+    bool loaded = false;
+    for (int r0 = rbeg; r0 < rend; r0 += kTrialBatch) {
+      const int B = min(kTrialBatch, rend - r0);
+      const int64_t mo = (int64_t)q * kWindowTrials * 3 + r0 * MM;
+      // lane t: the qualifying models of hypothesis t (bit k)
+      uint32_t qual = 0;
+      if (lane < B) {
+        const int nml = K == KIND_F ? nmod[(int64_t)q * kWindowTrials + r0 + lane] : 1;
+#pragma unroll
+        for (int k = 0; k < MM; ++k) {
+          const uint32_t u = k < nml ? ucnt[mo + lane * MM + k] : 0u;
+          if (u && cnts[mo + lane * MM + k] + u >= best0) qual |= 1u << k;
+        }
+      }
+      uint64_t any = __ballot(qual != 0);
+      if (!any) continue;
+      if (!loaded) {
+#pragma unroll
+        for (int qq = 0; qq < kScorePch / 2; ++qq) {
+          const int i0 = base + (2 * qq) * 64 + lane, i1 = i0 + 64;
+          const float4 v0 = i0 < n ? xyf[i0] : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float4 v1 = i1 < n ? xyf[i1] : make_float4(0.f, 0.f, 0.f, 0.f);
+          x0[qq] = f32x2{v0.x, v1.x};
+          x1[qq] = f32x2{v0.y, v1.y};
+          y0[qq] = f32x2{v0.z, v1.z};
+          y1[qq] = f32x2{v0.w, v1.w};
+        }
+        loaded = true;
+      }
+      const bool full = base + kScoreChunk <= n;
+      const double* mb = mods + mo * MS;
+      const float* cb = fcon + mo * 12;
+      while (any) {
+        const int t = (int)__builtin_ctzll(any);
+        any &= any - 1;
+        const uint32_t qt = __builtin_amdgcn_readlane(qual, t);
+        for (int k = 0; k < MM; ++k) {
+          if (!(qt & (1u << k))) continue;
+          const int m = t * MM + k;
+          int nslow = 0, sure = 0, c;
+          if (K == KIND_F) {
+            const FFilt f = f_filter_load(cb + m * 12, maxrf);
+            c = full ? score_f_chunk<kScorePch, true>(f, mb + m * MS, x0, x1, y0, y1, n, base,
+                                                      maxr, &nslow, nullptr, 0, nullptr, &sure)
+                     : score_f_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
+                                                       maxr, &nslow, nullptr, 0, nullptr, &sure);
+          } else {
+            const HFilt f = h_filter_load(cb + m * 12, maxrf);
+            c = full ? score_h_chunk<kScorePch, true>(f, mb + m * MS, x0, x1, y0, y1, n, base,
+                                                      maxr, &nslow, nullptr, 0, nullptr, &sure)
+                     : score_h_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
+                                                       maxr, &nslow, nullptr, 0, nullptr, &sure);
+          }
+          if (lane == 0 && c > sure) atomicAdd(&cnts[mo + m], (uint32_t)(c - sure));
+        }
       }
     }
   }
@@ -2308,11 +2453,12 @@ __global__ __launch_bounds__(64) void rs_draw2_kernel(
     VerifyRoundBufs rh, int cur, int W, int split) {
   if ((int)blockIdx.x < split)
     rs_draw_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[cur], rf.nact + cur,
-                         rf.nact + (cur ^ 1), rf.samp, rf.cnts, rf.wsnap, W, blockIdx.x, split);
+                         rf.nact + (cur ^ 1), rf.samp, rf.cnts, rf.ucnt, rf.wsnap, W, blockIdx.x,
+                         split);
   else
     rs_draw_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[cur], rh.nact + cur,
-                         rh.nact + (cur ^ 1), rh.samp, rh.cnts, rh.wsnap, W, blockIdx.x - split,
-                         gridDim.x - split);
+                         rh.nact + (cur ^ 1), rh.samp, rh.cnts, rh.ucnt, rh.wsnap, W,
+                         blockIdx.x - split, gridDim.x - split);
 }
 
 __global__ __launch_bounds__(64) void rs_shuffle2_kernel(
@@ -2430,14 +2576,38 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                          rh.rst, rh.act[cur], rh.nact + cur, rh.samp, rh.nmod, rh.fcon, rh.mods,
                          W, P.max_residual);
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r], stream);
-    if (f)
-      hipLaunchKernelGGL(rs_score_kernel<KIND_F>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs,
-                         xyf, rf.rst, rf.act[cur], rf.nact + cur, rf.nmod, rf.fcon, rf.mods,
-                         rf.cnts, max_chunks, W, P.max_residual, prof);
-    if (h)
-      hipLaunchKernelGGL(rs_score_kernel<KIND_H>, dim3(8192), dim3(kScoreThreads), 0, stream, pairs,
-                         xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon, rh.mods,
-                         rh.cnts, max_chunks, W, P.max_residual, prof);
+    // Scoring per kind: split (filter counts + undecided counts, then exact
+    // tests only for the models that can reach the best; the runtime's
+    // choice for H) or one pass with the exact tests of every undecided point
+    // (round buffers without ucnt; F).
+    if (f) {
+      if (rf.ucnt) {
+        hipLaunchKernelGGL((rs_score_kernel<KIND_F, true>), dim3(8192), dim3(kScoreThreads), 0,
+                           stream, pairs, xyf, rf.rst, rf.act[cur], rf.nact + cur, rf.nmod, rf.fcon,
+                           rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual, prof);
+        hipLaunchKernelGGL(rs_exact_kernel<KIND_F>, dim3(8192), dim3(kScoreThreads), 0, stream,
+                           pairs, xyf, rf.rst, rf.act[cur], rf.nact + cur, rf.nmod, rf.fcon,
+                           rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual);
+      } else {
+        hipLaunchKernelGGL((rs_score_kernel<KIND_F, false>), dim3(8192), dim3(kScoreThreads), 0,
+                           stream, pairs, xyf, rf.rst, rf.act[cur], rf.nact + cur, rf.nmod, rf.fcon,
+                           rf.mods, rf.cnts, nullptr, max_chunks, W, P.max_residual, prof);
+      }
+    }
+    if (h) {
+      if (rh.ucnt) {
+        hipLaunchKernelGGL((rs_score_kernel<KIND_H, true>), dim3(8192), dim3(kScoreThreads), 0,
+                           stream, pairs, xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon,
+                           rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, prof);
+        hipLaunchKernelGGL(rs_exact_kernel<KIND_H>, dim3(8192), dim3(kScoreThreads), 0, stream,
+                           pairs, xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon,
+                           rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual);
+      } else {
+        hipLaunchKernelGGL((rs_score_kernel<KIND_H, false>), dim3(8192), dim3(kScoreThreads), 0,
+                           stream, pairs, xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon,
+                           rh.mods, rh.cnts, nullptr, max_chunks, W, P.max_residual, prof);
+      }
+    }
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r + 1], stream);
     hipLaunchKernelGGL(rs_replay2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
                        out, masks, rf, rh, cur, P, prof, xyf, s1);
