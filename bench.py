@@ -68,6 +68,8 @@ def parse():
     p.add_argument("--stencil-rows", type=int, default=128,
                    help="rows of the Scanner drop-in path (scm_execute_batch) timed after the "
                         "table run, rank 0 at N = 1 (0 = skip)")
+    p.add_argument("--no-isolated", dest="isolated", action="store_false",
+                   help="skip the extra serialised step that measures isolated kernel rates")
     p.add_argument("--stencil-batches", default="1,64",
                    help="Scanner batch sizes (stencils per execute() call) to time")
     return p.parse_args()
@@ -371,6 +373,27 @@ def main():
             else:
                 cpu, ref = cpu_baseline(sample_imgs, check_pairs)
             parity = parity_check(ctx, last["packed"], lr_b, ref, check_pairs)
+        # Isolated kernel rates: one extra untimed step with matching and verification
+        # serialised (scm_set_serial; same bytes), so no stage shares the CUs.
+        iso = None
+        if world == 1 and args.isolated:
+            ctx.set_serial(True)
+            ti = step()
+            ctx.set_serial(False)
+            ops1 = 2.0 * 128.0 * gdesc
+            sf1 = (SAMPSON_FLOPS + 1) * ti["evals_f"] + (TRANSFER_FLOPS + 1) * ti["evals_h"]
+            iso = {"match_tops": round(ops1 / (ti["match_ms"] * 1e-3) / 1e12, 2),
+                   "match_frac": round(ops1 / (ti["match_ms"] * 1e-3) / 1e12 / peak, 4),
+                   "score_tflops": (round(sf1 / (ti["score_ms"] * 1e-3) / 1e12, 2)
+                                    if ti["score_ms"] > 0 else None),
+                   "score_frac": (round(sf1 / (ti["score_ms"] * 1e-3) / 1e12 / FP32_VECTOR_PEAK_TFLOPS, 4)
+                                  if ti["score_ms"] > 0 else None),
+                   "ms": {"match": round(ti["match_ms"], 3), "finalize": round(ti["finalize_ms"], 3),
+                          "verify": round(ti["verify_ms"], 3), "score": round(ti["score_ms"], 3),
+                          "wall": round(ti["wall_ms"], 3)},
+                   "how": ("one extra untimed step after the timed region with matching and "
+                           "verification serialised (scm_set_serial, output bytes identical): "
+                           "each kernel alone on the GPU, HIP events")}
         drop_in = stencil_bench(ctx, stencil_src, overlap, srows,
                                 [int(x) for x in args.stencil_batches.split(",") if x]) if srows else None
         score_flops = (SAMPSON_FLOPS + 1) * evals_f + (TRANSFER_FLOPS + 1) * evals_h
@@ -434,6 +457,7 @@ def main():
                                 "157.3 TF (MI355X_MICROARCH.md): the kernels evaluate packed "
                                 "fp32 filters with fp64 exact tests for undecided points"),
             },
+            "isolated": iso,
             "stage_ms_per_step": {"match": round(match_ms / steps, 3),
                                   "finalize": round(final_ms / steps, 3),
                                   "verify": round(verify_ms / steps, 3)},

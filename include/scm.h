@@ -223,6 +223,12 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset,
  * t[5] = inlier-scoring kernels (F + H), t[6] / t[7] = F / H (model, point)
  * residual evaluations of the sequential LO-RANSAC up to its stop. */
 int scm_table_timings(scm_context* ctx, double* t, int32_t n);
+/* Measurement only: serial != 0 runs the following table runs with matching
+ * and verification one after the other instead of overlapped (no stage
+ * shares the GPU), so scm_table_timings reports isolated kernel times; the
+ * output bytes are identical.  Off by default (SCM_SERIAL=1 sets the initial
+ * value). */
+int scm_set_serial(scm_context* ctx, int32_t serial);
 
 #ifdef __cplusplus
 }

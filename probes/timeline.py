@@ -8,7 +8,7 @@ rows = [r for r in csv.DictReader(open(sys.argv[1]))]
 ev = []
 for r in rows:
     n = r['Kernel_Name']
-    kind = 'M' if 'match_tiles' in n or 'match_finalize' in n else ('V' if 'scm::' in n else None)
+    kind = 'M' if 'match_' in n else ('V' if 'scm::' in n else None)
     if kind:
         ev.append((int(r['Start_Timestamp']), int(r['End_Timestamp']), kind))
 ev.sort()

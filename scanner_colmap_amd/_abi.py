@@ -17,7 +17,8 @@ from ctypes import (POINTER, Structure, byref, c_char_p, c_double, c_float,
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libscm.so")
+# SCM_LIB (diagnostics only): load another build of the library, e.g. a probes/build variant.
+LIB_PATH = os.environ.get("SCM_LIB") or os.path.join(_HERE, "lib", "libscm.so")
 
 SCM_OK = 0
 SCM_E_INVALID = -1
@@ -35,7 +36,7 @@ EXPORTS = (
     "scm_table_load",
     "scm_table_run", "scm_table_run_packed", "scm_set_keep_matches",
     "scm_set_keep_matches_range",
-    "scm_table_matches", "scm_table_timings",
+    "scm_table_matches", "scm_table_timings", "scm_set_serial",
 )
 
 
@@ -116,6 +117,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.scm_table_matches.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64,
                                       POINTER(c_int64)]
     lib.scm_table_timings.argtypes = [c_void_p, POINTER(c_double), c_int32]
+    lib.scm_set_serial.argtypes = [c_void_p, c_int32]
     for name in EXPORTS:
         if name not in ("scm_abi_version", "scm_last_error", "scm_default_options",
                         "scm_pair_seed", "scm_blob_free", "scm_context_destroy"):
@@ -307,6 +309,10 @@ class Context:
         _check(self._lib.scm_table_run_packed(self._ptr, overlap, row_begin, row_end, byref(b),
                                               offs.ctypes.data))
         return PackedRows(b, offs)
+
+    def set_serial(self, serial: bool = True) -> None:
+        """Measurement only: stages one after the other (isolated kernel times)."""
+        _check(self._lib.scm_set_serial(self._ptr, 1 if serial else 0))
 
     def set_keep_matches(self, keep: bool = True) -> None:
         _check(self._lib.scm_set_keep_matches(self._ptr, 1 if keep else 0))

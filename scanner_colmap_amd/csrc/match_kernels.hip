@@ -858,6 +858,9 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
   uint32_t* csc = reinterpret_cast<uint32_t*>(lds + kG8CscOff);
   int64_t* meta = reinterpret_cast<int64_t*>(lds + kG8MetaOff);
 
+#ifdef SCM_G8_WPRIO  // diagnostics: whole-kernel wave issue priority over co-resident kernels
+  __builtin_amdgcn_s_setprio(SCM_G8_WPRIO);
+#endif
   const MatchJob job = jobs[blockIdx.x];
   if (job.npairs == 0 || job.n1 <= 0) return;  // padding job of the XCD order (whole block)
   const PairDesc* __restrict__ P = pairs + job.pair0;

@@ -1669,6 +1669,15 @@ int scm_table_run_packed(scm_context* ctx, int64_t overlap, int64_t row_begin, i
   return SCM_OK;
 }
 
+int scm_set_serial(scm_context* ctx, int32_t serial) {
+  if (!ctx) {
+    set_error("null context");
+    return SCM_E_INVALID;
+  }
+  ctx->serial = serial != 0;
+  return SCM_OK;
+}
+
 int scm_set_keep_matches(scm_context* ctx, int32_t keep) {
   if (!ctx) {
     set_error("null context");

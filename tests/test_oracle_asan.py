@@ -1,0 +1,55 @@
+"""Memory and undefined-behaviour check of the CPU oracle (the
+reference has no race detection or sanitizer runs; the plan is an ASan build
+of the CPU restatement).  oracle/asan_driver.cc runs oracle_table_run over a
+small seeded table in a binary built with -fsanitize=address,undefined
+(`make -C oracle asan`, runtimes linked statically); the test fails on any
+sanitizer report and checks that the instrumented build writes the same io.cc
+rows as the regular liboracle.so."""
+import os
+import struct
+import subprocess
+
+import pytest
+
+from oracle import oracle
+from scanner_colmap_amd.codecs import table_rows
+from scanner_colmap_amd.synthetic import Corridor
+
+ORACLE_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle")
+DRIVER = os.path.join(ORACLE_DIR, "build", "oracle_asan")
+
+
+def _blob(b: bytes) -> bytes:
+    return struct.pack("<Q", len(b)) + b
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("n,kpts,overlap,seed", [(5, 700, 3, 31), (4, 300, 4, 32)])
+def test_oracle_table_run_under_asan(tmp_path, n, kpts, overlap, seed):
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "asan"], check=True)
+    imgs = Corridor(n, kpts, overlap, seed=seed).images()
+    if seed == 32:  # an empty image and a repeated id (the dedup branch, sequential_matching.cc:141-144)
+        imgs[2] = (imgs[2][0], imgs[2][1][:0], imgs[2][2][:0])
+        imgs[3] = (imgs[1][0],) + tuple(imgs[3][1:])
+    ids, kps, descs = table_rows(imgs)
+    src = tmp_path / "table.bin"
+    dst = tmp_path / "rows.bin"
+    with open(src, "wb") as f:
+        f.write(struct.pack("<Q", n))
+        for i in range(n):
+            f.write(_blob(ids[i]) + _blob(kps[i]) + _blob(descs[i]))
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:abort_on_error=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([DRIVER, str(src), str(dst), str(overlap)], env=env,
+                       capture_output=True, text=True, timeout=580)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
+    data = dst.read_bytes()
+    got, off = [], 0
+    while off < len(data):
+        (k,) = struct.unpack_from("<Q", data, off)
+        got.append(data[off + 8: off + 8 + k])
+        off += 8 + k
+    ref_ids, ref_tvg = oracle.table_run(ids, kps, descs, overlap, 0, n)
+    assert got[0::2] == ref_ids
+    assert got[1::2] == ref_tvg
