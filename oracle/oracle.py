@@ -318,3 +318,88 @@ def table_run_fast(images, overlap, row_begin, row_end, opts=None, threads=8,
         body = b"".join(tvgs[(r, s)] for s in sel)
         pb.append(struct.pack("<Qi", 12 + len(body), len(sel)) + body)
     return pa, pb
+
+
+# ---------------------------------------------------------------------------
+# SIFT extraction op (oracle/sift_oracle.cc).
+# ---------------------------------------------------------------------------
+def _frame(frame) -> tuple:
+    f = np.ascontiguousarray(frame, dtype=np.uint8)
+    if f.ndim == 2:
+        f = f[:, :, None]
+    h, w, c = f.shape
+    return f, w, h, c
+
+
+def sift_extract(frame, image_id: int = 0) -> tuple[bytes, bytes, bytes]:
+    """SiftExtractionKernel::execute on one frame (H x W x C uint8): the
+    keypoints, descriptors and camera io.cc elements."""
+    f, w, h, c = _frame(frame)
+    L = lib()
+    L.oracle_sift_extract.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_uint64,
+                                      POINTER(POINTER(c_uint8)), POINTER(c_size_t),
+                                      POINTER(POINTER(c_uint8)), POINTER(c_size_t),
+                                      POINTER(POINTER(c_uint8)), POINTER(c_size_t)]
+    ps = [POINTER(c_uint8)() for _ in range(3)]
+    ns = [c_size_t() for _ in range(3)]
+    rc = L.oracle_sift_extract(f.ctypes.data, w, h, c, image_id, byref(ps[0]), byref(ns[0]),
+                               byref(ps[1]), byref(ns[1]), byref(ps[2]), byref(ns[2]))
+    if rc != 0:
+        raise ValueError(f"oracle_sift_extract failed ({rc})")
+    return tuple(_take(p, n.value) for p, n in zip(ps, ns))
+
+
+def sift_grey(frame) -> np.ndarray:
+    f, w, h, c = _frame(frame)
+    out = np.zeros((h, w), np.uint8)
+    L = lib()
+    L.oracle_sift_grey.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p]
+    L.oracle_sift_grey(f.ctypes.data, w, h, c, out.ctypes.data)
+    return out
+
+
+def sift_octave(grey, octave: int) -> np.ndarray:
+    """Gaussian scale space of one octave (levels s = -1 .. 4) of a grey image."""
+    g = np.ascontiguousarray(grey, dtype=np.uint8)
+    h, w = g.shape
+    L = lib()
+    L.oracle_sift_octave.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_void_p,
+                                     POINTER(c_int32), POINTER(c_int32)]
+    ow, oh = c_int32(), c_int32()
+    assert L.oracle_sift_octave(g.ctypes.data, w, h, octave, None, byref(ow), byref(oh)) == 0
+    out = np.zeros((6, oh.value, ow.value), np.float32)
+    L.oracle_sift_octave(g.ctypes.data, w, h, octave, out.ctypes.data, byref(ow), byref(oh))
+    return out
+
+
+def sift_keypoints(grey) -> np.ndarray:
+    """Detected keypoints of every octave, rows (octave, is, ix, iy, x, y,
+    sigma, orientation count), before the level selection."""
+    g = np.ascontiguousarray(grey, dtype=np.uint8)
+    h, w = g.shape
+    L = lib()
+    L.oracle_sift_keypoints.argtypes = [c_void_p, c_int32, c_int32, c_void_p, c_int64]
+    L.oracle_sift_keypoints.restype = c_int64
+    n = L.oracle_sift_keypoints(g.ctypes.data, w, h, None, 0)
+    out = np.zeros((max(1, n), 8), np.float64)
+    L.oracle_sift_keypoints(g.ctypes.data, w, h, out.ctypes.data, n)
+    return out[:n]
+
+
+def sift_math():
+    """vl/mathop.h helpers and the smoothing taps, for known-answer tests."""
+    L = lib()
+    L.oracle_fast_atan2_f.argtypes = [c_float, c_float]
+    L.oracle_fast_atan2_f.restype = c_float
+    L.oracle_fast_sqrt_f.argtypes = [c_float]
+    L.oracle_fast_sqrt_f.restype = c_float
+    L.oracle_fast_expn.argtypes = [c_double]
+    L.oracle_fast_expn.restype = c_double
+    L.oracle_gauss_taps.argtypes = [c_double, c_void_p, c_int32]
+    L.oracle_gauss_taps.restype = c_int32
+
+    def taps(sigma):
+        out = np.zeros(64, np.float32)
+        n = L.oracle_gauss_taps(sigma, out.ctypes.data, 64)
+        return out[:n]
+    return L.oracle_fast_atan2_f, L.oracle_fast_sqrt_f, L.oracle_fast_expn, taps

@@ -238,3 +238,47 @@ def descriptors_for_matches(matches: np.ndarray, n1: int, n2: int, seed: int):
     d2 = random_descriptors(n2, seed + 1)
     d2[matches[:, 1]] = d1[matches[:, 0]]
     return d1, d2
+
+
+def synthetic_frame(height: int, width: int, seed: int, channels: int = 3,
+                    blobs: int | None = None) -> np.ndarray:
+    """A deterministic textured frame (H x W x C uint8) for the SIFT extraction
+    path: a smooth background, Gaussian blobs of random size, sign and
+    position (the DoG detector's natural keypoints), a few oriented bars (so
+    orientations and descriptors vary) and mild per-pixel noise; the colour
+    channels differ so the grey conversion's channel weights matter."""
+    rng = np.random.default_rng(seed)
+    h, w = height, width
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    img = np.zeros((h, w), np.float32)
+    img += 0.3 + 0.15 * np.sin(xx / max(8.0, w / 7.0)) * np.cos(yy / max(8.0, h / 5.0))
+    nb = blobs if blobs is not None else max(8, (h * w) // 500)
+    for _ in range(nb):
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        s = float(np.exp(rng.uniform(np.log(1.2), np.log(max(2.0, min(h, w) / 30.0)))))
+        a = rng.uniform(-0.5, 0.5)
+        r = int(4 * s) + 1
+        x0, x1 = max(0, int(cx) - r), min(w, int(cx) + r + 1)
+        y0, y1 = max(0, int(cy) - r), min(h, int(cy) + r + 1)
+        if x0 >= x1 or y0 >= y1:
+            continue
+        sx, sy = s * rng.uniform(0.6, 1.6), s
+        th = rng.uniform(0, np.pi)
+        dx, dy = xx[y0:y1, x0:x1] - cx, yy[y0:y1, x0:x1] - cy
+        u = np.cos(th) * dx + np.sin(th) * dy
+        v = -np.sin(th) * dx + np.cos(th) * dy
+        img[y0:y1, x0:x1] += a * np.exp(-0.5 * ((u / sx) ** 2 + (v / sy) ** 2))
+    for _ in range(max(2, nb // 20)):  # oriented bars
+        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+        th = rng.uniform(0, np.pi)
+        ln, wd = rng.uniform(10, max(12.0, min(h, w) / 4)), rng.uniform(1.0, 3.0)
+        u = np.cos(th) * (xx - cx) + np.sin(th) * (yy - cy)
+        v = -np.sin(th) * (xx - cx) + np.cos(th) * (yy - cy)
+        img += rng.uniform(-0.3, 0.3) * ((np.abs(u) < ln) & (np.abs(v) < wd))
+    img += rng.normal(0, 0.01, img.shape).astype(np.float32)
+    base = np.clip(img, 0.0, 1.0) * 255.0
+    chans = [np.clip(base * g + o, 0, 255) for g, o in ((1.0, 0.0), (0.9, 12.0), (1.1, -10.0))]
+    out = np.stack(chans[:max(1, min(3, channels))], axis=2)
+    if channels == 4:
+        out = np.concatenate([out, np.full((h, w, 1), 255.0, np.float32)], axis=2)
+    return np.rint(out).astype(np.uint8)
