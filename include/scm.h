@@ -230,6 +230,30 @@ int scm_table_timings(scm_context* ctx, double* t, int32_t n);
  * value). */
 int scm_set_serial(scm_context* ctx, int32_t serial);
 
+/* ---- SIFT extraction (the producer of the
+ * `extraction` table; replaces SiftExtractionKernel::execute,
+ * integration/op_cpp/extraction_op.cc:70-121, REGISTER_OP(SiftExtraction)
+ * :124-130: input image_id + frame, outputs keypoints, descriptors, cameras).
+ * A frame is a Scanner Frame's buffer: height x width x channels bytes,
+ * row-major, channels 1, 3 or 4; as the reference's raw-bits FreeImage
+ * bitmap, channel 2 takes the red weight of the grey conversion. */
+typedef struct scm_frame {
+  const uint8_t* data;
+  int32_t width;
+  int32_t height;
+  int32_t channels;
+} scm_frame;
+/* n frames -> per frame the keypoints element (write_vector_to_element),
+ * the descriptors element (write_matrix_to_element, u8 128 per row) and the
+ * camera element (write_camera_to_element, io.cc:307-335); each blob
+ * library-allocated (scm_blob_free).  COLMAP's default
+ * SiftExtractionOptions; frames larger than max_image_size (3200) are
+ * rejected with SCM_E_INVALID (the reference rescales them with FreeImage,
+ * not implemented), as are frames below 16 x 16. */
+int scm_extract_frames(scm_context* ctx, int64_t n, const uint64_t* image_ids,
+                       const scm_frame* frames, scm_blob* keypoints_out,
+                       scm_blob* descriptors_out, scm_blob* cameras_out);
+
 #ifdef __cplusplus
 }
 #endif

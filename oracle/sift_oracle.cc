@@ -656,7 +656,9 @@ int oracle_sift_extract(const uint8_t* frame, int32_t width, int32_t height, int
                         uint64_t image_id, uint8_t** kp_out, size_t* kp_size, uint8_t** desc_out,
                         size_t* desc_size, uint8_t** cam_out, size_t* cam_size) {
   const SiftOpts o;
-  if (!frame || width < 1 || height < 1 || !(channels == 1 || channels == 3 || channels == 4))
+  // frames below 16 x 16 are rejected like the product's (4 octaves of an
+  // image that small have no interior pixels left; VLFeat would still run)
+  if (!frame || width < 16 || height < 16 || !(channels == 1 || channels == 3 || channels == 4))
     return SCM_E_INVALID;
   if (width > o.max_image_size || height > o.max_image_size) return SCM_E_INVALID;
   std::vector<uint8_t> grey;

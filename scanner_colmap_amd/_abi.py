@@ -36,7 +36,7 @@ EXPORTS = (
     "scm_table_load",
     "scm_table_run", "scm_table_run_packed", "scm_set_keep_matches",
     "scm_set_keep_matches_range",
-    "scm_table_matches", "scm_table_timings", "scm_set_serial",
+    "scm_table_matches", "scm_table_timings", "scm_set_serial", "scm_extract_frames",
 )
 
 
@@ -62,6 +62,12 @@ class MatchingOptions(Structure):
 
 class Element(Structure):
     _fields_ = [("buffer", POINTER(c_uint8)), ("size", c_size_t)]
+
+
+class Frame(Structure):
+    """scm_frame: a Scanner Frame's buffer (height x width x channels bytes)."""
+    _fields_ = [("data", POINTER(c_uint8)), ("width", c_int32), ("height", c_int32),
+                ("channels", c_int32)]
 
 
 class Blob(Structure):
@@ -118,6 +124,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                       POINTER(c_int64)]
     lib.scm_table_timings.argtypes = [c_void_p, POINTER(c_double), c_int32]
     lib.scm_set_serial.argtypes = [c_void_p, c_int32]
+    lib.scm_extract_frames.argtypes = [c_void_p, c_int64, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p]
     for name in EXPORTS:
         if name not in ("scm_abi_version", "scm_last_error", "scm_default_options",
                         "scm_pair_seed", "scm_blob_free", "scm_context_destroy"):
@@ -309,6 +317,26 @@ class Context:
         _check(self._lib.scm_table_run_packed(self._ptr, overlap, row_begin, row_end, byref(b),
                                               offs.ctypes.data))
         return PackedRows(b, offs)
+
+    def extract_frames(self, frames, image_ids=None) -> list:
+        """SiftExtractionKernel::execute on each frame (H x W x C uint8 arrays;
+        extraction_op.cc:70-121): a list of (keypoints, descriptors, camera)
+        io.cc element bytes."""
+        n = len(frames)
+        ids = np.asarray(image_ids if image_ids is not None else range(n), dtype=np.uint64)
+        keep = []
+        arr = (Frame * max(1, n))()
+        for i, f in enumerate(frames):
+            a = np.ascontiguousarray(f, dtype=np.uint8)
+            if a.ndim == 2:
+                a = a[:, :, None]
+            keep.append(a)
+            arr[i].data = a.ctypes.data_as(POINTER(c_uint8))
+            arr[i].height, arr[i].width, arr[i].channels = a.shape
+        outs = [(Blob * max(1, n))() for _ in range(3)]
+        _check(self._lib.scm_extract_frames(self._ptr, n, ids.ctypes.data, arr, outs[0], outs[1],
+                                            outs[2]))
+        return [tuple(_blob_bytes(o[i]) for o in outs) for i in range(n)]
 
     def set_serial(self, serial: bool = True) -> None:
         """Measurement only: stages one after the other (isolated kernel times)."""

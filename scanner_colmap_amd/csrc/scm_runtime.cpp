@@ -190,6 +190,7 @@ struct scm_context {
   int64_t keep_begin = 0, keep_end = INT64_MAX;  // rows whose matches are kept
   int64_t last_begin = 0, last_end = 0;
   std::vector<std::vector<std::pair<int64_t, std::vector<Match>>>> last_matches;
+  SiftState* sift = nullptr;  // SIFT extraction slots (scm_extract_frames), created on first use
 };
 
 namespace {
@@ -1359,6 +1360,8 @@ void scm_context_destroy(scm_context* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
   drain(ctx);
+  sift_state_destroy(ctx->sift);
+  ctx->sift = nullptr;
   if (ctx->profile && ctx->prof_pairs > 0) {
     static const char* names[] = {"sample",    "solve",   "score",  "cand_res", "seqsum",
                                   "lo_gather", "lo_est",  "lo_res", "other",    "n_batch",
@@ -1667,6 +1670,17 @@ int scm_table_run_packed(scm_context* ctx, int64_t overlap, int64_t row_begin, i
   rows_out->data = pk.data ? pk.data : (uint8_t*)std::malloc(1);
   rows_out->size = pk.size;
   return SCM_OK;
+}
+
+int scm_extract_frames(scm_context* ctx, int64_t n, const uint64_t* image_ids,
+                       const scm_frame* frames, scm_blob* keypoints_out,
+                       scm_blob* descriptors_out, scm_blob* cameras_out) {
+  if (!ctx) {
+    set_error("null context");
+    return SCM_E_INVALID;
+  }
+  return sift_extract_frames(&ctx->sift, ctx->device, n, image_ids, frames, keypoints_out,
+                             descriptors_out, cameras_out);
 }
 
 int scm_set_serial(scm_context* ctx, int32_t serial) {

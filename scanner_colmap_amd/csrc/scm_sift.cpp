@@ -1,0 +1,334 @@
+// Host side of the GPU SIFT extraction: the
+// SiftExtractionKernel::execute replacement (reference
+// integration/op_cpp/extraction_op.cc:70-121) behind scm_extract_frames.
+//
+// Per frame: upload (pinned staging), grey + 2x upsampling, the six Gaussian
+// levels of each of the 4 octaves, detection / refinement, orientations and
+// descriptors (sift_kernels.hip), then the counts and the features come back
+// and the host writes the three io.cc elements: COLMAP's DoG-level selection
+// of max_num_features (ExtractSiftFeaturesCPU keeps the coarsest levels whose
+// keypoint count first exceeds it), FeatureKeypoint(x, y, scale, orientation)
+// with the host libm's cosf / sinf, and the extractCamera SIMPLE_RADIAL camera.
+// Frames rotate over a few image slots, each with its own stream and HBM
+// workspace, so consecutive frames overlap (upload, kernels, read-back).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+
+#include "scm_internal.h"
+#include "sift_kernels.h"
+
+namespace scm {
+
+namespace {
+
+constexpr int kMaxImageSize = 3200;  // SiftExtractionOptions::max_image_size
+constexpr int kMinImageSize = 16;    // 4 octaves need >= 2 interior pixels in the last
+constexpr int kMaxNumFeatures = 8192;
+constexpr double kPeakThreshold = 0.02 / 3;
+constexpr double kEdgeThreshold = 10.0;
+constexpr int kSlots = 4;
+
+struct Slot {
+  hipStream_t st = nullptr;
+  DevBuf frame, ws, counts;
+  HostBuf pin_in, pin_cnt, pin_out;
+  SiftDev dev{};
+  int64_t nel_cap = 0;  // first-octave pixels the workspace holds
+  int64_t pending = -1; // frame index whose results are in flight
+  int w = 0, h = 0;
+};
+
+template <typename T>
+T* carve(uint8_t*& p, size_t n) {
+  T* r = reinterpret_cast<T*>(p);
+  p += (n * sizeof(T) + 255) & ~(size_t)255;
+  return r;
+}
+
+}  // namespace
+
+struct SiftState {
+  int device = 0;
+  DevBuf consts;
+  SiftConsts c{};
+  int widths[6] = {0, 0, 0, 0, 0, 0};
+  Slot slots[kSlots];
+};
+
+void sift_state_destroy(SiftState* s) {
+  if (!s) return;
+  (void)hipSetDevice(s->device);
+  for (Slot& sl : s->slots) {
+    if (sl.st) {
+      (void)hipStreamSynchronize(sl.st);
+      (void)hipStreamDestroy(sl.st);
+    }
+    sl.frame.release();
+    sl.ws.release();
+    sl.counts.release();
+    sl.pin_in.release();
+    sl.pin_cnt.release();
+    sl.pin_out.release();
+  }
+  s->consts.release();
+  delete s;
+}
+
+namespace {
+
+// _vl_sift_smooth's taps for one sigma (host libm exp, as the reference).
+int gauss_taps(double sigma, float* g) {
+  const int W = std::max((int)std::ceil(4.0 * sigma), 1);
+  float acc = 0;
+  for (int j = 0; j < 2 * W + 1; ++j) {
+    const float d = ((float)(j - W)) / ((float)sigma);
+    g[j] = (float)std::exp(-0.5 * (d * d));
+    acc += g[j];
+  }
+  for (int j = 0; j < 2 * W + 1; ++j) g[j] /= acc;
+  return W;
+}
+
+int init_state(SiftState* s) {
+  // VLFeat: sigmak = 2^(1/S), sigma0 = 1.6 sigmak, dsigma0 = sigma0 sqrt(1 - 1/sigmak^2),
+  // first level of the first octave: sd = sqrt(sa^2 - sb^2), sa = sigma0 sigmak^-1,
+  // sb = 0.5 * 2^1; level s: dsigma0 sigmak^s.
+  const double sigmak = std::pow(2.0, 1.0 / 3), sigma0 = 1.6 * sigmak;
+  const double dsigma0 = sigma0 * std::sqrt(1.0 - 1.0 / (sigmak * sigmak));
+  std::vector<float> taps(6 * kSiftMaxTaps, 0.0f);
+  const double sa = sigma0 * std::pow(sigmak, -1), sb = 0.5 * std::pow(2.0, 1);
+  s->widths[0] = gauss_taps(std::sqrt(sa * sa - sb * sb), taps.data());
+  for (int l = 0; l < 5; ++l)
+    s->widths[1 + l] = gauss_taps(dsigma0 * std::pow(sigmak, l), taps.data() + (1 + l) * kSiftMaxTaps);
+  double expn[257];
+  for (int k = 0; k < 257; ++k) expn[k] = std::exp(-(double)k * (25.0 / 256));
+  const size_t tb = taps.size() * sizeof(float), wb = 256, eb = sizeof(expn);
+  SCM_TRY(s->consts.ensure(tb + wb + eb));
+  uint8_t* base = s->consts.as<uint8_t>();
+  s->c.taps = reinterpret_cast<float*>(base);
+  s->c.widths = reinterpret_cast<int32_t*>(base + tb);
+  s->c.expn = reinterpret_cast<double*>(base + tb + wb);
+  SCM_HIP(hipMemcpy(s->c.taps, taps.data(), tb, hipMemcpyHostToDevice));
+  SCM_HIP(hipMemcpy(s->c.widths, s->widths, sizeof(s->widths), hipMemcpyHostToDevice));
+  SCM_HIP(hipMemcpy(s->c.expn, expn, eb, hipMemcpyHostToDevice));
+  for (Slot& sl : s->slots) SCM_HIP(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
+  return SCM_OK;
+}
+
+// Workspace of a slot for a frame whose first octave has nel pixels (2w x 2h).
+int ensure_slot(Slot& sl, int w, int h) {
+  const int64_t ow = 2 * (int64_t)w, oh = 2 * (int64_t)h, nel = ow * oh;
+  if (nel <= sl.nel_cap && sl.dev.cnt) return SCM_OK;
+  const int cand_cap = (int)std::min<int64_t>(std::max<int64_t>(65536, nel / 16), 1 << 22);
+  const int key_cap = std::min(cand_cap, 1 << 18);
+  const int feat_cap = 2 * key_cap;
+  const size_t bytes = 18 * (size_t)nel * 4 + 2 * (3 * (size_t)oh + 1) * 4 +
+                       (size_t)cand_cap * (16 + 32 + 8) +
+                       (size_t)key_cap * (32 + 4 + 16 + 4) +
+                       (size_t)feat_cap * (16 + 512 + 128 + 4) + 64 * 256;
+  SCM_TRY(sl.ws.ensure(bytes));
+  SCM_TRY(sl.counts.ensure(sizeof(SiftCounts)));
+  uint8_t* p = sl.ws.as<uint8_t>();
+  SiftDev& d = sl.dev;
+  d.levels = carve<float>(p, kSiftLevels * (size_t)nel);
+  d.temp = carve<float>(p, (size_t)nel);
+  d.dog = carve<float>(p, kSiftDogLevels * (size_t)nel);
+  d.grad = carve<float2>(p, 3 * (size_t)nel);
+  d.rowcnt = carve<int32_t>(p, 3 * (size_t)oh + 1);
+  d.rowoff = carve<int32_t>(p, 3 * (size_t)oh + 1);
+  d.cand = carve<SiftCand>(p, cand_cap);
+  d.ktmp = carve<SiftKey>(p, cand_cap);
+  d.flag = carve<int32_t>(p, cand_cap);
+  d.foff = carve<int32_t>(p, cand_cap);
+  d.keys = carve<SiftKey>(p, key_cap);
+  d.nori = carve<int32_t>(p, key_cap);
+  d.ang = carve<double>(p, 2 * (size_t)key_cap);
+  d.koff = carve<int32_t>(p, key_cap);
+  d.feat = carve<SiftFeat>(p, feat_cap);
+  d.descf = carve<float>(p, 128 * (size_t)feat_cap);
+  d.desc = carve<uint8_t>(p, 128 * (size_t)feat_cap);
+  d.stale = carve<int32_t>(p, feat_cap);
+  d.cnt = sl.counts.as<SiftCounts>();
+  d.cand_cap = cand_cap;
+  d.key_cap = key_cap;
+  d.feat_cap = feat_cap;
+  if ((size_t)(p - sl.ws.as<uint8_t>()) > sl.ws.bytes) {
+    set_error("sift workspace layout exceeds its allocation");
+    return SCM_E_INVALID;
+  }
+  sl.nel_cap = nel;
+  return SCM_OK;
+}
+
+int enqueue_frame(SiftState* s, Slot& sl, const scm_frame& f) {
+  const int w = f.width, h = f.height, ch = f.channels;
+  SCM_TRY(ensure_slot(sl, w, h));
+  const size_t fb = (size_t)w * h * ch;
+  SCM_TRY(sl.pin_in.ensure(fb));
+  SCM_TRY(sl.frame.ensure(fb));
+  std::memcpy(sl.pin_in.ptr, f.data, fb);
+  hipStream_t st = sl.st;
+  SCM_HIP(hipMemcpyAsync(sl.frame.ptr, sl.pin_in.ptr, fb, hipMemcpyHostToDevice, st));
+  SCM_HIP(hipMemsetAsync(sl.dev.cnt, 0, sizeof(SiftCounts), st));
+  SiftDev& d = sl.dev;
+  int ow = 2 * w, oh = 2 * h, pw = 0, ph = 0;  // this octave's and the previous octave's size
+  for (int o = -1; o < kSiftOctaves - 1; ++o) {
+    if (o >= 0) {  // VLFeat octave size: width >> o (width << 1 for o = -1)
+      pw = ow;
+      ph = oh;
+      ow = w >> o;
+      oh = h >> o;
+    }
+    const size_t so = (size_t)ow * oh;
+    if (o == -1) {
+      SCM_HIP(sift_upsample(sl.frame.as<uint8_t>(), w, h, ch, d.levels, st));
+      SCM_HIP(sift_smooth(d.levels, d.levels, d.temp, ow, oh, s->c, 0, s->widths[0], st));
+    } else {
+      // copy_and_downsample of level s_best = 2 (index 3) of the previous
+      // octave: every other pixel; no extra smoothing (sa == sb).  The source
+      // [3 pw ph, 4 pw ph) lies past the destination [0, ow oh).
+      SCM_HIP(sift_downsample(d.levels + 3 * (size_t)pw * ph, pw, d.levels, ow, oh, st));
+    }
+    for (int l = 1; l < kSiftLevels; ++l)
+      SCM_HIP(sift_smooth(d.levels + (l - 1) * so, d.levels + l * so, d.temp, ow, oh, s->c, l,
+                          s->widths[l], st));
+    SCM_HIP(sift_octave_detect(d, s->c, ow, oh, o, kPeakThreshold, kEdgeThreshold, st));
+    SCM_HIP(sift_octave_describe(d, s->c, ow, oh, o, st));
+  }
+  SCM_HIP(sift_fixup(d, st));
+  SCM_TRY(sl.pin_cnt.ensure(sizeof(SiftCounts)));
+  SCM_HIP(hipMemcpyAsync(sl.pin_cnt.ptr, d.cnt, sizeof(SiftCounts), hipMemcpyDeviceToHost, st));
+  sl.w = w;
+  sl.h = h;
+  return SCM_OK;
+}
+
+template <typename T>
+void put(std::vector<uint8_t>* b, const T& v) {
+  const uint8_t* q = reinterpret_cast<const uint8_t*>(&v);
+  b->insert(b->end(), q, q + sizeof(T));
+}
+
+// Wait for a slot's frame and write its three elements.
+int harvest(Slot& sl, uint64_t image_id, scm_blob* kp_out, scm_blob* desc_out, scm_blob* cam_out) {
+  SCM_HIP(hipStreamSynchronize(sl.st));
+  const SiftCounts cnt = *sl.pin_cnt.as<SiftCounts>();
+  if (cnt.overflow) {
+    set_error("sift: a frame exceeded the extractor's candidate / keypoint capacity");
+    return SCM_E_CAPACITY;
+  }
+  const int nf = cnt.nfeat;
+  // COLMAP: keep the coarsest DoG levels; the level whose keypoints first push
+  // the count past max_num_features is kept whole.
+  int first_keep = 0, acc = 0;
+  for (int l = kSiftOctaves * 3 - 1; l >= 0; --l) {
+    if (cnt.level_keys[l] == 0) continue;  // no such level in COLMAP's list
+    acc += cnt.level_keys[l];
+    if (acc > kMaxNumFeatures) {
+      first_keep = l;
+      break;
+    }
+  }
+  int start = 0;
+  for (int l = 0; l < first_keep; ++l) start += cnt.level_feats[l];
+  const int n = nf - start;
+  const size_t fbytes = (size_t)nf * sizeof(SiftFeat), dbytes = (size_t)nf * 128;
+  SCM_TRY(sl.pin_out.ensure(fbytes + dbytes + 64));
+  if (nf > 0) {
+    SCM_HIP(hipMemcpyAsync(sl.pin_out.ptr, sl.dev.feat, fbytes, hipMemcpyDeviceToHost, sl.st));
+    SCM_HIP(hipMemcpyAsync(sl.pin_out.as<uint8_t>() + fbytes, sl.dev.desc, dbytes,
+                           hipMemcpyDeviceToHost, sl.st));
+    SCM_HIP(hipStreamSynchronize(sl.st));
+  }
+  const SiftFeat* feat = sl.pin_out.as<SiftFeat>() + start;
+  const uint8_t* desc = sl.pin_out.as<uint8_t>() + fbytes + (size_t)start * 128;
+  std::vector<uint8_t> kb, db, cb;
+  kb.reserve(8 + 24 * (size_t)n);
+  put(&kb, (uint64_t)n);
+  for (int i = 0; i < n; ++i) {
+    const SiftFeat& f = feat[i];
+    const float sc = f.scale, ori = f.orientation;
+    const float kp[6] = {f.x, f.y, sc * std::cos(ori), -sc * std::sin(ori + 0.0f),
+                         sc * std::sin(ori), sc * std::cos(ori + 0.0f)};
+    for (float v : kp) put(&kb, v);
+  }
+  db.reserve(16 + 128 * (size_t)n);
+  put(&db, (uint64_t)n);
+  put(&db, (uint64_t)128);
+  db.insert(db.end(), desc, desc + 128 * (size_t)n);
+  // create_camera_buffer (io.cc:307-333) of extractCamera's SIMPLE_RADIAL camera.
+  const double focal = 1.2 * std::max(sl.w, sl.h);
+  const double params[4] = {focal, sl.w / 2.0, sl.h / 2.0, 0.0};
+  put(&cb, (uint64_t)(8 + 4 + 4 + 8 + 8 + 1 + 8 + 4 * 8));
+  put(&cb, (uint32_t)image_id);
+  put(&cb, (int32_t)2);
+  put(&cb, (uint64_t)sl.w);
+  put(&cb, (uint64_t)sl.h);
+  put(&cb, (uint8_t)0);
+  put(&cb, (uint64_t)4);
+  for (double p : params) put(&cb, p);
+  SCM_TRY(make_blob(kb, kp_out));
+  SCM_TRY(make_blob(db, desc_out));
+  SCM_TRY(make_blob(cb, cam_out));
+  return SCM_OK;
+}
+
+}  // namespace
+
+int sift_extract_frames(SiftState** state, int device, int64_t n, const uint64_t* ids,
+                        const scm_frame* frames, scm_blob* kp_out, scm_blob* desc_out,
+                        scm_blob* cam_out) {
+  if (n < 0 || (n > 0 && (!ids || !frames || !kp_out || !desc_out || !cam_out))) {
+    set_error("scm_extract_frames: null argument");
+    return SCM_E_INVALID;
+  }
+  for (int64_t i = 0; i < n; ++i) {
+    const scm_frame& f = frames[i];
+    if (!f.data || !(f.channels == 1 || f.channels == 3 || f.channels == 4) ||
+        f.width < kMinImageSize || f.height < kMinImageSize) {
+      set_error("scm_extract_frames: frame " + std::to_string(i) +
+                " is not a >= 16 x 16 frame of 1, 3 or 4 channels");
+      return SCM_E_INVALID;
+    }
+    if (f.width > kMaxImageSize || f.height > kMaxImageSize) {
+      set_error("scm_extract_frames: frame " + std::to_string(i) +
+                " exceeds max_image_size 3200 (the reference rescales it with FreeImage; not "
+                "implemented)");
+      return SCM_E_INVALID;
+    }
+  }
+  SCM_HIP(hipSetDevice(device));
+  if (!*state) {
+    std::unique_ptr<SiftState> s(new SiftState());
+    s->device = device;
+    SCM_TRY(init_state(s.get()));
+    *state = s.release();
+  }
+  SiftState* s = *state;
+  for (Slot& sl : s->slots) sl.pending = -1;
+  int rc = SCM_OK;
+  for (int64_t i = 0; i < n && rc == SCM_OK; ++i) {
+    Slot& sl = s->slots[i % kSlots];
+    if (sl.pending >= 0) {
+      const int64_t j = sl.pending;
+      sl.pending = -1;
+      rc = harvest(sl, ids[j], &kp_out[j], &desc_out[j], &cam_out[j]);
+      if (rc != SCM_OK) break;
+    }
+    rc = enqueue_frame(s, sl, frames[i]);
+    if (rc == SCM_OK) sl.pending = i;
+  }
+  for (int64_t i = std::max<int64_t>(0, n - kSlots); i < n; ++i) {
+    Slot& sl = s->slots[i % kSlots];
+    if (sl.pending == i) {
+      sl.pending = -1;
+      const int r = harvest(sl, ids[i], &kp_out[i], &desc_out[i], &cam_out[i]);
+      if (rc == SCM_OK) rc = r;
+    }
+  }
+  return rc;
+}
+
+}  // namespace scm

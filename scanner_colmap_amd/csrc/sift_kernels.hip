@@ -1,0 +1,644 @@
+// GPU SIFT extraction kernels.
+//
+// Replaces SiftExtractionKernel::execute (reference
+// integration/op_cpp/extraction_op.cc:70-121): the op's grey conversion, then
+// colmap::ExtractSiftFeaturesCPU, i.e. the VLFeat covariant SIFT filter
+// (vl/sift.c) with COLMAP's default SiftExtractionOptions (first_octave -1,
+// 4 octaves, 3 levels, peak 0.02 / 3, edge 10, 2 orientations, L1-root).
+// Every floating-point value follows the reference's operation sequence
+// (built with -ffp-contract=off; the same sequence as oracle/sift_oracle.cc),
+// so the keypoints and descriptors are the oracle's bit for bit:
+//   * Gaussian smoothing: vl_imconvcol_vf's sum over the window in ascending
+//     source order (multiply, then add, float), vertical pass first, edge
+//     samples repeated (VL_PAD_BY_CONTINUITY); one output per thread, the
+//     window staged in LDS (HBM-bound: one read and one write per pass);
+//   * detection in VLFeat's scan order (s, y, x) by per-row counts, one
+//     exclusive scan and an ordered write (ballot prefix within each wave);
+//   * refinement, orientation histograms and descriptors one thread per
+//     keypoint, sequential in VLFeat's loop order (the per-keypoint work is
+//     a serial float / double accumulation whose rounding the reference
+//     fixes), the descriptor's 128 bins in LDS (bin-major, lane-minor: no bank
+//     conflicts).
+// Layout: one image slot holds the first octave's six levels (the largest),
+// later octaves reuse the same buffers at their smaller size.
+#include "sift_kernels.h"
+
+namespace scm {
+namespace {
+
+constexpr double kPi = 3.141592653589793;        // VL_PI
+constexpr float kEpsF = 1.19209290E-07F;         // VL_EPSILON_F
+constexpr double kEpsD = 2.220446049250313e-16;  // VL_EPSILON_D
+constexpr int kSMin = -1, kSMax = 4, kS = 3;
+constexpr int kVTile = 64;   // vertical pass: 64 columns x 64 rows per block
+constexpr int kHTile = 1024; // horizontal pass: 1024 outputs of a row per block
+constexpr int kGrid = 2048;  // grid-stride kernels over device-side counts
+
+// The op's grey value (FreeImage B, G, R memory order; LUMA_REC709 + 0.5)
+// as the float the SIFT filter reads (grey / 255.0f).
+__device__ __forceinline__ float grey_at(const uint8_t* f, int w, int ch, int y, int x) {
+  const uint8_t* p = f + ((size_t)y * w + x) * ch;
+  uint8_t g;
+  if (ch == 1) {
+    g = p[0];
+  } else {
+    const float r = p[2], gg = p[1], b = p[0];
+    g = (uint8_t)(0.2126F * r + 0.7152F * gg + 0.0722F * b + 0.5F);
+  }
+  return (float)g / 255.0f;
+}
+
+// copy_and_upsample_rows twice (x first, then y): out is 2w x 2h.
+__global__ void upsample_kernel(const uint8_t* __restrict__ f, int w, int h, int ch,
+                                float* __restrict__ out) {
+  const int X = blockIdx.x * blockDim.x + threadIdx.x, Y = blockIdx.y;
+  if (X >= 2 * w) return;
+  const int i = X >> 1;
+  auto row_up = [&](int yy) -> float {
+    const float a = grey_at(f, w, ch, yy, i);
+    if ((X & 1) == 0 || i + 1 >= w) return a;
+    return (a + grey_at(f, w, ch, yy, i + 1)) * 0.5f;
+  };
+  const int y = Y >> 1;
+  const float a = row_up(y);
+  float v = a;
+  if ((Y & 1) && y + 1 < h) v = (a + row_up(y + 1)) * 0.5f;
+  out[(size_t)Y * 2 * w + X] = v;
+}
+
+__global__ __launch_bounds__(256) void smooth_v_kernel(const float* __restrict__ in,
+                                                       float* __restrict__ out, int w, int h,
+                                                       const float* __restrict__ taps, int W) {
+  __shared__ float tile[(kVTile + kSiftMaxTaps - 1) * kVTile];
+  __shared__ float g[kSiftMaxTaps];
+  const int tx = threadIdx.x & (kVTile - 1), ty = threadIdx.x / kVTile;
+  const int x = blockIdx.x * kVTile + tx;
+  const int y0 = blockIdx.y * kVTile;
+  if ((int)threadIdx.x < 2 * W + 1) g[threadIdx.x] = taps[threadIdx.x];
+  const int nrows = min(kVTile, h - y0) + 2 * W;
+  for (int r = ty; r < nrows; r += 256 / kVTile) {
+    const int p = min(max(y0 - W + r, 0), h - 1);
+    tile[r * kVTile + tx] = x < w ? in[(size_t)p * w + x] : 0.0f;
+  }
+  __syncthreads();
+  if (x >= w) return;
+  for (int yl = ty; yl < kVTile; yl += 256 / kVTile) {
+    const int y = y0 + yl;
+    if (y >= h) break;
+    float acc = 0.0f;
+    for (int k = 0; k <= 2 * W; ++k) acc += tile[(yl + k) * kVTile + tx] * g[2 * W - k];
+    out[(size_t)y * w + x] = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void smooth_h_kernel(const float* __restrict__ in,
+                                                       float* __restrict__ out, int w, int h,
+                                                       const float* __restrict__ taps, int W) {
+  __shared__ float row[kHTile + kSiftMaxTaps - 1];
+  __shared__ float g[kSiftMaxTaps];
+  const int y = blockIdx.y, x0 = blockIdx.x * kHTile;
+  if ((int)threadIdx.x < 2 * W + 1) g[threadIdx.x] = taps[threadIdx.x];
+  const float* src = in + (size_t)y * w;
+  const int n = min(kHTile, w - x0) + 2 * W;
+  for (int i = threadIdx.x; i < n; i += 256) row[i] = src[min(max(x0 - W + i, 0), w - 1)];
+  __syncthreads();
+  for (int xl = threadIdx.x; xl < kHTile; xl += 256) {
+    const int x = x0 + xl;
+    if (x >= w) break;
+    float acc = 0.0f;
+    for (int k = 0; k <= 2 * W; ++k) acc += row[xl + k] * g[2 * W - k];
+    out[(size_t)y * w + x] = acc;
+  }
+}
+
+__global__ void downsample_kernel(const float* __restrict__ in, int w_in, float* __restrict__ out,
+                                  int w, int h) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x < w) out[(size_t)y * w + x] = in[(size_t)(2 * y) * w_in + 2 * x];
+}
+
+__global__ void dog_kernel(const float* __restrict__ lev, float* __restrict__ dog, size_t so) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < so;
+       i += (size_t)gridDim.x * blockDim.x)
+#pragma unroll
+    for (int l = 0; l < kSiftDogLevels; ++l) dog[l * so + i] = lev[(l + 1) * so + i] - lev[l * so + i];
+}
+
+// vl_sift_detect's 26-neighbour strict extremum test at DoG level s.
+__device__ __forceinline__ bool is_extremum(const float* __restrict__ dog, int w, size_t so, int x,
+                                            int y, int s, double tp) {
+  const float* pt = dog + so * (size_t)(s - kSMin) + (size_t)y * w + x;
+  const float v = *pt;
+  bool mx = v >= 0.8 * tp, mn = v <= -0.8 * tp;
+  if (!(mx || mn)) return false;
+  for (int ds = -1; ds <= 1; ++ds)
+    for (int dy = -1; dy <= 1; ++dy)
+      for (int dx = -1; dx <= 1; ++dx) {
+        if (!ds && !dy && !dx) continue;
+        const float u = *(pt + (ptrdiff_t)ds * (ptrdiff_t)so + (ptrdiff_t)dy * w + dx);
+        mx = mx && v > u;
+        mn = mn && v < u;
+      }
+  return mx || mn;
+}
+
+// Extrema per (level l = s, row y): grid (h, 3).
+__global__ __launch_bounds__(256) void detect_count_kernel(const float* __restrict__ dog, int w,
+                                                           int h, double tp,
+                                                           int32_t* __restrict__ rowcnt) {
+  __shared__ int c;
+  const int y = blockIdx.x, s = blockIdx.y;
+  if (threadIdx.x == 0) c = 0;
+  __syncthreads();
+  int mine = 0;
+  if (y >= 1 && y < h - 1)
+    for (int x = 1 + threadIdx.x; x < w - 1; x += 256)
+      mine += is_extremum(dog, w, (size_t)w * h, x, y, s, tp);
+  if (mine) atomicAdd(&c, mine);
+  __syncthreads();
+  if (threadIdx.x == 0) rowcnt[s * h + y] = c;
+}
+
+// The extrema of one (level, row) in x order at rowoff[level h + row].
+__global__ __launch_bounds__(256) void detect_write_kernel(const float* __restrict__ dog, int w,
+                                                           int h, double tp,
+                                                           const int32_t* __restrict__ rowoff,
+                                                           SiftCand* __restrict__ cand, int cap) {
+  __shared__ int wsum[4];
+  const int y = blockIdx.x, s = blockIdx.y;
+  if (y < 1 || y >= h - 1) return;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int base = rowoff[s * h + y];
+  for (int x0 = 1; x0 < w - 1; x0 += 256) {
+    const int x = x0 + threadIdx.x;
+    const bool f = x < w - 1 && is_extremum(dog, w, (size_t)w * h, x, y, s, tp);
+    const uint64_t b = __ballot(f);
+    if (lane == 0) wsum[wave] = __popcll(b);
+    __syncthreads();
+    int off = 0;
+    for (int k = 0; k < wave; ++k) off += wsum[k];
+    const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    if (f) {
+      const int idx = base + off + __popcll(b & ((1ull << lane) - 1ull));
+      if (idx < cap) cand[idx] = SiftCand{x, y, s, 0};
+    }
+    base += tot;
+    __syncthreads();
+  }
+}
+
+// Exclusive scan of n = (n_dev ? *n_dev : n_const) counts, one workgroup;
+// out[i] = base + prefix with base = (acc ? *acc : 0); *total = sum,
+// *acc = base + sum.
+__global__ __launch_bounds__(1024) void scan_kernel(const int32_t* __restrict__ in,
+                                                    int32_t* __restrict__ out,
+                                                    const int32_t* __restrict__ n_dev, int n_const,
+                                                    int cap, int32_t* __restrict__ total,
+                                                    int32_t* __restrict__ acc) {
+  __shared__ int buf[1024];
+  const int tid = threadIdx.x;
+  const int n = min(n_dev ? *n_dev : n_const, cap);
+  const int base = acc ? *acc : 0;
+  int run = base;
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    const int v = c0 + tid < n ? in[c0 + tid] : 0;
+    buf[tid] = v;
+    __syncthreads();
+    for (int d = 1; d < 1024; d <<= 1) {
+      const int t = tid >= d ? buf[tid - d] : 0;
+      __syncthreads();
+      buf[tid] += t;
+      __syncthreads();
+    }
+    if (c0 + tid < n) out[c0 + tid] = run + buf[tid] - v;
+    run += buf[1023];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (total) *total = run - base;
+    if (acc) *acc = run;
+  }
+}
+
+__global__ void set_count_kernel(SiftCounts* cnt, const int32_t* __restrict__ tot, int which,
+                                 int cap) {
+  const int v = *tot;
+  if (v > cap) cnt->overflow = 1;
+  if (which == 0) cnt->ncand = min(v, cap);
+  else cnt->nkey = min(v, cap);
+}
+
+// Keypoint refinement of vl_sift_detect (quadratic fit, <= 5 moves, Gauss
+// elimination with partial pivoting, peak / edge / bounds tests).
+__global__ __launch_bounds__(64) void refine_kernel(const float* __restrict__ dog, int w, int h,
+                                                    const SiftCand* __restrict__ cand,
+                                                    const SiftCounts* __restrict__ cnt,
+                                                    SiftKey* __restrict__ out,
+                                                    int32_t* __restrict__ flag, double tp,
+                                                    double te, double sigma0, int octave) {
+  const int n = cnt->ncand;
+  const size_t so = (size_t)w * h;
+  const double xper = ldexp(1.0, octave);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const SiftCand c = cand[i];
+    int x = c.x, y = c.y;
+    const int s = c.s;
+    double Dx = 0, Dy = 0, Ds = 0, Dxx = 0, Dyy = 0, Dss = 0, Dxy = 0, Dxs = 0, Dys = 0;
+    double A[9], b[3];
+    int dx = 0, dy = 0;
+    const float* pt = nullptr;
+    for (int iter = 0; iter < 5; ++iter) {
+      x += dx;
+      y += dy;
+      pt = dog + (size_t)x + (size_t)y * w + so * (size_t)(s - kSMin);
+#define AT(ax, ay, as) ((double)*(pt + (ax) + (ptrdiff_t)(ay) * w + (ptrdiff_t)(as) * (ptrdiff_t)so))
+      Dx = 0.5 * (AT(1, 0, 0) - AT(-1, 0, 0));
+      Dy = 0.5 * (AT(0, 1, 0) - AT(0, -1, 0));
+      Ds = 0.5 * (AT(0, 0, 1) - AT(0, 0, -1));
+      Dxx = (AT(1, 0, 0) + AT(-1, 0, 0) - 2.0 * AT(0, 0, 0));
+      Dyy = (AT(0, 1, 0) + AT(0, -1, 0) - 2.0 * AT(0, 0, 0));
+      Dss = (AT(0, 0, 1) + AT(0, 0, -1) - 2.0 * AT(0, 0, 0));
+      Dxy = 0.25 * (AT(1, 1, 0) + AT(-1, -1, 0) - AT(-1, 1, 0) - AT(1, -1, 0));
+      Dxs = 0.25 * (AT(1, 0, 1) + AT(-1, 0, -1) - AT(-1, 0, 1) - AT(1, 0, -1));
+      Dys = 0.25 * (AT(0, 1, 1) + AT(0, -1, -1) - AT(0, -1, 1) - AT(0, 1, -1));
+#undef AT
+      A[0] = Dxx; A[4] = Dyy; A[8] = Dss;
+      A[3] = A[1] = Dxy;
+      A[6] = A[2] = Dxs;
+      A[7] = A[5] = Dys;
+      b[0] = -Dx; b[1] = -Dy; b[2] = -Ds;
+      for (int j = 0; j < 3; ++j) {
+        double maxa = 0, maxabsa = 0;
+        int maxi = -1;
+        for (int ii = j; ii < 3; ++ii) {
+          const double av = A[ii + 3 * j], absa = fabs(av);
+          if (absa > maxabsa) {
+            maxa = av;
+            maxabsa = absa;
+            maxi = ii;
+          }
+        }
+        if (maxabsa < 1e-10f) {
+          b[0] = b[1] = b[2] = 0;
+          break;
+        }
+        const int r = maxi;
+        for (int jj = j; jj < 3; ++jj) {
+          const double t = A[r + 3 * jj];
+          A[r + 3 * jj] = A[j + 3 * jj];
+          A[j + 3 * jj] = t;
+          A[j + 3 * jj] /= maxa;
+        }
+        const double t = b[j];
+        b[j] = b[r];
+        b[r] = t;
+        b[j] /= maxa;
+        for (int ii = j + 1; ii < 3; ++ii) {
+          const double xx = A[ii + 3 * j];
+          for (int jj = j; jj < 3; ++jj) A[ii + 3 * jj] -= xx * A[j + 3 * jj];
+          b[ii] -= xx * b[j];
+        }
+      }
+      for (int ii = 2; ii > 0; --ii) {
+        const double xx = b[ii];
+        for (int k = ii - 1; k >= 0; --k) b[k] -= xx * A[k + 3 * ii];
+      }
+      dx = ((b[0] > 0.6 && x < w - 2) ? 1 : 0) + ((b[0] < -0.6 && x > 1) ? -1 : 0);
+      dy = ((b[1] > 0.6 && y < h - 2) ? 1 : 0) + ((b[1] < -0.6 && y > 1) ? -1 : 0);
+      if (dx == 0 && dy == 0) break;
+    }
+    const double val = (double)*pt + 0.5 * (Dx * b[0] + Dy * b[1] + Ds * b[2]);
+    const double score = (Dxx + Dyy) * (Dxx + Dyy) / (Dxx * Dyy - Dxy * Dxy);
+    const double xn = x + b[0], yn = y + b[1], sn = s + b[2];
+    const bool ok = fabs(val) > tp && score < (te + 1) * (te + 1) / te && score >= 0 &&
+                    fabs(b[0]) < 1.5 && fabs(b[1]) < 1.5 && fabs(b[2]) < 1.5 && xn >= 0 &&
+                    xn <= w - 1 && yn >= 0 && yn <= h - 1 && sn >= kSMin && sn <= kSMax;
+    flag[i] = ok ? 1 : 0;
+    if (ok) {
+      SiftKey k;
+      k.o = octave;
+      k.ix = x;
+      k.iy = y;
+      k.is = s;
+      k.s = (float)sn;
+      k.x = (float)(xn * xper);
+      k.y = (float)(yn * xper);
+      k.sigma = (float)(sigma0 * pow(2.0, sn / kS) * xper);
+      out[i] = k;
+    }
+  }
+}
+
+__global__ void compact_keys_kernel(const SiftKey* __restrict__ ktmp, const int32_t* __restrict__ flag,
+                                    const int32_t* __restrict__ off, SiftCounts* __restrict__ cnt,
+                                    SiftKey* __restrict__ keys, int cap, int octave) {
+  const int n = cnt->ncand;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+    if (flag[i]) {
+      const int j = off[i];
+      if (j < cap) {
+        keys[j] = ktmp[i];
+        atomicAdd(&cnt->level_keys[(octave + 1) * 3 + ktmp[i].is], 1);
+      }
+    }
+}
+
+// vl/mathop.h
+__device__ __forceinline__ float fast_resqrt_f(float x) {
+  const float xhalf = 0.5F * x;
+  float y = __int_as_float(0x5f3759df - (__float_as_int(x) >> 1));
+  y = y * (1.5F - xhalf * y * y);
+  y = y * (1.5F - xhalf * y * y);
+  return y;
+}
+__device__ __forceinline__ float fast_sqrt_f(float x) { return (x < 1e-8) ? 0 : x * fast_resqrt_f(x); }
+__device__ __forceinline__ float fast_atan2_f(float y, float x) {
+  const float c3 = 0.1821F, c1 = 0.9675F;
+  const float abs_y = fabsf(y) + kEpsF;
+  float angle, r;
+  if (x >= 0) {
+    r = (x - abs_y) / (x + abs_y);
+    angle = (float)(kPi / 4);
+  } else {
+    r = (x + abs_y) / (abs_y - x);
+    angle = (float)(3 * kPi / 4);
+  }
+  angle += (c3 * r * r - c1) * r;
+  return (y < 0) ? -angle : angle;
+}
+__device__ __forceinline__ float mod_2pi_f(float x) {
+  while (x > (float)(2 * kPi)) x -= (float)(2 * kPi);
+  while (x < 0.0F) x += (float)(2 * kPi);
+  return x;
+}
+__device__ __forceinline__ double fast_expn(const double* __restrict__ tab, double x) {
+  if (x > 25.0) return 0.0;
+  x *= 256 / 25.0;
+  const int i = (int)floor(x);
+  const double r = x - i;
+  const double a = tab[i], b = tab[i + 1];
+  return a + r * (b - a);
+}
+
+// update_gradient for levels s = 0 .. 2: (modulus, angle in [0, 2 pi]).
+__global__ void gradient_kernel(const float* __restrict__ lev, float2* __restrict__ grad, int w,
+                                int h) {
+  const size_t so = (size_t)w * h;
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y, l = blockIdx.z;
+  if (x >= w) return;
+  const float* p = lev + so * (size_t)(l + 1) + (size_t)y * w + x;
+  float gx, gy;
+  if (x == 0) gx = p[1] - p[0];
+  else if (x == w - 1) gx = p[0] - p[-1];
+  else gx = (p[1] - p[-1]) * 0.5f;
+  if (y == 0) gy = p[w] - p[0];
+  else if (y == h - 1) gy = p[0] - p[-w];
+  else gy = (p[w] - p[-w]) * 0.5f;
+  grad[so * l + (size_t)y * w + x] =
+      make_float2(fast_sqrt_f(gx * gx + gy * gy), mod_2pi_f((float)(fast_atan2_f(gy, gx) + 2 * kPi)));
+}
+
+// vl_sift_calc_keypoint_orientations, one thread per keypoint.
+__global__ __launch_bounds__(64) void orient_kernel(const float2* __restrict__ grad, int w, int h,
+                                                    const SiftKey* __restrict__ keys,
+                                                    SiftCounts* __restrict__ cnt,
+                                                    int32_t* __restrict__ nori,
+                                                    double* __restrict__ ang,
+                                                    const double* __restrict__ expn, int octave) {
+  const int n = cnt->nkey;
+  const double xper = ldexp(1.0, octave);
+  const size_t so = (size_t)w * h;
+  constexpr int nbins = 36;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const SiftKey k = keys[i];
+    const double x = k.x / xper, y = k.y / xper, sigma = k.sigma / xper;
+    const int xi = (int)(x + 0.5), yi = (int)(y + 0.5), si = k.is;
+    const double sigmaw = 1.5 * sigma;
+    const int W = max((int)floor(3.0 * sigmaw), 1);
+    int na = 0;
+    double out[4] = {0, 0, 0, 0};
+    if (!(xi < 0 || xi > w - 1 || yi < 0 || yi > h - 1 || si < kSMin + 1 || si > kSMax - 2)) {
+      double hist[nbins];
+      for (int b = 0; b < nbins; ++b) hist[b] = 0;
+      const float2* pt = grad + so * (size_t)(si - kSMin - 1) + (size_t)yi * w + xi;
+      for (int ys = max(-W, -yi); ys <= min(W, h - 1 - yi); ++ys)
+        for (int xs = max(-W, -xi); xs <= min(W, w - 1 - xi); ++xs) {
+          const double dx = (double)(xi + xs) - x, dy = (double)(yi + ys) - y;
+          const double r2 = dx * dx + dy * dy;
+          if (r2 >= W * W + 0.6) continue;
+          const double wgt = fast_expn(expn, r2 / (2 * sigmaw * sigmaw));
+          const float2 g = pt[xs + (ptrdiff_t)ys * w];
+          const double mod = g.x, an = g.y;
+          const int bin = (int)floor(nbins * an / (2 * kPi));
+          hist[bin % nbins] += mod * wgt;
+        }
+      for (int iter = 0; iter < 6; ++iter) {
+        double prev = hist[nbins - 1];
+        const double first = hist[0];
+        int b;
+        for (b = 0; b < nbins - 1; ++b) {
+          const double nh = (prev + hist[b] + hist[(b + 1) % nbins]) / 3.0;
+          prev = hist[b];
+          hist[b] = nh;
+        }
+        hist[b] = (prev + hist[b] + first) / 3.0;
+      }
+      double maxh = 0;
+      for (int b = 0; b < nbins; ++b) maxh = fmax(maxh, hist[b]);
+      for (int b = 0; b < nbins; ++b) {
+        const double h0 = hist[b], hm = hist[(b - 1 + nbins) % nbins], hp = hist[(b + 1 + nbins) % nbins];
+        if (h0 > 0.8 * maxh && h0 > hm && h0 > hp) {
+          const double di = -0.5 * (hp - hm) / (hp + hm - 2 * h0);
+          out[na++] = 2 * kPi * (b + di + 0.5) / nbins;
+          if (na == 4) break;
+        }
+      }
+    }
+    const int nu = min(na, 2);
+    nori[i] = nu;
+    ang[2 * i] = out[0];
+    ang[2 * i + 1] = out[1];
+    if (nu) atomicAdd(&cnt->level_feats[(octave + 1) * 3 + si], nu);
+  }
+}
+
+// COLMAP L1RootNormalizeFeatureDescriptors + FeatureDescriptorsToUnsignedByte
+// + TransformVLFeatToUBCFeatureDescriptors on one 128-float descriptor.
+__device__ void l1root_u8(float* d, int stride, uint8_t* __restrict__ out) {
+  float norm = 0;
+  for (int i = 0; i < 128; ++i) norm += fabsf(d[i * stride]);
+  for (int i = 0; i < 128; ++i) d[i * stride] = d[i * stride] / norm;
+  for (int i = 0; i < 128; ++i) d[i * stride] = sqrtf(d[i * stride]);
+  for (int c = 0; c < 16; ++c)
+    for (int k = 0; k < 8; ++k) {
+      const float v = roundf(512.0f * d[(8 * c + k) * stride]);
+      const float lo = (0.0f < v) ? v : 0.0f;  // std::max(0.0f, v)
+      const float hi = (lo < 255.0f) ? lo : 255.0f;  // std::min(255.0f, lo)
+      out[8 * c + ((8 - k) & 7)] = (uint8_t)hi;
+    }
+}
+
+// vl_sift_calc_keypoint_descriptor + the COLMAP conversions, one thread per
+// keypoint (its <= 2 orientations in order).  The 4 x 4 x 8 histogram lives
+// in LDS, bin b of lane L at hist[b * 64 + L].
+__global__ __launch_bounds__(64) void descriptor_kernel(
+    const float2* __restrict__ grad, int w, int h, const SiftKey* __restrict__ keys,
+    SiftCounts* __restrict__ cnt, const int32_t* __restrict__ nori, const double* __restrict__ ang,
+    const int32_t* __restrict__ koff, SiftFeat* __restrict__ feat, float* __restrict__ descf,
+    uint8_t* __restrict__ desc, int32_t* __restrict__ stale, const double* __restrict__ expn,
+    int feat_cap, int octave) {
+  __shared__ float hist[128 * 64];
+  constexpr int NBP = 4, NBO = 8;
+  const int lane = threadIdx.x;
+  float* hb = hist + lane;
+  const int n = cnt->nkey;
+  const double xper = ldexp(1.0, octave);
+  const size_t so = (size_t)w * h;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const SiftKey k = keys[i];
+    for (int o = 0; o < nori[i]; ++o) {
+      const int fi = koff[i] + o;
+      if (fi >= feat_cap) {
+        cnt->overflow = 1;
+        break;
+      }
+      const double angle0 = ang[2 * i + o];
+      feat[fi] = SiftFeat{k.x + 0.5f, k.y + 0.5f, k.sigma, (float)angle0};
+      const double x = k.x / xper, y = k.y / xper, sigma = k.sigma / xper;
+      const int xi = (int)(x + 0.5), yi = (int)(y + 0.5), si = k.is;
+      if (xi < 0 || xi >= w || yi < 0 || yi >= h - 1 || si < kSMin + 1 || si > kSMax - 2) {
+        // vl_sift_calc_keypoint_descriptor returns before writing: COLMAP
+        // re-normalises the previous descriptor's buffer (sift_fixup)
+        stale[fi] = 1;
+        atomicAdd(&cnt->nstale, 1);
+        continue;
+      }
+      stale[fi] = 0;
+      const double st0 = sin(angle0), ct0 = cos(angle0);
+      const double SBP = 3.0 * sigma + kEpsD;
+      const int W = (int)floor(sqrt(2.0) * SBP * (NBP + 1) / 2.0 + 0.5);
+      for (int b = 0; b < 128; ++b) hb[b * 64] = 0.0f;
+      const float2* pt = grad + so * (size_t)(si - kSMin - 1) + (size_t)yi * w + xi;
+      for (int dyi = max(-W, 1 - yi); dyi <= min(W, h - yi - 2); ++dyi)
+        for (int dxi = max(-W, 1 - xi); dxi <= min(W, w - xi - 2); ++dxi) {
+          const float2 g = pt[dxi + (ptrdiff_t)dyi * w];
+          const float mod = g.x, angle = g.y;
+          const float theta = mod_2pi_f((float)(angle - angle0));
+          const float dx = (float)(xi + dxi - x);
+          const float dy = (float)(yi + dyi - y);
+          const float nx = (float)((ct0 * dx + st0 * dy) / SBP);
+          const float ny = (float)((-st0 * dx + ct0 * dy) / SBP);
+          const float nt = (float)(NBO * theta / (2 * kPi));
+          const float wsigma = 2.0f;
+          const float win = (float)fast_expn(expn, (nx * nx + ny * ny) / (2.0 * wsigma * wsigma));
+          const int binx = (int)floorf((float)(nx - 0.5));
+          const int biny = (int)floorf((float)(ny - 0.5));
+          const int bint = (int)floorf(nt);
+          const float rbinx = (float)(nx - (binx + 0.5));
+          const float rbiny = (float)(ny - (biny + 0.5));
+          const float rbint = nt - bint;
+          for (int dbinx = 0; dbinx < 2; ++dbinx)
+            for (int dbiny = 0; dbiny < 2; ++dbiny)
+              for (int dbint = 0; dbint < 2; ++dbint)
+                if (binx + dbinx >= -(NBP / 2) && binx + dbinx < (NBP / 2) &&
+                    biny + dbiny >= -(NBP / 2) && biny + dbiny < (NBP / 2)) {
+                  const float weight = win * mod * fabsf(1 - dbinx - rbinx) *
+                                       fabsf(1 - dbiny - rbiny) * fabsf(1 - dbint - rbint);
+                  const int bin = ((bint + dbint) % NBO) + (biny + dbiny + NBP / 2) * NBO * NBP +
+                                  (binx + dbinx + NBP / 2) * NBO;
+                  hb[bin * 64] += weight;
+                }
+        }
+      for (int pass = 0; pass < 2; ++pass) {  // normalize, truncate at 0.2, normalize
+        float norm = 0;
+        for (int b = 0; b < 128; ++b) norm += hb[b * 64] * hb[b * 64];
+        norm = fast_sqrt_f(norm) + kEpsF;
+        for (int b = 0; b < 128; ++b) hb[b * 64] /= norm;
+        if (pass == 0)
+          for (int b = 0; b < 128; ++b)
+            if (hb[b * 64] > 0.2) hb[b * 64] = 0.2f;
+      }
+      l1root_u8(hb, 64, desc + (size_t)fi * 128);
+      float* df = descf + (size_t)fi * 128;
+      for (int b = 0; b < 128; ++b) df[b] = hb[b * 64];
+    }
+  }
+}
+
+// The unwritten descriptors in feature order: each is the L1-root of the
+// previous feature's (float) buffer, the first one's of zeros.
+__global__ void fixup_kernel(const SiftCounts* __restrict__ cnt, const int32_t* __restrict__ stale,
+                             float* __restrict__ descf, uint8_t* __restrict__ desc, int feat_cap) {
+  if (threadIdx.x != 0 || cnt->nstale == 0) return;
+  const int n = min(cnt->nfeat, feat_cap);
+  for (int i = 0; i < n; ++i)
+    if (stale[i]) {
+      float* d = descf + (size_t)i * 128;
+      for (int b = 0; b < 128; ++b) d[b] = i ? d[b - 128] : 0.0f;
+      l1root_u8(d, 1, desc + (size_t)i * 128);
+    }
+}
+
+int blocks_for(size_t n, int t) { return (int)((n + t - 1) / t); }
+
+}  // namespace
+
+hipError_t sift_upsample(const uint8_t* frame, int w, int h, int ch, float* out, hipStream_t st) {
+  dim3 grid(blocks_for(2 * (size_t)w, 256), 2 * h);
+  upsample_kernel<<<grid, 256, 0, st>>>(frame, w, h, ch, out);
+  return hipGetLastError();
+}
+
+hipError_t sift_smooth(const float* in, float* out, float* tmp, int w, int h, const SiftConsts& c,
+                       int tap_set, int W, hipStream_t st) {
+  const float* taps = c.taps + tap_set * kSiftMaxTaps;
+  smooth_v_kernel<<<dim3(blocks_for(w, kVTile), blocks_for(h, kVTile)), 256, 0, st>>>(in, tmp, w, h,
+                                                                                     taps, W);
+  smooth_h_kernel<<<dim3(blocks_for(w, kHTile), h), 256, 0, st>>>(tmp, out, w, h, taps, W);
+  return hipGetLastError();
+}
+
+hipError_t sift_downsample(const float* in, int w_in, float* out, int w, int h, hipStream_t st) {
+  downsample_kernel<<<dim3(blocks_for(w, 256), h), 256, 0, st>>>(in, w_in, out, w, h);
+  return hipGetLastError();
+}
+
+hipError_t sift_octave_detect(const SiftDev& d, const SiftConsts& c, int w, int h, int octave,
+                              double tp, double te, hipStream_t st) {
+  (void)c;
+  const size_t so = (size_t)w * h;
+  dog_kernel<<<min(4096, blocks_for(so, 256)), 256, 0, st>>>(d.levels, d.dog, so);
+  detect_count_kernel<<<dim3(h, 3), 256, 0, st>>>(d.dog, w, h, tp, d.rowcnt);
+  // rowoff[3h] = total (the candidate count), written by the scan's total
+  scan_kernel<<<1, 1024, 0, st>>>(d.rowcnt, d.rowoff, nullptr, 3 * h, 3 * h, d.rowoff + 3 * h,
+                                  nullptr);
+  set_count_kernel<<<1, 1, 0, st>>>(d.cnt, d.rowoff + 3 * h, 0, d.cand_cap);
+  detect_write_kernel<<<dim3(h, 3), 256, 0, st>>>(d.dog, w, h, tp, d.rowoff, d.cand, d.cand_cap);
+  const double sigma0 = 1.6 * pow(2.0, 1.0 / kS);
+  refine_kernel<<<kGrid, 64, 0, st>>>(d.dog, w, h, d.cand, d.cnt, d.ktmp, d.flag, tp, te, sigma0,
+                                      octave);
+  scan_kernel<<<1, 1024, 0, st>>>(d.flag, d.foff, &d.cnt->ncand, 0, d.cand_cap, d.rowcnt, nullptr);
+  set_count_kernel<<<1, 1, 0, st>>>(d.cnt, d.rowcnt, 1, d.key_cap);
+  compact_keys_kernel<<<kGrid, 64, 0, st>>>(d.ktmp, d.flag, d.foff, d.cnt, d.keys, d.key_cap,
+                                            octave);
+  return hipGetLastError();
+}
+
+hipError_t sift_octave_describe(const SiftDev& d, const SiftConsts& c, int w, int h, int octave,
+                                hipStream_t st) {
+  gradient_kernel<<<dim3(blocks_for(w, 256), h, 3), 256, 0, st>>>(d.levels, d.grad, w, h);
+  orient_kernel<<<kGrid, 64, 0, st>>>(d.grad, w, h, d.keys, d.cnt, d.nori, d.ang, c.expn, octave);
+  scan_kernel<<<1, 1024, 0, st>>>(d.nori, d.koff, &d.cnt->nkey, 0, d.key_cap, nullptr,
+                                  &d.cnt->nfeat);
+  descriptor_kernel<<<kGrid, 64, 0, st>>>(d.grad, w, h, d.keys, d.cnt, d.nori, d.ang, d.koff,
+                                          d.feat, d.descf, d.desc, d.stale, c.expn, d.feat_cap,
+                                          octave);
+  return hipGetLastError();
+}
+
+hipError_t sift_fixup(const SiftDev& d, hipStream_t st) {
+  fixup_kernel<<<1, 64, 0, st>>>(d.cnt, d.stale, d.descf, d.desc, d.feat_cap);
+  return hipGetLastError();
+}
+
+}  // namespace scm

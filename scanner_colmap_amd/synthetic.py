@@ -272,9 +272,13 @@ def synthetic_frame(height: int, width: int, seed: int, channels: int = 3,
         cx, cy = rng.uniform(0, w), rng.uniform(0, h)
         th = rng.uniform(0, np.pi)
         ln, wd = rng.uniform(10, max(12.0, min(h, w) / 4)), rng.uniform(1.0, 3.0)
-        u = np.cos(th) * (xx - cx) + np.sin(th) * (yy - cy)
-        v = -np.sin(th) * (xx - cx) + np.cos(th) * (yy - cy)
-        img += rng.uniform(-0.3, 0.3) * ((np.abs(u) < ln) & (np.abs(v) < wd))
+        r = int(ln + wd) + 1
+        x0, x1 = max(0, int(cx) - r), min(w, int(cx) + r + 1)
+        y0, y1 = max(0, int(cy) - r), min(h, int(cy) + r + 1)
+        dx, dy = xx[y0:y1, x0:x1] - cx, yy[y0:y1, x0:x1] - cy
+        u = np.cos(th) * dx + np.sin(th) * dy
+        v = -np.sin(th) * dx + np.cos(th) * dy
+        img[y0:y1, x0:x1] += rng.uniform(-0.3, 0.3) * ((np.abs(u) < ln) & (np.abs(v) < wd))
     img += rng.normal(0, 0.01, img.shape).astype(np.float32)
     base = np.clip(img, 0.0, 1.0) * 255.0
     chans = [np.clip(base * g + o, 0, 255) for g, o in ((1.0, 0.0), (0.9, 12.0), (1.1, -10.0))]
