@@ -7,3 +7,9 @@ O=$R/gpurun_out/$S
 mkdir -p $O
 cd $R
 timeout -k 10 400 python -u -m pytest tests/test_gpu_sift.py -x -v --timeout 200 --timeout-method thread > $O/sift_tests.log 2>&1
+if [ "${2:-}" = "prof" ]; then
+  timeout -k 10 300 python -u probes/sift_probe.py 1080 1920 16 > $O/probe_1080p.log 2>&1
+  timeout -k 10 300 python -u probes/sift_probe.py 2304 3072 8 > $O/probe_3072.log 2>&1
+  cd /tmp && export TMPDIR=/tmp
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/probes/sift_probe.py 1080 1920 16 > $O/trace.log 2>&1
+fi

@@ -14,11 +14,12 @@
 //     window staged in LDS (HBM-bound: one read and one write per pass);
 //   * detection in VLFeat's scan order (s, y, x) by per-row counts, one
 //     exclusive scan and an ordered write (ballot prefix within each wave);
-//   * refinement, orientation histograms and descriptors one thread per
-//     keypoint, sequential in VLFeat's loop order (the per-keypoint work is
-//     a serial float / double accumulation whose rounding the reference
-//     fixes), the descriptor's 128 bins in LDS (bin-major, lane-minor: no bank
-//     conflicts).
+//   * refinement one thread per candidate; orientation histograms and
+//     descriptors one wave per keypoint: the window's samples are prepared 64
+//     at a time (one per lane) and each histogram bin is owned by one lane,
+//     which adds the chunk's contributions in VLFeat's sample order -- the
+//     reference's serial float / double sums, bit for bit, with 64-way
+//     parallelism per keypoint.
 // Layout: one image slot holds the first octave's six levels (the largest),
 // later octaves reuse the same buffers at their smaller size.
 #include "sift_kernels.h"
@@ -398,129 +399,225 @@ __global__ void gradient_kernel(const float* __restrict__ lev, float2* __restric
       make_float2(fast_sqrt_f(gx * gx + gy * gy), mod_2pi_f((float)(fast_atan2_f(gy, gx) + 2 * kPi)));
 }
 
-// vl_sift_calc_keypoint_orientations, one thread per keypoint.
+// vl_sift_calc_keypoint_orientations, one wave per keypoint.  The window's
+// samples are visited 64 at a time in VLFeat's (ys, xs) order: each lane
+// prepares one sample (mod * wgt) and marks it in its bin's 64-bit sample
+// mask, then lane b < 36 adds its bin's samples in mask-bit (= sample) order
+// -- the same double additions in the same order as the serial histogram.
+// Smoothing and peak search by lane 0.
 __global__ __launch_bounds__(64) void orient_kernel(const float2* __restrict__ grad, int w, int h,
                                                     const SiftKey* __restrict__ keys,
                                                     SiftCounts* __restrict__ cnt,
                                                     int32_t* __restrict__ nori,
                                                     double* __restrict__ ang,
                                                     const double* __restrict__ expn, int octave) {
+  constexpr int nbins = 36;
+  __shared__ unsigned long long smask[nbins];  // per bin: the chunk's samples adding to it
+  __shared__ double sval[64];
+  __shared__ double hist[nbins];
+  const int lane = threadIdx.x;
   const int n = cnt->nkey;
   const double xper = ldexp(1.0, octave);
   const size_t so = (size_t)w * h;
-  constexpr int nbins = 36;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  if (lane < nbins) smask[lane] = 0;
+  __syncthreads();
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const SiftKey k = keys[i];
     const double x = k.x / xper, y = k.y / xper, sigma = k.sigma / xper;
     const int xi = (int)(x + 0.5), yi = (int)(y + 0.5), si = k.is;
     const double sigmaw = 1.5 * sigma;
     const int W = max((int)floor(3.0 * sigmaw), 1);
-    int na = 0;
-    double out[4] = {0, 0, 0, 0};
-    if (!(xi < 0 || xi > w - 1 || yi < 0 || yi > h - 1 || si < kSMin + 1 || si > kSMax - 2)) {
-      double hist[nbins];
-      for (int b = 0; b < nbins; ++b) hist[b] = 0;
+    const bool valid =
+        !(xi < 0 || xi > w - 1 || yi < 0 || yi > h - 1 || si < kSMin + 1 || si > kSMax - 2);
+    if (valid) {
+      const int ys0 = max(-W, -yi), ys1 = min(W, h - 1 - yi);
+      const int xs0 = max(-W, -xi), xs1 = min(W, w - 1 - xi);
+      const int ncols = xs1 - xs0 + 1, total = (ys1 - ys0 + 1) * ncols;
       const float2* pt = grad + so * (size_t)(si - kSMin - 1) + (size_t)yi * w + xi;
-      for (int ys = max(-W, -yi); ys <= min(W, h - 1 - yi); ++ys)
-        for (int xs = max(-W, -xi); xs <= min(W, w - 1 - xi); ++xs) {
+      double acc = 0.0;
+      for (int t0 = 0; t0 < total; t0 += 64) {
+        const int t = t0 + lane;
+        int bin = -1;
+        double v = 0.0;
+        if (t < total) {
+          const int ys = ys0 + t / ncols, xs = xs0 + t % ncols;
           const double dx = (double)(xi + xs) - x, dy = (double)(yi + ys) - y;
           const double r2 = dx * dx + dy * dy;
-          if (r2 >= W * W + 0.6) continue;
-          const double wgt = fast_expn(expn, r2 / (2 * sigmaw * sigmaw));
-          const float2 g = pt[xs + (ptrdiff_t)ys * w];
-          const double mod = g.x, an = g.y;
-          const int bin = (int)floor(nbins * an / (2 * kPi));
-          hist[bin % nbins] += mod * wgt;
+          if (r2 < W * W + 0.6) {
+            const double wgt = fast_expn(expn, r2 / (2 * sigmaw * sigmaw));
+            const float2 g = pt[xs + (ptrdiff_t)ys * w];
+            const double mod = g.x, an = g.y;
+            bin = (int)floor(nbins * an / (2 * kPi)) % nbins;
+            v = mod * wgt;
+          }
         }
-      for (int iter = 0; iter < 6; ++iter) {
-        double prev = hist[nbins - 1];
-        const double first = hist[0];
-        int b;
-        for (b = 0; b < nbins - 1; ++b) {
-          const double nh = (prev + hist[b] + hist[(b + 1) % nbins]) / 3.0;
-          prev = hist[b];
-          hist[b] = nh;
+        sval[lane] = v;
+        if (bin >= 0) atomicOr(&smask[bin], 1ull << lane);
+        __syncthreads();
+        if (lane < nbins) {
+          uint64_t m = smask[lane];
+          while (m) {  // this bin's samples of the chunk, in order
+            acc += sval[__builtin_ctzll(m)];
+            m &= m - 1;
+          }
         }
-        hist[b] = (prev + hist[b] + first) / 3.0;
+        __syncthreads();
+        if (lane < nbins) smask[lane] = 0;
       }
-      double maxh = 0;
-      for (int b = 0; b < nbins; ++b) maxh = fmax(maxh, hist[b]);
-      for (int b = 0; b < nbins; ++b) {
-        const double h0 = hist[b], hm = hist[(b - 1 + nbins) % nbins], hp = hist[(b + 1 + nbins) % nbins];
-        if (h0 > 0.8 * maxh && h0 > hm && h0 > hp) {
-          const double di = -0.5 * (hp - hm) / (hp + hm - 2 * h0);
-          out[na++] = 2 * kPi * (b + di + 0.5) / nbins;
-          if (na == 4) break;
-        }
-      }
+      if (lane < nbins) hist[lane] = acc;
+      __syncthreads();
     }
-    const int nu = min(na, 2);
-    nori[i] = nu;
-    ang[2 * i] = out[0];
-    ang[2 * i + 1] = out[1];
-    if (nu) atomicAdd(&cnt->level_feats[(octave + 1) * 3 + si], nu);
+    if (lane == 0) {
+      int na = 0;
+      double out[4] = {0, 0, 0, 0};
+      if (valid) {
+        double hs[nbins];
+        for (int b = 0; b < nbins; ++b) hs[b] = hist[b];
+        for (int iter = 0; iter < 6; ++iter) {
+          double prev = hs[nbins - 1];
+          const double first = hs[0];
+          int b;
+          for (b = 0; b < nbins - 1; ++b) {
+            const double nh = (prev + hs[b] + hs[(b + 1) % nbins]) / 3.0;
+            prev = hs[b];
+            hs[b] = nh;
+          }
+          hs[b] = (prev + hs[b] + first) / 3.0;
+        }
+        double maxh = 0;
+        for (int b = 0; b < nbins; ++b) maxh = fmax(maxh, hs[b]);
+        for (int b = 0; b < nbins; ++b) {
+          const double h0 = hs[b], hm = hs[(b - 1 + nbins) % nbins], hp = hs[(b + 1 + nbins) % nbins];
+          if (h0 > 0.8 * maxh && h0 > hm && h0 > hp) {
+            const double di = -0.5 * (hp - hm) / (hp + hm - 2 * h0);
+            out[na++] = 2 * kPi * (b + di + 0.5) / nbins;
+            if (na == 4) break;
+          }
+        }
+      }
+      const int nu = min(na, 2);
+      nori[i] = nu;
+      ang[2 * i] = out[0];
+      ang[2 * i + 1] = out[1];
+      if (nu) atomicAdd(&cnt->level_feats[(octave + 1) * 3 + si], nu);
+    }
+    __syncthreads();
   }
 }
 
-// COLMAP L1RootNormalizeFeatureDescriptors + FeatureDescriptorsToUnsignedByte
-// + TransformVLFeatToUBCFeatureDescriptors on one 128-float descriptor.
-__device__ void l1root_u8(float* d, int stride, uint8_t* __restrict__ out) {
-  float norm = 0;
-  for (int i = 0; i < 128; ++i) norm += fabsf(d[i * stride]);
-  for (int i = 0; i < 128; ++i) d[i * stride] = d[i * stride] / norm;
-  for (int i = 0; i < 128; ++i) d[i * stride] = sqrtf(d[i * stride]);
-  for (int c = 0; c < 16; ++c)
-    for (int k = 0; k < 8; ++k) {
-      const float v = roundf(512.0f * d[(8 * c + k) * stride]);
-      const float lo = (0.0f < v) ? v : 0.0f;  // std::max(0.0f, v)
-      const float hi = (lo < 255.0f) ? lo : 255.0f;  // std::min(255.0f, lo)
-      out[8 * c + ((8 - k) & 7)] = (uint8_t)hi;
+// The descriptor tail of one feature by one wave, bins b = lane and lane + 64
+// in a0 / a1 (VLFeat bin order): normalise, truncate at 0.2, normalise
+// (vl_sift_calc_keypoint_descriptor), then COLMAP's L1-root, x512 rounding
+// with TruncateCast and the UBC orientation-bin order.  The sums run serially
+// in bin order on lane 0 (the reference's float sums), the elementwise steps
+// on every lane.
+__device__ void descriptor_finish(float a0, float a1, float* __restrict__ sh, float* __restrict__ df,
+                                  uint8_t* __restrict__ out) {
+  const int lane = threadIdx.x;
+  for (int pass = 0; pass < 2; ++pass) {
+    sh[lane] = a0;
+    sh[lane + 64] = a1;
+    __syncthreads();
+    if (lane == 0) {
+      float norm = 0;
+      for (int b = 0; b < 128; ++b) norm += sh[b] * sh[b];
+      sh[128] = fast_sqrt_f(norm) + kEpsF;
     }
+    __syncthreads();
+    const float norm = sh[128];
+    a0 /= norm;
+    a1 /= norm;
+    if (pass == 0) {
+      if (a0 > 0.2) a0 = 0.2f;
+      if (a1 > 0.2) a1 = 0.2f;
+    }
+    __syncthreads();
+  }
+  sh[lane] = a0;
+  sh[lane + 64] = a1;
+  __syncthreads();
+  if (lane == 0) {
+    float norm = 0;
+    for (int b = 0; b < 128; ++b) norm += fabsf(sh[b]);
+    sh[128] = norm;
+  }
+  __syncthreads();
+  const float l1 = sh[128];
+  float v[2] = {sqrtf(a0 / l1), sqrtf(a1 / l1)};
+  for (int q = 0; q < 2; ++q) {
+    const int b = lane + 64 * q;
+    df[b] = v[q];
+    const float r = roundf(512.0f * v[q]);
+    const float lo = (0.0f < r) ? r : 0.0f;        // std::max(0.0f, r)
+    const float hi = (lo < 255.0f) ? lo : 255.0f;  // std::min(255.0f, lo)
+    out[(b & ~7) + ((8 - (b & 7)) & 7)] = (uint8_t)hi;
+  }
+  __syncthreads();
 }
 
-// vl_sift_calc_keypoint_descriptor + the COLMAP conversions, one thread per
-// keypoint (its <= 2 orientations in order).  The 4 x 4 x 8 histogram lives
-// in LDS, bin b of lane L at hist[b * 64 + L].
+// vl_sift_calc_keypoint_descriptor + the COLMAP conversions, one wave per
+// keypoint (its <= 2 orientations in turn).  The sample rectangle is visited
+// 64 samples at a time in VLFeat's (dyi, dxi) order: each lane prepares one
+// sample (win * mod, bins and fractional offsets) and marks it in the 64-bit
+// sample masks of the (up to 8) bins it reaches, then lane L accumulates bins
+// L and L + 64 over their samples in mask-bit (= sample) order.  A sample
+// reaches a bin through at most one corner, so every bin sees VLFeat's float
+// additions in VLFeat's order.
 __global__ __launch_bounds__(64) void descriptor_kernel(
     const float2* __restrict__ grad, int w, int h, const SiftKey* __restrict__ keys,
     SiftCounts* __restrict__ cnt, const int32_t* __restrict__ nori, const double* __restrict__ ang,
     const int32_t* __restrict__ koff, SiftFeat* __restrict__ feat, float* __restrict__ descf,
     uint8_t* __restrict__ desc, int32_t* __restrict__ stale, const double* __restrict__ expn,
     int feat_cap, int octave) {
-  __shared__ float hist[128 * 64];
   constexpr int NBP = 4, NBO = 8;
+  __shared__ float s_wm[64], s_rx[64], s_ry[64], s_rt[64];
+  __shared__ int s_b[64];  // binx + 3 | (biny + 3) << 8 | bint << 16 (bint in 0 .. 8)
+  __shared__ unsigned long long s_mask[128];  // per bin: the chunk's samples adding to it
+  __shared__ float sh[129];
   const int lane = threadIdx.x;
-  float* hb = hist + lane;
+  const int bt0 = lane & 7, bx0 = (lane >> 3) & 3, by0 = lane >> 5, by1 = 2 + (lane >> 5);
   const int n = cnt->nkey;
+  s_mask[lane] = 0;
+  s_mask[lane + 64] = 0;
+  __syncthreads();
   const double xper = ldexp(1.0, octave);
   const size_t so = (size_t)w * h;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+  for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const SiftKey k = keys[i];
-    for (int o = 0; o < nori[i]; ++o) {
+    const int nu = nori[i];
+    for (int o = 0; o < nu; ++o) {
       const int fi = koff[i] + o;
       if (fi >= feat_cap) {
-        cnt->overflow = 1;
+        if (lane == 0) cnt->overflow = 1;
         break;
       }
       const double angle0 = ang[2 * i + o];
-      feat[fi] = SiftFeat{k.x + 0.5f, k.y + 0.5f, k.sigma, (float)angle0};
+      if (lane == 0) feat[fi] = SiftFeat{k.x + 0.5f, k.y + 0.5f, k.sigma, (float)angle0};
       const double x = k.x / xper, y = k.y / xper, sigma = k.sigma / xper;
       const int xi = (int)(x + 0.5), yi = (int)(y + 0.5), si = k.is;
       if (xi < 0 || xi >= w || yi < 0 || yi >= h - 1 || si < kSMin + 1 || si > kSMax - 2) {
         // vl_sift_calc_keypoint_descriptor returns before writing: COLMAP
-        // re-normalises the previous descriptor's buffer (sift_fixup)
-        stale[fi] = 1;
-        atomicAdd(&cnt->nstale, 1);
+        // re-normalises the previous descriptor's buffer (fixup_kernel)
+        if (lane == 0) {
+          stale[fi] = 1;
+          atomicAdd(&cnt->nstale, 1);
+        }
         continue;
       }
-      stale[fi] = 0;
+      if (lane == 0) stale[fi] = 0;
       const double st0 = sin(angle0), ct0 = cos(angle0);
       const double SBP = 3.0 * sigma + kEpsD;
       const int W = (int)floor(sqrt(2.0) * SBP * (NBP + 1) / 2.0 + 0.5);
-      for (int b = 0; b < 128; ++b) hb[b * 64] = 0.0f;
+      const int dy0 = max(-W, 1 - yi), dy1 = min(W, h - yi - 2);
+      const int dx0 = max(-W, 1 - xi), dx1 = min(W, w - xi - 2);
+      const int ncols = dx1 - dx0 + 1, nrows = dy1 - dy0 + 1;
+      const int total = (ncols > 0 && nrows > 0) ? ncols * nrows : 0;
       const float2* pt = grad + so * (size_t)(si - kSMin - 1) + (size_t)yi * w + xi;
-      for (int dyi = max(-W, 1 - yi); dyi <= min(W, h - yi - 2); ++dyi)
-        for (int dxi = max(-W, 1 - xi); dxi <= min(W, w - xi - 2); ++dxi) {
+      float a0 = 0.0f, a1 = 0.0f;
+      for (int t0 = 0; t0 < total; t0 += 64) {
+        const int t = t0 + lane;
+        if (t < total) {
+          const int dyi = dy0 + t / ncols, dxi = dx0 + t % ncols;
           const float2 g = pt[dxi + (ptrdiff_t)dyi * w];
           const float mod = g.x, angle = g.y;
           const float theta = mod_2pi_f((float)(angle - angle0));
@@ -534,49 +631,76 @@ __global__ __launch_bounds__(64) void descriptor_kernel(
           const int binx = (int)floorf((float)(nx - 0.5));
           const int biny = (int)floorf((float)(ny - 0.5));
           const int bint = (int)floorf(nt);
-          const float rbinx = (float)(nx - (binx + 0.5));
-          const float rbiny = (float)(ny - (biny + 0.5));
-          const float rbint = nt - bint;
+          s_wm[lane] = win * mod;
+          s_rx[lane] = (float)(nx - (binx + 0.5));
+          s_ry[lane] = (float)(ny - (biny + 0.5));
+          s_rt[lane] = nt - bint;
+          // corners binx + {0, 1} etc. (binx + 3 >= 0 for every sample that
+          // reaches bin -2); mark the sample in each reachable bin's mask
+          s_b[lane] = (binx + 3) | ((biny + 3) << 8) | (bint << 16);
           for (int dbinx = 0; dbinx < 2; ++dbinx)
             for (int dbiny = 0; dbiny < 2; ++dbiny)
               for (int dbint = 0; dbint < 2; ++dbint)
                 if (binx + dbinx >= -(NBP / 2) && binx + dbinx < (NBP / 2) &&
-                    biny + dbiny >= -(NBP / 2) && biny + dbiny < (NBP / 2)) {
-                  const float weight = win * mod * fabsf(1 - dbinx - rbinx) *
-                                       fabsf(1 - dbiny - rbiny) * fabsf(1 - dbint - rbint);
-                  const int bin = ((bint + dbint) % NBO) + (biny + dbiny + NBP / 2) * NBO * NBP +
-                                  (binx + dbinx + NBP / 2) * NBO;
-                  hb[bin * 64] += weight;
-                }
+                    biny + dbiny >= -(NBP / 2) && biny + dbiny < (NBP / 2))
+                  atomicOr(&s_mask[((bint + dbint) % NBO) + (biny + dbiny + NBP / 2) * NBO * NBP +
+                                   (binx + dbinx + NBP / 2) * NBO],
+                           1ull << lane);
         }
-      for (int pass = 0; pass < 2; ++pass) {  // normalize, truncate at 0.2, normalize
-        float norm = 0;
-        for (int b = 0; b < 128; ++b) norm += hb[b * 64] * hb[b * 64];
-        norm = fast_sqrt_f(norm) + kEpsF;
-        for (int b = 0; b < 128; ++b) hb[b * 64] /= norm;
-        if (pass == 0)
-          for (int b = 0; b < 128; ++b)
-            if (hb[b * 64] > 0.2) hb[b * 64] = 0.2f;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+          uint64_t m = s_mask[lane + 64 * q];
+          const int byq = q ? by1 : by0;
+          float a = q ? a1 : a0;
+          while (m) {  // this bin's samples of the chunk, in sample order
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            const int sb = s_b[j];
+            const int dbx = bx0 + 1 - (sb & 0xFF), dby = byq + 1 - ((sb >> 8) & 0xFF);
+            const int dbt = (bt0 - (sb >> 16)) & 7;
+            a += s_wm[j] * fabsf(1 - dbx - s_rx[j]) * fabsf(1 - dby - s_ry[j]) *
+                 fabsf(1 - dbt - s_rt[j]);
+          }
+          if (q) a1 = a;
+          else a0 = a;
+        }
+        __syncthreads();
+        s_mask[lane] = 0;
+        s_mask[lane + 64] = 0;
       }
-      l1root_u8(hb, 64, desc + (size_t)fi * 128);
-      float* df = descf + (size_t)fi * 128;
-      for (int b = 0; b < 128; ++b) df[b] = hb[b * 64];
+      descriptor_finish(a0, a1, sh, descf + (size_t)fi * 128, desc + (size_t)fi * 128);
     }
   }
 }
 
 // The unwritten descriptors in feature order: each is the L1-root of the
-// previous feature's (float) buffer, the first one's of zeros.
+// previous feature's (float) buffer, the first one's of zeros.  The wave
+// finds them 64 flags at a time; lane 0 recomputes each in order.
 __global__ void fixup_kernel(const SiftCounts* __restrict__ cnt, const int32_t* __restrict__ stale,
                              float* __restrict__ descf, uint8_t* __restrict__ desc, int feat_cap) {
-  if (threadIdx.x != 0 || cnt->nstale == 0) return;
+  if (cnt->nstale == 0) return;
+  const int lane = threadIdx.x;
   const int n = min(cnt->nfeat, feat_cap);
-  for (int i = 0; i < n; ++i)
-    if (stale[i]) {
-      float* d = descf + (size_t)i * 128;
-      for (int b = 0; b < 128; ++b) d[b] = i ? d[b - 128] : 0.0f;
-      l1root_u8(d, 1, desc + (size_t)i * 128);
-    }
+  for (int base = 0; base < n; base += 64) {
+    uint64_t m = __ballot(base + lane < n && stale[base + lane]);
+    if (lane == 0)
+      while (m) {
+        const int i = base + __builtin_ctzll(m);
+        m &= m - 1;
+        float* d = descf + (size_t)i * 128;
+        for (int b = 0; b < 128; ++b) d[b] = i ? d[b - 128] : 0.0f;
+        float norm = 0;
+        for (int b = 0; b < 128; ++b) norm += fabsf(d[b]);
+        for (int b = 0; b < 128; ++b) d[b] = sqrtf(d[b] / norm);
+        for (int b = 0; b < 128; ++b) {
+          const float r = roundf(512.0f * d[b]);
+          const float lo = (0.0f < r) ? r : 0.0f;
+          const float hi = (lo < 255.0f) ? lo : 255.0f;
+          desc[(size_t)i * 128 + (b & ~7) + ((8 - (b & 7)) & 7)] = (uint8_t)hi;
+        }
+      }
+  }
 }
 
 int blocks_for(size_t n, int t) { return (int)((n + t - 1) / t); }
@@ -627,10 +751,10 @@ hipError_t sift_octave_detect(const SiftDev& d, const SiftConsts& c, int w, int 
 hipError_t sift_octave_describe(const SiftDev& d, const SiftConsts& c, int w, int h, int octave,
                                 hipStream_t st) {
   gradient_kernel<<<dim3(blocks_for(w, 256), h, 3), 256, 0, st>>>(d.levels, d.grad, w, h);
-  orient_kernel<<<kGrid, 64, 0, st>>>(d.grad, w, h, d.keys, d.cnt, d.nori, d.ang, c.expn, octave);
+  orient_kernel<<<4 * kGrid, 64, 0, st>>>(d.grad, w, h, d.keys, d.cnt, d.nori, d.ang, c.expn, octave);
   scan_kernel<<<1, 1024, 0, st>>>(d.nori, d.koff, &d.cnt->nkey, 0, d.key_cap, nullptr,
                                   &d.cnt->nfeat);
-  descriptor_kernel<<<kGrid, 64, 0, st>>>(d.grad, w, h, d.keys, d.cnt, d.nori, d.ang, d.koff,
+  descriptor_kernel<<<4 * kGrid, 64, 0, st>>>(d.grad, w, h, d.keys, d.cnt, d.nori, d.ang, d.koff,
                                           d.feat, d.descf, d.desc, d.stale, c.expn, d.feat_cap,
                                           octave);
   return hipGetLastError();
