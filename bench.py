@@ -70,6 +70,10 @@ def parse():
                         "table run, rank 0 at N = 1 (0 = skip)")
     p.add_argument("--no-isolated", dest="isolated", action="store_false",
                    help="skip the extra serialised step that measures isolated kernel rates")
+    p.add_argument("--extract-frames", type=int, default=32,
+                   help="frames of the SIFT extraction leg (§8f rank 4; 0 = skip), rank 0 at N = 1")
+    p.add_argument("--extract-height", type=int, default=1080)
+    p.add_argument("--extract-width", type=int, default=1920)
     p.add_argument("--stencil-batches", default="1,64",
                    help="Scanner batch sizes (stencils per execute() call) to time")
     return p.parse_args()
@@ -203,6 +207,47 @@ def stencil_bench(ctx, src, overlap: int, rows: int, batches: list) -> dict:
         res[f"batch{b}"] = {"pairs_per_s": round(npairs / dt, 1), "ms_per_call": round(dt / len(calls) * 1e3, 2),
                             "calls": len(calls), "pairs": npairs,
                             "images_uploaded": u1_ - u0_, "images_reused": r1_ - r0_}
+    return res
+
+
+def extraction_bench(ctx, frames: int, height: int, width: int, check: bool, cpu: bool) -> dict:
+    """§8f rank 4, the producer of the table: scm_extract_frames (GPU SIFT,
+    SiftExtractionKernel::execute, extraction_op.cc:70-121) on `frames`
+    synthetic frames (4 distinct textures, host buffers in: PCIe inside the
+    timed region), its parity on one frame against the oracle, and the
+    oracle's frames/s on the job's CPU share (one frame per thread)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from scanner_colmap_amd.codecs import decode_keypoints
+    from scanner_colmap_amd.synthetic import synthetic_frame
+
+    uniq = [synthetic_frame(height, width, 300 + i) for i in range(4)]
+    batch = [uniq[i % 4] for i in range(frames)]
+    ctx.extract_frames(batch[:4])  # warm-up (slots, workspaces)
+    t0 = time.perf_counter()
+    out = ctx.extract_frames(batch, list(range(frames)))
+    dt = time.perf_counter() - t0
+    res = {"frames": frames, "size": f"{width}x{height}x3", "frames_per_s": round(frames / dt, 2),
+           "ms_per_frame": round(dt / frames * 1e3, 3),
+           "features_per_frame": round(sum(len(decode_keypoints(o[0])) for o in out) / frames, 1),
+           "inputs": "host frame buffers (PCIe inside the timed region)",
+           "dominant_kernel": "descriptor_kernel (profiles/r02_sift_kernel_stats.csv)"}
+    if check or cpu:
+        from oracle import oracle
+    if check:
+        ref = oracle.sift_extract(batch[1], 1)
+        res["parity"] = {"frames": 1, "elements_byte_equal": out[1] == ref,
+                         "checked_against": "oracle/sift_oracle.cc"}
+    if cpu:
+        threads, aff, quota = cpu_threads()
+        n = min(threads, 16)
+        t0 = time.perf_counter()
+        with ThreadPoolExecutor(max_workers=n) as ex:
+            list(ex.map(lambda i: oracle.sift_extract(uniq[i % 4], i), range(n)))
+        cdt = time.perf_counter() - t0
+        res["cpu_baseline"] = {"value": round(n / cdt, 3), "unit": "frames/s", "cores": n,
+                               "kind": "port", "sample": f"{n} frames of {width}x{height}, one per "
+                               f"thread, {cdt:.1f} s wall (oracle/sift_oracle.cc, scalar VLFeat "
+                               "restatement)"}
     return res
 
 
@@ -394,6 +439,10 @@ def main():
                    "how": ("one extra untimed step after the timed region with matching and "
                            "verification serialised (scm_set_serial, output bytes identical): "
                            "each kernel alone on the GPU, HIP events")}
+        extraction = (extraction_bench(ctx, args.extract_frames, args.extract_height,
+                                       args.extract_width, check=bool(check_pairs),
+                                       cpu=not args.no_cpu_baseline)
+                      if world == 1 and args.extract_frames > 0 else None)
         drop_in = stencil_bench(ctx, stencil_src, overlap, srows,
                                 [int(x) for x in args.stencil_batches.split(",") if x]) if srows else None
         score_flops = (SAMPSON_FLOPS + 1) * evals_f + (TRANSFER_FLOPS + 1) * evals_h
@@ -464,6 +513,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
             "drop_in": drop_in,
+            "extraction": extraction,
             "table_load_ms": round(table_load_ms, 1),
             "pcie_inclusive_pairs_per_s": round(total_pairs / (elapsed / steps + table_load_ms * 1e-3), 2),
             "gen_s": round(gen_s, 1),
