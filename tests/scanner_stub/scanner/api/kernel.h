@@ -1,5 +1,6 @@
 // Test stub (see tests/scanner_stub/README.md): Scanner kernel interfaces.
 #pragma once
+#include <cstdlib>
 #include <vector>
 
 #include "scanner/util/common.h"
@@ -22,5 +23,21 @@ class StenciledBatchedKernel {
   KernelConfig config_;
 };
 
+// Non-batched, non-stenciled kernel: one element per column per call.
+class Kernel {
+ public:
+  explicit Kernel(const KernelConfig& config) : config_(config) {}
+  virtual ~Kernel() = default;
+  virtual void execute(const Elements& input_cols, Elements& output_cols) = 0;
+
+ protected:
+  KernelConfig config_;
+};
+
 class VideoKernel {};
+
+// Frames handed to a CPU kernel live in host memory.
+inline void check_frame(const DeviceHandle& device, const Element& e) {
+  if (device.type != DeviceType::CPU || !e.is_frame) std::abort();
+}
 }  // namespace scanner

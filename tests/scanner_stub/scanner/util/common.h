@@ -16,9 +16,20 @@ struct DeviceHandle {
 
 inline const DeviceHandle CPU_DEVICE = {DeviceType::CPU, 0};
 
+// A decoded video frame (height x width x channels bytes, row-major).
+struct Frame {
+  int32_t w = 0, h = 0, c = 0;
+  u8* data = nullptr;
+  int32_t width() const { return w; }
+  int32_t height() const { return h; }
+  int32_t channels() const { return c; }
+};
+
 struct Element {
-  u8* buffer = nullptr;
+  u8* buffer = nullptr;  // for a frame column: the Frame (as_const_frame)
   size_t size = 0;
+  bool is_frame = false;
+  const Frame* as_const_frame() const { return reinterpret_cast<const Frame*>(buffer); }
 };
 
 using Elements = std::vector<Element>;

@@ -19,4 +19,9 @@ inline void insert_element(Elements& col, u8* buffer, size_t size) {
   e.size = size;
   col.push_back(e);
 }
+// Output element of a non-batched kernel (io.cc insert_element(element, ...)).
+inline void insert_element(Element& element, u8* buffer, size_t size) {
+  element.buffer = buffer;
+  element.size = size;
+}
 }  // namespace scanner

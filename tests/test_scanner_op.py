@@ -127,3 +127,67 @@ def test_op_batched_rows_match_table_oracle(tmp_path, batch):
     for row in range(n):
         assert (d / f"out_0_{row}").read_bytes() == ref_ids[row], row
         assert (d / f"out_1_{row}").read_bytes() == ref_tvgs[row], row
+
+
+# ---------------------------------------------------------------------------
+# SiftExtractionGPU (scanner_colmap_amd/scanner_op/sift_extraction_gpu.cc), the
+# drop-in for the reference's SiftExtraction op (extraction_op.cc:22-130).
+# ---------------------------------------------------------------------------
+SIFT_OP_SRC = os.path.join(ROOT, "scanner_colmap_amd", "scanner_op", "sift_extraction_gpu.cc")
+
+
+def _build_frame_driver(tmp_path):
+    exe = tmp_path / "drive_frame_op"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-I", STUB, "-I",
+                    os.path.join(ROOT, "include"), os.path.join(STUB, "drive_frame_op.cc"),
+                    SIFT_OP_SRC, "-L", LIB_DIR, "-lscm", f"-Wl,-rpath,{LIB_DIR}", "-o", str(exe)],
+                   check=True)
+    return exe
+
+
+def _write_frames(d, frames, ids):
+    import struct
+    for r, (f, i) in enumerate(zip(frames, ids)):
+        a = np.ascontiguousarray(f, dtype=np.uint8)
+        if a.ndim == 2:
+            a = a[:, :, None]
+        (d / f"in_0_{r}").write_bytes(struct.pack("<Q", i))
+        (d / f"frame_{r}").write_bytes(a.tobytes())
+        (d / f"shape_{r}").write_text(f"{a.shape[1]} {a.shape[0]} {a.shape[2]}")
+
+
+def test_sift_op_compiles_against_scanner_api_and_links(tmp_path):
+    _build_frame_driver(tmp_path)
+
+
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")
+def test_sift_op_aborts_without_gpu(tmp_path):
+    from scanner_colmap_amd.synthetic import synthetic_frame
+    exe = _build_frame_driver(tmp_path)
+    d = tmp_path / "io"
+    d.mkdir()
+    _write_frames(d, [synthetic_frame(32, 40, 1)], [3])
+    r = subprocess.run([str(exe), "SiftExtractionGPU", str(d), "1"], capture_output=True, text=True)
+    assert r.returncode != 0
+    assert "scm_context_create failed" in r.stderr
+
+
+@pytest.mark.gpu
+def test_sift_op_execute_matches_oracle(tmp_path):
+    """execute() per row, as a Scanner worker runs the op over a frame table:
+    the three output elements equal the oracle's SiftExtractionKernel."""
+    from oracle import oracle
+    from scanner_colmap_amd.synthetic import synthetic_frame
+    exe = _build_frame_driver(tmp_path)
+    d = tmp_path / "io"
+    d.mkdir()
+    frames = [synthetic_frame(120, 160, 1), synthetic_frame(90, 70, 2, channels=1),
+              synthetic_frame(64, 200, 3, channels=4)]
+    ids = [11, 12, 13]
+    _write_frames(d, frames, ids)
+    subprocess.run([str(exe), "SiftExtractionGPU", str(d), str(len(frames))], check=True,
+                   timeout=120)
+    for r, (f, i) in enumerate(zip(frames, ids)):
+        ref = oracle.sift_extract(f, i)
+        got = tuple((d / f"out_{c}_{r}").read_bytes() for c in range(3))
+        assert got == ref, f"row {r}"
