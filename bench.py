@@ -70,6 +70,9 @@ def parse():
                         "table run, rank 0 at N = 1 (0 = skip)")
     p.add_argument("--no-isolated", dest="isolated", action="store_false",
                    help="skip the extra serialised step that measures isolated kernel rates")
+    p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                   help="nccl = RCCL over xGMI, one GPU per rank (the measured path); gloo = a "
+                        "rehearsal of the N > 1 sharding and gather with ranks sharing GPUs")
     p.add_argument("--extract-frames", type=int, default=32,
                    help="frames of the SIFT extraction leg (§8f rank 4; 0 = skip), rank 0 at N = 1")
     p.add_argument("--extract-height", type=int, default=1080)
@@ -317,11 +320,15 @@ def main():
     from scanner_colmap_amd import Context
 
     device = None
-    if world > 1:
+    gpu = local_rank if world > 1 else 0
+    if world > 1 and args.dist_backend == "nccl":
         torch.cuda.set_device(local_rank)
         device = torch.device("cuda", local_rank)
         dist.init_process_group("nccl", device_id=device)
-    ctx = Context(local_rank if world > 1 else 0)
+    elif world > 1:  # rehearsal of the N > 1 path on fewer GPUs: gloo gather, ranks share GPUs
+        gpu = local_rank % max(1, torch.cuda.device_count())
+        dist.init_process_group("gloo")
+    ctx = Context(gpu)
     t_load = time.perf_counter()
     ctx.table_load(ids, kps, descs)
     if torch.cuda.is_available():
@@ -378,7 +385,8 @@ def main():
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed, float(npairs), gdesc], dtype=torch.float64, device=device)
+        t = torch.tensor([elapsed, float(npairs), gdesc], dtype=torch.float64,
+                         device=device if device is not None else "cpu")
         mx = t.clone()
         dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
         tot = t.clone()
@@ -465,7 +473,8 @@ def main():
             "data": "synthetic (seeded corridor scene, RootSIFT u8 descriptors; no dataset)",
             "config": {"workload": args.workload, "description": wl["desc"],
                        "images": total_images, "kpts": kpts, "overlap": overlap,
-                       "pairs_per_step": int(total_pairs), "parallelism": f"pairs sharded x{world}"},
+                       "pairs_per_step": int(total_pairs), "parallelism": f"pairs sharded x{world}",
+                       "dist_backend": (args.dist_backend if world > 1 else None)},
             "roofline": {
                 "bound": "mfma",
                 "kernel": kernel,

@@ -1,0 +1,65 @@
+"""The N > 1 path with the real GPU stage: two ranks of
+bench.py's own ShardPlan (pivot rows balanced by pair count, stencil halo),
+each running scm_table_run_packed on a GPU context over its slice, the rows
+gathered to rank 0 (gloo here: the ranks share the one GPU of the box, which
+RCCL does not allow), compared with the oracle's whole-table rows.  The
+CPU-only twin with the oracle as the stage is tests/test_distributed.py."""
+import multiprocessing as mp
+import os
+import socket
+
+import pytest
+
+from scanner_colmap_amd import distributed as sd
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, n, K, scaling, q):
+    import torch.distributed as dist
+
+    from oracle import oracle
+    from scanner_colmap_amd import Context
+    from scanner_colmap_amd.codecs import table_rows
+    from scanner_colmap_amd.synthetic import Corridor
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        plan = sd.ShardPlan(n, K, world, rank, scaling)
+        c = Corridor(plan.total_images, 900, K, seed=57)
+        with Context(0) as ctx:
+            ctx.table_load(*table_rows(c.images(plan.table_begin, plan.table_end)))
+            _, got = plan.step(ctx)
+        if rank == 0:
+            rows_a, rows_b = sd.merge_gathered(got)
+            ids, kps, descs = table_rows(c.images())
+            ref = oracle.table_run(ids, kps, descs, K, 0, plan.total_images)
+            q.put((rows_a == ref[0], rows_b == ref[1], len(rows_a), plan.total_images))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,K,scaling", [(11, 4, "strong"), (6, 3, "weak")])
+def test_gpu_shard_step_world2(n, K, scaling):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, K, scaling, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    codes = [p.exitcode for p in procs]
+    assert codes == [0, 0], codes
+    ok_a, ok_b, nrows, total = q.get(timeout=5)
+    assert ok_a and ok_b and nrows == total
+    assert total == (n if scaling == "strong" else n * world)
