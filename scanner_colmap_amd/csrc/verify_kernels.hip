@@ -33,9 +33,7 @@ using namespace geom;
 enum { KIND_F = 0, KIND_H = 1, KIND_T = 2 };
 
 template <int K> struct KindTraits;
-// tb: hypotheses per round (the F round is halved so that its fp64 models
-// fit in LDS next to their filter constants).
-constexpr int kTrialBatchF = kTrialBatch / 2;
+// tb: hypotheses per round of the sequential (watermark) LO-RANSAC.
 template <> struct KindTraits<KIND_F> { static constexpr int kmin = 7, kmin_local = 8, mm = 3, ms = 9, tb = kTrialBatch; };
 template <> struct KindTraits<KIND_H> { static constexpr int kmin = 4, kmin_local = 4, mm = 1, ms = 9, tb = kTrialBatch; };
 template <> struct KindTraits<KIND_T> { static constexpr int kmin = 1, kmin_local = 1, mm = 1, ms = 2, tb = kTrialBatch; };
@@ -60,18 +58,8 @@ struct __attribute__((aligned(16))) VerifyLds {
   int32_t best_n;
   int32_t best_sum_valid;
   int32_t pad_;
-  // Tail: the sequential LO-RANSAC of verify_final_kernel only.
+  // Tail: the sequential LO-RANSAC of verify_final_kernel only (the watermark).
   uint16_t samples[kTrialBatch][8];
-  union {
-    struct {
-      float hcs[kTrialBatch][12];   // homography filter constants per hypothesis
-      double hmod[kTrialBatch][9];  // the hypotheses' fp64 models (exact fallback)
-    };
-    struct {
-      float fcs[kTrialBatchF * 3][12];   // Sampson filter constants per 7-point model
-      double fmod[kTrialBatchF * 3][9];  // the 7-point models (exact fallback)
-    };
-  };
 };
 #ifndef SCM_REPLAY_ATTR
 #define SCM_REPLAY_ATTR
@@ -337,57 +325,65 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
 }
 
 // Constants of the packed-fp32 homography inlier filter (score_h_chunk).
-// For one fp64 model H and points with |coordinate| <= S (exact in fp32:
-// keypoints are float32) the filter evaluates, in fp32 with explicit FMAs,
-//   Q_i = H_i0 s0 + H_i1 s1 + H_i2,  w_j = d_j Q_2 - Q_j,
-//   lhs = w_0^2 + w_1^2,  rhs = maxr Q_2^2,  diff = lhs - rhs
-// and decides the reference test  fl64(transfer error) <= maxr  (i.e.
-// W_0^2 + W_1^2 <= maxr P_2^2 on the exact values, up to the reference's own
-// fp64 rounding, 2^29 times finer) whenever |diff| > mg = a2 rhs + a0.
-// Error bounds (u = 2^-24; Hf = fl32(H)): |Q_i - P_i| <= 3u A_i =: al_i with
-// A_i = (|H_i0| + |H_i1|) S + |H_i2|; |w_j - W_j| <= b + u |W_j| with
-// b = S al_2 + max(al_0, al_1); hence |lhs - L| <= 2.85 b sqrt(L) + 2.01 b^2
-// + 4.1u L and |rhs - R| <= maxr al_2 (2|Q_2| + 3 al_2) + 3.01u rhs; both
-// sides are monotone in L, so evaluating them at the threshold L = R bounds
-// the decision error by  c1 |Q_2| + c0 + 7.2u rhs  with
-//   c1 = 2 maxr al_2 + 2.85 b sqrt(maxr),
-//   c0 = 3 maxr al_2^2 + 2.85 b sqrt(maxr) al_2 + 2.01 b^2.
-// The |Q_2| term is folded into the other two with c1 |Q_2| <= c1 (Q_2^2 /
-// (2 tau) + tau / 2) for any tau > 0 (tau = |Q_2| at the image middle), and
-// Q_2^2 <= 1.01 rhs / maxr; everything is scaled by 1.5.  A model whose fp32
-// evaluation could overflow gets constants that leave every point undecided
-// (it is then scored exactly).
+// The reference test fl64(transfer error) <= maxr is, on exact values,
+// W_0^2 + W_1^2 <= maxr P_2^2 with P_i = H_i0 s0 + H_i1 s1 + H_i2 and
+// W_j = d_j P_2 - P_j (up to the reference's own fp64 rounding, 2^29 times
+// finer than the margin below).  The filter divides it by maxr: with
+// r = 1/sqrt(maxr), rows 0 and 1 of H scaled by r and the destination point
+// scaled by r when the chunk is loaded (d' = fl(d fl(r)): exact for maxr =
+// 4^k, e.g. the default 16), it evaluates in fp32 with explicit FMAs
+//   q_i = h'_i0 s0 + h'_i1 s1 + h'_i2,  w_j = d'_j q_2 - q_j,
+//   diff = w_0^2 + w_1^2 - q_2^2           (11 packed ops per 2 points)
+// against one per-model margin M: diff < -M is surely inside, diff > M
+// surely outside, anything else undecided (exact fp64 test).
+// Error bound (u = 2^-24; |coordinates| <= S, exact in fp32; A'_i = (|H'_i0|
+// + |H'_i1|) S + |H'_i2| with H' = H r in rows 0, 1 and H in row 2):
+//   |q_i - P'_i| <= al_i = 3.01u A'_i,
+//   |w_j - W'_j| <= b + u|W'_j|,  b = S r (1.0001 al_2 + 2.02u A'_2) + max(al_0, al_1)
+//   (the 2.02u term is the rounding of d'), so with L = W'_0^2 + W'_1^2,
+//   |lhs - L| <= 2.85 b sqrt(L) + 2.01 b^2 + 4.1u L, |q_2^2 - P_2^2| <= al_2 (2|P_2| + al_2),
+//   and the final rounding adds u max(lhs, q_2^2).  For D = L - P_2^2 <= 0,
+//   sqrt(L) <= |P_2| <= A'_2; for D > 0 the decision error is largest at
+//   L = P_2^2 (or, when |P_2| < 1.43 b, at sqrt(L) = 1.43 b: the 6.1 b^2 term),
+// so |diff - D| <= E = (2.85 b + 2 al_2) A'_2 + 6.1 b^2 + al_2^2 + 5.2u A'_2^2 on
+// every point the decision depends on; M = 1.5 E (rounded up) also covers the
+// reference's fp64 rounding.  A model whose fp32 evaluation could overflow
+// gets constants that leave every point undecided (q = 0, M = 1).
 __device__ __forceinline__ void h_filter_consts(const double* H, double S, double maxr,
                                                 float* c) {
   const double u = 0x1p-24;
-  const double A0 = (fabs(H[0]) + fabs(H[1])) * S + fabs(H[2]);
-  const double A1 = (fabs(H[3]) + fabs(H[4])) * S + fabs(H[5]);
-  const double A2 = (fabs(H[6]) + fabs(H[7])) * S + fabs(H[8]);
-  const double al0 = 3.01 * u * A0, al1 = 3.01 * u * A1, al2 = 3.01 * u * A2;
-  const double b = S * al2 + fmax(al0, al1);
-  const double sq = sqrt(maxr);
-  const double c1 = 2.0 * maxr * al2 + 2.85 * b * sq;
-  const double c0 = 3.0 * maxr * al2 * al2 + 2.85 * b * sq * al2 + 2.01 * b * b;
-  double tau = fabs(H[6] * (0.5 * S) + H[7] * (0.5 * S) + H[8]);
-  if (!(tau > 1e-30 && tau < 1e30)) tau = A2 > 1e-30 ? A2 : 1e-30;
-  const double a2 = 1.5 * (7.2 * u + 1.01 * c1 / (2.0 * tau * maxr));
-  double a0 = 1.5 * (c0 + 0.5 * c1 * tau) + 1e-30;
-  const double wmax = S * A2 + fmax(A0, A1);
-  const double lmax = 2.0 * wmax * wmax, rmax = maxr * A2 * A2;
+  const double r = 1.0 / sqrt(maxr);
+  double Hs[9];
 #pragma unroll
-  for (int j = 0; j < 9; ++j) c[j] = (float)H[j];
-  c[9] = __double2float_ru(a0);
-  c[10] = __double2float_ru(a2 * maxr);  // a2 maxr: mg = a2mr Q2^2 + a0 (h_filter_pair)
+  for (int j = 0; j < 6; ++j) Hs[j] = H[j] * r;
+#pragma unroll
+  for (int j = 6; j < 9; ++j) Hs[j] = H[j];
+  const double A0 = (fabs(Hs[0]) + fabs(Hs[1])) * S + fabs(Hs[2]);
+  const double A1 = (fabs(Hs[3]) + fabs(Hs[4])) * S + fabs(Hs[5]);
+  const double A2 = (fabs(Hs[6]) + fabs(Hs[7])) * S + fabs(Hs[8]);
+  const double al0 = 3.01 * u * A0, al1 = 3.01 * u * A1, al2 = 3.01 * u * A2;
+  const double b = S * r * (1.0001 * al2 + 2.02 * u * A2) + fmax(al0, al1);
+  const double E = (2.85 * b + 2.0 * al2) * A2 + 6.1 * b * b + al2 * al2 + 5.2 * u * A2 * A2;
+  const double M = 1.5 * E + 1e-30;
+  const double wmax = S * r * A2 + fmax(A0, A1);
+  const double lmax = 2.0 * wmax * wmax, rmax = A2 * A2;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) c[j] = (float)Hs[j];
+  c[9] = __double2float_ru(M);
+  c[10] = 0.0f;
   c[11] = 0.0f;
-  if (!(lmax < 1e36 && rmax < 1e36 && a2 < 1e30 && a0 < 1e36)) {
-    // fp32 evaluation unsafe: Q = 0, mg = 1 marks every point undecided, so
+  if (!(lmax < 1e36 && rmax < 1e36 && M < 1e36)) {
+    // fp32 evaluation unsafe: q = 0, M = 1 marks every point undecided, so
     // every point takes the exact test.
 #pragma unroll
     for (int j = 0; j < 9; ++j) c[j] = 0.0f;
     c[9] = 1.0f;
-    c[10] = 0.0f;
   }
 }
+
+// The destination-point scale fl32(1/sqrt(maxr)) of the homography filter
+// (h_filter_consts), applied to d when a chunk is loaded.
+__device__ __forceinline__ float h_point_scale(double maxr) { return (float)(1.0 / sqrt(maxr)); }
 
 // Lanes of point slot p (point base + 64 p + lane) that hold a point.
 __device__ __forceinline__ uint64_t slot_mask(int n, int base, int p) {
@@ -408,32 +404,26 @@ __device__ __forceinline__ uint64_t slot_mask(int n, int base, int p) {
       : "=v"(d) : "v"(a), "v"(b), "v"(c))
 
 // Filter constants as the register pairs of their LDS loads:
-// (h0,h1) (h2,h3) (h4,h5) (h6,h7) (h8,a0) (a2,-), and maxr splat.
+// (h'0,h'1) (h'2,h'3) (h'4,h'5) (h6,h7) (h8,M).
 struct HFilt {
-  f32x2 p01, p23, p45, p67, p8a, pa2, mr;
+  f32x2 p01, p23, p45, p67, p8m;
 };
 
-// Filter quantities of one packed pair of points: surely inside iff
-// diff <= -mg, undecided iff |diff| <= mg, surely outside otherwise.
-__device__ __forceinline__ void h_filter_pair(const HFilt& f, f32x2 s0, f32x2 s1, f32x2 d0,
-                                              f32x2 d1, f32x2* diff, f32x2* mg) {
-  f32x2 t0, t1, t2, q0, q1, q2, m;
-  SCM_PKFMA_BB(t0, f.p01, s1, f.p23, 1, 0);  // h1 s1 + h2
-  SCM_PKFMA_BB(t1, f.p45, s1, f.p45, 0, 1);  // h4 s1 + h5
-  SCM_PKFMA_BB(t2, f.p67, s1, f.p8a, 1, 0);  // h7 s1 + h8
-  SCM_PKFMA_BV(q0, f.p01, s0, t0, 0);        // h0 s0 + (h1 s1 + h2)
-  SCM_PKFMA_BV(q1, f.p23, s0, t1, 1);        // h3 s0 + (h4 s1 + h5)
+// diff of one packed pair of points (s0, s1, scaled d0', d1'): surely inside
+// iff diff < -M, undecided iff |diff| <= M, surely outside otherwise.
+__device__ __forceinline__ f32x2 h_filter_pair(const HFilt& f, f32x2 s0, f32x2 s1, f32x2 d0,
+                                               f32x2 d1) {
+  f32x2 t0, t1, t2, q0, q1, q2;
+  SCM_PKFMA_BB(t0, f.p01, s1, f.p23, 1, 0);  // h'1 s1 + h'2
+  SCM_PKFMA_BB(t1, f.p45, s1, f.p45, 0, 1);  // h'4 s1 + h'5
+  SCM_PKFMA_BB(t2, f.p67, s1, f.p8m, 1, 0);  // h7 s1 + h8
+  SCM_PKFMA_BV(q0, f.p01, s0, t0, 0);        // h'0 s0 + (h'1 s1 + h'2)
+  SCM_PKFMA_BV(q1, f.p23, s0, t1, 1);        // h'3 s0 + (h'4 s1 + h'5)
   SCM_PKFMA_BV(q2, f.p67, s0, t2, 0);        // h6 s0 + (h7 s1 + h8)
   const f32x2 w0 = __builtin_elementwise_fma(d0, q2, -q0);
   const f32x2 w1 = __builtin_elementwise_fma(d1, q2, -q1);
   const f32x2 lhs = __builtin_elementwise_fma(w0, w0, w1 * w1);
-  const f32x2 qq = q2 * q2;
-  // rhs = maxr Q2^2 enters fused (one rounding fewer than fl(maxr fl(Q2^2)),
-  // inside the bound), and the margin a2 rhs + a0 as (a2 maxr) Q2^2 + a0 with
-  // a2 maxr rounded up in h_filter_consts.
-  SCM_PKFMA_BB(m, f.pa2, qq, f.p8a, 0, 1);  // a2mr Q2^2 + a0
-  *mg = m;
-  *diff = __builtin_elementwise_fma(-f.mr, qq, lhs);
+  return __builtin_elementwise_fma(-q2, q2, lhs);
 }
 
 // Exact fp64 test (HomographyMatrixEstimator::Residuals) of the undecided
@@ -451,18 +441,16 @@ __device__ __attribute__((noinline)) bool h_exact_pt(const double* mk, float sx,
 // The hypothesis' constants (LDS, broadcast read), kept in vector registers:
 // no readfirstlane / SGPR copies per model (filter loop 20 % faster,
 // probes/score_bench.hip).
-__device__ __forceinline__ HFilt h_filter_load(const float* hc, float maxrf) {
+__device__ __forceinline__ HFilt h_filter_load(const float* hc) {
   const float4 c0 = reinterpret_cast<const float4*>(hc)[0];
   const float4 c1 = reinterpret_cast<const float4*>(hc)[1];
-  const float4 c2 = reinterpret_cast<const float4*>(hc)[2];
+  const float2 c2 = reinterpret_cast<const float2*>(hc)[4];
   HFilt f;
   f.p01 = f32x2{c0.x, c0.y};
   f.p23 = f32x2{c0.z, c0.w};
   f.p45 = f32x2{c1.x, c1.y};
   f.p67 = f32x2{c1.z, c1.w};
-  f.p8a = f32x2{c2.x, c2.y};
-  f.pa2 = f32x2{c2.z, c2.w};
-  f.mr = f32x2(maxrf);
+  f.p8m = f32x2{c2.x, c2.y};
   return f;
 }
 
@@ -494,30 +482,49 @@ __device__ __forceinline__ bool defer_push(DeferQ* d, uint64_t um, int p, int m)
   return true;
 }
 
-// UND: no exact tests -- return the sure inliers and write the number of
-// undecided points to *nund (the exact pass, rs_exact_kernel, tests them
-// only for models that can still reach the pair's best count).  Otherwise
-// the sure count goes to *nsure (when given) before the exact tests.
-template <int PCH, bool FULL, bool UND = false>
-__device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, const f32x2* s0,
-                                             const f32x2* s1, const f32x2* d0, const f32x2* d1,
-                                             int n, int base, double maxr, int* nslow,
-                                             DeferQ* dq = nullptr, int dm = 0,
-                                             int* nund = nullptr, int* nsure = nullptr) {
+// Inlier count of one homography (filter f, fp64 model mk) over the points
+// [base, base + 64 PCH) (point base + 64 p + lane in slot p, destination
+// coordinates pre-scaled, h_filter_consts; FULL: every slot holds a point).
+// NOTOUT: one compare per point, no exact tests -- return the number of
+// points not surely outside, an upper bound of the count (the first pass of
+// the split scoring; rs_exact_kernel counts exactly the models whose bound
+// reaches the pair's best).  Otherwise the sure inliers plus the exact fp64
+// test (the point reloaded from xyf) of the undecided ones; the sure count
+// goes to *nsure (when given) before the exact tests.
+template <int PCH, bool FULL, bool NOTOUT = false>
+__device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, const float4* xyf,
+                                             const f32x2* s0, const f32x2* s1, const f32x2* d0,
+                                             const f32x2* d1, int n, int base, double maxr,
+                                             int* nslow, DeferQ* dq = nullptr, int dm = 0,
+                                             int* nsure = nullptr) {
+  const float M = f.p8m.y;
   int cnt = 0;
+  if (NOTOUT) {
+#pragma unroll
+    for (int q = 0; q < PCH / 2; ++q) {
+      if (!FULL && base + 128 * q >= n) continue;  // slot pair past the last point
+      const f32x2 diff = h_filter_pair(f, s0[q], s1[q], d0[q], d1[q]);
+      uint64_t o0 = __ballot(diff.x <= M), o1 = __ballot(diff.y <= M);
+      if (!FULL) {
+        o0 &= slot_mask(n, base, 2 * q);
+        o1 &= slot_mask(n, base, 2 * q + 1);
+      }
+      cnt += __popcll(o0) + __popcll(o1);
+    }
+    return cnt;
+  }
   uint64_t any = 0;
   uint64_t um[PCH];  // per point slot: lanes the filter left undecided
 #pragma unroll
   for (int q = 0; q < PCH / 2; ++q) {
-    if (!FULL && base + 128 * q >= n) {  // slot pair past the last point
+    if (!FULL && base + 128 * q >= n) {
       um[2 * q] = um[2 * q + 1] = 0;
       continue;
     }
-    f32x2 diff, mg;
-    h_filter_pair(f, s0[q], s1[q], d0[q], d1[q], &diff, &mg);
+    const f32x2 diff = h_filter_pair(f, s0[q], s1[q], d0[q], d1[q]);
     // strict: a point on the band's edge is undecided, never counted twice
-    uint64_t i0 = __ballot(diff.x < -mg.x), i1 = __ballot(diff.y < -mg.y);
-    uint64_t u0 = __ballot(fabsf(diff.x) <= mg.x), u1 = __ballot(fabsf(diff.y) <= mg.y);
+    uint64_t i0 = __ballot(diff.x < -M), i1 = __ballot(diff.y < -M);
+    uint64_t u0 = __ballot(fabsf(diff.x) <= M), u1 = __ballot(fabsf(diff.y) <= M);
     if (!FULL) {
       const uint64_t ok0 = slot_mask(n, base, 2 * q), ok1 = slot_mask(n, base, 2 * q + 1);
       i0 &= ok0;
@@ -533,13 +540,6 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
 #ifdef SCM_DIAG_SCORE_NOSLOW
   any = 0;  // diagnostics only: undecided points counted as outliers
 #endif
-  if (UND) {
-    int u = 0;
-#pragma unroll
-    for (int p = 0; p < PCH; ++p) u += __popcll(um[p]);
-    *nund = u;
-    return cnt;
-  }
   if (nsure) *nsure = cnt;
   if (any) {  // rare: exact test of the undecided points only (queued when dq)
     ++*nslow;
@@ -550,15 +550,13 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
     }
     const uint64_t me = 1ull << threadIdx.x;
 #pragma unroll
-    for (int q = 0; q < PCH / 2; ++q) {
-      if (um[2 * q]) {
+    for (int p = 0; p < PCH; ++p) {
+      if (um[p]) {
         bool e = false;
-        if (um[2 * q] & me) e = h_exact_pt(mk, s0[q].x, s1[q].x, d0[q].x, d1[q].x, maxr);
-        cnt += __popcll(__ballot(e));
-      }
-      if (um[2 * q + 1]) {
-        bool e = false;
-        if (um[2 * q + 1] & me) e = h_exact_pt(mk, s0[q].y, s1[q].y, d0[q].y, d1[q].y, maxr);
+        if (um[p] & me) {
+          const float4 pt = xyf[base + 64 * p + threadIdx.x];
+          e = h_exact_pt(mk, pt.x, pt.y, pt.z, pt.w, maxr);
+        }
         cnt += __popcll(__ballot(e));
       }
     }
@@ -1197,8 +1195,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                                       const double* xy2, int n, int max_trials,
                                       const VerifyParams P, double* res0, double* res1,
                                       double* xin1, double* xin2, uint32_t* snap,
-                                      double* mbuf, Prof pf, const float4* xyf = nullptr,
-                                      double S = 0.0) {
+                                      double* mbuf, Prof pf) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   const int lane = threadIdx.x;
@@ -1275,99 +1272,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
     // -- score: every lane reloads its own trial's models into registers; the
     //    points are streamed once in register chunks and each model is
     //    broadcast with v_readlane; exact inlier counts via ballot.
-    if constexpr (K == KIND_F) {
-      // Packed-fp32 Sampson filter with exact fp64 fallback (f_filter_consts);
-      // up to 3 models per trial, constants broadcast from LDS.
-      if (lane < B) {
-        const int nm = s.nmodels[lane];
-        for (int k = 0; k < nm; ++k) {
-          const double* mf = mbuf + (lane * MM + k) * MS;
-          f_filter_consts(mf, S, maxr, &s.fcs[lane * MM + k][0]);
-#pragma unroll
-          for (int j = 0; j < 9; ++j) s.fmod[lane * MM + k][j] = mf[j];
-        }
-      }
-      wsync();
-      const float maxrf = (float)maxr;
-      int nslow = 0;
-      uint32_t cnt0 = 0, cnt1 = 0, cnt2 = 0;  // lane t: counts of trial t's models
-      constexpr int PCH = 8;
-      for (int base = 0; base < n; base += 64 * PCH) {
-        f32x2 x0[PCH / 2], x1[PCH / 2], y0[PCH / 2], y1[PCH / 2];
-#pragma unroll
-        for (int q = 0; q < PCH / 2; ++q) {
-          const int i0 = base + (2 * q) * 64 + lane, i1 = i0 + 64;
-          const float4 v0 = i0 < n ? xyf[i0] : make_float4(0.f, 0.f, 0.f, 0.f);
-          const float4 v1 = i1 < n ? xyf[i1] : make_float4(0.f, 0.f, 0.f, 0.f);
-          x0[q] = f32x2{v0.x, v1.x};
-          x1[q] = f32x2{v0.y, v1.y};
-          y0[q] = f32x2{v0.z, v1.z};
-          y1[q] = f32x2{v0.w, v1.w};
-        }
-        const bool full = base + 64 * PCH <= n;
-        for (int t = 0; t < B; ++t) {
-          const int nmt = __builtin_amdgcn_readfirstlane(s.nmodels[t]);
-          for (int k = 0; k < nmt; ++k) {
-            const FFilt f = f_filter_load(&s.fcs[t * MM + k][0], maxrf);
-            const double* mk = &s.fmod[t * MM + k][0];
-            const int c = full ? score_f_chunk<PCH, true>(f, mk, x0, x1, y0, y1, n, base, maxr,
-                                                          &nslow)
-                               : score_f_chunk<PCH, false>(f, mk, x0, x1, y0, y1, n, base, maxr,
-                                                           &nslow);
-            const uint32_t add = (lane == t) ? (uint32_t)c : 0u;
-            if (k == 0) cnt0 += add;
-            else if (k == 1) cnt1 += add;
-            else cnt2 += add;
-          }
-        }
-      }
-      if (lane < B) {
-        s.counts[lane * MM] = cnt0;
-        s.counts[lane * MM + 1] = cnt1;
-        s.counts[lane * MM + 2] = cnt2;
-      }
-      pf.count(PR_N_HCHUNK, (uint64_t)B * (uint64_t)((n + 64 * PCH - 1) / (64 * PCH)));
-      pf.count(PR_N_HSLOW, (uint64_t)nslow);
-    } else if constexpr (K == KIND_H) {
-      // Packed-fp32 filter with exact fp64 fallback (h_filter_consts); the
-      // hypotheses' constants are broadcast from LDS.
-      if (lane < B) {
-        const double* mh = mbuf + lane * (MM * MS);
-        h_filter_consts(mh, S, maxr, &s.hcs[lane][0]);
-#pragma unroll
-        for (int j = 0; j < 9; ++j) s.hmod[lane][j] = mh[j];
-      }
-      wsync();
-      const float maxrf = (float)maxr;
-      int nslow = 0;
-      uint32_t cnt_lane = 0;  // lane t accumulates hypothesis t's inlier count
-      constexpr int PCH = 8;
-      for (int base = 0; base < n; base += 64 * PCH) {
-        f32x2 s0[PCH / 2], s1[PCH / 2], d0[PCH / 2], d1[PCH / 2];
-#pragma unroll
-        for (int q = 0; q < PCH / 2; ++q) {
-          const int i0 = base + (2 * q) * 64 + lane, i1 = i0 + 64;
-          const float4 v0 = i0 < n ? xyf[i0] : make_float4(0.f, 0.f, 0.f, 0.f);
-          const float4 v1 = i1 < n ? xyf[i1] : make_float4(0.f, 0.f, 0.f, 0.f);
-          s0[q] = f32x2{v0.x, v1.x};
-          s1[q] = f32x2{v0.y, v1.y};
-          d0[q] = f32x2{v0.z, v1.z};
-          d1[q] = f32x2{v0.w, v1.w};
-        }
-        const bool full = base + 64 * PCH <= n;
-        for (int t = 0; t < B; ++t) {
-          const HFilt f = h_filter_load(&s.hcs[t][0], maxrf);
-          const int c = full ? score_h_chunk<PCH, true>(f, &s.hmod[t][0], s0, s1, d0, d1, n, base,
-                                                        maxr, &nslow)
-                             : score_h_chunk<PCH, false>(f, &s.hmod[t][0], s0, s1, d0, d1, n,
-                                                         base, maxr, &nslow);
-          cnt_lane += (lane == t) ? (uint32_t)c : 0u;
-        }
-      }
-      if (lane < B) s.counts[lane] = cnt_lane;
-      pf.count(PR_N_HCHUNK, (uint64_t)B * (uint64_t)((n + 64 * PCH - 1) / (64 * PCH)));
-      pf.count(PR_N_HSLOW, (uint64_t)nslow);
-    } else {
+    {
     double m[MM][MS];
     int nm = 0;
     if (lane < B) {
@@ -1986,6 +1891,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
   const int lane = threadIdx.x;
   const int na = *nact;
   const float maxrf = (float)maxr;
+  const f32x2 dsc = f32x2(h_point_scale(maxr));
   // Work item = (active pair, chunk, run of rpi rounds of the window): late
   // windows (few far pairs left) split their rounds over separate items so
   // that they still fill the GPU; busy windows keep long runs (points loaded
@@ -2016,6 +1922,10 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
       x1[qq] = f32x2{v0.y, v1.y};
       y0[qq] = f32x2{v0.z, v1.z};
       y1[qq] = f32x2{v0.w, v1.w};
+      if (K == KIND_H) {  // destination scaled by 1/sqrt(maxr) (h_filter_consts)
+        y0[qq] *= dsc;
+        y1[qq] *= dsc;
+      }
     }
     const bool full = base + kScoreChunk <= n;
     for (int r0 = rbeg; r0 < rend; r0 += kTrialBatch) {
@@ -2050,13 +1960,19 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
                                                               base, maxr, &nslow,
                                                               SPLIT ? nullptr : &dq, m, &u);
           } else {
-            const HFilt f = h_filter_load(&lc[m][0], maxrf);
-            c = full ? score_h_chunk<kScorePch, true, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
-                                                             base, maxr, &nslow,
-                                                             SPLIT ? nullptr : &dq, m, &u)
-                     : score_h_chunk<kScorePch, false, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
-                                                              base, maxr, &nslow,
-                                                              SPLIT ? nullptr : &dq, m, &u);
+            const HFilt f = h_filter_load(&lc[m][0]);
+            if (SPLIT) {  // points not surely outside (bound); exact counts in rs_exact_kernel
+              c = 0;
+              u = full ? score_h_chunk<kScorePch, true, true>(f, mb + m * MS, xyf, x0, x1, y0, y1,
+                                                              n, base, maxr, &nslow)
+                       : score_h_chunk<kScorePch, false, true>(f, mb + m * MS, xyf, x0, x1, y0,
+                                                               y1, n, base, maxr, &nslow);
+            } else {
+              c = full ? score_h_chunk<kScorePch, true>(f, mb + m * MS, xyf, x0, x1, y0, y1, n,
+                                                        base, maxr, &nslow, &dq, m)
+                       : score_h_chunk<kScorePch, false>(f, mb + m * MS, xyf, x0, x1, y0, y1, n,
+                                                         base, maxr, &nslow, &dq, m);
+            }
           }
           const uint32_t add = (lane == t) ? (uint32_t)c : 0u;
           const uint32_t uadd = (lane == t) ? (uint32_t)u : 0u;
@@ -2106,12 +2022,14 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
 // Exact pass of the split scoring (after rs_score_kernel<K, true>): a model's
 // count is needed exactly only if it can be a candidate of the sequential
 // replay, i.e. reach the pair's best count -- and the best only grows, so a
-// model whose sure + undecided inliers stay below the best at the start of
-// the window (rst.best_n) can never be one; its count stays the sure count
-// (a lower bound below the best, which the replay reads exactly as it would
-// read the exact count).  For the others the undecided points of every chunk
-// take the exact fp64 test here.  Same work items as the scoring kernel;
-// items with no such model exit without loading their points.
+// model whose upper bound stays below the best at the start of the window
+// (rst.best_n) can never be one.  F: the bound is sure + undecided inliers and
+// the count stays the sure count; H: the bound is the number of points not
+// surely outside and the count stays 0 -- either way a value below the best,
+// which the replay reads exactly as it would read the exact count.  For the
+// others the exact count is completed here (F: the undecided points' exact
+// tests; H: the whole count).  Same work items as the scoring kernel; items
+// with no such model exit without loading their points.
 template <int K>
 __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
     const VerifyPair* __restrict__ pairs, const float4* __restrict__ xyf_all,
@@ -2125,6 +2043,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
   const int lane = threadIdx.x;
   const int na = *nact;
   const float maxrf = (float)maxr;
+  const f32x2 dsc = f32x2(h_point_scale(maxr));
   const int rpi = max(1, min(W, (int)(((int64_t)na * max_chunks * W) / kScoreTargetItems)));
   const int nri = (W + rpi - 1) / rpi;
   const int per_pair = max_chunks * nri;
@@ -2154,7 +2073,8 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
 #pragma unroll
         for (int k = 0; k < MM; ++k) {
           const uint32_t u = k < nml ? ucnt[mo + lane * MM + k] : 0u;
-          if (u && cnts[mo + lane * MM + k] + u >= best0) qual |= 1u << k;
+          const uint32_t bound = K == KIND_H ? u : cnts[mo + lane * MM + k] + u;
+          if (u && bound >= best0) qual |= 1u << k;
         }
       }
       uint64_t any = __ballot(qual != 0);
@@ -2169,6 +2089,10 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
           x1[qq] = f32x2{v0.y, v1.y};
           y0[qq] = f32x2{v0.z, v1.z};
           y1[qq] = f32x2{v0.w, v1.w};
+          if (K == KIND_H) {
+            y0[qq] *= dsc;
+            y1[qq] *= dsc;
+          }
         }
         loaded = true;
       }
@@ -2190,11 +2114,11 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
                      : score_f_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
                                                        maxr, &nslow, nullptr, 0, nullptr, &sure);
           } else {
-            const HFilt f = h_filter_load(cb + m * 12, maxrf);
-            c = full ? score_h_chunk<kScorePch, true>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                      maxr, &nslow, nullptr, 0, nullptr, &sure)
-                     : score_h_chunk<kScorePch, false>(f, mb + m * MS, x0, x1, y0, y1, n, base,
-                                                       maxr, &nslow, nullptr, 0, nullptr, &sure);
+            const HFilt f = h_filter_load(cb + m * 12);
+            c = full ? score_h_chunk<kScorePch, true>(f, mb + m * MS, xyf, x0, x1, y0, y1, n,
+                                                      base, maxr, &nslow)
+                     : score_h_chunk<kScorePch, false>(f, mb + m * MS, xyf, x0, x1, y0, y1, n,
+                                                       base, maxr, &nslow);
           }
           if (lane == 0 && c > sure) atomicAdd(&cnts[mo + m], (uint32_t)(c - sure));
         }
