@@ -247,9 +247,10 @@ typedef struct scm_frame {
  * the descriptors element (write_matrix_to_element, u8 128 per row) and the
  * camera element (write_camera_to_element, io.cc:307-335); each blob
  * library-allocated (scm_blob_free).  COLMAP's default
- * SiftExtractionOptions; frames larger than max_image_size (3200) are
- * rejected with SCM_E_INVALID (the reference rescales them with FreeImage,
- * not implemented), as are frames below 16 x 16. */
+ * SiftExtractionOptions; a frame larger than max_image_size (3200) is
+ * first reduced as resizeBitmap does (extraction_op.cc:28-39: grey, FreeImage
+ * bilinear rescale by 3200 / max(w, h)); frames below 16 x 16 (after that
+ * rescale) are rejected with SCM_E_INVALID. */
 int scm_extract_frames(scm_context* ctx, int64_t n, const uint64_t* image_ids,
                        const scm_frame* frames, scm_blob* keypoints_out,
                        scm_blob* descriptors_out, scm_blob* cameras_out);

@@ -358,6 +358,27 @@ def sift_grey(frame) -> np.ndarray:
     return out
 
 
+def sift_fit_size(width: int, height: int) -> tuple[int, int]:
+    """resizeBitmap's target size (extraction_op.cc:28-39) for max_image_size 3200."""
+    L = lib()
+    L.oracle_sift_fit_size.argtypes = [c_int32, c_int32, POINTER(c_int32), POINTER(c_int32)]
+    nw, nh = c_int32(), c_int32()
+    L.oracle_sift_fit_size(width, height, byref(nw), byref(nh))
+    return nw.value, nh.value
+
+
+def sift_rescale(grey, nw: int, nh: int) -> np.ndarray:
+    """FreeImage_Rescale(FILTER_BILINEAR) of an 8-bit grey image to nw x nh."""
+    g = np.ascontiguousarray(grey, dtype=np.uint8)
+    h, w = g.shape
+    out = np.zeros((nh, nw), np.uint8)
+    L = lib()
+    L.oracle_sift_rescale.argtypes = [c_void_p, c_int32, c_int32, c_int32, c_int32, c_void_p]
+    if L.oracle_sift_rescale(g.ctypes.data, w, h, nw, nh, out.ctypes.data) != 0:
+        raise ValueError("oracle_sift_rescale failed")
+    return out
+
+
 def sift_octave(grey, octave: int) -> np.ndarray:
     """Gaussian scale space of one octave (levels s = -1 .. 4) of a grey image."""
     g = np.ascontiguousarray(grey, dtype=np.uint8)

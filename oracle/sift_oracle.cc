@@ -13,8 +13,13 @@
 //     call copies them as they are), grey = (BYTE)(0.2126F R + 0.7152F G +
 //     0.0722F B + 0.5F) (FreeImage 3.17 Utilities.h LUMA_REC709 / GREY), i.e.
 //     frame channel 2 is weighted as red and channel 0 as blue;
-//   * resizeBitmap (:29-39) -- only checked: an image larger than
-//     max_image_size (3200) is rejected (FreeImage_Rescale is not restated);
+//   * resizeBitmap (:28-39): a grey image larger than max_image_size (3200) in
+//     either dimension is scaled by 3200 / max(w, h) (new sizes truncated) with
+//     Bitmap::Rescale -> FreeImage_Rescale(FILTER_BILINEAR) (FreeImage 3.17
+//     Resize.cpp: CWeightsTable of CBilinearFilter, one 8-bit pass per axis in
+//     FreeImage's bottom-up scanline order, xy or yx by the smaller
+//     intermediate, fp64 sums rounded to BYTE after each pass) -- restated from
+//     FreeImage's published source (not vendored in the reference);
 //   * colmap::ExtractSiftFeaturesCPU (COLMAP 3.4 src/feature/sift.cc) with the
 //     default SiftExtractionOptions (max_num_features 8192, first_octave -1,
 //     num_octaves 4, octave_resolution 3, peak_threshold 0.02 / 3,
@@ -566,6 +571,103 @@ void frame_to_grey(const uint8_t* frame, int w, int h, int ch, std::vector<uint8
   }
 }
 
+// FreeImage 3.17 CWeightsTable (Resize.cpp) of CBilinearFilter (width 1) for
+// a src -> dst line: per destination pixel the source range [left, left +
+// cnt) and its normalised weights.
+struct RescaleTable {
+  std::vector<int> left, cnt;
+  std::vector<std::vector<double>> w;
+};
+
+RescaleTable rescale_table(int dst, int src) {
+  RescaleTable t;
+  const double filter_width = 1.0;
+  const double scale = double(dst) / double(src);
+  double width, fscale;
+  if (scale < 1.0) {
+    width = filter_width / scale;
+    fscale = scale;
+  } else {
+    width = filter_width;
+    fscale = 1.0;
+  }
+  const double offset = 0.5 / scale;
+  for (int u = 0; u < dst; ++u) {
+    const double center = (double)u / scale + offset;
+    const int lo = std::max(0, (int)(center - width + 0.5));
+    const int hi = std::min((int)(center + width + 0.5), src);
+    std::vector<double> w;
+    double total = 0;
+    for (int i = lo; i < hi; ++i) {
+      const double x = std::fabs(fscale * ((double)i + 0.5 - center));
+      const double weight = fscale * (x < filter_width ? filter_width - x : 0.0);
+      w.push_back(weight);
+      total += weight;
+    }
+    if (total > 0 && total != 1)
+      for (double& x : w) x /= total;
+    int right = hi;
+    while (right > lo && w[right - lo - 1] == 0) --right;  // trailing null weights
+    w.resize(right - lo);
+    t.left.push_back(lo);
+    t.cnt.push_back(right - lo);
+    t.w.push_back(w);
+  }
+  return t;
+}
+
+inline uint8_t to_byte(double v) { return (uint8_t)std::min(std::max((int)(v + 0.5), 0), 255); }
+
+// FreeImage_Rescale(FILTER_BILINEAR) of an 8-bit grey image (top-down rows
+// here; FreeImage's scanline j is row h - 1 - j, which the vertical pass's
+// weight table indexes).
+void rescale_grey(const std::vector<uint8_t>& g, int w, int h, int nw, int nh,
+                  std::vector<uint8_t>* out) {
+  const RescaleTable th = rescale_table(nw, w), tv = rescale_table(nh, h);
+  auto horiz = [&](const std::vector<uint8_t>& src, int rows, std::vector<uint8_t>* dst) {
+    dst->assign((size_t)nw * rows, 0);
+    for (int y = 0; y < rows; ++y)
+      for (int x = 0; x < nw; ++x) {
+        double v = 0;
+        for (int i = 0; i < th.cnt[x]; ++i)
+          v += th.w[x][i] * (double)src[(size_t)y * w + th.left[x] + i];
+        (*dst)[(size_t)y * nw + x] = to_byte(v);
+      }
+  };
+  auto vert = [&](const std::vector<uint8_t>& src, int cols, std::vector<uint8_t>* dst) {
+    dst->assign((size_t)cols * nh, 0);
+    for (int r = 0; r < nh; ++r) {
+      const int u = nh - 1 - r;  // destination scanline
+      for (int x = 0; x < cols; ++x) {
+        double v = 0;
+        for (int i = 0; i < tv.cnt[u]; ++i)
+          v += tv.w[u][i] * (double)src[(size_t)(h - 1 - (tv.left[u] + i)) * cols + x];
+        (*dst)[(size_t)r * cols + x] = to_byte(v);
+      }
+    }
+  };
+  std::vector<uint8_t> tmp;
+  if ((int64_t)nw * h <= (int64_t)nh * w) {  // xy: the smaller intermediate
+    horiz(g, h, &tmp);
+    vert(tmp, nw, out);
+  } else {
+    vert(g, w, &tmp);
+    horiz(tmp, nh, out);
+  }
+}
+
+// resizeBitmap (extraction_op.cc:28-39): the new size, or (w, h) when the
+// image fits.
+void fit_size(int w, int h, int max_size, int* nw, int* nh) {
+  *nw = w;
+  *nh = h;
+  if (w > max_size || h > max_size) {
+    const double scale = (double)max_size / std::max(w, h);
+    *nw = (int)(w * scale);
+    *nh = (int)(h * scale);
+  }
+}
+
 // colmap::ExtractSiftFeaturesCPU.
 void extract(const std::vector<uint8_t>& grey, int w, int h, const SiftOpts& o,
              std::vector<Feature>* out, std::vector<int>* level_sizes) {
@@ -660,9 +762,17 @@ int oracle_sift_extract(const uint8_t* frame, int32_t width, int32_t height, int
   // image that small have no interior pixels left; VLFeat would still run)
   if (!frame || width < 16 || height < 16 || !(channels == 1 || channels == 3 || channels == 4))
     return SCM_E_INVALID;
-  if (width > o.max_image_size || height > o.max_image_size) return SCM_E_INVALID;
   std::vector<uint8_t> grey;
   frame_to_grey(frame, width, height, channels, &grey);
+  int nw, nh;
+  fit_size(width, height, o.max_image_size, &nw, &nh);
+  if (nw != width || nh != height) {
+    std::vector<uint8_t> small;
+    rescale_grey(grey, width, height, nw, nh, &small);
+    grey.swap(small);
+    width = nw;
+    height = nh;
+  }
   std::vector<Feature> f;
   extract(grey, width, height, o, &f, nullptr);
   std::vector<uint8_t> kb, db, cb;
@@ -699,6 +809,22 @@ int oracle_sift_grey(const uint8_t* frame, int32_t width, int32_t height, int32_
   std::vector<uint8_t> g;
   frame_to_grey(frame, width, height, channels, &g);
   std::memcpy(out, g.data(), g.size());
+  return SCM_OK;
+}
+
+// Diagnostics for the tests: FreeImage_Rescale(FILTER_BILINEAR) of an 8-bit
+// grey image (top-down rows) to nw x nh, and the op's fitted size.
+int oracle_sift_rescale(const uint8_t* grey, int32_t width, int32_t height, int32_t nw, int32_t nh,
+                        uint8_t* out) {
+  if (!grey || width < 1 || height < 1 || nw < 1 || nh < 1) return SCM_E_INVALID;
+  std::vector<uint8_t> g(grey, grey + (size_t)width * height), r;
+  rescale_grey(g, width, height, nw, nh, &r);
+  std::memcpy(out, r.data(), r.size());
+  return SCM_OK;
+}
+
+int oracle_sift_fit_size(int32_t width, int32_t height, int32_t* nw, int32_t* nh) {
+  fit_size(width, height, SiftOpts().max_image_size, nw, nh);
   return SCM_OK;
 }
 

@@ -11,6 +11,10 @@
 // with the host libm's cosf / sinf, and the extractCamera SIMPLE_RADIAL camera.
 // Frames rotate over a few image slots, each with its own stream and HBM
 // workspace, so consecutive frames overlap (upload, kernels, read-back).
+// A frame larger than max_image_size is first reduced as resizeBitmap does
+// (extraction_op.cc:28-39): grey bytes, FreeImage's bilinear rescale by
+// 3200 / max(w, h) (host-built weight tables, one GPU pass per axis), then the
+// same pipeline on the smaller grey image.
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -32,8 +36,9 @@ constexpr int kSlots = 4;
 
 struct Slot {
   hipStream_t st = nullptr;
-  DevBuf frame, ws, counts;
-  HostBuf pin_in, pin_cnt, pin_out;
+  DevBuf frame, ws, counts, rs, rtab;  // rs: grey + rescale images; rtab: weight tables
+  HostBuf pin_in, pin_cnt, pin_out, pin_rtab;
+  int rtab_w = 0, rtab_h = 0;  // source size the uploaded tables are for
   SiftDev dev{};
   int64_t nel_cap = 0;  // first-octave pixels the workspace holds
   int64_t pending = -1; // frame index whose results are in flight
@@ -66,6 +71,9 @@ void sift_state_destroy(SiftState* s) {
       (void)hipStreamDestroy(sl.st);
     }
     sl.frame.release();
+    sl.rs.release();
+    sl.rtab.release();
+    sl.pin_rtab.release();
     sl.ws.release();
     sl.counts.release();
     sl.pin_in.release();
@@ -117,6 +125,48 @@ int init_state(SiftState* s) {
   return SCM_OK;
 }
 
+// resizeBitmap's target size: scale 3200 / max(w, h), sizes truncated.
+void fit_size(int w, int h, int* nw, int* nh) {
+  *nw = w;
+  *nh = h;
+  if (w > kMaxImageSize || h > kMaxImageSize) {
+    const double scale = (double)kMaxImageSize / std::max(w, h);
+    *nw = (int)(w * scale);
+    *nh = (int)(h * scale);
+  }
+}
+
+// FreeImage 3.17 CWeightsTable of CBilinearFilter (width 1) for a src -> dst
+// line: per destination pixel (left, count) and count normalised weights
+// (padded to win, the window size table_layout also computes).  Returns win.
+int bilinear_table(int dst, int src, std::vector<int32_t>* hdr, std::vector<double>* wt) {
+  const double scale = double(dst) / double(src);
+  const double width = scale < 1.0 ? 1.0 / scale : 1.0, fscale = scale < 1.0 ? scale : 1.0;
+  const int win = 2 * (int)std::ceil(width) + 1;
+  const double offset = 0.5 / scale;
+  hdr->assign(2 * (size_t)dst, 0);
+  wt->assign((size_t)dst * win, 0.0);
+  for (int u = 0; u < dst; ++u) {
+    const double center = (double)u / scale + offset;
+    const int lo = std::max(0, (int)(center - width + 0.5));
+    const int hi = std::min((int)(center + width + 0.5), src);
+    double* w = wt->data() + (size_t)u * win;
+    double total = 0;
+    for (int i = lo; i < hi; ++i) {
+      const double x = std::fabs(fscale * ((double)i + 0.5 - center));
+      w[i - lo] = fscale * (x < 1.0 ? 1.0 - x : 0.0);
+      total += w[i - lo];
+    }
+    if (total > 0 && total != 1)
+      for (int i = lo; i < hi; ++i) w[i - lo] /= total;
+    int right = hi;
+    while (right > lo && w[right - lo - 1] == 0) --right;  // trailing null weights
+    (*hdr)[2 * (size_t)u] = lo;
+    (*hdr)[2 * (size_t)u + 1] = right - lo;
+  }
+  return win;
+}
+
 // Workspace of a slot for a frame whose first octave has nel pixels (2w x 2h).
 int ensure_slot(Slot& sl, int w, int h) {
   const int64_t ow = 2 * (int64_t)w, oh = 2 * (int64_t)h, nel = ow * oh;
@@ -162,16 +212,95 @@ int ensure_slot(Slot& sl, int w, int h) {
   return SCM_OK;
 }
 
+// Byte offsets of the rescale tables in Slot::rtab for an nw x nh target:
+// horizontal (left, count) pairs, vertical pairs, horizontal weights,
+// vertical weights.
+struct TableLayout {
+  int winh, winv;
+  size_t o1, o2, o3, bytes;
+};
+
+TableLayout table_layout(int w, int h, int nw, int nh) {
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  auto win = [](int dst, int src) {
+    const double scale = double(dst) / double(src);
+    return 2 * (int)std::ceil(scale < 1.0 ? 1.0 / scale : 1.0) + 1;
+  };
+  TableLayout L;
+  L.winh = win(nw, w);
+  L.winv = win(nh, h);
+  L.o1 = up(2 * (size_t)nw * 4);
+  L.o2 = L.o1 + up(2 * (size_t)nh * 4);
+  L.o3 = L.o2 + up((size_t)nw * L.winh * 8);
+  L.bytes = L.o3 + (size_t)nh * L.winv * 8;
+  return L;
+}
+
+// resizeBitmap on the GPU: grey bytes of the frame in slot.frame, then the
+// two bilinear passes (xy or yx: FreeImage filters first along the axis that
+// gives the smaller intermediate); the nw x nh grey image ends in *out.
+// The slot's stream is idle here (its previous frame was harvested).
+int enqueue_rescale(Slot& sl, int w, int h, int ch, int nw, int nh, const uint8_t** out) {
+  hipStream_t st = sl.st;
+  const TableLayout L = table_layout(w, h, nw, nh);
+  if (sl.rtab_w != w || sl.rtab_h != h) {  // weight tables for this source size
+    std::vector<int32_t> hh, hv;
+    std::vector<double> wh, wv;
+    bilinear_table(nw, w, &hh, &wh);
+    bilinear_table(nh, h, &hv, &wv);
+    SCM_TRY(sl.pin_rtab.ensure(L.bytes));
+    SCM_TRY(sl.rtab.ensure(L.bytes));
+    uint8_t* p = sl.pin_rtab.as<uint8_t>();
+    std::memcpy(p, hh.data(), hh.size() * 4);
+    std::memcpy(p + L.o1, hv.data(), hv.size() * 4);
+    std::memcpy(p + L.o2, wh.data(), wh.size() * 8);
+    std::memcpy(p + L.o3, wv.data(), wv.size() * 8);
+    SCM_HIP(hipMemcpyAsync(sl.rtab.ptr, p, L.bytes, hipMemcpyHostToDevice, st));
+    sl.rtab_w = w;
+    sl.rtab_h = h;
+  }
+  const uint8_t* tb = sl.rtab.as<uint8_t>();
+  const int2* hh = reinterpret_cast<const int2*>(tb);
+  const int2* hv = reinterpret_cast<const int2*>(tb + L.o1);
+  const double* wh = reinterpret_cast<const double*>(tb + L.o2);
+  const double* wv = reinterpret_cast<const double*>(tb + L.o3);
+  const bool xy = (int64_t)nw * h <= (int64_t)nh * w;
+  auto up = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t g = (size_t)w * h, t = xy ? (size_t)nw * h : (size_t)w * nh, o = (size_t)nw * nh;
+  SCM_TRY(sl.rs.ensure(up(g) + up(t) + o));
+  uint8_t* grey = sl.rs.as<uint8_t>();
+  uint8_t* tmp = grey + up(g);
+  uint8_t* res = tmp + up(t);
+  SCM_HIP(sift_grey(sl.frame.as<uint8_t>(), w, h, ch, grey, st));
+  if (xy) {
+    SCM_HIP(sift_rescale_rows(grey, w, h, tmp, nw, hh, wh, L.winh, st));
+    SCM_HIP(sift_rescale_cols(tmp, nw, h, res, nh, hv, wv, L.winv, st));
+  } else {
+    SCM_HIP(sift_rescale_cols(grey, w, h, tmp, nh, hv, wv, L.winv, st));
+    SCM_HIP(sift_rescale_rows(tmp, w, nh, res, nw, hh, wh, L.winh, st));
+  }
+  *out = res;
+  return SCM_OK;
+}
+
 int enqueue_frame(SiftState* s, Slot& sl, const scm_frame& f) {
-  const int w = f.width, h = f.height, ch = f.channels;
+  const int fw = f.width, fh = f.height;
+  int w, h;
+  fit_size(fw, fh, &w, &h);
+  int ch = f.channels;
   SCM_TRY(ensure_slot(sl, w, h));
-  const size_t fb = (size_t)w * h * ch;
+  const size_t fb = (size_t)fw * fh * ch;
   SCM_TRY(sl.pin_in.ensure(fb));
   SCM_TRY(sl.frame.ensure(fb));
-  std::memcpy(sl.pin_in.ptr, f.data, fb);
   hipStream_t st = sl.st;
+  std::memcpy(sl.pin_in.ptr, f.data, fb);
   SCM_HIP(hipMemcpyAsync(sl.frame.ptr, sl.pin_in.ptr, fb, hipMemcpyHostToDevice, st));
   SCM_HIP(hipMemsetAsync(sl.dev.cnt, 0, sizeof(SiftCounts), st));
+  const uint8_t* src = sl.frame.as<uint8_t>();
+  if (w != fw || h != fh) {
+    SCM_TRY(enqueue_rescale(sl, fw, fh, ch, w, h, &src));
+    ch = 1;
+  }
   SiftDev& d = sl.dev;
   int ow = 2 * w, oh = 2 * h, pw = 0, ph = 0;  // this octave's and the previous octave's size
   for (int o = -1; o < kSiftOctaves - 1; ++o) {
@@ -183,7 +312,7 @@ int enqueue_frame(SiftState* s, Slot& sl, const scm_frame& f) {
     }
     const size_t so = (size_t)ow * oh;
     if (o == -1) {
-      SCM_HIP(sift_upsample(sl.frame.as<uint8_t>(), w, h, ch, d.levels, st));
+      SCM_HIP(sift_upsample(src, w, h, ch, d.levels, st));
       SCM_HIP(sift_smooth(d.levels, d.levels, d.temp, ow, oh, s->c, 0, s->widths[0], st));
     } else {
       // copy_and_downsample of level s_best = 2 (index 3) of the previous
@@ -292,10 +421,11 @@ int sift_extract_frames(SiftState** state, int device, int64_t n, const uint64_t
                 " is not a >= 16 x 16 frame of 1, 3 or 4 channels");
       return SCM_E_INVALID;
     }
-    if (f.width > kMaxImageSize || f.height > kMaxImageSize) {
+    int nw, nh;
+    fit_size(f.width, f.height, &nw, &nh);
+    if (nw < kMinImageSize || nh < kMinImageSize) {
       set_error("scm_extract_frames: frame " + std::to_string(i) +
-                " exceeds max_image_size 3200 (the reference rescales it with FreeImage; not "
-                "implemented)");
+                " is below 16 x 16 after the max_image_size rescale");
       return SCM_E_INVALID;
     }
   }

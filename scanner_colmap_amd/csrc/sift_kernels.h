@@ -73,6 +73,13 @@ struct SiftConsts {
   double* expn;     // 257
 };
 
+// Frames above max_image_size: grey bytes, then FreeImage's bilinear rescale
+// one axis at a time (weight tables built on the host, scm_sift.cpp).
+hipError_t sift_grey(const uint8_t* frame, int w, int h, int ch, uint8_t* out, hipStream_t st);
+hipError_t sift_rescale_rows(const uint8_t* src, int sw, int rows, uint8_t* dst, int dw,
+                             const int2* hdr, const double* wt, int win, hipStream_t st);
+hipError_t sift_rescale_cols(const uint8_t* src, int cols, int sh, uint8_t* dst, int dh,
+                             const int2* hdr, const double* wt, int win, hipStream_t st);
 hipError_t sift_upsample(const uint8_t* frame, int w, int h, int ch, float* out, hipStream_t st);
 hipError_t sift_smooth(const float* in, float* out, float* tmp, int w, int h, const SiftConsts& c,
                        int tap_set, int W, hipStream_t st);

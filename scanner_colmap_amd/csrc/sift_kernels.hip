@@ -35,18 +35,63 @@ constexpr int kVTile = 64;   // vertical pass: 64 columns x 64 rows per block
 constexpr int kHTile = 1024; // horizontal pass: 1024 outputs of a row per block
 constexpr int kGrid = 2048;  // grid-stride kernels over device-side counts
 
-// The op's grey value (FreeImage B, G, R memory order; LUMA_REC709 + 0.5)
-// as the float the SIFT filter reads (grey / 255.0f).
-__device__ __forceinline__ float grey_at(const uint8_t* f, int w, int ch, int y, int x) {
+// The op's grey value (FreeImage B, G, R memory order; LUMA_REC709 + 0.5).
+__device__ __forceinline__ uint8_t grey_u8_at(const uint8_t* f, int w, int ch, int y, int x) {
   const uint8_t* p = f + ((size_t)y * w + x) * ch;
-  uint8_t g;
-  if (ch == 1) {
-    g = p[0];
-  } else {
-    const float r = p[2], gg = p[1], b = p[0];
-    g = (uint8_t)(0.2126F * r + 0.7152F * gg + 0.0722F * b + 0.5F);
-  }
-  return (float)g / 255.0f;
+  if (ch == 1) return p[0];
+  const float r = p[2], gg = p[1], b = p[0];
+  return (uint8_t)(0.2126F * r + 0.7152F * gg + 0.0722F * b + 0.5F);
+}
+
+// ... as the float the SIFT filter reads (grey / 255.0f).
+__device__ __forceinline__ float grey_at(const uint8_t* f, int w, int ch, int y, int x) {
+  return (float)grey_u8_at(f, w, ch, y, x) / 255.0f;
+}
+
+// Grey image of a frame larger than max_image_size (the input of the rescale).
+__global__ void grey_kernel(const uint8_t* __restrict__ f, int w, int h, int ch,
+                            uint8_t* __restrict__ out) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x < w) out[(size_t)y * w + x] = grey_u8_at(f, w, ch, y, x);
+}
+
+// FreeImage_Rescale(FILTER_BILINEAR) of the 8-bit grey bitmap (resizeBitmap,
+// extraction_op.cc:28-39), one axis per launch: each output pixel is the fp64
+// sum, in ascending source order, of the CWeightsTable weights times the
+// source bytes, rounded to BYTE ((int)(v + 0.5), clamped) -- FreeImage 3.17
+// Resize.cpp's 8-bit horizontalFilter / verticalFilter.  The vertical table is
+// indexed in FreeImage's bottom-up scanline order (scanline j = row h - 1 - j).
+__device__ __forceinline__ uint8_t rescale_byte(double v) {
+  const int i = (int)(v + 0.5);
+  return (uint8_t)(i < 0 ? 0 : (i > 255 ? 255 : i));
+}
+
+__global__ void rescale_rows_kernel(const uint8_t* __restrict__ src, int sw,
+                                    uint8_t* __restrict__ dst, int dw,
+                                    const int2* __restrict__ hdr, const double* __restrict__ wt,
+                                    int win) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
+  if (x >= dw) return;
+  const int2 lc = hdr[x];
+  const uint8_t* s = src + (size_t)y * sw + lc.x;
+  const double* wx = wt + (size_t)x * win;
+  double v = 0.0;
+  for (int i = 0; i < lc.y; ++i) v += wx[i] * (double)s[i];
+  dst[(size_t)y * dw + x] = rescale_byte(v);
+}
+
+__global__ void rescale_cols_kernel(const uint8_t* __restrict__ src, int w, int sh,
+                                    uint8_t* __restrict__ dst, int dh,
+                                    const int2* __restrict__ hdr, const double* __restrict__ wt,
+                                    int win) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x, r = blockIdx.y;
+  if (x >= w) return;
+  const int u = dh - 1 - r;  // destination scanline
+  const int2 lc = hdr[u];
+  const double* wu = wt + (size_t)u * win;
+  double v = 0.0;
+  for (int i = 0; i < lc.y; ++i) v += wu[i] * (double)src[(size_t)(sh - 1 - (lc.x + i)) * w + x];
+  dst[(size_t)r * w + x] = rescale_byte(v);
 }
 
 // copy_and_upsample_rows twice (x first, then y): out is 2w x 2h.
@@ -710,6 +755,25 @@ int blocks_for(size_t n, int t) { return (int)((n + t - 1) / t); }
 hipError_t sift_upsample(const uint8_t* frame, int w, int h, int ch, float* out, hipStream_t st) {
   dim3 grid(blocks_for(2 * (size_t)w, 256), 2 * h);
   upsample_kernel<<<grid, 256, 0, st>>>(frame, w, h, ch, out);
+  return hipGetLastError();
+}
+
+hipError_t sift_grey(const uint8_t* frame, int w, int h, int ch, uint8_t* out, hipStream_t st) {
+  grey_kernel<<<dim3(blocks_for(w, 256), h), 256, 0, st>>>(frame, w, h, ch, out);
+  return hipGetLastError();
+}
+
+hipError_t sift_rescale_rows(const uint8_t* src, int sw, int rows, uint8_t* dst, int dw,
+                             const int2* hdr, const double* wt, int win, hipStream_t st) {
+  rescale_rows_kernel<<<dim3(blocks_for(dw, 256), rows), 256, 0, st>>>(src, sw, dst, dw, hdr, wt,
+                                                                       win);
+  return hipGetLastError();
+}
+
+hipError_t sift_rescale_cols(const uint8_t* src, int cols, int sh, uint8_t* dst, int dh,
+                             const int2* hdr, const double* wt, int win, hipStream_t st) {
+  rescale_cols_kernel<<<dim3(blocks_for(cols, 256), dh), 256, 0, st>>>(src, cols, sh, dst, dh, hdr,
+                                                                       wt, win);
   return hipGetLastError();
 }
 

@@ -95,9 +95,22 @@ def test_extracted_table_feeds_the_matcher(ctx):
     assert got_ids == ref_ids and got_tvg == ref_tvg
 
 
-def test_rejects_oversize_and_tiny_frames(ctx):
+@pytest.mark.parametrize("h,w,ch,seed", [(2160, 3840, 3, 31),   # 4K: xy order (horizontal first)
+                                          (2500, 3300, 3, 32),   # yx order
+                                          (60, 3500, 1, 33)])
+def test_oversize_frames_rescaled_bit_exact(ctx, h, w, ch, seed):
+    # resizeBitmap (extraction_op.cc:28-39): grey, FreeImage bilinear rescale to
+    # 3200 / max(w, h), then extraction; camera of the rescaled size
+    f = synthetic_frame(h, w, seed, channels=ch, blobs=4000 if h * w > 1e6 else None)
+    got = ctx.extract_frames([f, f[:120, :160]], [seed, seed + 1])
+    ref = oracle.sift_extract(f, seed)
+    assert got[0] == ref, _diff(got[0], ref, f"{h}x{w}x{ch} rescaled")
+    assert got[1] == oracle.sift_extract(f[:120, :160], seed + 1)
+
+
+def test_rejects_tiny_frames(ctx):
     from scanner_colmap_amd import ScmError
     with pytest.raises(ScmError):
-        ctx.extract_frames([np.zeros((20, 3201, 3), np.uint8)])
-    with pytest.raises(ScmError):
         ctx.extract_frames([np.zeros((15, 40, 3), np.uint8)])
+    with pytest.raises(ScmError):  # 15 rows become 14 after the max_image_size rescale
+        ctx.extract_frames([np.zeros((15, 3300, 3), np.uint8)])

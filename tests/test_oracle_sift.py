@@ -161,6 +161,51 @@ def test_rotation_covariance():
     assert hits > 0.6 * len(k0), (hits, len(k0))
 
 
-def test_oversize_frame_rejected():
-    with pytest.raises(ValueError):
-        oracle.sift_extract(np.zeros((10, 3201, 1), np.uint8))
+@pytest.mark.parametrize("w,h", [(3840, 2160), (3300, 2500), (3200, 3200), (20, 3201),
+                                 (5000, 3333), (100, 100), (3201, 3201)])
+def test_fit_size_is_resize_bitmap(w, h):
+    # extraction_op.cc:28-39: scale = 3200 / max(w, h), sizes truncated (C double arithmetic)
+    if w > 3200 or h > 3200:
+        s = 3200.0 / max(w, h)
+        want = (int(w * s), int(h * s))
+    else:
+        want = (w, h)
+    assert oracle.sift_fit_size(w, h) == want
+
+
+def test_rescale_known_answers():
+    rng = np.random.default_rng(11)
+    # constant image, and identity size
+    assert (oracle.sift_rescale(np.full((30, 50), 77, np.uint8), 37, 21) == 77).all()
+    g = rng.integers(0, 256, (33, 47), dtype=np.uint8)
+    assert (oracle.sift_rescale(g, 47, 33) == g).all()
+    # exact 2:1 minification: bilinear (width 1) stretched by 2 gives the taps
+    # 1/8, 3/8, 3/8, 1/8 on source pixels 2u-1 .. 2u+2 (exact in fp64)
+    row = rng.integers(0, 256, 64).astype(np.float64)
+    r = oracle.sift_rescale(np.repeat(row[None, :].astype(np.uint8), 6, 0), 32, 3)
+    want = [int(0.125 * row[2 * u - 1] + 0.375 * row[2 * u] + 0.375 * row[2 * u + 1]
+                + 0.125 * row[2 * u + 2] + 0.5) for u in range(1, 31)]
+    assert (r[:, 1:31] == np.array(want)).all()
+    col = rng.integers(0, 256, 64).astype(np.float64)
+    r = oracle.sift_rescale(np.repeat(col[:, None].astype(np.uint8), 6, 1), 3, 32)
+    want = [int(0.125 * col[2 * u - 1] + 0.375 * col[2 * u] + 0.375 * col[2 * u + 1]
+                + 0.125 * col[2 * u + 2] + 0.5) for u in range(1, 31)]
+    assert (r[1:31, :] == np.array(want)[:, None]).all()
+    # first pixel: the window is clipped at the border and renormalised by its
+    # total 7/8 (FreeImage divides each weight, then sums in source order)
+    v = 0.0
+    for wgt, c in zip((0.375 / 0.875, 0.375 / 0.875, 0.125 / 0.875), col[:3]):
+        v += wgt * c
+    assert r[0, 0] == int(v + 0.5)
+
+
+def test_oversize_frame_is_rescaled_before_extraction():
+    # resizeBitmap then extraction == extraction of the rescaled grey image
+    f = synthetic_frame(40, 3300, 21)
+    nw, nh = oracle.sift_fit_size(3300, 40)
+    small = oracle.sift_rescale(oracle.sift_grey(f), nw, nh)
+    got = oracle.sift_extract(f, 5)
+    assert got == oracle.sift_extract(small[:, :, None], 5)
+    assert np.frombuffer(got[2][16:32], np.uint64).tolist() == [nw, nh]  # camera: rescaled size
+    with pytest.raises(ValueError):  # below 16 rows after the rescale
+        oracle.sift_extract(np.zeros((15, 3300, 3), np.uint8))
