@@ -759,13 +759,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
   std::vector<int64_t> order;
   if (verify) {
     for (int64_t k = 0; k < P; ++k)
-      if (counts[k] >= std::max(1, ctx->opts.min_num_inliers)) {
-        if (counts[k] > kMaxVerifyMatches) {
-          set_error("more than 65535 matches in one pair (verifier index limit)");
-          return SCM_E_INVALID;
-        }
-        order.push_back(k);
-      }
+      if (counts[k] >= std::max(1, ctx->opts.min_num_inliers)) order.push_back(k);
     std::stable_sort(order.begin(), order.end(),
                      [&](int64_t x, int64_t y) { return counts[x] > counts[y]; });
   }
@@ -842,7 +836,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
                           DevBuf& cnts, DevBuf& ucnt, DevBuf& wsnap, DevBuf& act, DevBuf& nact,
                           bool split, VerifyRoundBufs* rb) -> int {
       SCM_TRY(rst.ensure(V * sizeof(RansacState)));
-      SCM_TRY(samp.ensure(V * kWindowTrials * 8 * sizeof(uint16_t)));
+      SCM_TRY(samp.ensure(V * kWindowTrials * 8 * sizeof(uint32_t)));
       SCM_TRY(nmod.ensure(V * kWindowTrials * sizeof(int32_t)));
       SCM_TRY(fcon.ensure(V * kWindowTrials * 3 * 12 * sizeof(float)));
       SCM_TRY(mods.ensure(V * kWindowTrials * 3 * 9 * sizeof(double)));
@@ -852,7 +846,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
       SCM_TRY(act.ensure(2 * V * sizeof(int32_t)));
       SCM_TRY(nact.ensure(2 * sizeof(int32_t)));
       rb->rst = rst.as<RansacState>();
-      rb->samp = samp.as<uint16_t>();
+      rb->samp = samp.as<uint32_t>();
       rb->nmod = nmod.as<int32_t>();
       rb->fcon = fcon.as<float>();
       rb->mods = mods.as<double>();
@@ -1110,7 +1104,7 @@ int64_t pair_workspace_bytes(int64_t n1, int64_t n2) {
   const int64_t verify_pts = slots * (16 + 16 + 16 + 8 + 1);  // xy1, xy2, xyf, dpack, dpmask
   const int64_t verify_pair = verify_scratch_doubles(slots) * 8 + kVerifySnapWords * 4 +
                               (int64_t)sizeof(RansacState) + (int64_t)sizeof(VerifyOut) +
-                              2 * ((int64_t)kWindowTrials * (8 * 2 + 4 + 3 * 12 * 4 + 3 * 9 * 8 + 2 * 3 * 4) +
+                              2 * ((int64_t)kWindowTrials * (8 * 4 + 4 + 3 * 12 * 4 + 3 * 9 * 8 + 2 * 3 * 4) +
                                    (int64_t)kMaxWindow * 640 * 4) + 256;  // F and H round buffers
   return match + verify_pts + verify_pair;
 }
@@ -1446,10 +1440,6 @@ int scm_verify_pair(scm_context* ctx, const float* kp1, int64_t n1, const float*
   if (!ctx || !tvg_out || n1 < 0 || n2 < 0 || num_matches < 0 ||
       (num_matches > 0 && (!matches || !kp1 || !kp2))) {
     set_error("invalid arguments");
-    return SCM_E_INVALID;
-  }
-  if (num_matches > kMaxVerifyMatches) {
-    set_error("more than 65535 matches in one pair");
     return SCM_E_INVALID;
   }
   for (int64_t i = 0; i < num_matches; ++i)

@@ -7,18 +7,17 @@ namespace scm {
 
 constexpr int kVerifyThreads = 64;    // one wavefront per pair
 constexpr int kTrialBatch = 64;       // hypotheses solved in parallel per round (one per lane)
-constexpr int kMaxVerifyMatches = 65535;  // uint16 sample indices in LDS
 constexpr int kVerifyModelDoubles = kTrialBatch * 27;  // per-pair model buffer
 // PRNG words per pair: for each of the two streams (F; H then watermark) the
 // handed-on mt19937 state (640) and the abort-rewind snapshot (640).
 constexpr int kVerifyStreamWords = 1280;
 constexpr int kVerifySnapWords = 2 * kVerifyStreamWords;
 // Per-pair scratch of one RANSAC kind (doubles): residuals / inlier gathers
-// (10 m), the model buffer, then the uint16 sample-index vector.  F and H run
+// (10 m), the model buffer, then the uint32 sample-index vector.  F and H run
 // concurrently, each in its own area (H's follows F's; the watermark RANSAC
 // reuses F's after both finished).
 __host__ __device__ inline int64_t verify_kind_scratch_doubles(int64_t m) {
-  return 10 * m + kVerifyModelDoubles + (m + 3) / 4 + 1;
+  return 10 * m + kVerifyModelDoubles + (m + 1) / 2 + 1;
 }
 inline int64_t verify_scratch_doubles(int64_t m) { return 2 * verify_kind_scratch_doubles(m); }
 
@@ -90,7 +89,7 @@ constexpr int kWindowTrials = kMaxWindow * kTrialBatch;
 // nact[2].
 struct VerifyRoundBufs {
   RansacState* rst;
-  uint16_t* samp;
+  uint32_t* samp;
   int32_t* nmod;
   float* fcon;
   double* mods;

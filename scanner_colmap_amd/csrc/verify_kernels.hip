@@ -39,7 +39,7 @@ template <> struct KindTraits<KIND_H> { static constexpr int kmin = 4, kmin_loca
 template <> struct KindTraits<KIND_T> { static constexpr int kmin = 1, kmin_local = 1, mm = 1, ms = 2, tb = kTrialBatch; };
 
 // Per-pair LDS (one wavefront); the sample-index vector of RandomSampler
-// (uint16, one per match) lives in the pair's global scratch so that the LDS
+// (uint32, one per match) lives in the pair's global scratch so that the LDS
 // footprint does not grow with the match count.
 struct __attribute__((aligned(16))) VerifyLds {
   // Head: everything the windowed kernels (rs_begin / rs_draw / rs_replay)
@@ -53,13 +53,13 @@ struct __attribute__((aligned(16))) VerifyLds {
   uint32_t mt[624];
   uint32_t counts[kTrialBatch * 3];
   int32_t nmodels[kTrialBatch];
-  uint16_t jbuf[kTrialBatch * 7];  // Shuffle targets of one batch of samples
+  uint32_t jbuf[kTrialBatch * 7];  // Shuffle targets of one batch of samples
   int32_t mt_idx;
   int32_t best_n;
   int32_t best_sum_valid;
   int32_t pad_;
   // Tail: the sequential LO-RANSAC of verify_final_kernel only (the watermark).
-  uint16_t samples[kTrialBatch][8];
+  uint32_t samples[kTrialBatch][8];
 };
 #ifndef SCM_REPLAY_ATTR
 #define SCM_REPLAY_ATTR
@@ -233,7 +233,7 @@ __device__ bool draw_targets_wave(VerifyLds& s, int D, uint32_t n) {
       const uint32_t range = n - i;
       const uint64_t prod = (uint64_t)outv[q] * (uint64_t)range;
       if ((uint32_t)prod < range) bad = true;
-      s.jbuf[r] = (uint16_t)(i + (uint32_t)(prod >> 32));
+      s.jbuf[r] = i + (uint32_t)(prod >> 32);
     }
   }
   const bool ok = __ballot(bad) == 0;
@@ -247,7 +247,7 @@ __device__ bool draw_targets_wave(VerifyLds& s, int D, uint32_t n) {
 // the kmin hot positions live in registers, cold targets are read from LDS
 // once per sample (several reads in flight) and written back in order.
 template <int KMIN>
-__device__ void shuffle_batch_lane0(VerifyLds& s, uint16_t* sidx, int B) {
+__device__ void shuffle_batch_lane0(VerifyLds& s, uint32_t* sidx, int B) {
   uint32_t R[KMIN];
 #pragma unroll
   for (int i = 0; i < KMIN; ++i) R[i] = sidx[i];
@@ -272,14 +272,14 @@ __device__ void shuffle_batch_lane0(VerifyLds& s, uint16_t* sidx, int B) {
 #pragma unroll
         for (int i2 = 0; i2 < i; ++i2) cur = (j[i2] == j[i]) ? w[i2] : cur;
         w[i] = R[i];
-        sidx[j[i]] = (uint16_t)R[i];
+        sidx[j[i]] = R[i];
         R[i] = cur;
       }
-      s.samples[b][i] = (uint16_t)R[i];
+      s.samples[b][i] = R[i];
     }
   }
 #pragma unroll
-  for (int i = 0; i < KMIN; ++i) sidx[i] = (uint16_t)R[i];
+  for (int i = 0; i < KMIN; ++i) sidx[i] = R[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -562,6 +562,36 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
     }
   }
   return cnt;
+}
+
+// Points not surely outside for two homographies at once over one chunk (the
+// split first pass): the two models' independent chains interleave, and the
+// loop overhead (constant loads, count selection) is paid once per pair.
+template <int PCH, bool FULL>
+__device__ __forceinline__ void score_h_notout2(const HFilt& fa, const HFilt& fb, const f32x2* s0,
+                                                const f32x2* s1, const f32x2* d0, const f32x2* d1,
+                                                int n, int base, int* ca, int* cb) {
+  const float Ma = fa.p8m.y, Mb = fb.p8m.y;
+  int na = 0, nb = 0;
+#pragma unroll
+  for (int q = 0; q < PCH / 2; ++q) {
+    if (!FULL && base + 128 * q >= n) continue;
+    const f32x2 da = h_filter_pair(fa, s0[q], s1[q], d0[q], d1[q]);
+    const f32x2 db = h_filter_pair(fb, s0[q], s1[q], d0[q], d1[q]);
+    uint64_t a0 = __ballot(da.x <= Ma), a1 = __ballot(da.y <= Ma);
+    uint64_t b0 = __ballot(db.x <= Mb), b1 = __ballot(db.y <= Mb);
+    if (!FULL) {
+      const uint64_t ok0 = slot_mask(n, base, 2 * q), ok1 = slot_mask(n, base, 2 * q + 1);
+      a0 &= ok0;
+      a1 &= ok1;
+      b0 &= ok0;
+      b1 &= ok1;
+    }
+    na += __popcll(a0) + __popcll(a1);
+    nb += __popcll(b0) + __popcll(b1);
+  }
+  *ca = na;
+  *cb = nb;
 }
 
 // ---------------------------------------------------------------------------
@@ -1191,7 +1221,7 @@ __device__ void ensure_best_sum(VerifyLds& s, const double* res_best, int n, dou
 // buffers (2n doubles each); snap: 625-word PRNG snapshot (global).  The
 // best model ends in s.best_model.
 template <int K>
-__device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& s, uint16_t* sidx, const double* xy1,
+__device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& s, uint32_t* sidx, const double* xy1,
                                       const double* xy2, int n, int max_trials,
                                       const VerifyParams P, double* res0, double* res1,
                                       double* xin1, double* xin2, uint32_t* snap,
@@ -1209,7 +1239,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
   }
   wsync();
   if (n < Tr::kmin) return out;
-  for (int i = lane; i < n; i += 64) sidx[i] = (uint16_t)i;
+  for (int i = lane; i < n; i += 64) sidx[i] = (uint32_t)i;
   double* res[2] = {res0, res1};
   int best_sel = 0;
   int dyn_max = max_trials;
@@ -1238,7 +1268,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
         for (int b = 0; b < B; ++b)
           for (int i = 0; i < Tr::kmin; ++i) {
             const uint32_t j = uniform_u32(s, (uint32_t)i, last);
-            const uint16_t t = sidx[i];
+            const uint32_t t = sidx[i];
             sidx[i] = sidx[j];
             sidx[j] = t;
             s.samples[b][i] = sidx[i];
@@ -1495,7 +1525,7 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
   pf.start();
   const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
   const int n = ps.n, lane = threadIdx.x;
-  uint16_t* sidx = reinterpret_cast<uint16_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
+  uint32_t* sidx = reinterpret_cast<uint32_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
   if (!(n >= P.min_num_inliers && n > 0)) return;
   const double* xy1 = xy1_all + ps.pp.pts_off;
   const double* xy2 = xy2_all + ps.pp.pts_off;
@@ -1606,8 +1636,8 @@ __device__ __forceinline__ PairSetup pair_at(const VerifyPair* pairs, int q, dou
   return ps;
 }
 
-__device__ __forceinline__ uint16_t* pair_sidx(const PairSetup& ps) {
-  return reinterpret_cast<uint16_t*>(ps.base + 10 * (int64_t)ps.n + kVerifyModelDoubles);
+__device__ __forceinline__ uint32_t* pair_sidx(const PairSetup& ps) {
+  return reinterpret_cast<uint32_t*>(ps.base + 10 * (int64_t)ps.n + kVerifyModelDoubles);
 }
 
 // Per-pair results of a finished RANSAC into the pair's VerifyOut (and, for
@@ -1668,8 +1698,8 @@ __device__ __attribute__((always_inline)) void rs_begin_body(
                              : pair_seed_h(P.base_seed, ps.pp.id1, ps.pp.id2));
     wsync();
     mt_save(s, ps.state);
-    uint16_t* sidx = pair_sidx(ps);
-    for (int i = lane; i < n; i += 64) sidx[i] = (uint16_t)i;
+    uint32_t* sidx = pair_sidx(ps);
+    for (int i = lane; i < n; i += 64) sidx[i] = (uint32_t)i;
     if (lane == 0) {
       RansacState& st = rst[q];
       st.n = n;
@@ -1703,7 +1733,7 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, RansacState* __restrict__ rst,
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
-    int32_t* __restrict__ nact_next, uint16_t* __restrict__ samp, uint32_t* __restrict__ cnts,
+    int32_t* __restrict__ nact_next, uint32_t* __restrict__ samp, uint32_t* __restrict__ cnts,
     uint32_t* __restrict__ ucnt, uint32_t* __restrict__ wsnap, int W, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
@@ -1718,7 +1748,7 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     const int Btot = min(kTrialBatch * W, rst[q].max_trials - rst[q].trial);
     wsync();
     mt_load(s, ps.state);
-    uint16_t* sq = samp + (int64_t)q * kWindowTrials * 8;
+    uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
     for (int w = 0; w * kTrialBatch < Btot; ++w) {
       const int B = min(kTrialBatch, Btot - w * kTrialBatch);
       uint32_t* snap = wsnap + ((int64_t)q * kMaxWindow + w) * 640;
@@ -1734,7 +1764,7 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
           s.mt_idx = (int32_t)snap[624];
           const uint32_t last = (uint32_t)(n - 1);
           for (int r = 0; r < B * Tr::kmin; ++r)
-            s.jbuf[r] = (uint16_t)uniform_u32(s, (uint32_t)(r % Tr::kmin), last);
+            s.jbuf[r] = uniform_u32(s, (uint32_t)(r % Tr::kmin), last);
         }
       }
       wsync();
@@ -1758,60 +1788,73 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
 // pairs' sample-index vectors are staged in LDS (SCM_SHUFFLE_LDS_KB per
 // block) so that every swap costs one LDS round trip.  The targets drawn by
 // rs_draw_kernel are read from samp and replaced by the trial's sample.
+// One pair's swap chain over Btot trials: the trial's kmin targets are read
+// from sq (next trial's in flight) and replaced by the trial's sample.  T:
+// uint16 for an LDS-staged vector, uint32 in global memory.
+template <int KM, typename T>
+__device__ __forceinline__ void shuffle_chain(T* sid, uint32_t* sq, int Btot) {
+  const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+  uint4 tn0 = Btot > 0 ? reinterpret_cast<const uint4*>(sq)[0] : z;
+  uint4 tn1 = Btot > 0 && KM > 4 ? reinterpret_cast<const uint4*>(sq)[1] : z;
+  for (int b = 0; b < Btot; ++b) {
+    const uint32_t wv[8] = {tn0.x, tn0.y, tn0.z, tn0.w, tn1.x, tn1.y, tn1.z, tn1.w};
+    if (b + 1 < Btot) {
+      tn0 = reinterpret_cast<const uint4*>(sq + (b + 1) * 8)[0];
+      if (KM > 4) tn1 = reinterpret_cast<const uint4*>(sq + (b + 1) * 8)[1];
+    }
+#pragma unroll
+    for (int i = 0; i < KM; ++i) {  // std::swap(sidx[i], sidx[j]), as the reference writes it
+      const uint32_t jj = wv[i];
+      const T ti = sid[i];
+      const T tj = sid[jj];
+      sid[i] = tj;
+      sid[jj] = ti;
+    }
+    uint4* o = reinterpret_cast<uint4*>(sq + b * 8);
+    o[0] = make_uint4(sid[0], sid[1], sid[2], sid[3]);
+    if (KM > 4) o[1] = make_uint4(sid[4], sid[5], sid[6], 0u);
+  }
+}
+
 template <int K>
 __device__ __attribute__((always_inline)) void rs_shuffle_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
     const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
-    const int32_t* __restrict__ nact, uint16_t* __restrict__ samp, int ppb, int stride, int bid, int nblk) {
+    const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, int ppb, int stride, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   uint16_t* lsidx = reinterpret_cast<uint16_t*>(dyn_lds);
   const int na = *nact;
   const int a0 = bid * ppb;
   if (a0 >= na) return;
   const int np = min(ppb, na - a0);
-  // Stage the sample-index vectors of this block's ppb pairs in LDS (every
-  // thread helps), run one pair's swap chain per lane, write them back.
-  for (int l = 0; l < np; ++l) {
-    const PairSetup pl = pair_at<K>(pairs, act[a0 + l], scratch, snaps, out);
-    const uint16_t* g = pair_sidx(pl);
-    for (int i = threadIdx.x; i < pl.n; i += 64) lsidx[l * stride + i] = g[i];
-  }
+  // Stage the sample-index vectors of this block's ppb pairs in LDS as uint16
+  // (every thread helps; batches whose pairs have at most 65536 matches), run
+  // one pair's swap chain per lane, write them back.  stride 0: larger pairs
+  // -- one pair per block, swapped in place in global memory (uint32).
+  const bool staged = stride > 0;
+  if (staged)
+    for (int l = 0; l < np; ++l) {
+      const PairSetup pl = pair_at<K>(pairs, act[a0 + l], scratch, snaps, out);
+      const uint32_t* g = pair_sidx(pl);
+      for (int i = threadIdx.x; i < pl.n; i += 64) lsidx[l * stride + i] = (uint16_t)g[i];
+    }
   __syncthreads();
   if ((int)threadIdx.x < np) {
-    // The swap chain as the reference writes it (std::swap of positions i and
-    // j of the persistent vector, i = 0..kmin-1), on LDS: one LDS round trip
-    // per swap, no register bookkeeping.
     constexpr int KM = KindTraits<K>::kmin;
     const int q = act[a0 + threadIdx.x];
-    uint16_t* sid = lsidx + threadIdx.x * stride;
-    uint16_t* sq = samp + (int64_t)q * kWindowTrials * 8;
+    uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
     const int Btot = rst[q].B;
-    uint4 tn = Btot > 0 ? *reinterpret_cast<const uint4*>(sq) : make_uint4(0u, 0u, 0u, 0u);
-    for (int b = 0; b < Btot; ++b) {
-      const uint4 tc = tn;
-      if (b + 1 < Btot) tn = *reinterpret_cast<const uint4*>(sq + (b + 1) * 8);
-      const uint32_t wv[4] = {tc.x, tc.y, tc.z, tc.w};
-#pragma unroll
-      for (int i = 0; i < KM; ++i) {
-        const uint32_t jj = (wv[i >> 1] >> (16 * (i & 1))) & 0xFFFFu;
-        const uint16_t ti = sid[i];
-        const uint16_t tj = sid[jj];
-        sid[i] = tj;
-        sid[jj] = ti;
-      }
-      uint32_t ow[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int i = 0; i < KM; ++i) ow[i >> 1] |= (uint32_t)sid[i] << (16 * (i & 1));
-      *reinterpret_cast<uint4*>(sq + b * 8) = make_uint4(ow[0], ow[1], ow[2], ow[3]);
-    }
+    if (staged) shuffle_chain<KM>(lsidx + threadIdx.x * stride, sq, Btot);
+    else shuffle_chain<KM>(pair_sidx(pair_at<K>(pairs, q, scratch, snaps, out)), sq, Btot);
   }
   __syncthreads();
-  for (int l = 0; l < np; ++l) {
-    const PairSetup pl = pair_at<K>(pairs, act[a0 + l], scratch, snaps, out);
-    uint16_t* g = pair_sidx(pl);
-    for (int i = threadIdx.x; i < pl.n; i += 64) g[i] = lsidx[l * stride + i];
-  }
+  if (staged)
+    for (int l = 0; l < np; ++l) {
+      const PairSetup pl = pair_at<K>(pairs, act[a0 + l], scratch, snaps, out);
+      uint32_t* g = pair_sidx(pl);
+      for (int i = threadIdx.x; i < pl.n; i += 64) g[i] = lsidx[l * stride + i];
+    }
 }
 
 
@@ -1822,7 +1865,7 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
     const double* __restrict__ xy2_all, const RansacState* __restrict__ rst,
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
-    const uint16_t* __restrict__ samp, int32_t* __restrict__ nmod, float* __restrict__ fcon,
+    const uint32_t* __restrict__ samp, int32_t* __restrict__ nmod, float* __restrict__ fcon,
     double* __restrict__ mods, int W, double maxr) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
@@ -1836,7 +1879,7 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
     const double S = rst[q].S;
     const double* xy1 = xy1_all + pp.pts_off;
     const double* xy2 = xy2_all + pp.pts_off;
-    const uint16_t* sq = samp + ((int64_t)q * kWindowTrials + h) * 8;
+    const uint32_t* sq = samp + ((int64_t)q * kWindowTrials + h) * 8;
     double a_[2 * 7], b_[2 * 7];
 #pragma unroll
     for (int i = 0; i < Tr::kmin; ++i) {
@@ -1867,6 +1910,10 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
 // the filter constants of one round at a time are broadcast from LDS and
 // lane t accumulates the count of hypothesis t of the round.
 constexpr int kScoreThreads = 64;
+#ifndef SCM_SCORE_H2
+#define SCM_SCORE_H2 1  // H split pass: two models per loop iteration
+#endif
+
 #ifndef SCM_SCORE_PCH
 #define SCM_SCORE_PCH 8
 #endif
@@ -1946,6 +1993,17 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
       int nslow = 0;
       uint32_t c0 = 0, c1 = 0, c2 = 0;  // lane t: counts of hypothesis t's models
       uint32_t u0 = 0, u1 = 0, u2 = 0;  // SPLIT: lane t: their undecided points
+      if (K == KIND_H && SPLIT && SCM_SCORE_H2) {
+        // H split pass: two models per iteration (every hypothesis has one model)
+        for (int t = 0; t < B; t += 2) {
+          const int t2 = t + 1 < B ? t + 1 : t;
+          const HFilt fa = h_filter_load(&lc[t][0]), fb = h_filter_load(&lc[t2][0]);
+          int ua, ub;
+          if (full) score_h_notout2<kScorePch, true>(fa, fb, x0, x1, y0, y1, n, base, &ua, &ub);
+          else score_h_notout2<kScorePch, false>(fa, fb, x0, x1, y0, y1, n, base, &ua, &ub);
+          u0 += (lane == t) ? (uint32_t)ua : ((lane == t + 1 && t2 != t) ? (uint32_t)ub : 0u);
+        }
+      } else
       for (int t = 0; t < B; ++t) {
         const int nmt = K == KIND_F ? __builtin_amdgcn_readfirstlane(lnm[t]) : 1;
         for (int k = 0; k < nmt; ++k) {
@@ -2477,10 +2535,18 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   // Shuffle blocks: as many pairs per block as fit SCM_SHUFFLE_LDS_KB of LDS sample-index
   // vectors (the swap chains are latency-bound; LDS instead of global memory
   // shortens every step of them).
-  const int sh_stride = (max_m + 7) / 8 * 8;
-  const int sh_ppb = std::max(1, std::min(64, (SCM_SHUFFLE_LDS_KB * 1024) / (2 * sh_stride)));
+  // (pairs above 65536 matches: vectors in global memory, stride 0, one pair per block)
+  const int sh_stride = max_m <= 65536 ? (max_m + 7) / 8 * 8 : 0;
+  const int sh_ppb =
+      sh_stride ? std::max(1, std::min(64, (SCM_SHUFFLE_LDS_KB * 1024) / (2 * sh_stride))) : 1;
   const int sh_blocks = (npairs + sh_ppb - 1) / sh_ppb;
-  int covered = 0, W = 1, r = 0;
+  // First window: one round per pair when the batch fills the GPU; a small
+  // batch (a single Scanner stencil) starts with wider windows -- its chain of
+  // windows is latency-bound, and the speculative rounds past an early stop
+  // cost idle CUs only (about 1024 pairs x rounds per window).
+  int W = 1;
+  while (W < kMaxWindow && (int64_t)npairs * 2 * W <= 1024) W *= 2;
+  int covered = 0, r = 0;
   while (covered < P.max_trials_F || covered < P.max_trials_H) {
     const int cur = r & 1;
     const bool f = covered < P.max_trials_F, h = covered < P.max_trials_H;

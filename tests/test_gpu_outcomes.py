@@ -68,3 +68,27 @@ def test_verify_option_variants(kw):
             kp1, kp2, mt = geometry_scene(kind, m, seed)
             got = ctx.verify_pair(kp1, kp2, mt, 3, 4)
             assert got == oracle.verify_pair(kp1, kp2, mt, 3, 4, o_ref), (kw, kind)
+
+
+def test_pair_with_more_than_65535_matches(gpu_ctx):
+    # 32-bit sample indices: a pair of 70,000 matches (images of 70,000
+    # keypoints) verifies like the oracle, through scm_verify_pair and through
+    # the table path (the LDS-staged shuffle falls back to global memory)
+    m = 70000
+    kp1, kp2, mt = geometry_scene("general", m, 15)
+    ref = oracle.verify_pair(kp1, kp2, mt, 3, 4)
+    assert decode_tvg(ref).config == 3 and len(decode_tvg(ref).inlier_matches) > 50000
+    assert gpu_ctx.verify_pair(kp1, kp2, mt, 3, 4) == ref
+    d1, d2 = descriptors_for_matches(mt, m, m, 15)
+    ids, kps, descs = table_rows([(3, kp1, d1), (4, kp2, d2)])
+    gpu_ctx.table_load(ids, kps, descs)
+    gpu_ctx.set_keep_matches(True)
+    got_ids, got_tvg = gpu_ctx.table_run(2, 0, 2)
+    got_m = gpu_ctx.table_matches(0, 1, cap=1 << 17)
+    gpu_ctx.set_keep_matches(False)
+    assert len(got_m) > 65535
+    # descriptors_for_matches crafts descriptors whose matches are exactly mt
+    # (oracle.match_pair_fast agrees at this size; a 20 GB dot matrix, not rerun here)
+    assert got_m.shape == mt.shape and (got_m == mt).all()
+    # the row's two_view_geometries element: size_t total, int count, then the TVG
+    assert got_tvg[0][12:] == oracle.verify_pair(kp1, kp2, got_m, 3, 4)
