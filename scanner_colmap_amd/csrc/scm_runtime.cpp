@@ -716,6 +716,12 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
                                       bs.colpart.as<uint2>(), clamp, sm));
     }
   SCM_HIP(hipEventRecord(bs.ev[1], sm));
+  // Finalize, the count read-back and (enqueue_verify) the verification run on
+  // the set's own stream, so the matcher of the next batch follows this one on
+  // the matching stream at once (the sets' buffers are disjoint; the set's
+  // stream is idle: its previous batch was collected before this one began).
+  hipStream_t sf = bs.vstream;
+  SCM_HIP(hipStreamWaitEvent(sf, bs.ev[1], 0));
   if (!given && !ctx->match_bf16 && !ctx->match_i8v1)
     SCM_HIP(launch_match_finalize_g8(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
                                      bs.colpart.as<uint2>(), bs.rowaux.as<uint2>(),
@@ -723,19 +729,19 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
                                      t.csum.as<int32_t>(), ctx->lut.as<float>(),
                                      (float)ctx->opts.max_ratio, (float)ctx->opts.max_distance,
                                      ctx->opts.cross_check, bs.matches.as<uint2>(),
-                                     bs.counts.as<int32_t>(), max_groups, sm));
+                                     bs.counts.as<int32_t>(), max_groups, sf));
   else if (!given)
     SCM_HIP(launch_match_finalize(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
                                   bs.colpart.as<uint2>(), bs.m21.as<int32_t>(),
                                   ctx->lut.as<float>(), (float)ctx->opts.max_ratio,
                                   (float)ctx->opts.max_distance, ctx->opts.cross_check,
                                   ctx->match_bf16 ? 0 : 1,
-                                  bs.matches.as<uint2>(), bs.counts.as<int32_t>(), sm));
-  SCM_HIP(hipEventRecord(bs.ev[2], sm));
+                                  bs.matches.as<uint2>(), bs.counts.as<int32_t>(), sf));
+  SCM_HIP(hipEventRecord(bs.ev[2], sf));
   uint8_t* outh = reinterpret_cast<uint8_t*>(bs.out.host);
   SCM_HIP(hipMemcpyAsync(outh + bs.off_counts, bs.counts.ptr, P * sizeof(int32_t),
-                         hipMemcpyDeviceToHost, sm));
-  SCM_HIP(hipEventRecord(bs.ev[3], sm));
+                         hipMemcpyDeviceToHost, sf));
+  SCM_HIP(hipEventRecord(bs.ev[3], sf));
   bs.pending = true;
   return SCM_OK;
 }
