@@ -40,11 +40,11 @@ def main():
                 if pat not in r["Kernel_Name"]:
                     continue
                 sums[r["Counter_Name"]] += float(r["Counter_Value"])
-                disp[r["Counter_Name"]].add(r["Dispatch_Id"])
+                disp[r["Counter_Name"]].add((d, r["Dispatch_Id"]))
         if not sums:
             continue
         per = {c: v / max(1, len(disp[c])) for c, v in sorted(sums.items())}
-        n = max(len(s) for s in disp.values())
+        n = max(len({i for _, i in s}) for s in disp.values())
         simd = per.get("GRBM_GUI_ACTIVE", 0.0) / 8 * 1024
         w = per.get("SQ_WAVE_CYCLES", 0.0)
         mf = per.get("SQ_INSTS_MFMA", 0.0)

@@ -1919,7 +1919,10 @@ constexpr int kScoreThreads = 64;
 #endif
 constexpr int kScorePch = SCM_SCORE_PCH;  // points per lane
 constexpr int kScoreChunk = kScoreThreads * kScorePch;
-constexpr int kScoreTargetItems = 65536;  // work items per score launch (8 per wave slot)
+#ifndef SCM_SCORE_ITEMS
+#define SCM_SCORE_ITEMS 65536  // 16K / 32K / 131K / 262K items: -1.5 to -6 % (profiles/r02_j_*vbench.log)
+#endif
+constexpr int kScoreTargetItems = SCM_SCORE_ITEMS;  // work items per score launch
 
 template <int K, bool SPLIT>
 __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
