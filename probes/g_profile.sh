@@ -1,13 +1,15 @@
 # GPU round profile set: GPU tests, plain bench, kernel-trace stats of the bench,
 # PMC passes of one bench step (HBM traffic, SQ instruction / busy counters).
-# usage (on the box): bash probes/g_profile.sh SET
+# usage (on the box): [SKIP_TESTS=1] bash probes/g_profile.sh SET
 set -e
 S=${1:-s}
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$S
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+if [ -z "$SKIP_TESTS" ]; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+fi
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench.log 2>&1
 cd /tmp && export TMPDIR=/tmp
 B="$R/bench.py --no-cpu-baseline --steps 1 --warmup 0 --gen-workers 1 --stencil-rows 0 --cpu-baseline-pairs 0"

@@ -564,34 +564,28 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
   return cnt;
 }
 
-// Points not surely outside for two homographies at once over one chunk (the
-// split first pass): the two models' independent chains interleave, and the
-// loop overhead (constant loads, count selection) is paid once per pair.
-template <int PCH, bool FULL>
-__device__ __forceinline__ void score_h_notout2(const HFilt& fa, const HFilt& fb, const f32x2* s0,
-                                                const f32x2* s1, const f32x2* d0, const f32x2* d1,
-                                                int n, int base, int* ca, int* cb) {
-  const float Ma = fa.p8m.y, Mb = fb.p8m.y;
-  int na = 0, nb = 0;
+// Points not surely outside for NM homographies at once over one chunk (the
+// split first pass): the models' independent chains interleave, and the loop
+// overhead (constant loads, count selection) is paid once per NM models.
+template <int PCH, bool FULL, int NM>
+__device__ __forceinline__ void score_h_notout_n(const HFilt* f, const f32x2* s0, const f32x2* s1,
+                                                 const f32x2* d0, const f32x2* d1, int n, int base,
+                                                 int* c) {
+#pragma unroll
+  for (int k = 0; k < NM; ++k) c[k] = 0;
 #pragma unroll
   for (int q = 0; q < PCH / 2; ++q) {
     if (!FULL && base + 128 * q >= n) continue;
-    const f32x2 da = h_filter_pair(fa, s0[q], s1[q], d0[q], d1[q]);
-    const f32x2 db = h_filter_pair(fb, s0[q], s1[q], d0[q], d1[q]);
-    uint64_t a0 = __ballot(da.x <= Ma), a1 = __ballot(da.y <= Ma);
-    uint64_t b0 = __ballot(db.x <= Mb), b1 = __ballot(db.y <= Mb);
-    if (!FULL) {
-      const uint64_t ok0 = slot_mask(n, base, 2 * q), ok1 = slot_mask(n, base, 2 * q + 1);
-      a0 &= ok0;
-      a1 &= ok1;
-      b0 &= ok0;
-      b1 &= ok1;
-    }
-    na += __popcll(a0) + __popcll(a1);
-    nb += __popcll(b0) + __popcll(b1);
+    f32x2 d[NM];
+#pragma unroll
+    for (int k = 0; k < NM; ++k) d[k] = h_filter_pair(f[k], s0[q], s1[q], d0[q], d1[q]);
+    const uint64_t ok0 = FULL ? ~0ull : slot_mask(n, base, 2 * q);
+    const uint64_t ok1 = FULL ? ~0ull : slot_mask(n, base, 2 * q + 1);
+#pragma unroll
+    for (int k = 0; k < NM; ++k)
+      c[k] += __popcll(__ballot(d[k].x <= f[k].p8m.y) & ok0) +
+              __popcll(__ballot(d[k].y <= f[k].p8m.y) & ok1);
   }
-  *ca = na;
-  *cb = nb;
 }
 
 // ---------------------------------------------------------------------------
@@ -1790,7 +1784,9 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
 // rs_draw_kernel are read from samp and replaced by the trial's sample.
 // One pair's swap chain over Btot trials: the trial's kmin targets are read
 // from sq (next trial's in flight) and replaced by the trial's sample.  T:
-// uint16 for an LDS-staged vector, uint32 in global memory.
+// uint16 for an LDS-staged vector, uint32 in global memory.  (Keeping the kmin
+// hot positions in registers with one batched read of the cold targets per
+// trial measured slower: divergent per-lane selects, profiles/r02_l.)
 template <int KM, typename T>
 __device__ __forceinline__ void shuffle_chain(T* sid, uint32_t* sq, int Btot) {
   const uint4 z = make_uint4(0u, 0u, 0u, 0u);
@@ -1910,8 +1906,8 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
 // the filter constants of one round at a time are broadcast from LDS and
 // lane t accumulates the count of hypothesis t of the round.
 constexpr int kScoreThreads = 64;
-#ifndef SCM_SCORE_H2
-#define SCM_SCORE_H2 1  // H split pass: two models per loop iteration
+#ifndef SCM_SCORE_HM
+#define SCM_SCORE_HM 4  // H split pass: models per loop iteration (1: the generic loop; 2, 3: -0.5 %)
 #endif
 
 #ifndef SCM_SCORE_PCH
@@ -1996,15 +1992,19 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
       int nslow = 0;
       uint32_t c0 = 0, c1 = 0, c2 = 0;  // lane t: counts of hypothesis t's models
       uint32_t u0 = 0, u1 = 0, u2 = 0;  // SPLIT: lane t: their undecided points
-      if (K == KIND_H && SPLIT && SCM_SCORE_H2) {
-        // H split pass: two models per iteration (every hypothesis has one model)
-        for (int t = 0; t < B; t += 2) {
-          const int t2 = t + 1 < B ? t + 1 : t;
-          const HFilt fa = h_filter_load(&lc[t][0]), fb = h_filter_load(&lc[t2][0]);
-          int ua, ub;
-          if (full) score_h_notout2<kScorePch, true>(fa, fb, x0, x1, y0, y1, n, base, &ua, &ub);
-          else score_h_notout2<kScorePch, false>(fa, fb, x0, x1, y0, y1, n, base, &ua, &ub);
-          u0 += (lane == t) ? (uint32_t)ua : ((lane == t + 1 && t2 != t) ? (uint32_t)ub : 0u);
+      if (K == KIND_H && SPLIT && SCM_SCORE_HM > 1) {
+        // H split pass: SCM_SCORE_HM models per iteration (one model per hypothesis)
+        constexpr int NM = SCM_SCORE_HM;
+        for (int t = 0; t < B; t += NM) {
+          HFilt f[NM];
+#pragma unroll
+          for (int k = 0; k < NM; ++k) f[k] = h_filter_load(&lc[min(t + k, B - 1)][0]);
+          int uc[NM];
+          if (full) score_h_notout_n<kScorePch, true, NM>(f, x0, x1, y0, y1, n, base, uc);
+          else score_h_notout_n<kScorePch, false, NM>(f, x0, x1, y0, y1, n, base, uc);
+#pragma unroll
+          for (int k = 0; k < NM; ++k)
+            if (t + k < B && lane == t + k) u0 += (uint32_t)uc[k];
         }
       } else
       for (int t = 0; t < B; ++t) {
