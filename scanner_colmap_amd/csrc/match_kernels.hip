@@ -1183,7 +1183,6 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     const float* __restrict__ lut, float max_ratio, float max_distance, int cross_check,
     uint2* __restrict__ matches, int32_t* __restrict__ counts, int phase) {
   __shared__ int32_t wave_tot[kFinThreads / 64];
-  __shared__ int32_t wave_off[kFinThreads / 64];
   __shared__ int32_t bcnt[32], bcur[32];
   const PairDesc pd = pairs[blockIdx.x];
   const int tid = threadIdx.x;
@@ -1195,8 +1194,6 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
   uint2* cp = colpart + pd.colpart_off;
   uint2* rr = rowres + pd.rowres_off;
   constexpr uint32_t kV = (1u << 19) - 1u;
-  const int per = (pd.n1 + kFinThreads - 1) / kFinThreads;
-  const int i0 = min(pd.n1, tid * per), i1 = min(pd.n1, i0 + per);
   if (phase == 0) {
   if (cross_check) {
     for (int j = tid; j < pd.n2; j += kFinThreads) {
@@ -1236,7 +1233,7 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     }
     __syncthreads();
   }
-  // Phase 2: per-row decisions, contiguous chunk per thread (phase 4 order).
+  // Phase 2: per-row decisions (rows strided over the threads, coalesced).
   // The rows' seconds are lower bounds (best of the other lanes, see
   // row_flush_best): a row that fails with it fails; a row that passes (and,
   // with the cross-check, can still be its column's match) is queued for the
@@ -1246,7 +1243,7 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
   uint2* ax = rowaux + pd.aux_off;
   if (tid < 32) bcnt[tid] = 0;
   __syncthreads();
-  for (int i = i0; i < i1; ++i) {
+  for (int i = tid; i < pd.n1; i += kFinThreads) {
     uint2 m = rr[i];
     int best_seg = 0;
     for (int sg = 1; sg < pd.nseg; ++sg) {
@@ -1281,34 +1278,39 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     rl[32] = acc;
   }
   __syncthreads();
-  for (int i = i0; i < i1; ++i) {
+  // (the order within a bucket is immaterial: every queued row is decided alone)
+  for (int i = tid; i < pd.n1; i += kFinThreads) {
     const uint2 st = rr[i];
     if (st.y == 3u) rl[33 + atomicAdd(&bcur[st.x & 31u], 1)] = i;
   }
   return;
   }
-  // Phase 4: ordered compaction.
-  int cnt = 0;
-  for (int i = i0; i < i1; ++i) cnt += rr[i].y == 1u;
-  int x = cnt;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const int y = __shfl_up(x, d);
-    if (lane >= d) x += y;
+  // Phase 4: ordered compaction (idx1 ascending), one tile of kFinThreads
+  // consecutive rows at a time: ballot prefixes within the waves, wave
+  // offsets through LDS, a running offset over the tiles.
+  int run = 0;
+  for (int t0 = 0; t0 < pd.n1; t0 += kFinThreads) {
+    const int i = t0 + tid;
+    const uint2 st = i < pd.n1 ? rr[i] : make_uint2(0u, 0u);
+    const bool f = st.y == 1u;
+    const uint64_t bm = __ballot(f);
+    if (lane == 0) wave_tot[wave] = __popcll(bm);
+    __syncthreads();
+    int off = run, tot = 0;
+    for (int w = 0; w < kFinThreads / 64; ++w) {
+      const int c = wave_tot[w];
+      off += w < wave ? c : 0;
+      tot += c;
+    }
+    if (f) {
+      const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+      matches[pd.match_off + off + pre] = make_uint2((uint32_t)i, st.x);
+    }
+    run += tot;
+    __syncthreads();  // wave_tot is rewritten by the next tile
   }
-  if (lane == 63) wave_tot[wave] = x;
-  __syncthreads();
-  if (tid == 0) {
-    int acc = 0;
-    for (int w = 0; w < kFinThreads / 64; ++w) { wave_off[w] = acc; acc += wave_tot[w]; }
-    counts[blockIdx.x] = acc;
-  }
-  __syncthreads();
-  int out = wave_off[wave] + x - cnt;
-  for (int i = i0; i < i1; ++i) {
-    const uint2 st = rr[i];
-    if (st.y == 1u) matches[pd.match_off + out++] = make_uint2((uint32_t)i, st.x);
-  }
+  if (tid == 0) counts[blockIdx.x] = run;
 }
 
 // Exact row seconds of the version-2 finalize (phase 2b).  The matcher keeps
