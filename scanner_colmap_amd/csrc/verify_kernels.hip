@@ -1856,6 +1856,9 @@ __device__ __attribute__((always_inline)) void rs_shuffle_body(
 
 // Minimal solvers, one thread per hypothesis of the window, plus the fp32
 // filter constants of every model.
+#ifndef SCM_SOLVE_GRID
+#define SCM_SOLVE_GRID 4096  // 1024 / 2048 / 3072: equal or slower (profiles/r02_m_solve_vbench.log)
+#endif
 template <int K>
 __global__ __launch_bounds__(64) void rs_solve_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
@@ -2561,11 +2564,11 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                        (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch, snaps,
                        out, rf, rh, cur, sh_ppb, sh_stride, s2);
     if (f)
-      hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(4096), dim3(64), 0, stream, pairs, xy1, xy2,
+      hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(SCM_SOLVE_GRID), dim3(64), 0, stream, pairs, xy1, xy2,
                          rf.rst, rf.act[cur], rf.nact + cur, rf.samp, rf.nmod, rf.fcon, rf.mods,
                          W, P.max_residual);
     if (h)
-      hipLaunchKernelGGL(rs_solve_kernel<KIND_H>, dim3(4096), dim3(64), 0, stream, pairs, xy1, xy2,
+      hipLaunchKernelGGL(rs_solve_kernel<KIND_H>, dim3(SCM_SOLVE_GRID), dim3(64), 0, stream, pairs, xy1, xy2,
                          rh.rst, rh.act[cur], rh.nact + cur, rh.samp, rh.nmod, rh.fcon, rh.mods,
                          W, P.max_residual);
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r], stream);
