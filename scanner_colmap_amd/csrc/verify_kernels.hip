@@ -2518,6 +2518,13 @@ size_t verify_lds_bytes(int max_m) {
 
 namespace {
 
+// Blocks of the wave-per-pair kernels (rs_begin / rs_draw / rs_replay) per
+// kind; pairs beyond it are taken in grid-stride order.
+#ifndef SCM_PAIR_GRID
+#define SCM_PAIR_GRID 4096  // 2048: -1 %, 16384 (a block per pair): +0.4 %, within noise (profiles/r02_o_pairgrid_vbench.log)
+#endif
+constexpr int kPairGrid = SCM_PAIR_GRID;
+
 template <typename F>
 void set_lds_attr(F f) {
   (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2534,7 +2541,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                        const VerifyRoundBufs& rh, int max_chunks, int max_m, uint64_t* prof,
                        hipStream_t stream, hipEvent_t* score_ev, int* nwin) {
   const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
-  const int gw = npairs < 4096 ? npairs : 4096;
+  const int gw = npairs < kPairGrid ? npairs : kPairGrid;
 #ifndef SCM_SHUFFLE_LDS_KB
 #define SCM_SHUFFLE_LDS_KB 16
 #endif
@@ -2636,7 +2643,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     attr = true;
   }
   const size_t lds = sizeof(VerifyLds);
-  const int gw = npairs < 4096 ? npairs : 4096;
+  const int gw = npairs < kPairGrid ? npairs : kPairGrid;
   const int max_chunks = (max_m + kScoreChunk - 1) / kScoreChunk;
   hipError_t err;
   // LORANSAC<7-pt, 8-pt> (F, then its inlier masks) and LORANSAC<H, H>, each
