@@ -1,9 +1,9 @@
-// Diagnostics (not product): host restatement of the scaled packed-fp32
+// Test helper (not product): host restatement of the scaled packed-fp32
 // homography filter (verify_kernels.hip: h_filter_consts / h_filter_pair) on
 // random homographies and points placed near the decision boundary; checks
 // that every decided point agrees with the fp64 reference residual and
 // reports the undecided fraction.
-// build: gcc -O2 -ffp-contract=off -o /tmp/hfc probes/hfilter_check.c -lm
+// build: gcc -O2 -ffp-contract=off -o hfc tests/hfilter_check.c -lm (tests/test_filter_bounds.py)
 #include <math.h>
 #include <stdint.h>
 #include <stdio.h>
