@@ -1,11 +1,15 @@
-"""The margin of the packed-fp32 homography inlier filter (verify_kernels.hip
-h_filter_consts / h_filter_pair) against the reference's fp64
-transfer residual (HomographyMatrixEstimator::Residuals), on a host
-restatement of the filter's fp32 FMA sequence (tests/hfilter_check.c):
-random homographies of arbitrary scale, destinations placed within 1e-7 and
-1e-3 (relative) of the threshold and uniformly around it.  Every point the
-filter decides must agree with the fp64 test; the undecided share on uniform
-radii must stay small (it only costs exact tests)."""
+"""The margins of the packed-fp32 inlier filters of the scoring kernels
+(verify_kernels.hip) against the reference's fp64 residuals,
+on host restatements of the filters' fp32 FMA sequences:
+  * homography (h_filter_consts / h_filter_pair) vs the transfer error of
+    HomographyMatrixEstimator::Residuals (tests/hfilter_check.c): random
+    homographies of arbitrary scale, destinations within 1e-7 and 1e-3
+    (relative) of the threshold and uniformly around it;
+  * Sampson (f_filter_consts / f_filter_pair) vs ComputeSquaredSampsonError
+    (tests/ffilter_check.c): random F = [t]x M of arbitrary scale, second
+    points placed along the epipolar line's normal at the same distances.
+Every point a filter decides must agree with the fp64 test; the undecided
+share on uniform residuals must stay small (it only costs exact tests)."""
 import os
 import re
 import subprocess
@@ -16,17 +20,22 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 @pytest.fixture(scope="module")
-def hfc(tmp_path_factory):
-    exe = str(tmp_path_factory.mktemp("hfc") / "hfc")
-    subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", exe,
-                    os.path.join(HERE, "hfilter_check.c"), "-lm"], check=True)
-    return exe
+def checkers(tmp_path_factory):
+    d = tmp_path_factory.mktemp("filters")
+    out = {}
+    for kind in ("h", "f"):
+        exe = str(d / f"{kind}fc")
+        subprocess.run(["gcc", "-O2", "-ffp-contract=off", "-o", exe,
+                        os.path.join(HERE, f"{kind}filter_check.c"), "-lm"], check=True)
+        out[kind] = exe
+    return out
 
 
+@pytest.mark.parametrize("kind", ["h", "f"])
 @pytest.mark.parametrize("maxr", ["16", "9", "2.5", "1"])
 @pytest.mark.parametrize("uniform", [False, True])
-def test_h_filter_margin_never_misdecides(hfc, maxr, uniform):
-    args = [hfc, maxr] + (["u"] if uniform else [])
+def test_filter_margin_never_misdecides(checkers, kind, maxr, uniform):
+    args = [checkers[kind], maxr] + (["u"] if uniform else [])
     r = subprocess.run(args, capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     m = re.search(r"undecided=(\d+) \(([\d.]+)%.*wrong=(\d+)", r.stdout)
