@@ -2598,7 +2598,9 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       }
     }
     if (h) {
-      if (rh.ucnt) {
+      // The first window starts from best 0, where every model would need the
+      // exact recount: it takes the one-pass kernel (exact tests inline).
+      if (rh.ucnt && r > 0) {
         hipLaunchKernelGGL((rs_score_kernel<KIND_H, true>), dim3(8192), dim3(kScoreThreads), 0,
                            stream, pairs, xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon,
                            rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, prof);
