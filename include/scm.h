@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SCM_ABI_VERSION 3
+#define SCM_ABI_VERSION 4
 
 enum {
   SCM_OK = 0,
@@ -167,9 +167,13 @@ int scm_execute_stencil(scm_context* ctx, int64_t stencil_size,
  * byte-identical to scm_execute_stencil on that stencil alone.  The
  * reference's execute() reads only batch element 0 (:106-108) and emits one
  * row; this entry point handles every element.  Images stay resident in HBM
- * from one call to the next (keyed by image id; an id whose feature counts
- * changed is uploaded again), so consecutive stencils upload only their new
- * images, and all pairs of the call run through the pipelined batch path. */
+ * from one call to the next, so consecutive stencils upload only their new
+ * images, and all pairs of the call run through the pipelined batch path.
+ * Images are identified by content (id, feature counts and 64-bit hashes of
+ * the keypoint and descriptor bytes), never by id alone: PrepareImage ids
+ * are per-instance counters (prepare_image.cc:11-20), so one id may name two
+ * images, and every element is matched with its own bytes as the reference
+ * decodes them (sequential_matching.cc:115-122). */
 int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
                       const scm_element* image_ids,
                       const scm_element* keypoints,
@@ -177,6 +181,11 @@ int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
                       scm_blob* pair_image_ids_out, scm_blob* tvgs_out);
 /* Images the execute() cache reused / uploaded so far (cumulative). */
 int scm_stencil_stats(scm_context* ctx, int64_t* reused, int64_t* uploaded);
+/* Drops the execute() image cache (Scanner Kernel::reset(), called when a
+ * kernel instance starts on a new stream of rows): the next call uploads
+ * every image it needs.  Never needed for correctness -- the cache is keyed
+ * by image content -- it returns the cache's HBM. */
+int scm_stencil_cache_clear(scm_context* ctx);
 
 /* ---- table granularity (HBM-resident batch path) ---------------------- */
 /* Decode and upload num_rows rows of the `extraction` table (columns

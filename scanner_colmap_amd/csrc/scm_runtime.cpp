@@ -68,6 +68,67 @@ struct PairSpec {
   int32_t a, b;  // image indices in the table
 };
 
+// Identity of one execute() image: the reference decodes every stencil
+// element's own bytes (sequential_matching.cc:115-122) and its image ids come
+// from PrepareImage's per-instance counter starting at 0 (prepare_image.cc:
+// 11-20), so an id alone does not name an image.  Two elements are the same
+// image when id, feature counts and 64-bit hashes of the keypoint and
+// descriptor bytes all agree.
+struct ImageKey {
+  uint32_t id = 0;
+  int64_t nkp = 0, ndesc = 0;
+  uint64_t hkp = 0, hdesc = 0;
+  bool operator==(const ImageKey& o) const {
+    return id == o.id && nkp == o.nkp && ndesc == o.ndesc && hkp == o.hkp && hdesc == o.hdesc;
+  }
+};
+struct ImageKeyHash {
+  size_t operator()(const ImageKey& k) const {
+    return (size_t)(k.hdesc ^ (k.hkp * 0x9E3779B97F4A7C15ULL) ^ ((uint64_t)k.id << 17));
+  }
+};
+
+// 64-bit content hash (the xxHash64 construction: four independent
+// multiply-rotate lanes over 32-byte stripes, then a tail and an avalanche).
+inline uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+uint64_t hash_bytes(const uint8_t* p, size_t n, uint64_t seed) {
+  constexpr uint64_t P1 = 0x9E3779B185EBCA87ULL, P2 = 0xC2B2AE3D27D4EB4FULL,
+                     P3 = 0x165667B19E3779F9ULL, P4 = 0x85EBCA77C2B2AE63ULL,
+                     P5 = 0x27D4EB2F165667C5ULL;
+  auto round = [](uint64_t acc, uint64_t w) { return rotl64(acc + w * P2, 31) * P1; };
+  auto load = [](const uint8_t* q) {
+    uint64_t w;
+    std::memcpy(&w, q, 8);
+    return w;
+  };
+  const uint8_t* const end = p + n;
+  uint64_t h;
+  if (n >= 32) {
+    uint64_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+    const uint8_t* const lim = end - 32;
+    do {
+      v1 = round(v1, load(p));
+      v2 = round(v2, load(p + 8));
+      v3 = round(v3, load(p + 16));
+      v4 = round(v4, load(p + 24));
+      p += 32;
+    } while (p <= lim);
+    h = rotl64(v1, 1) + rotl64(v2, 7) + rotl64(v3, 12) + rotl64(v4, 18);
+    for (uint64_t v : {v1, v2, v3, v4}) h = (h ^ round(0, v)) * P1 + P4;
+  } else {
+    h = seed + P5;
+  }
+  h += (uint64_t)n;
+  for (; p + 8 <= end; p += 8) h = rotl64(h ^ round(0, load(p)), 27) * P1 + P4;
+  for (; p < end; ++p) h = rotl64(h ^ ((uint64_t)*p * P5), 11) * P1;
+  h ^= h >> 33;
+  h *= P2;
+  h ^= h >> 29;
+  h *= P3;
+  h ^= h >> 32;
+  return h;
+}
+
 // Pinned host result buffer: the DMA target of each batch's results.
 struct PinnedOut {
   void* host = nullptr;
@@ -161,10 +222,11 @@ struct scm_context {
   ImageTable table, scratch_table;
   bool table_loaded = false;
   // execute() image cache: the images of the previous call stay in HBM
-  // (call_tab[call_cur], id -> table index in call_map); the next call's
-  // table reuses them by device-to-device copy and uploads only new images.
+  // (call_tab[call_cur], image key -> table index in call_map); the next
+  // call's table reuses them by device-to-device copy and uploads only new
+  // images.  Keyed by content (ImageKey), never by id alone.
   ImageTable call_tab[2];
-  std::unordered_map<uint32_t, int32_t> call_map[2];
+  std::unordered_map<ImageKey, int32_t, ImageKeyHash> call_map[2];
   int call_cur = -1;
   int64_t call_reused = 0, call_uploaded = 0;  // images, cumulative (scm_stencil_stats)
   BatchSet sets[3];
@@ -304,19 +366,79 @@ int upload_table(scm_context* ctx, ImageTable* t, const std::vector<RowView>& ro
   return SCM_OK;
 }
 
-// Table of one execute() call over the call's unique images `rows`:
-// images already resident in the previous call's table (same id and feature
-// counts) are copied device-to-device, the rest are staged, uploaded and
+// Content keys of a call's elements.  Elements that share their buffers
+// (Scanner hands consecutive stencils the same element buffers) are hashed
+// once; distinct buffers are hashed on the context's host threads.
+void hash_elements(scm_context* ctx, const std::vector<RowView>& rows, std::vector<ImageKey>* keys) {
+  const int64_t n = (int64_t)rows.size();
+  keys->assign(n, ImageKey());
+  struct Src {
+    const float* kp;
+    int64_t nkp;
+    const uint8_t* desc;
+    int64_t ndesc;
+    bool operator==(const Src& o) const {
+      return kp == o.kp && nkp == o.nkp && desc == o.desc && ndesc == o.ndesc;
+    }
+  };
+  struct SrcHash {
+    size_t operator()(const Src& s) const {
+      return std::hash<const void*>()(s.desc) ^ (std::hash<const void*>()(s.kp) * 31) ^
+             (size_t)(s.nkp * 0x9E3779B97F4A7C15ULL) ^ (size_t)s.ndesc;
+    }
+  };
+  std::unordered_map<Src, int64_t, SrcHash> first;  // buffers -> first element
+  std::vector<int64_t> of(n), todo;
+  size_t bytes = 0;
+  for (int64_t e = 0; e < n; ++e) {
+    const RowView& r = rows[e];
+    auto it = first.emplace(Src{r.kp, r.nkp, r.desc, r.ndesc}, e).first;
+    of[e] = it->second;
+    if (it->second == e) {
+      todo.push_back(e);
+      bytes += (size_t)r.nkp * 24 + (size_t)r.ndesc * 128;
+    }
+  }
+  auto work = [&](int64_t i) {
+    const RowView& r = rows[todo[i]];
+    ImageKey& k = (*keys)[todo[i]];
+    k.nkp = r.nkp;
+    k.ndesc = r.ndesc;
+    k.hkp = hash_bytes(reinterpret_cast<const uint8_t*>(r.kp), (size_t)r.nkp * 24, 0x6B70ULL);
+    k.hdesc = hash_bytes(r.desc, (size_t)r.ndesc * 128, 0x64657363ULL);
+  };
+  const int64_t nt = (int64_t)todo.size();
+  const int T = (int)std::min<int64_t>(ctx->threads, nt);
+  if (T <= 1 || bytes < ((size_t)4 << 20)) {
+    for (int64_t i = 0; i < nt; ++i) work(i);
+  } else {
+    std::vector<std::thread> ts;
+    for (int t = 0; t < T; ++t)
+      ts.emplace_back([&, t] {
+        for (int64_t i = t; i < nt; i += T) work(i);
+      });
+    for (auto& th : ts) th.join();
+  }
+  for (int64_t e = 0; e < n; ++e) {
+    (*keys)[e] = (*keys)[of[e]];
+    (*keys)[e].id = rows[e].id;
+  }
+}
+
+// Table of one execute() call over the call's unique images `rows` (content
+// keys `keys`): images already resident in the previous call's table (same
+// ImageKey) are copied device-to-device, the rest are staged, uploaded and
 // converted in one tail range.  Layout: reused images first (in their old
 // order, so consecutive ones coalesce into single copies), then new ones.
 // (*idx)[i] = table index of rows[i].
-int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows, std::vector<int32_t>* idx) {
+int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows,
+                      const std::vector<ImageKey>& keys, std::vector<int32_t>* idx) {
   const int nxt = ctx->call_cur < 0 ? 0 : 1 - ctx->call_cur;
   const ImageTable* old = ctx->call_cur < 0 ? nullptr : &ctx->call_tab[ctx->call_cur];
-  const std::unordered_map<uint32_t, int32_t>* omap =
+  const std::unordered_map<ImageKey, int32_t, ImageKeyHash>* omap =
       ctx->call_cur < 0 ? nullptr : &ctx->call_map[ctx->call_cur];
   ImageTable* t = &ctx->call_tab[nxt];
-  std::unordered_map<uint32_t, int32_t>& nmap = ctx->call_map[nxt];
+  std::unordered_map<ImageKey, int32_t, ImageKeyHash>& nmap = ctx->call_map[nxt];
   nmap.clear();
   const int64_t n = (int64_t)rows.size();
   std::vector<int32_t> from(n, -1);  // old table index, or -1 (upload)
@@ -328,9 +450,8 @@ int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows, std::v
       return SCM_E_INVALID;
     }
     if (omap) {
-      auto it = omap->find(r.id);
-      if (it != omap->end() && old->nkp[it->second] == r.nkp && old->ndesc[it->second] == r.ndesc)
-        from[i] = it->second;
+      auto it = omap->find(keys[i]);
+      if (it != omap->end()) from[i] = it->second;
     }
     (from[i] >= 0 ? reuse : fresh).push_back(i);
   }
@@ -355,7 +476,7 @@ int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows, std::v
       tail_kp = total_kp;
     }
     (*idx)[i] = (int32_t)k;
-    nmap[r.id] = (int32_t)k;
+    nmap[keys[i]] = (int32_t)k;
     t->ids[k] = r.id;
     t->nkp[k] = (int32_t)r.nkp;
     t->ndesc[k] = (int32_t)r.ndesc;
@@ -1489,24 +1610,27 @@ int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
   const int64_t ne = batch * stencil_size;
   std::vector<RowView> rows;
   SCM_TRY(decode_rows(ne, image_ids, keypoints, descriptors, &rows));
-  // Unique images of the call (by id: the `extraction` table's image_id is
-  // its key); an id that arrives with different feature counts is an error.
-  std::unordered_map<uint32_t, int32_t> uid;
+  // Unique images of the call, by content (ImageKey): every element is
+  // matched with its own bytes, as the reference decodes each stencil
+  // element (sequential_matching.cc:115-122); an id that reappears with other
+  // bytes is simply another image.
+  std::vector<ImageKey> ekey;
+  hash_elements(ctx, rows, &ekey);
+  std::unordered_map<ImageKey, int32_t, ImageKeyHash> uid;
   std::vector<RowView> uniq;
+  std::vector<ImageKey> ukeys;
   std::vector<int32_t> elem_u(ne);
   for (int64_t e = 0; e < ne; ++e) {
-    auto it = uid.find(rows[e].id);
+    auto it = uid.find(ekey[e]);
     if (it == uid.end()) {
-      it = uid.emplace(rows[e].id, (int32_t)uniq.size()).first;
+      it = uid.emplace(ekey[e], (int32_t)uniq.size()).first;
       uniq.push_back(rows[e]);
-    } else if (uniq[it->second].nkp != rows[e].nkp || uniq[it->second].ndesc != rows[e].ndesc) {
-      set_error("image id " + std::to_string(rows[e].id) + " arrives with different features");
-      return SCM_E_INVALID;
+      ukeys.push_back(ekey[e]);
     }
     elem_u[e] = it->second;
   }
   std::vector<int32_t> uidx;
-  int rc = upload_call_table(ctx, uniq, &uidx);
+  int rc = upload_call_table(ctx, uniq, ukeys, &uidx);
   if (rc != SCM_OK) {
     ctx->call_cur = -1;  // the cache may be half written
     drain(ctx);
@@ -1573,6 +1697,21 @@ int scm_stencil_stats(scm_context* ctx, int64_t* reused, int64_t* uploaded) {
   }
   *reused = ctx->call_reused;
   *uploaded = ctx->call_uploaded;
+  return SCM_OK;
+}
+
+int scm_stencil_cache_clear(scm_context* ctx) {
+  if (!ctx) {
+    set_error("null context");
+    return SCM_E_INVALID;
+  }
+  SCM_HIP(hipSetDevice(ctx->device));
+  drain(ctx);
+  ctx->call_cur = -1;
+  for (int i = 0; i < 2; ++i) {
+    ctx->call_tab[i].release();
+    ctx->call_map[i].clear();
+  }
   return SCM_OK;
 }
 

@@ -45,6 +45,10 @@ class SequentialMatchingGPUKernel : public scanner::StenciledBatchedKernel,
 
   ~SequentialMatchingGPUKernel() override { scm_context_destroy(ctx_); }
 
+  // A new run of rows: drop the HBM image cache.  The cache is keyed by image
+  // content, so this only returns its memory; outputs never depend on it.
+  void reset() override { scm_check(scm_stencil_cache_clear(ctx_), "scm_stencil_cache_clear"); }
+
   // Reference execute (sequential_matching.cc:103-185): column c, batch
   // element b, stencil offset s -> input_cols[c][b][s].  The reference reads
   // only b = 0 and emits one row (:106-108); every element of the batch is

@@ -18,6 +18,8 @@ class StenciledBatchedKernel {
   virtual ~StenciledBatchedKernel() = default;
   virtual void execute(const StenciledBatchedElements& input_cols,
                        BatchedElements& output_cols) = 0;
+  // Scanner calls reset() when an instance starts on a new run of rows.
+  virtual void reset() {}
 
  protected:
   KernelConfig config_;

@@ -71,14 +71,60 @@ def test_execute_stencil_repeated_ids_and_table_interleave():
         assert (a, b) == oracle.execute_stencil(*st2)
 
 
-def test_execute_batch_rejects_conflicting_images():
-    ids, kps, descs = table_rows(Corridor(3, 300, 3, seed=64).images())
-    other = table_rows(Corridor(3, 200, 3, seed=65).images())
+def _variant(kp, desc, seed, what):
+    """Same id, same counts, other bytes: descriptors or keypoints changed."""
+    rng = np.random.default_rng(seed)
+    d = np.frombuffer(desc, np.uint8).copy()
+    k = np.frombuffer(kp, np.uint8).copy()
+    if what == "desc":
+        body = d[16:].reshape(-1, 128)
+        rows = rng.choice(len(body), size=max(1, len(body) // 3), replace=False)
+        body[rows] = body[rng.permutation(rows)][:, rng.permutation(128)]
+    else:
+        xy = k[8:].view(np.float32).reshape(-1, 6)
+        xy[:, :2] += rng.normal(0, 3.0, size=(len(xy), 2)).astype(np.float32)
+    return k.tobytes(), d.tobytes()
+
+
+@pytest.mark.parametrize("what", ["desc", "kp"])
+def test_execute_batch_id_collisions_per_element(what):
+    """PrepareImage ids are per-instance counters (prepare_image.cc:11-20), so
+    one id can name two images.  The reference matches every stencil element
+    with its own bytes (sequential_matching.cc:115-122) and dedups ids only
+    inside one stencil (:139-146): within a batch and across consecutive calls
+    (the HBM image cache) an id reused for other bytes -- equal or unequal
+    feature counts -- must give exactly the oracle's per-stencil rows."""
+    n, K = 6, 4
+    ids, kps, descs = table_rows(Corridor(n, 700, K, seed=66).images())
+    other = table_rows(Corridor(n, 520, K, seed=67).images())
+    kv, dv = _variant(kps[2], descs[2], 68, what)      # id 2, equal counts, other bytes
+    ku, du = other[1][3], other[2][3]                  # id 3, other counts
+    stencils = [
+        ([ids[0], ids[1], ids[2], ids[3]], [kps[0], kps[1], kps[2], kps[3]],
+         [descs[0], descs[1], descs[2], descs[3]]),
+        ([ids[1], ids[2], ids[3], ids[4]], [kps[1], kv, ku, kps[4]],
+         [descs[1], dv, du, descs[4]]),
+        # in-stencil duplicate id with other bytes: the first occurrence wins
+        ([ids[2], ids[3], ids[3], ids[5]], [kps[2], ku, kps[3], kps[5]],
+         [descs[2], du, descs[3], descs[5]]),
+        ([ids[2], ids[0], ids[3], ids[4]], [kv, kps[0], kps[3], kps[4]],
+         [dv, descs[0], descs[3], descs[4]]),
+    ]
+    ref = [oracle.execute_stencil(*st) for st in stencils]
     with Context(0) as ctx:
-        bad = [([ids[0], ids[1]], [kps[0], kps[1]], [descs[0], descs[1]]),
-               ([ids[1], ids[2]], [other[1][1], kps[2]], [other[2][1], descs[2]])]
-        with pytest.raises(ScmError):
-            ctx.execute_batch(bad)
-        # the context stays usable
-        a, b = ctx.execute_stencil(ids, kps, descs)
-        assert (a, b) == oracle.execute_stencil(ids, kps, descs)
+        # one batch holding every variant
+        a, b = ctx.execute_batch(stencils)
+        assert list(zip(a, b)) == ref
+        # consecutive single-stencil calls: the cache must never serve stale bytes
+        for st, r in zip(stencils + stencils[::-1], ref + ref[::-1]):
+            assert ctx.execute_stencil(*st) == r
+        # batches of two, then a cache reset, then the batch again
+        for j in range(0, len(stencils), 2):
+            a, b = ctx.execute_batch(stencils[j:j + 2])
+            assert list(zip(a, b)) == ref[j:j + 2]
+        ctx.stencil_cache_clear()
+        a, b = ctx.execute_batch(stencils)
+        assert list(zip(a, b)) == ref
+    # the variant really changes the outputs of the rows that use it
+    assert ref[1] != oracle.execute_stencil(*([x[:1] + [y] + x[2:] for x, y in
+                                               zip(stencils[1], (ids[2], kps[2], descs[2]))]))
