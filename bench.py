@@ -111,6 +111,37 @@ def sample_pairs(n_per_img: list, overlap: int, npairs: int) -> list:
     return out
 
 
+def late_pairs(n_per_img: list, overlap: int, row: int = 500, first: int = 12,
+               tail_rows: int = 4) -> list:
+    """Parity pairs past the first batch boundary (8,192 pairs = 431 rows of the
+    default workload): the first `first` pairs of pivot row `row`, and every
+    pair of the last `tail_rows` pivot rows that have pairs (the stencil
+    clamped at the table's end, the short last batch)."""
+    T = len(n_per_img)
+    out = []
+    if row < T - 1:
+        out += [(row, j) for j in range(row + 1, min(row + overlap, T))][:first]
+    for r in range(max(row + 1, T - 1 - tail_rows), T - 1):
+        out += [(r, j) for j in range(r + 1, min(r + overlap, T))]
+    return out
+
+
+def oracle_fast(imgs: dict, pairs: list) -> dict:
+    """The oracle's outputs for `pairs` with its BLAS-dot matcher
+    (oracle.match_pair_fast, pinned to the scalar matcher by
+    tests/test_oracle_match.py) and its LO-RANSAC; a thread per pair."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import oracle
+
+    def one(pr):
+        i, j = pr
+        m = oracle.match_pair_fast(imgs[i][2], imgs[j][2])
+        return pr, (m, oracle.verify_pair(imgs[i][1], imgs[j][1], m, imgs[i][0], imgs[j][0]))
+
+    with ThreadPoolExecutor(max_workers=max(1, cpu_threads()[0])) as ex:
+        return dict(ex.map(one, pairs))
+
+
 def cpu_baseline(imgs: dict, pairs: list) -> tuple[dict, dict]:
     """The CPU oracle (faithful restatement of the reference op's matcher +
     TwoViewGeometry, SURVEY.md §8d: scalar ColMajor-strided integer dot
@@ -310,7 +341,9 @@ def main():
     # Pairs the CPU baseline times and the parity check compares (rank 0, N = 1).
     check_pairs = (sample_pairs(n_per_img, overlap, args.cpu_baseline_pairs)
                    if world == 1 and args.cpu_baseline_pairs > 0 else [])
-    keep_rows = sorted({i for p in check_pairs for i in p})
+    # ... and pairs past the first batch boundary and at the table's end (parity only).
+    tail_pairs = late_pairs(n_per_img, overlap) if check_pairs else []
+    keep_rows = sorted({i for p in check_pairs + tail_pairs for i in p})
     sample_imgs = {i: imgs[i] for i in keep_rows}
     keep_hi = max([i for i, _ in check_pairs], default=-1) + 1
     del imgs
@@ -350,6 +383,8 @@ def main():
 
     if keep_hi > 0:  # raw matches of the parity rows are kept in every step (bounded copy)
         ctx.set_keep_matches_range(0, keep_hi)
+        for r in sorted({i for i, _ in tail_pairs}):
+            ctx.add_keep_matches_range(r, r + 1)
     last = {}
 
     def step():
@@ -425,7 +460,9 @@ def main():
                                                          sample_imgs[i][0], sample_imgs[j][0]))
             else:
                 cpu, ref = cpu_baseline(sample_imgs, check_pairs)
-            parity = parity_check(ctx, last["packed"], lr_b, ref, check_pairs)
+            ref.update(oracle_fast(sample_imgs, tail_pairs))
+            parity = parity_check(ctx, last["packed"], lr_b, ref, check_pairs + tail_pairs)
+            parity["rows"] = sorted({i for i, _ in check_pairs + tail_pairs})
         # Isolated kernel rates: one extra untimed step with matching and verification
         # serialised (scm_set_serial; same bytes), so no stage shares the CUs.
         iso = None

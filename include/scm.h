@@ -218,6 +218,10 @@ int scm_set_keep_matches(scm_context* ctx, int32_t keep);
  * the bench keeps a few rows of its timed run for the parity check);
  * row_end == row_begin turns keeping off. */
 int scm_set_keep_matches_range(scm_context* ctx, int64_t row_begin, int64_t row_end);
+/* Also keep the pairs whose pivot row lies in [row_begin, row_end), beside the
+ * ranges already kept (the bench's parity sample: the first rows and rows
+ * past the first batch boundary and at the table's end). */
+int scm_add_keep_matches_range(scm_context* ctx, int64_t row_begin, int64_t row_end);
 /* Raw cross-checked matches of the most recent scm_table_run for the pair
  * (row, row + offset), offset in [1, overlap); the debug `matches` output the
  * bit-exact checks read.  Requires scm_set_keep_matches. */

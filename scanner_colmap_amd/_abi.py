@@ -36,7 +36,7 @@ EXPORTS = (
     "scm_stencil_cache_clear",
     "scm_table_load",
     "scm_table_run", "scm_table_run_packed", "scm_set_keep_matches",
-    "scm_set_keep_matches_range",
+    "scm_set_keep_matches_range", "scm_add_keep_matches_range",
     "scm_table_matches", "scm_table_timings", "scm_set_serial", "scm_extract_frames",
 )
 
@@ -122,6 +122,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                          POINTER(Blob), c_void_p]
     lib.scm_set_keep_matches.argtypes = [c_void_p, c_int32]
     lib.scm_set_keep_matches_range.argtypes = [c_void_p, c_int64, c_int64]
+    lib.scm_add_keep_matches_range.argtypes = [c_void_p, c_int64, c_int64]
     lib.scm_table_matches.argtypes = [c_void_p, c_int64, c_int64, c_void_p, c_int64,
                                       POINTER(c_int64)]
     lib.scm_table_timings.argtypes = [c_void_p, POINTER(c_double), c_int32]
@@ -353,6 +354,9 @@ class Context:
 
     def set_keep_matches_range(self, row_begin: int, row_end: int) -> None:
         _check(self._lib.scm_set_keep_matches_range(self._ptr, row_begin, row_end))
+
+    def add_keep_matches_range(self, row_begin: int, row_end: int) -> None:
+        _check(self._lib.scm_add_keep_matches_range(self._ptr, row_begin, row_end))
 
     def table_matches(self, row: int, offset: int, cap: int = 1 << 16) -> np.ndarray:
         out = np.zeros((max(1, cap), 2), dtype=np.uint32)

@@ -30,9 +30,10 @@
 //    below (64 lane-strided partial sums, then a fixed binary tree), so a
 //    64-lane wavefront reproduces them exactly;
 //  * RANSAC::ComputeNumTrials evaluates pow/log with basic operations
-//    (num_trials() below) instead of libm, so host and device agree; it can
-//    differ from a libm evaluation only when the trial count lies within a
-//    few ulp of an integer.
+//    (num_trials() below) instead of libm, so host and device agree; the
+//    power is rounded once (as std::pow), and the counts equal the libm
+//    formula's on every (inliers <= samples <= 16384) checked exhaustively
+//    (tests/test_num_trials.py).
 #pragma once
 
 #if defined(__HIPCC__)
@@ -101,18 +102,47 @@ SCM_HD inline double det_log(double x) {
   return ((double)e * ln2_lo + logm) + (double)e * ln2_hi;
 }
 
+// ratio^k rounded once: the power in double-double (Dekker products, exact
+// for the normal doubles ratio^k reaches here), so the result is the
+// correctly rounded value that std::pow returns (glibc's pow is correctly
+// rounded outside hard cases).  Repeated double multiplication is not: one ulp
+// of ratio^k moves 1 - ratio^k across a rounding boundary and, for small
+// ratios, the trial count by more than one (tests/num_trials_check.cc).
+SCM_HD inline void two_prod(double a, double b, double* p, double* e) {
+  *p = a * b;
+  const double c = 134217729.0;  // 2^27 + 1 (Dekker split)
+  double t = c * a;
+  const double ah = t - (t - a), al = a - ah;
+  t = c * b;
+  const double bh = t - (t - b), bl = b - bh;
+  *e = ((ah * bh - *p) + ah * bl + al * bh) + al * bl;
+}
+
+SCM_HD inline double pow_int_rounded(double x, int k) {
+  if (k <= 1) return k == 1 ? x : 1.0;
+  double h = x, l = 0.0;
+  for (int i = 1; i < k; ++i) {
+    double p, e;
+    two_prod(h, x, &p, &e);
+    e = e + l * x;
+    h = p + e;  // quick two-sum: |e| <= ulp(p)
+    l = e - (h - p);
+  }
+  return h;
+}
+
 // colmap::RANSAC::ComputeNumTrials [upstream optim/ransac.h] with
-// pow(ratio, kmin) as kmin - 1 ordered multiplications and det_log.  The
-// final static_cast<size_t> mirrors gcc/x86-64 for out-of-range values
-// (-inf -> 2^63, >= 2^64 -> 0).
+// pow(ratio, kmin) by pow_int_rounded and log by det_log.  The final
+// static_cast<size_t> mirrors gcc/x86-64 for out-of-range values
+// (-inf -> 2^63, >= 2^64 -> 0).  Equal to the libm formula on every
+// (inliers <= samples <= 16384) at kmin 1/4/7/8 and several confidences and
+// multipliers (tests/test_num_trials.py).
 SCM_HD inline uint64_t num_trials(uint64_t num_inliers, uint64_t num_samples,
                                   double confidence, double multiplier, int kmin) {
   const double inlier_ratio = (double)num_inliers / (double)num_samples;
   const double nom = 1.0 - confidence;
   if (nom <= 0.0) return ~0ull;
-  double p = inlier_ratio;
-  for (int k = 1; k < kmin; ++k) p = p * inlier_ratio;
-  const double denom = 1.0 - p;
+  const double denom = 1.0 - pow_int_rounded(inlier_ratio, kmin);
   if (denom <= 0.0) return 1;
   const double q = det_log(nom) / det_log(denom) * multiplier;
   // ceil without libm: integers >= 2^52 are already integral.

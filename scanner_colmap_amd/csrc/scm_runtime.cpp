@@ -249,7 +249,12 @@ struct scm_context {
   int64_t prof_pairs = 0;
   // raw matches of the last table run (scm_set_keep_matches)
   bool keep_matches = false;
-  int64_t keep_begin = 0, keep_end = INT64_MAX;  // rows whose matches are kept
+  std::vector<std::pair<int64_t, int64_t>> keep_ranges;  // rows whose matches are kept
+  bool kept(int64_t row) const {
+    for (const auto& r : keep_ranges)
+      if (row >= r.first && row < r.second) return true;
+    return false;
+  }
   int64_t last_begin = 0, last_end = 0;
   std::vector<std::vector<std::pair<int64_t, std::vector<Match>>>> last_matches;
   SiftState* sift = nullptr;  // SIFT extraction slots (scm_extract_frames), created on first use
@@ -1353,7 +1358,7 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
     if (keep)
       for (int64_t p = 0; p < v.P; ++p) {
         const int64_t row = b.specs[p].a, o = v.offsets[p];
-        if (row < ctx->keep_begin || row >= ctx->keep_end) continue;
+        if (!ctx->kept(row)) continue;
         ctx->last_matches[row - row_begin].push_back(
             {b.specs[p].b - row, std::vector<Match>(v.matches + o, v.matches + o + v.counts[p])});
       }
@@ -1833,8 +1838,7 @@ int scm_set_keep_matches(scm_context* ctx, int32_t keep) {
     return SCM_E_INVALID;
   }
   ctx->keep_matches = keep != 0;
-  ctx->keep_begin = 0;
-  ctx->keep_end = INT64_MAX;
+  ctx->keep_ranges.assign(1, {0, INT64_MAX});
   if (!keep) ctx->last_matches.clear();
   return SCM_OK;
 }
@@ -1845,9 +1849,21 @@ int scm_set_keep_matches_range(scm_context* ctx, int64_t row_begin, int64_t row_
     return SCM_E_INVALID;
   }
   ctx->keep_matches = row_end > row_begin;
-  ctx->keep_begin = row_begin;
-  ctx->keep_end = row_end;
+  ctx->keep_ranges.assign(1, {row_begin, row_end});
   if (!ctx->keep_matches) ctx->last_matches.clear();
+  return SCM_OK;
+}
+
+int scm_add_keep_matches_range(scm_context* ctx, int64_t row_begin, int64_t row_end) {
+  if (!ctx || row_begin < 0 || row_end < row_begin) {
+    set_error("invalid arguments");
+    return SCM_E_INVALID;
+  }
+  if (row_end > row_begin) {
+    if (!ctx->keep_matches) ctx->keep_ranges.clear();
+    ctx->keep_ranges.push_back({row_begin, row_end});
+    ctx->keep_matches = true;
+  }
   return SCM_OK;
 }
 
@@ -1861,8 +1877,7 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset, uint32_t* m
     set_error("call scm_set_keep_matches(ctx, 1) before scm_table_run");
     return SCM_E_STATE;
   }
-  if (row < ctx->last_begin || row >= ctx->last_end || row < ctx->keep_begin ||
-      row >= ctx->keep_end ||
+  if (row < ctx->last_begin || row >= ctx->last_end || !ctx->kept(row) ||
       ctx->last_matches.size() != (size_t)(ctx->last_end - ctx->last_begin)) {
     set_error("row outside the last scm_table_run");
     return SCM_E_INVALID;

@@ -76,9 +76,10 @@ def test_pair_8192_ragged_and_reversed(gpu_ctx):
 
 
 def test_gerrard_hall_shape_table():
-    """Configs 1/2 shape: 100 images, overlap 10 (855 pairs), every output row
+    """Configs 1/2 at the metric's size: 100 images x 8192 keypoints, overlap
+    10 (855 pairs, the bench's gerrard-hall-synth workload), every output row
     and every pair's raw matches bit-identical to the CPU op's."""
-    imgs = Corridor(100, 4096, 10, seed=20251).images()
+    imgs = Corridor(100, 8192, 10, seed=20251).images()
     with Context(0) as ctx:
         configs = _check_table(ctx, imgs, 10)
     assert len(configs) == 855
