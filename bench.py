@@ -441,9 +441,7 @@ def main():
         launches = max(1, launches)  # matcher launches the library reported
         avg_n = float(np.mean(n_per_img)) if n_per_img else 0.0
         bf16 = os.environ.get("SCM_MATCH_BF16", "0") == "1"  # else the default i8 matcher
-        kernel = ("match_tiles_kernel" if bf16 else
-                  "match_tiles_i8_kernel" if os.environ.get("SCM_MATCH_I8V1", "0") == "1"
-                  else "match_g8_kernel")
+        kernel = "match_tiles_kernel" if bf16 else "match_g8_kernel"
         peak = BF16_DENSE_PEAK_TFLOPS if bf16 else I8_DENSE_PEAK_TOPS
         # descriptors of both images, bf16 (2 B) or offset i8 (1 B) per element
         alg_bytes_launch = npairs * steps / launches * 2 * avg_n * 128 * (2 if bf16 else 1)

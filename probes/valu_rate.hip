@@ -17,6 +17,9 @@ constexpr int kIter = 2048;
 #define FMAF(d, a) asm volatile("v_fma_f32 %0, %1, %1, %0" : "+v"(d) : "v"(a))
 #define PKFMA(d, a) asm volatile("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(d) : "v"(a))
 #define FMA64(d, a) asm volatile("v_fma_f64 %0, %1, %1, %0" : "+v"(d) : "v"(a))
+#define LSHLADD64(d, a, s) asm volatile("v_lshl_add_u64 %0, %1, 8, %2" : "=v"(d) : "v"(a), "v"(s))
+#define LSHLADD32(d, a, s) asm volatile("v_lshl_add_u32 %0, %1, 8, %2" : "=v"(d) : "v"(a), "v"(s))
+#define MAX3U(d, a, b) asm volatile("v_max3_u32 %0, %1, %2, %0" : "+v"(d) : "v"(a), "v"(b))
 #define CMPF(a, b) asm volatile("v_cmp_le_f32 vcc, %0, %1" : : "v"(a), "v"(b) : "vcc")
 
 // MODE: 0 max, 1 med3, 2 lshl_or, 3 add, 4 mfma only, 5 mfma + NV valu (epilogue mix) per mfma,
@@ -63,6 +66,17 @@ __global__ __launch_bounds__(1024) void rate_kernel(uint32_t* out, long long* cy
     } else if (MODE == 10) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) CMPF(x[i], y);
+    } else if (MODE == 11) {
+      uint64_t* xq = reinterpret_cast<uint64_t*>(x);
+      const uint64_t kq = ((uint64_t)z << 32) | z;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { uint64_t t; LSHLADD64(t, xq[i], kq); xq[i] = t; }
+    } else if (MODE == 12) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) { uint32_t t; LSHLADD32(t, x[i], z); x[i] = t; }
+    } else if (MODE == 13) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) MAX3U(x[i], y, z);
     } else if (MODE == 4) {
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc0, 0, 0, 0);
     } else if (MODE == 5) {
@@ -123,6 +137,11 @@ void run(const char* name, int threads, double ops_per_iter) {
 }
 
 int main() {
+  for (int threads : {256, 512}) {
+    run<11, 0>("v_lshl_add_u64 x8", threads, 8);
+    run<12, 0>("v_lshl_add_u32 x16", threads, 16);
+    run<13, 0>("v_max3_u32 x16", threads, 16);
+  }
   for (int threads : {256, 512, 1024}) {
     run<7, 0>("v_fma_f32 x16", threads, 16);
     run<8, 0>("v_pk_fma_f32 x8", threads, 8);

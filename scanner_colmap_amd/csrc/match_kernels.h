@@ -54,9 +54,6 @@ struct PairDesc {
 hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int njobs,
                               const PairDesc* pairs, uint2* rowres, uint2* colpart,
                               bool clamp, hipStream_t stream);
-hipError_t launch_match_tiles_i8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
-                                 int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
-                                 bool clamp, hipStream_t stream);
 // Version-2 i8 matcher (LDS-DMA staging, best-only column partials) and its
 // finalize (exact recompute of the deciding column seconds).
 hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,

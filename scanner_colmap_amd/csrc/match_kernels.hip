@@ -9,10 +9,10 @@
 // ComputeSiftDistanceMatrix + FindBestMatchesOneWay x2 + FindBestMatches
 // (SURVEY.md §8a a5-a7).  The int32 N1 x N2 matrix is never materialised.
 //
-// Two matchers produce the same keys and partial results and share the
-// finalize kernel: match_tiles_i8_kernel (default: integer MFMA on offset
-// operands, see its section) and match_tiles_kernel (bf16 MFMA, selected by
-// SCM_MATCH_BF16=1).
+// Two matchers: match_g8_kernel (default: integer MFMA on offset operands,
+// see the i8 sections) with match_finalize_g8_kernel and its exact rechecks,
+// and match_tiles_kernel (bf16 MFMA, SCM_MATCH_BF16=1 or max_ratio > 1) with
+// match_finalize_kernel.
 //
 // Exactness (SURVEY.md §8a "Exactness facts"):
 //  * bf16: u8 descriptors are exact in bf16; each MFMA chain starts from an
@@ -132,22 +132,27 @@ __device__ __forceinline__ void row_flush(const uint32_t (&b1r)[2][16], const ui
   }
 }
 
-// Row flush of the v2 matcher (best-only row state): each lane holds, per
-// row, the best key over ITS columns only (column = lane + 32 t); re-keyed
-// with the column and reduced over the 32 lanes this gives the row's exact
-// best and, as second, the best of the OTHER lanes: a lower bound of the
-// row's second that misses only the second within the winning lane
-// (recomputed exactly by match_rowcheck_g8_kernel where it matters).
-__device__ __forceinline__ void row_flush_best(const uint32_t (&b1r)[2][16], uint2* rr, int row0,
-                                               int n1, int r, int h) {
+// Row flush of match_g8_kernel: each lane holds, per row, the best VALUE
+// (dot + 2^22) over ITS columns only (j = lane + 32 t); reduced over the 32
+// lanes of a half this gives the row's exact best with the lane of the best
+// (the column's residue mod 32; ties between lanes need no tie-break: the
+// second then equals the best and the row fails the ratio test) and, as
+// second, the best of the OTHER lanes: a lower bound of the row's second that
+// misses only the second within the winning lane.  The best column itself and
+// the exact second come from match_rowcheck_g8_kernel for the rows that can
+// still pass.  Stored as (dot << 13) | (kIdxMask - lane), (second << 13);
+// CLAMP: min(dot, 2^18) (acosf(min(d 2^-18, 1)) is 0 for every d >= 2^18).
+template <bool CLAMP>
+__device__ __forceinline__ void row_flush_values(const uint32_t (&b1r)[2][16], uint2* rr, int row0,
+                                                 int n1, int r, int h) {
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const uint32_t k1 = b1r[s][i];
-      const uint32_t tl = (uint32_t)(kTilesPerSeg - 1) - (k1 & 255u);
-      const uint32_t col = tl * 32u + (uint32_t)r;
-      uint32_t B1 = (k1 & ~kIdxMask) | (kIdxMask - col);
+      uint32_t v = k1 >= (1u << 22) ? k1 - (1u << 22) : 0u;
+      if (CLAMP) v = min(v, kLutMax);
+      uint32_t B1 = (v << kIdxBits) | (kIdxMask - (uint32_t)r);
       uint32_t B2 = 0u;
 #pragma unroll
       for (int x = 1; x < 32; x <<= 1) {
@@ -190,14 +195,6 @@ template <bool CLAMP>
 __device__ __forceinline__ uint2 subtile_epilogue(const f32x16& acc, uint32_t tbits,
                                                   uint32_t (&b1r)[16], uint32_t (&b2r)[16],
                                                   uint32_t row_base) {
-#ifdef SCM_DIAG_MATCH_SKELETON
-  // diagnostics only: MFMA + LDS + staging skeleton, results discarded
-  uint32_t x = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x ^= __float_as_uint(acc[i]);
-  b1r[0] ^= x;
-  return make_uint2(x, x);
-#endif
   uint32_t key[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) {
@@ -368,23 +365,6 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
 // t-bits), which is (dot << 13) | t-bits mod 2^32 (the 2^22 offset shifts out).
 // Per element: 1 (key) + 2 (row state) + ~1.3 (column tree) VALU ops.
 // ===========================================================================
-#ifndef SCM_DIAG_MERGE
-#define SCM_DIAG_MERGE 1  // diagnostics: 0 drops the column merge (wrong results)
-#endif
-// LDS ring: tile t + 3 is staged at the end of tile t and first read in tile
-// t + 2 (the B-fragment prefetch).  One barrier per kBarTiles tiles (2: 2-3 %
-// faster than 1): waves may then be two tiles apart, so the ring holds 6 tiles
-// and the column partials 4 buffers; every staging write still has a barrier
-// before its first read.  (4 would need staging further ahead: with t + 3 a
-// group of 4 leaves writes and reads of a tile without a barrier between.)
-#ifndef SCM_I8_BAR_TILES
-#define SCM_I8_BAR_TILES 2
-#endif
-constexpr int kBarTiles = SCM_I8_BAR_TILES;
-static_assert(kBarTiles == 1 || kBarTiles == 2, "barrier group");
-constexpr int kStages8 = kBarTiles == 1 ? 4 : 6;
-constexpr int kCscBufs = 2 * kBarTiles;
-constexpr int kAhead8 = 3;
 constexpr int kTiles8PerSeg = kTilesPerSeg / 2;  // 64-column tiles per 8192-column segment
 
 // Byte offset of 16-B chunk c (of 8) of column col in an i8 LDS tile.  The
@@ -433,261 +413,42 @@ __device__ __forceinline__ uint32_t merge_second_values(uint32_t b1a, uint32_t b
   return max(max(b2a, b2b), min(b1a, b1b));
 }
 
-// Column value partial of one 32-column sub-tile of a wave (both row
-// sub-tiles, both lane halves); lanes of half 0 store it for the workgroup merge.
-__device__ __forceinline__ void wave_col_partial_values(uint2 c0, uint2 c1, uint2* dst, int h, int r) {
-  uint32_t B1 = max(c0.x, c1.x), B2 = merge_second_values(c0.x, c0.y, c1.x, c1.y);
-  const uint32_t o1 = __shfl_xor(B1, 32);
-  const uint32_t o2 = __shfl_xor(B2, 32);
-  B2 = merge_second_values(B1, B2, o1, o2);
-  B1 = max(B1, o1);
-  if (h == 0) dst[r] = make_uint2(B1, B2);
-}
-
-// Row keys of a finished sub-tile and the row top-2 state update; returns the
-// column value partial.  kc = (cb_j << 13) | t-bits; cbm = cb_j - 2^22.
-template <bool CLAMP>
-__device__ __forceinline__ uint2 subtile_epilogue8(const i32x16& acc, uint32_t kc, uint32_t cbm,
-                                                   uint32_t tbits, uint32_t (&b1r)[16],
-                                                   uint32_t (&b2r)[16]) {
-#ifdef SCM_DIAG_MATCH_SKELETON
-  // diagnostics only: MFMA + LDS + staging skeleton, results discarded
-  uint32_t x = 0;
-#pragma unroll
-  for (int i = 0; i < 16; ++i) x ^= (uint32_t)acc[i];
-  b1r[0] ^= x;
-  return make_uint2(x, x);
-#endif
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const uint32_t x = (uint32_t)acc[i];
-    const uint32_t key = CLAMP ? (min(x + cbm, kLutMax) << 13) | tbits : (x << 13) + kc;
-    b2r[i] = med3_u32(key, b1r[i], b2r[i]);
-    b1r[i] = max(b1r[i], key);
-  }
-  return column_top2_values(acc);
-}
-
-// Merge of the kMatch8Waves wave partials of tile k's 64 columns (one wave;
-// lane = column 32 h + r) and store of the columns' top-2 dot values.
-template <bool CLAMP>
-__device__ __forceinline__ void merge_cols8(const uint2* colscratch, int k, int h, int r, int lane,
-                                            uint32_t cbm_col, uint2* dst) {
-  const uint2* src = colscratch + (k % kCscBufs) * 2 * kMatch8Waves * 32 + h * kMatch8Waves * 32 + r;
-  uint2 m = src[0];
-#pragma unroll
-  for (int w = 1; w < kMatch8Waves; ++w) {
-    const uint2 o = src[w * 32];
-    m.y = merge_second_values(m.x, m.y, o.x, o.y);
-    m.x = max(m.x, o.x);
-  }
-  m.x += cbm_col;
-  m.y += cbm_col;
-  if (CLAMP) {
-    m.x = min(m.x, kLutMax);
-    m.y = min(m.y, kLutMax);
-  }
-  dst[lane] = m;
-}
-
-// One workgroup = one MatchJob (512 pivot rows, 8 waves x 64) swept against
-// every column of its neighbour images, 64 columns per LDS tile.  Per wave
-// and tile: four 4-MFMA chains (row sub-tile s, column sub-tile c), software
-// pipelined so that each chain runs under the epilogue of the previous one:
-//   (s1,c0) || epi(s0,c0);  (s0,c1) || epi(s1,c0);  (s1,c1) || epi(s0,c1);
-//   (t+1: s0,c0) || epi(s1,c1).
-// Tiles rotate through a 4-stage LDS ring; one barrier per tile.
-template <bool CLAMP>
-__global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_tiles_i8_kernel(
-    const uint8_t* __restrict__ desc8,  // a ^ 0x80, [rows][128]
-    const int32_t* __restrict__ csum,   // 128 * sum_d a_d per row
-    const MatchJob* __restrict__ jobs, const PairDesc* __restrict__ pairs,
-    uint2* __restrict__ rowres,         // per pair [nseg][n1]
-    uint2* __restrict__ colpart) {      // per pair [nrb][n2pad]
-  __shared__ __attribute__((aligned(16))) uint8_t
-      lds[kStages8 * kTile8Bytes + kCscBufs * 2 * kMatch8Waves * 32 * 8];
-  // column partials: [tile parity][column sub-tile][wave][32]
-  uint2* colscratch = reinterpret_cast<uint2*>(lds + kStages8 * kTile8Bytes);
-
-  const MatchJob job = jobs[blockIdx.x];
-  if (job.npairs == 0 || job.n1 <= 0) return;  // padding job of the XCD order (whole block)
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int r = lane & 31;
-  const int h = lane >> 5;
-  const int row0 = job.rb * kRowsPerBlock8 + wave * 64;
-
-  // ---- A fragments (rows row0 + 32 s + r, chunks 4h + q) and the
-  // accumulator offsets of the rows this lane's results belong to.
-  i32x4 afrag[2][4];
-  i32x16 ra[2];
-#pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int row = row0 + 32 * s + r;
-    const bool ok = row < job.n1;
-    const i32x4* src =
-        reinterpret_cast<const i32x4*>(desc8 + (job.a_row + (ok ? row : 0)) * 128) + h * 4;
-    const int z = (int)0x80808080u;  // a = 0
-#pragma unroll
-    for (int q = 0; q < 4; ++q) afrag[s][q] = ok ? src[q] : i32x4{z, z, z, z};
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int rw = row0 + 32 * s + 4 * h + (i & 3) + 8 * (i >> 2);
-      // unconditional load (clamped row), then select: no branch / wait per element
-      const uint32_t cs = (uint32_t)csum[job.a_row + min(rw, job.n1 - 1)];
-      ra[s][i] = (int)((rw < job.n1 ? cs : 0u) + (1u << 21));
-    }
-  }
-
-  // Staging role of this thread: kSt 16-B chunks of the 8 KiB tile (chunk
-  // tid + kMatch8Threads * u = 8 col + c).
-  constexpr int kTileChunks = kTile8Cols * 8;  // 16-B chunks per tile
-  constexpr int kSt = kTileChunks / kMatch8Threads;
-  static_assert(kSt * kMatch8Threads == kTileChunks, "staging covers the tile");
-  int st_lds[kSt], st_off[kSt];
-#pragma unroll
-  for (int u = 0; u < kSt; ++u) {
-    const int ch = tid + kMatch8Threads * u;
-    st_lds[u] = sw8(ch >> 3, ch & 7);
-    st_off[u] = (ch >> 3) * 8 + (ch & 7);  // in 16-B chunks from the tile's first column
-  }
-
-  for (int p = 0; p < job.npairs; ++p) {
-    const PairDesc pd = pairs[job.pair0 + p];
-    const int ntiles_total = (pd.n2 + kTile8Cols - 1) / kTile8Cols;
-    uint2* colp = colpart + pd.colpart_off + (int64_t)job.rb * pd.n2pad;
-    const int32_t* bsum = csum + pd.b_row;
-    const i32x4* src0 = reinterpret_cast<const i32x4*>(desc8 + pd.b_row * 128);
-    for (int seg = 0; seg < pd.nseg; ++seg) {
-      const int t_begin = seg * kTiles8PerSeg;
-      const int t_end = min(ntiles_total, t_begin + kTiles8PerSeg);
-      const int tlast = t_end - 1;
-      uint32_t b1r[2][16], b2r[2][16];
-#pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) { b1r[s][i] = 0u; b2r[s][i] = 0u; }
-      // Prologue: stage tiles t_begin .. t_begin + 2, the column offsets of
-      // the first three, and the chain (t_begin: s0, c0).
-#pragma unroll
-      for (int j = 0; j < kAhead8; ++j)
-#pragma unroll
-        for (int u = 0; u < kSt; ++u)
-          *reinterpret_cast<i32x4*>(lds + j * kTile8Bytes + st_lds[u]) =
-              src0[(int64_t)min(t_begin + j, tlast) * kTileChunks + st_off[u]];
-      const int t1 = min(t_begin + 1, tlast), t2 = min(t_begin + 2, tlast);
-      uint32_t cb0 = (uint32_t)bsum[t_begin * kTile8Cols + r];
-      uint32_t cb1 = (uint32_t)bsum[t_begin * kTile8Cols + 32 + r];
-      uint32_t cn0 = (uint32_t)bsum[t1 * kTile8Cols + r];
-      uint32_t cn1 = (uint32_t)bsum[t1 * kTile8Cols + 32 + r];
-      uint32_t cm0 = (uint32_t)bsum[t2 * kTile8Cols + r];
-      uint32_t cm1 = (uint32_t)bsum[t2 * kTile8Cols + 32 + r];
-      __syncthreads();
-      i32x4 bf0[4], bf1[4];
-      load_bfrag8(lds, r, h, bf0);
-      i32x16 acc = chain8(afrag[0], bf0, ra[0]);
-
-      for (int k = 0; k < t_end - t_begin; ++k) {
-        const int t = t_begin + k;
-        const int t3 = min(t + 3, tlast);
-        i32x4 nxt[kSt];
-#pragma unroll
-        for (int u = 0; u < kSt; ++u) nxt[u] = src0[(int64_t)t3 * kTileChunks + st_off[u]];
-        const uint32_t cf0 = (uint32_t)bsum[t3 * kTile8Cols + r];
-        const uint32_t cf1 = (uint32_t)bsum[t3 * kTile8Cols + 32 + r];
-        const uint32_t tb0 = (uint32_t)(kTilesPerSeg - 1 - 2 * k), tb1 = tb0 - 1u;
-        const uint8_t* cur = lds + (k % kStages8) * kTile8Bytes;
-        uint2* csc = colscratch + (k % kCscBufs) * 2 * kMatch8Waves * 32;
-        const uint32_t kc0 = (cb0 << 13) | tb0, kc1 = (cb1 << 13) | tb1;
-        const uint32_t cbm0 = cb0 - (1u << 22), cbm1 = cb1 - (1u << 22);
-        // (s1, c0) || epilogue (s0, c0)
-        i32x16 acc2 = chain8(afrag[1], bf0, ra[1]);
-        const uint2 e00 = subtile_epilogue8<CLAMP>(acc, kc0, cbm0, tb0, b1r[0], b2r[0]);
-        __builtin_amdgcn_sched_barrier(0);
-        // (s0, c1) || epilogue (s1, c0)
-        load_bfrag8(cur, 32 + r, h, bf1);
-        acc = chain8(afrag[0], bf1, ra[0]);
-        const uint2 e10 = subtile_epilogue8<CLAMP>(acc2, kc0, cbm0, tb0, b1r[1], b2r[1]);
-        wave_col_partial_values(e00, e10, csc + wave * 32, h, r);
-        __builtin_amdgcn_sched_barrier(0);
-        // (s1, c1) || epilogue (s0, c1)
-        acc2 = chain8(afrag[1], bf1, ra[1]);
-        const uint2 e01 = subtile_epilogue8<CLAMP>(acc, kc1, cbm1, tb1, b1r[0], b2r[0]);
-        __builtin_amdgcn_sched_barrier(0);
-        // (t + 1: s0, c0) || epilogue (s1, c1)
-        load_bfrag8(lds + ((k + 1) % kStages8) * kTile8Bytes, r, h, bf0);
-        acc = chain8(afrag[0], bf0, ra[0]);
-        const uint2 e11 = subtile_epilogue8<CLAMP>(acc2, kc1, cbm1, tb1, b1r[1], b2r[1]);
-        wave_col_partial_values(e01, e11, csc + (kMatch8Waves + wave) * 32, h, r);
-#pragma unroll
-        for (int u = 0; u < kSt; ++u)
-          *reinterpret_cast<i32x4*>(lds + ((k + 3) % kStages8) * kTile8Bytes + st_lds[u]) = nxt[u];
-        // this lane's column in the merge below: 32 h + r of tile t
-        const uint32_t cbm_col = h ? cbm1 : cbm0;
-        cb0 = cn0;
-        cb1 = cn1;
-        cn0 = cm0;
-        cn1 = cm1;
-        cm0 = cf0;
-        cm1 = cf1;
-        if ((k + 1) % kBarTiles == 0) {
-#ifndef SCM_DIAG_NOBARRIER  // diagnostics only: no barrier (races; timing of the barrier)
-          __syncthreads();
-#endif
-          // One wave merges the 8 wave partials of the last kBarTiles tiles'
-          // 64 columns each and stores the columns' top-2 dot values.  (All
-          // waves sharing the merge, 8 columns each, measured 6 % slower:
-          // every wave then waits on LDS right after the barrier.)
-          if (SCM_DIAG_MERGE && wave == ((k / kBarTiles) & (kMatch8Waves - 1))) {
-#pragma unroll
-            for (int g = kBarTiles - 1; g > 0; --g)
-              merge_cols8<CLAMP>(colscratch, k - g, h, r, lane,
-                                 (uint32_t)bsum[(t - g) * kTile8Cols + lane] - (1u << 22),
-                                 colp + (t - g) * kTile8Cols);
-            merge_cols8<CLAMP>(colscratch, k, h, r, lane, cbm_col, colp + t * kTile8Cols);
-          }
-        }
-      }
-      if (const int rest = (t_end - t_begin) % kBarTiles) {  // tiles after the last barrier
-        __syncthreads();
-        const int kl = t_end - t_begin - 1;
-        if (SCM_DIAG_MERGE && wave == ((kl / kBarTiles) & (kMatch8Waves - 1)))
-          for (int g = rest - 1; g >= 0; --g)
-            merge_cols8<CLAMP>(colscratch, kl - g, h, r, lane,
-                               (uint32_t)bsum[(t_end - 1 - g) * kTile8Cols + lane] - (1u << 22),
-                               colp + (t_end - 1 - g) * kTile8Cols);
-      }
-      __syncthreads();  // every wave done with the LDS tiles before the next segment
-      row_flush(b1r, b2r, rowres + pd.rowres_off + (int64_t)seg * pd.n1, row0, pd.n1, r, h);
-    }
-  }
-}
-
 // ===========================================================================
-// i8 matcher, version 2 (default): LDS-DMA staging, best-only columns.
-//
-// Same MFMA chains, accumulator offsets and row keys as match_tiles_i8_kernel
-// (above), with two changes that target what bounds it (VALU issue and
-// wave stalls on the staging loads):
+// match_g8_kernel (default i8 matcher): LDS-DMA staging, packed row keys,
+// best-only columns.
 //  * B tiles and their column sums reach LDS by global_load_lds_dwordx4
 //    (LDS-DMA: no staging VGPRs, no ds_write, no wave waiting for a load in
 //    the tile it is issued): each wave moves 1 KiB of the 8 KiB tile, the
 //    XOR-swizzled LDS image is produced by permuting the per-lane SOURCE
 //    addresses (the destination of one instruction is lane-linear), tiles are
-//    issued three ahead into a 4-stage ring, and one raw s_barrier per tile is
-//    preceded by a counted vmcnt that retires exactly the next tile.
+//    issued three groups ahead into a 16-stage ring, and one raw s_barrier per
+//    group of 4 tiles is preceded by a counted vmcnt that retires exactly the
+//    next group.
+//  * Rows by VALUE: the chain ends at x = dot - cb_j + 2^22 (< 2^24), and
+//    x + cb_j = dot + 2^22 for two accumulators of the lane's column (two
+//    adjacent rows) is ONE v_lshl_add_u64 on the register pair; the row state
+//    takes the values of the tile's two column sub-tiles with one v_max3 per
+//    row: 1 VALU op per element (a keyed row state with the column index in
+//    the low bits costs 1.5: v_lshl_add_u32 per element + half a max3).  Each
+//    lane keeps, per row, the best value over ITS columns (j = lane mod 32);
+//    row_flush_values reduces them over the lanes with the lane of the best.
+//    Which column of that lane's residue class holds the best, and the exact
+//    second, come from match_rowcheck_g8_kernel (an exact MFMA pass over the
+//    class) for the rows that can still pass.  CLAMP variant: the same values,
+//    min(dot, 2^18) applied at the flush (max commutes with the clamp).
 //  * Column side by BEST VALUE ONLY: per lane a max3 tree over its 16 raw
-//    accumulators (8 ops instead of the 21 of a top-2 tree), then the two
-//    row sub-tiles and the two lane halves (best of the wave's 64 rows); the
-//    workgroup merge keeps, per column, the best value B1, the largest best
-//    of the OTHER waves B2', and the wave of B1.  The column's true second is
-//    max(B2', second within that wave's 64 rows): match_finalize_kernel
-//    recomputes the 64 dots of that group exactly (sdot4 on the same offset
-//    operands) for the few columns whose cross-check outcome depends on it.
-// Per element: 1 (row key) + 2 (row state) + ~0.6 (column) VALU ops.
-// colpart entry (per row block, column): x = B1 (exact dot, clamped like the
-// row keys in the CLAMP variant), y = (B2' << 3) | wave of B1.
+//    accumulators (x; cb_j is constant within a column), then the two row
+//    sub-tiles and the two lane halves (best of the wave's 64 rows); the
+//    workgroup merge keeps, per column, the best value B1, the largest best of
+//    the OTHER waves B2', and the wave of B1.  The column's true second is
+//    max(B2', second within that wave's 64 rows), recomputed exactly by
+//    match_recheck_g8_kernel for the columns whose cross-check outcome depends
+//    on it.  With max_ratio <= 1 a column whose best value is tied fails the
+//    ratio test, so the column's best row need not be tracked (the runtime
+//    selects the bf16 kernel, which keeps the lowest-row rule, otherwise).
+// Per element: 1 (rows) + ~0.55 (columns) VALU ops.
+// colpart entry (per row block, column): x = B1 (raw accumulator units), y =
+// (B2' << 3) | wave of B1.
 // ===========================================================================
 constexpr int kG8T = 4;                                        // tiles per barrier group
 constexpr int kG8Q = 4;                                        // groups in the LDS ring
@@ -743,60 +504,39 @@ __device__ __forceinline__ void g8_next(const uint8_t* lds, int g, int r, int h,
   cb1 = (uint32_t)cbs[32 + r];
 }
 
-// One 4-MFMA chain of the v2 kernel; SCM_G8_PRIO (diagnostics) raises the
-// wave's issue priority around it.
-__device__ __forceinline__ i32x16 g8_chain(const i32x4 (&a)[4], const i32x4 (&b)[4],
-                                           const i32x16& ra) {
-#ifdef SCM_G8_PRIO
-  __builtin_amdgcn_s_setprio(1);
-  const i32x16 r = chain8(a, b, ra);
-  __builtin_amdgcn_s_setprio(0);
-  return r;
-#elif defined(SCM_DIAG_G9_TIMING)
-  // diagnostics only: a fifth MFMA per chain (the digit block), B from the
-  // first chunk's registers as a stand-in for its LDS fragment
-  i32x16 acc = chain8(a, b, ra);
-  const i32x4 c127 = {0x7F7F7F7F, 0x7F7F7F7F, 0x7F7F7F7F, 0x7F7F7F7F};
-  return __builtin_amdgcn_mfma_i32_32x32x32_i8(c127, b[0], acc, 0, 0, 0);
-#else
-  return chain8(a, b, ra);
-#endif
+// Row values, two accumulators per VALU op: v_lshl_add_u64 (shift 0) on a
+// register pair, x + (cb_j : cb_j) = (dot + 2^22) for two adjacent rows of
+// the lane's column (x + cb_j < 2^24: no carry crosses into the high half).
+// The compiler does not apply the MFMA-result read hazard (wait states) to
+// inline asm, so every use takes `dep`, a value computed by ordinary VALU code
+// from the same MFMA result (the column max): that code has waited for the
+// result, and the asm cannot issue before it.
+typedef unsigned long long u64;
+__device__ __forceinline__ u64 add_pair_u64(u64 x, u64 k, uint32_t dep) {
+  u64 d;
+  asm("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(d) : "v"(x), "v"(k), "v"(dep));
+  return d;
 }
 
-// Row keys and row state of a finished sub-tile (as subtile_epilogue8) and
-// the largest raw accumulator of the lane's 16 rows (column side).
-template <bool CLAMP>
-__device__ __forceinline__ uint32_t g8_epilogue(const i32x16& acc, uint32_t kc, uint32_t cbm,
-                                                uint32_t tbits, uint32_t (&b1r)[16]) {
-#ifdef SCM_DIAG_MATCH_SKELETON
-  // diagnostics only: MFMA + LDS + staging skeleton, results discarded
-  uint32_t xs = 0;
+// Row values of one finished sub-tile (this lane's column, its 16 rows);
+// `cm` = g8_colmax(acc) (the hazard dependency above).
+__device__ __forceinline__ void g8_keys(const i32x16& acc, u64 kq, uint32_t cm, u64 (&k)[8]) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) xs ^= (uint32_t)acc[i];
-  b1r[0] ^= xs;
-  return xs;
-#endif
-#ifdef SCM_DIAG_G9_TIMING
-  // diagnostics only (wrong results): the row state as a raw max, as the
-  // digit-MFMA design would keep it
+  for (int m = 0; m < 8; ++m)
+    k[m] = add_pair_u64(((u64)(uint32_t)acc[2 * m + 1] << 32) | (uint32_t)acc[2 * m], kq, cm);
+}
+
+// Row state update with the values of the tile's two column sub-tiles.
+__device__ __forceinline__ void g8_rows(const u64 (&ka)[8], const u64 (&kb)[8], uint32_t (&b1r)[16]) {
 #pragma unroll
-  for (int i = 0; i < 16; ++i) b1r[i] = max(b1r[i], (uint32_t)acc[i]);
-#else
-#pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const uint32_t x = (uint32_t)acc[i];
-    const uint32_t key = CLAMP ? (min(x + cbm, kLutMax) << 13) | tbits : (x << 13) + kc;
-    b1r[i] = max(b1r[i], key);
+  for (int m = 0; m < 8; ++m) {
+    b1r[2 * m] = max(max(b1r[2 * m], (uint32_t)ka[m]), (uint32_t)kb[m]);
+    b1r[2 * m + 1] = max(max(b1r[2 * m + 1], (uint32_t)(ka[m] >> 32)), (uint32_t)(kb[m] >> 32));
   }
-#endif
-#ifdef SCM_DIAG_G8_TOP2
-  // diagnostics only: the cost of the exact column top-2 tree (result unchanged:
-  // the second's bit 31 is always clear)
-  {
-    const uint2 t2 = column_top2_values(acc);
-    return t2.x | (t2.y & 0x80000000u);
-  }
-#endif
+}
+
+// Largest raw accumulator of the lane's 16 rows (column side).
+__device__ __forceinline__ uint32_t g8_colmax(const i32x16& acc) {
   uint32_t v[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) v[i] = (uint32_t)acc[i];
@@ -858,9 +598,6 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
   uint32_t* csc = reinterpret_cast<uint32_t*>(lds + kG8CscOff);
   int64_t* meta = reinterpret_cast<int64_t*>(lds + kG8MetaOff);
 
-#ifdef SCM_G8_WPRIO  // diagnostics: whole-kernel wave issue priority over co-resident kernels
-  __builtin_amdgcn_s_setprio(SCM_G8_WPRIO);
-#endif
   const MatchJob job = jobs[blockIdx.x];
   if (job.npairs == 0 || job.n1 <= 0) return;  // padding job of the XCD order (whole block)
   const PairDesc* __restrict__ P = pairs + job.pair0;
@@ -937,12 +674,9 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
     for (int i = 0; i < 16; ++i) b1r[s][i] = 0u;
 
   i32x4 bf0[4], bf1[4];
-#ifdef SCM_G8_STAGGER  // diagnostics: delay waves 4-7 (the second half of each SIMD pair)
-  if (wave >= 4) __builtin_amdgcn_s_sleep(SCM_G8_STAGGER);
-#endif
   uint32_t cbn0, cbn1;
   g8_next(lds, 0, r, h, bf0, cbn0, cbn1);
-  i32x16 acc = g8_chain(afrag[0], bf0, ra[0]);
+  i32x16 acc = chain8(afrag[0], bf0, ra[0]);
 
   for (int g = 0; g < G; ++g) {
     const int stage = g & (kG8Stages - 1);
@@ -950,28 +684,31 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
     const uint32_t cb0 = cbn0, cb1 = cbn1;  // read with the tile's c0 fragments
     if (tid == 0) meta[stage] = cpi + (int64_t)t * kTile8Cols;
     const int k = t & (kTiles8PerSeg - 1);  // 64-column tile within the segment
-    const uint32_t tb0 = (uint32_t)(kTilesPerSeg - 1 - 2 * k), tb1 = tb0 - 1u;
-    const uint32_t kc0 = (cb0 << 13) | tb0, kc1 = (cb1 << 13) | tb1;
-    const uint32_t cbm0 = cb0 - (1u << 22), cbm1 = cb1 - (1u << 22);
+    const u64 kq0 = ((u64)cb0 << 32) | cb0, kq1 = ((u64)cb1 << 32) | cb1;  // row value addends
+    u64 k00[8], k10[8], k01[8], k11[8];
     const int m = g / kG8T;
     uint32_t* cscw =
         csc + (((m % kG8CscGroups) * kG8T + (g & (kG8T - 1))) * kMatch8Waves + wave) * kTile8Cols;
     const bool group_end = (g & (kG8T - 1)) == kG8T - 1;
     // (s1, c0) || epilogue (s0, c0); the c1 fragments load under the epilogue
-    i32x16 acc2 = g8_chain(afrag[1], bf0, ra[1]);
+    i32x16 acc2 = chain8(afrag[1], bf0, ra[1]);
     load_bfrag8(cur, 32 + r, h, bf1);
-    const uint32_t e00 = g8_epilogue<CLAMP>(acc, kc0, cbm0, tb0, b1r[0]);
+    const uint32_t e00 = g8_colmax(acc);
+    g8_keys(acc, kq0, e00, k00);
     __builtin_amdgcn_sched_barrier(0);
     // (s0, c1) || epilogue (s1, c0)
-    acc = g8_chain(afrag[0], bf1, ra[0]);
-    const uint32_t e10 = g8_epilogue<CLAMP>(acc2, kc0, cbm0, tb0, b1r[1]);
+    acc = chain8(afrag[0], bf1, ra[0]);
+    const uint32_t e10 = g8_colmax(acc2);
+    g8_keys(acc2, kq0, e10, k10);
     g8_col_partial(e00, e10, cscw, h, r);
     __builtin_amdgcn_sched_barrier(0);
     // (s1, c1) || epilogue (s0, c1); inside a group the next tile's c0
     // fragments load under the epilogue (at a group end only after the barrier)
-    acc2 = g8_chain(afrag[1], bf1, ra[1]);
+    acc2 = chain8(afrag[1], bf1, ra[1]);
     if (!group_end) g8_next(lds, g + 1, r, h, bf0, cbn0, cbn1);
-    const uint32_t e01 = g8_epilogue<CLAMP>(acc, kc1, cbm1, tb1, b1r[0]);
+    const uint32_t e01 = g8_colmax(acc);
+    g8_keys(acc, kq1, e01, k01);
+    g8_rows(k00, k01, b1r[0]);
     __builtin_amdgcn_sched_barrier(0);
     if (group_end) {
       // Barrier m.  This wave's DMA of group m + 1 (issued at barrier m - 2)
@@ -980,13 +717,9 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
       // ((j - 1) & 1) == w / 4); after a row flush (many stores) drain.
       const int half = wave >> 2;
       const int st = (m >= 3 && (((m - 3) & 1) == half)) + (m >= 2 && (((m - 2) & 1) == half));
-#ifndef SCM_DIAG_NOBARRIER  // diagnostics only (races): timing without the group barrier
       g8_wait_vm(g - flushed <= 2 * kG8T ? 0 : kG8T * gpt + st);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
-#else
-      (void)st;
-#endif
       dma_group(m + kG8Q - 1);
       if (m >= 1 && (((m - 1) & 1) == half)) {  // merge tile (wave & 3) of group m - 1
         const int tg = (m - 1) * kG8T + (wave & (kG8T - 1));
@@ -997,12 +730,14 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
       g8_next(lds, g + 1, r, h, bf0, cbn0, cbn1);
     }
     // (g + 1: s0, c0) || epilogue (s1, c1)
-    acc = g8_chain(afrag[0], bf0, ra[0]);
-    const uint32_t e11 = g8_epilogue<CLAMP>(acc2, kc1, cbm1, tb1, b1r[1]);
+    acc = chain8(afrag[0], bf0, ra[0]);
+    const uint32_t e11 = g8_colmax(acc2);
+    g8_keys(acc2, kq1, e11, k11);
+    g8_rows(k10, k11, b1r[1]);
     g8_col_partial(e01, e11, cscw + 32, h, r);
     // Row flush at the end of a segment (or of the pair).
     if (k == kTiles8PerSeg - 1 || t + 1 == nt) {
-      row_flush_best(b1r, rowres + pd.rowres_off + (int64_t)(t / kTiles8PerSeg) * pd.n1, row0,
+      row_flush_values<CLAMP>(b1r, rowres + pd.rowres_off + (int64_t)(t / kTiles8PerSeg) * pd.n1, row0,
                 pd.n1, r, h);
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -1193,7 +928,6 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
   }
   uint2* cp = colpart + pd.colpart_off;
   uint2* rr = rowres + pd.rowres_off;
-  constexpr uint32_t kV = (1u << 19) - 1u;
   if (phase == 0) {
   if (cross_check) {
     for (int j = tid; j < pd.n2; j += kFinThreads) {
@@ -1234,33 +968,26 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     __syncthreads();
   }
   // Phase 2: per-row decisions (rows strided over the threads, coalesced).
-  // The rows' seconds are lower bounds (best of the other lanes, see
-  // row_flush_best): a row that fails with it fails; a row that passes (and,
-  // with the cross-check, can still be its column's match) is queued for the
-  // exact second in the bucket of its best column's lane residue (state 3,
-  // match_rowcheck_g8_kernel).
+  // The matcher's rows carry their best VALUE, the residue (mod 32) of the
+  // best column, and as second a lower bound (best of the other lanes, see
+  // row_flush_values): a row that fails with it fails; a row that passes is
+  // queued in the bucket of its residue (state 3) for
+  // match_rowcheck_g8_kernel, which finds the best column, the exact second
+  // and (with the cross-check) whether the row can still be its column's match.
   int32_t* rl = rlist + pd.rlist_off;
   uint2* ax = rowaux + pd.aux_off;
   if (tid < 32) bcnt[tid] = 0;
   __syncthreads();
   for (int i = tid; i < pd.n1; i += kFinThreads) {
     uint2 m = rr[i];
-    int best_seg = 0;
     for (int sg = 1; sg < pd.nseg; ++sg) {
       const uint2 o = rr[(int64_t)sg * pd.n1 + i];
       m.y = merge_second(m.x, m.y, o.x, o.y);
-      if (o.x > m.x) { m.x = o.x; best_seg = sg; }
+      m.x = max(m.x, o.x);
     }
     const uint32_t best = m.x >> kIdxBits, second = m.y >> kIdxBits;
-    const int32_t col = best_seg * (kTilesPerSeg * 32) + (int32_t)(kIdxMask - (m.x & kIdxMask));
-    uint32_t state = passes(lut, best, second, max_ratio, max_distance) ? 3u : 0u;
-    if (state && cross_check) {
-      const uint2 c = cp[col];
-      const uint32_t b1 = c.x & kV, rb = c.x >> 19, w = c.y & 7u, b2 = c.y >> 3;
-      const uint32_t grp = rb * (uint32_t)(kRowsPerBlock8 / 64) + w;
-      if (b1 != best || grp != (uint32_t)(i >> 6) || !passes(lut, b1, b2, max_ratio, max_distance))
-        state = 0u;
-    }
+    const int32_t col = (int32_t)((kIdxMask - (m.x & kIdxMask)) & 31u);  // residue of the best
+    const uint32_t state = passes(lut, best, second, max_ratio, max_distance) ? 3u : 0u;
     rr[i] = make_uint2((uint32_t)col, state);
     if (state == 3u) {
       ax[i] = make_uint2(best, second);
@@ -1313,22 +1040,27 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
   if (tid == 0) counts[blockIdx.x] = run;
 }
 
-// Exact row seconds of the version-2 finalize (phase 2b).  The matcher keeps
-// per lane only the best key of each row over that lane's columns (j = lane +
-// 32 t), so the row's second is known up to the second within the winning
-// lane.  One workgroup per (pair, lane residue b): the queued rows whose best
-// column is ≡ b (mod 32) against every column ≡ b (mod 32) of the neighbour
-// (staged in LDS, 256 at a time), on the matcher's own MFMA with the same
-// offset operands: A = those columns (C operand = their sums), B = the rows;
-// per row the exact top-2 (multiset) over the residue class.  With it the
-// row's second is exact (max of the lower bound and the in-class second) and
-// the ratio / distance test final: the row becomes a candidate of the
-// column check (2, cross-check) or a match (1).
+// Best column and exact second of the queued rows (finalize phase 2b).  The
+// matcher keeps per lane only the best VALUE of each row over that lane's
+// columns (j = lane + 32 t), so a row is known by its best value, the residue
+// b of its best column and a lower bound of its second (the best of the other
+// lanes).  One workgroup per (pair, residue b): the queued rows of bucket b
+// against every column = b (mod 32) of the neighbour (staged in LDS, 256 at a
+// time), on the matcher's own MFMA with the same offset operands: A = those
+// columns (C operand = their sums), B = the rows; per row the exact top-2
+// (multiset) over the residue class and the LOWEST column holding the class
+// best (FindBestMatchesOneWay keeps the first maximum).  The row's second is
+// then exact (max of the lower bound and the in-class second) and the ratio /
+// distance test final; with the cross-check the row stays a candidate (state
+// 2, match_recheck_g8_kernel) only if its column's best value equals the
+// row's best, sits in the row's 64-row group and passes the column's test with
+// the column's second lower bound; otherwise it is a match (1) or rejected (0).
 constexpr int kRcThreads = 256;
 constexpr int kRcChunk = 256;  // columns of one residue class staged per pass (32 KiB)
 
 __global__ __launch_bounds__(kRcThreads) void match_rowcheck_g8_kernel(
     const PairDesc* __restrict__ pairs, uint2* __restrict__ rowres,
+    const uint2* __restrict__ colpart,
     const uint2* __restrict__ rowaux, const int32_t* __restrict__ rlist,
     const uint8_t* __restrict__ desc8, const int32_t* __restrict__ csum,
     const float* __restrict__ lut, float max_ratio, float max_distance, int cross_check) {
@@ -1357,6 +1089,7 @@ __global__ __launch_bounds__(kRcThreads) void match_rowcheck_g8_kernel(
       for (int q = 0; q < 4; ++q) bfr[q] = src[q];
     }
     int t1 = INT_MIN, t2 = INT_MIN;  // this lane's top-2 (multiset) over its columns
+    int j1 = 0;                      // column of t1 (first maximum in column order)
     for (int c = 0; c < nchunks; ++c) {
       const int cbeg = c * kRcChunk, cn = min(kRcChunk, Cb - cbeg);
       if (nchunks > 1 || g0 == 0) {
@@ -1377,11 +1110,13 @@ __global__ __launch_bounds__(kRcThreads) void match_rowcheck_g8_kernel(
 #pragma unroll
         for (int i = 0; i < 16; ++i) cinit[i] = lcs[ct * 32 + 4 * h + (i & 3) + 8 * (i >> 2)];
         const i32x16 acc = chain8(afr, bfr, cinit);  // a'.b' + cs(column): dot - cs(row) + 2^21
+        // this lane's columns in ascending order: x = ct*32 + 4h + (i & 3) + 8 (i >> 2)
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
           const int x = ct * 32 + 4 * h + (i & 3) + 8 * (i >> 2);
           const int v = x < cn ? acc[i] : INT_MIN;
           t2 = max(t2, min(t1, v));
+          j1 = v > t1 ? cbeg + x : j1;
           t1 = max(t1, v);
         }
       }
@@ -1390,15 +1125,28 @@ __global__ __launch_bounds__(kRcThreads) void match_rowcheck_g8_kernel(
     // each 32-column tile: merge them (symmetric in the two halves).
     const auto e1 = __builtin_amdgcn_permlane32_swap(t1, t1, false, false);
     const auto e2 = __builtin_amdgcn_permlane32_swap(t2, t2, false, false);
+    const auto ej = __builtin_amdgcn_permlane32_swap(j1, j1, false, false);
     if (h == 0 && rv) {
       const int s2 = max(max((int)e2[0], (int)e2[1]), min((int)e1[0], (int)e1[1]));
+      // a tie between the halves makes the second equal the best: the row fails
+      // whichever column is taken
+      const int jb = (int)e1[1] > (int)e1[0] ? (int)ej[1] : (int)ej[0];
+      const int32_t col = b + 32 * jb;
       const uint2 a = ax[row];
       const int32_t rowsum = csum[pd.a_row + row] - (1 << 21);
       uint32_t d2 = s2 == INT_MIN ? 0u : (uint32_t)(s2 + rowsum);  // one column only: second 0
       if (pd.clamp) d2 = min(d2, kLutMax);
       const uint32_t second = max(a.y, d2);
-      const bool ok = passes(lut, a.x, second, max_ratio, max_distance);
-      rr[row] = make_uint2(rr[row].x, ok ? (cross_check ? 2u : 1u) : 0u);
+      uint32_t state = passes(lut, a.x, second, max_ratio, max_distance) ? (cross_check ? 2u : 1u) : 0u;
+      if (state == 2u) {  // can the row still be its column's match? (colpart merged by phase 0)
+        constexpr uint32_t kV = (1u << 19) - 1u;
+        const uint2 c = colpart[pd.colpart_off + col];
+        const uint32_t b1 = c.x & kV, rb = c.x >> 19, w = c.y & 7u, b2 = c.y >> 3;
+        const uint32_t grp = rb * (uint32_t)(kRowsPerBlock8 / 64) + w;
+        if (b1 != a.x || grp != (uint32_t)(row >> 6) || !passes(lut, b1, b2, max_ratio, max_distance))
+          state = 0u;
+      }
+      rr[row] = make_uint2((uint32_t)col, state);
     }
   }
 }
@@ -1548,19 +1296,6 @@ hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int nj
   return hipGetLastError();
 }
 
-hipError_t launch_match_tiles_i8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
-                                 int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
-                                 bool clamp, hipStream_t stream) {
-  if (njobs <= 0) return hipSuccess;
-  if (clamp)
-    hipLaunchKernelGGL(match_tiles_i8_kernel<true>, dim3(njobs), dim3(kMatch8Threads), 0, stream,
-                       desc8, csum, jobs, pairs, rowres, colpart);
-  else
-    hipLaunchKernelGGL(match_tiles_i8_kernel<false>, dim3(njobs), dim3(kMatch8Threads), 0, stream,
-                       desc8, csum, jobs, pairs, rowres, colpart);
-  return hipGetLastError();
-}
-
 hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
                            int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
                            bool clamp, hipStream_t stream) {
@@ -1585,7 +1320,7 @@ hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* ro
                      rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
                      cross_check, matches, counts, 0);
   hipLaunchKernelGGL(match_rowcheck_g8_kernel, dim3(32, npairs), dim3(kRcThreads), 0, stream,
-                     pairs, rowres, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
+                     pairs, rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
                      cross_check);
   if (cross_check && max_groups > 0)
     hipLaunchKernelGGL(match_recheck_g8_kernel, dim3((unsigned)((max_groups + 3) / 4), npairs),

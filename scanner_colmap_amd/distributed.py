@@ -93,10 +93,14 @@ def gather_to_root(payload, device=None) -> list[bytes] | None:
     """Gather every rank's byte payload (bytes or a uint8 numpy array) to
     rank 0 (None elsewhere).
 
-    Sizes are exchanged with an all_gather of one int64 per rank; then every
-    rank r > 0 sends exactly its payload to rank 0 point-to-point (isend /
-    irecv, no padding) -- on the `nccl` (RCCL) backend each peer's bytes
-    travel over its own xGMI link to GPU 0, all receives in flight at once."""
+    Sizes are exchanged with an all_gather of one int64 per rank; then ONE
+    batch_isend_irecv group moves every rank's exact payload to rank 0 (no
+    padding): rank r > 0 posts its send, rank 0 posts all receives at once into
+    views of one flat buffer.  On the `nccl` backend (RCCL over xGMI) the
+    group is device-resident end to end -- each sender stages its payload once
+    host -> device (the library's io.cc rows live in pinned host memory), each
+    peer's bytes travel over its own xGMI link to GPU 0, and rank 0 copies the
+    flat buffer to the host once; on gloo the same group runs on CPU tensors."""
     import torch
     import torch.distributed as dist
 
@@ -111,17 +115,22 @@ def gather_to_root(payload, device=None) -> list[bytes] | None:
     sizes = [int(s.item()) for s in sizes]
     if rank != 0:
         if sizes[rank]:
-            t = torch.from_numpy(src.copy() if not src.flags.writeable else src).to(dev)
-            dist.send(t, dst=0)
+            host = torch.from_numpy(src if src.flags.writeable else src.copy())
+            t = host.to(dev, non_blocking=False) if dev.type != "cpu" else host
+            for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, 0)]):
+                w.wait()
         return None
-    bufs = {r: torch.empty(sizes[r], dtype=torch.uint8, device=dev)
-            for r in range(1, world) if sizes[r]}
-    reqs = [dist.irecv(b, src=r) for r, b in bufs.items()]
-    for q in reqs:
-        q.wait()
+    offs = np.concatenate([[0], np.cumsum(sizes[1:])]).astype(np.int64)
+    flat = torch.empty(int(offs[-1]), dtype=torch.uint8, device=dev)
+    ops = [dist.P2POp(dist.irecv, flat[int(offs[r - 1]):int(offs[r])], r)
+           for r in range(1, world) if sizes[r]]
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    host = flat.cpu().numpy() if dev.type != "cpu" else flat.numpy()
     out = [src.tobytes()]
     for r in range(1, world):
-        out.append(bufs[r].cpu().numpy().tobytes() if r in bufs else b"")
+        out.append(host[int(offs[r - 1]):int(offs[r])].tobytes())
     return out
 
 

@@ -110,6 +110,61 @@ def test_gloo_shard_step_world2(n, K, scaling):
     assert total == (n if scaling == "strong" else n * world)
 
 
+def _gather_main(rank, world, port, sizes, q):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        rng = np.random.default_rng(rank)
+        payload = rng.integers(0, 256, sizes[rank], dtype=np.uint8)
+        got = sd.gather_to_root(payload if rank % 2 else payload.tobytes())
+        if rank == 0:
+            ref = [np.random.default_rng(r).integers(0, 256, sizes[r], dtype=np.uint8).tobytes()
+                   for r in range(world)]
+            q.put(got == ref)
+        else:
+            q.put(got is None)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("sizes", [[5, 0, 70000, 1], [0, 0, 0, 0], [0, 3, 0, 12345]])
+def test_gloo_gather_world4_uneven_and_empty(sizes):
+    """gather_to_root (one batch_isend_irecv group) at world 4: empty payloads
+    on any rank (rank 0 included), uneven sizes, bytes and numpy inputs."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gather_main, args=(r, world, port, sizes, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert [p.exitcode for p in procs] == [0] * world
+    assert all(q.get(timeout=5) for _ in range(world))
+
+
+@pytest.mark.parametrize("n,K,scaling", [(6, 4, "strong"), (3, 5, "weak")])
+def test_gloo_shard_step_world4(n, K, scaling):
+    """ShardPlan.step at world 4: with 6 images strong-scaled some ranks own one
+    row (or none with pairs), and the last rank's rows have no pairs at all."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, K, scaling, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert [p.exitcode for p in procs] == [0] * world
+    ok_a, ok_b, nrows, total = q.get(timeout=5)
+    assert ok_a and ok_b and nrows == total
+
+
 def test_shard_plan_scaling():
     weak = [sd.ShardPlan(1000, 20, 8, r, "weak") for r in range(8)]
     strong = [sd.ShardPlan(10000, 50, 8, r, "strong") for r in range(8)]
