@@ -8,10 +8,10 @@ for spec in "$@"; do
   name=${spec%%:*}; flags=${spec#*:}
   out=../../probes/build/$name
   mkdir -p $out/obj
-  for f in match_kernels verify_kernels; do
+  for f in match_kernels verify_kernels sift_kernels; do
     /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC -ffp-contract=off --offload-arch=gfx950 $flags -c $f.hip -o $out/obj/$f.o &
   done
-  for f in scm_runtime scm_codec; do
+  for f in scm_runtime scm_codec scm_sift; do
     /opt/rocm/bin/hipcc -std=c++17 -O3 -fPIC -ffp-contract=off --offload-arch=gfx950 $flags -x hip -c $f.cpp -o $out/obj/$f.o &
   done
   wait
