@@ -10,9 +10,13 @@
 //        elements: image id, keypoints, descriptors;
 //   OUT: per output row two length-prefixed elements, pair_image_ids and
 //        two_view_geometries (oracle_table_run over every row).
+// usage: oracle_asan --sift WIDTH HEIGHT CHANNELS SEED
+//   the SIFT extraction op (oracle_sift_extract) on a seeded pseudo-random
+//   frame; prints the three element sizes.
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "../include/scm.h"
@@ -24,6 +28,9 @@ int oracle_table_run(const scm_matching_options* o, int64_t num_rows, const scm_
                      int64_t row_begin, int64_t row_end, uint8_t** ids_out, size_t* ids_sizes,
                      uint8_t** tvg_out, size_t* tvg_sizes);
 void oracle_free(uint8_t* p);
+int oracle_sift_extract(const uint8_t* frame, int32_t width, int32_t height, int32_t channels,
+                        uint64_t image_id, uint8_t** kp_out, size_t* kp_size, uint8_t** desc_out,
+                        size_t* desc_size, uint8_t** cam_out, size_t* cam_size);
 }
 
 namespace {
@@ -44,7 +51,30 @@ void write_blob(FILE* f, const uint8_t* p, uint64_t n) {
 
 }  // namespace
 
+int sift_main(int w, int h, int c, uint32_t seed) {
+  std::vector<uint8_t> f((size_t)w * h * c);
+  uint32_t x = seed * 2654435761u + 1u;
+  for (size_t i = 0; i < f.size(); ++i) {  // smooth-ish texture: blobs plus noise
+    x = x * 1664525u + 1013904223u;
+    const size_t p = i / c;
+    const int yy = (int)(p / w), xx = (int)(p % w);
+    f[i] = (uint8_t)(((xx * 37 + yy * 61) % 97) * 2 + (x >> 28));
+  }
+  uint8_t *a = nullptr, *b = nullptr, *d = nullptr;
+  size_t na = 0, nb = 0, nd = 0;
+  const int rc = oracle_sift_extract(f.data(), w, h, c, 1, &a, &na, &b, &nb, &d, &nd);
+  if (rc != 0) return 3;
+  std::printf("%zu %zu %zu\n", na, nb, nd);
+  oracle_free(a);
+  oracle_free(b);
+  oracle_free(d);
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  if (argc == 6 && std::string(argv[1]) == "--sift")
+    return sift_main(std::atoi(argv[2]), std::atoi(argv[3]), std::atoi(argv[4]),
+                     (uint32_t)std::atoi(argv[5]));
   if (argc != 4) {
     std::fprintf(stderr, "usage: %s IN OUT OVERLAP\n", argv[0]);
     return 2;

@@ -495,13 +495,17 @@ bool detect_watermark(const scm_matching_options& o, const std::vector<double>& 
 // EstimateUncalibrated (dummy cameras have no prior focal length); the op's
 // post-filter is verify_pair_filtered below.
 TVG verify_pair(const scm_matching_options& o, const float* kp1, const float* kp2,
-                const std::vector<Match>& matches, uint32_t id1, uint32_t id2) {
+                const std::vector<Match>& matches, uint32_t id1, uint32_t id2,
+                uint32_t iteration = 0) {
   TVG tvg;
   // Two PRNG streams per pair: F from pair_seed, H (then the watermark
   // RANSAC) from pair_seed_h (geom_solvers.h; the reference's single
   // thread-local generator is time-seeded, so either is a realisation of it).
-  std::mt19937 prng(oracle_pair_seed(o.ransac_seed, id1, id2));
-  std::mt19937 prng_h(oracle_pair_seed(o.ransac_seed ^ 0x6A09E667u, id1, id2));
+  // Estimate number `iteration` of EstimateMultiple starts from
+  // geom::iteration_seed (0: the plain Estimate).
+  const uint32_t base = scm::geom::iteration_seed(o.ransac_seed, iteration);
+  std::mt19937 prng(oracle_pair_seed(base, id1, id2));
+  std::mt19937 prng_h(oracle_pair_seed(base ^ 0x6A09E667u, id1, id2));
   const size_t min_num_inliers = (size_t)o.min_num_inliers;
   if (matches.size() < min_num_inliers) {
     tvg.config = SCM_TVG_DEGENERATE;
@@ -543,11 +547,57 @@ TVG verify_pair(const scm_matching_options& o, const float* kp1, const float* kp
   return tvg;
 }
 
-// verify_pair followed by the op's post-filter (sequential_matching.cc:173-178):
-// too few inliers -> TwoViewGeometry() (config 0, zero models).
+// TwoViewGeometry::EstimateMultiple [upstream estimators/two_view_geometry.cc],
+// taken when multiple_models is set (sequential_matching.cc:94-96):
+// Estimate on the remaining matches until it is DEGENERATE, keeping every
+// geometry except WATERMARK ones (Options::multiple_ignore_watermark, default
+// true), the remaining matches being ExtractOutlierMatches(remaining,
+// inlier_matches); one kept geometry is the result, several give MULTIPLE
+// with their inlier matches concatenated (F, H unset: zeros), none gives
+// DEGENERATE.  Estimate k draws from the iteration-k seeds.  (The reference
+// would loop forever on a non-degenerate Estimate without inlier matches;
+// the loop stops there.)
+TVG verify_pair_multiple(const scm_matching_options& o, const float* kp1, const float* kp2,
+                         const std::vector<Match>& matches, uint32_t id1, uint32_t id2) {
+  std::vector<Match> remaining = matches;
+  std::vector<TVG> kept;
+  for (uint32_t k = 0;; ++k) {
+    const TVG g = verify_pair(o, kp1, kp2, remaining, id1, id2, k);
+    if (g.config == SCM_TVG_DEGENERATE) break;
+    if (g.config != SCM_TVG_WATERMARK) kept.push_back(g);
+    if (g.inlier_matches.empty()) break;
+    std::vector<Match> out;  // ExtractOutlierMatches (matches are unique pairs)
+    size_t j = 0;
+    for (const Match& m : remaining) {
+      if (j < g.inlier_matches.size() && g.inlier_matches[j].idx1 == m.idx1 &&
+          g.inlier_matches[j].idx2 == m.idx2)
+        ++j;  // the inlier matches are a subsequence of `remaining`
+      else
+        out.push_back(m);
+    }
+    remaining.swap(out);
+  }
+  TVG tvg;
+  if (kept.empty()) {
+    tvg.config = SCM_TVG_DEGENERATE;
+  } else if (kept.size() == 1) {
+    tvg = kept[0];
+  } else {
+    tvg.config = SCM_TVG_MULTIPLE;
+    for (const TVG& g : kept)
+      tvg.inlier_matches.insert(tvg.inlier_matches.end(), g.inlier_matches.begin(),
+                                g.inlier_matches.end());
+  }
+  return tvg;
+}
+
+// verifyTwoViewGeometry (Estimate, or EstimateMultiple with multiple_models)
+// followed by the op's post-filter (sequential_matching.cc:173-178): too few
+// inliers -> TwoViewGeometry() (config 0, zero models).
 TVG verify_pair_filtered(const scm_matching_options& o, const float* kp1, const float* kp2,
                          const std::vector<Match>& matches, uint32_t id1, uint32_t id2) {
-  TVG tvg = verify_pair(o, kp1, kp2, matches, id1, id2);
+  TVG tvg = o.multiple_models ? verify_pair_multiple(o, kp1, kp2, matches, id1, id2)
+                              : verify_pair(o, kp1, kp2, matches, id1, id2);
   if (tvg.inlier_matches.size() < (size_t)o.min_num_inliers) tvg = TVG();
   return tvg;
 }

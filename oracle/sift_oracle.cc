@@ -166,6 +166,24 @@ void smooth(const float* in, float* out, float* tmp, int w, int h, const std::ve
     }
 }
 
+// Gradient and Hessian of the DoG at a sample (vl_sift_refine_keypoints,
+// VLFeat sift.c): at() reads vl_sift_pix (float), so the sums and
+// differences round in float; only the products with the double literals
+// (0.5, 2.0, 0.25) widen to double (C's usual arithmetic conversions).
+// D = Dx, Dy, Ds, Dxx, Dyy, Dss, Dxy, Dxs, Dys.
+static void refine_terms(const float* pt, ptrdiff_t yo, ptrdiff_t so, double* D) {
+  auto at = [&](int ax, int ay, int as) -> float { return *(pt + ax + ay * yo + as * so); };
+  D[0] = 0.5 * (at(1, 0, 0) - at(-1, 0, 0));
+  D[1] = 0.5 * (at(0, 1, 0) - at(0, -1, 0));
+  D[2] = 0.5 * (at(0, 0, 1) - at(0, 0, -1));
+  D[3] = (at(1, 0, 0) + at(-1, 0, 0) - 2.0 * at(0, 0, 0));
+  D[4] = (at(0, 1, 0) + at(0, -1, 0) - 2.0 * at(0, 0, 0));
+  D[5] = (at(0, 0, 1) + at(0, 0, -1) - 2.0 * at(0, 0, 0));
+  D[6] = 0.25 * (at(1, 1, 0) + at(-1, -1, 0) - at(-1, 1, 0) - at(1, -1, 0));
+  D[7] = 0.25 * (at(1, 0, 1) + at(-1, 0, -1) - at(-1, 0, 1) - at(1, 0, -1));
+  D[8] = 0.25 * (at(0, 1, 1) + at(0, -1, -1) - at(0, -1, 1) - at(0, 1, -1));
+}
+
 struct Keypoint {  // VlSiftKeypoint
   int o, ix, iy, is;
   float x, y, s, sigma;
@@ -307,18 +325,11 @@ struct Sift {
         x += dx;
         y += dy;
         pt = dog.data() + (size_t)x + (size_t)y * w + so * (s - s_min);
-        auto at = [&](int ax, int ay, int as) -> double {
-          return *(pt + ax + (ptrdiff_t)ay * w + (ptrdiff_t)as * (ptrdiff_t)so);
-        };
-        Dx = 0.5 * (at(1, 0, 0) - at(-1, 0, 0));
-        Dy = 0.5 * (at(0, 1, 0) - at(0, -1, 0));
-        Ds = 0.5 * (at(0, 0, 1) - at(0, 0, -1));
-        Dxx = (at(1, 0, 0) + at(-1, 0, 0) - 2.0 * at(0, 0, 0));
-        Dyy = (at(0, 1, 0) + at(0, -1, 0) - 2.0 * at(0, 0, 0));
-        Dss = (at(0, 0, 1) + at(0, 0, -1) - 2.0 * at(0, 0, 0));
-        Dxy = 0.25 * (at(1, 1, 0) + at(-1, -1, 0) - at(-1, 1, 0) - at(1, -1, 0));
-        Dxs = 0.25 * (at(1, 0, 1) + at(-1, 0, -1) - at(-1, 0, 1) - at(1, 0, -1));
-        Dys = 0.25 * (at(0, 1, 1) + at(0, -1, -1) - at(0, -1, 1) - at(0, 1, -1));
+        double D[9];
+        refine_terms(pt, w, (ptrdiff_t)so, D);
+        Dx = D[0]; Dy = D[1]; Ds = D[2];
+        Dxx = D[3]; Dyy = D[4]; Dss = D[5];
+        Dxy = D[6]; Dxs = D[7]; Dys = D[8];
         // A column-major: A[i + 3 j]
         A[0] = Dxx; A[4] = Dyy; A[8] = Dss;
         A[3] = A[1] = Dxy;
@@ -751,6 +762,13 @@ uint8_t* to_heap(const std::vector<uint8_t>& v, size_t* n) {
 
 extern "C" {
 
+// Test hook: refine_terms on a 3 x 3 x 3 float patch p[s][y][x] (centre
+// p[1][1][1]) -> the nine derivative terms.
+void oracle_sift_refine_terms(const float* p27, double* out9) {
+  refine_terms(p27 + 13, 3, 9, out9);
+}
+
+
 // SiftExtractionKernel::execute for one frame (height x width x channels
 // bytes, row-major; channels 1, 3 or 4): the keypoints, descriptors and
 // camera elements (io.cc byte layouts), library-allocated (oracle_free).
@@ -758,9 +776,10 @@ int oracle_sift_extract(const uint8_t* frame, int32_t width, int32_t height, int
                         uint64_t image_id, uint8_t** kp_out, size_t* kp_size, uint8_t** desc_out,
                         size_t* desc_size, uint8_t** cam_out, size_t* cam_size) {
   const SiftOpts o;
-  // frames below 16 x 16 are rejected like the product's (4 octaves of an
-  // image that small have no interior pixels left; VLFeat would still run)
-  if (!frame || width < 16 || height < 16 || !(channels == 1 || channels == 3 || channels == 4))
+  // any size >= 1 x 1, as VLFeat (vl_sift_new / vl_sift_process_*_octave put no
+  // floor on it: octaves of an image that small simply have no interior
+  // pixels, so no keypoints, and the op still emits its three elements)
+  if (!frame || width < 1 || height < 1 || !(channels == 1 || channels == 3 || channels == 4))
     return SCM_E_INVALID;
   std::vector<uint8_t> grey;
   frame_to_grey(frame, width, height, channels, &grey);

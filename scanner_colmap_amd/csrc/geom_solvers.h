@@ -168,6 +168,12 @@ SCM_HD inline uint32_t pair_seed(uint32_t base, uint32_t id1, uint32_t id2) {
   return h;
 }
 
+// Base seed of the k-th Estimate of TwoViewGeometry::EstimateMultiple
+// (multiple_models; k = 0 is the plain Estimate's): the reference continues
+// its one time-seeded generator from Estimate to Estimate, so any fresh
+// per-iteration seeding is an equally valid realisation of it.
+SCM_HD inline uint32_t iteration_seed(uint32_t base, uint32_t k) { return base ^ (k * 0x9E3779B1u); }
+
 // Seed of the pair's second stream: the homography LO-RANSAC (and the
 // watermark RANSAC after it) draw from std::mt19937(pair_seed_h(...)), so
 // that the F and H estimations are independent and run concurrently.  (In

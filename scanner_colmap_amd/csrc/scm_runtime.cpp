@@ -582,7 +582,9 @@ int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows,
   return SCM_OK;
 }
 
-VerifyParams make_params(const scm_matching_options& o) {
+// `iteration` > 0: the k-th Estimate of TwoViewGeometry::EstimateMultiple
+// (multiple_models), whose PRNG streams start from geom::iteration_seed.
+VerifyParams make_params(const scm_matching_options& o, int iteration = 0) {
   VerifyParams p;
   std::memset(&p, 0, sizeof(p));
   const double max_error = (double)o.max_error;
@@ -595,7 +597,7 @@ VerifyParams make_params(const scm_matching_options& o) {
   p.min_num_trials = o.min_num_trials;
   p.min_num_inliers = o.min_num_inliers;
   p.detect_watermark = o.detect_watermark;
-  p.base_seed = o.ransac_seed;
+  p.base_seed = geom::iteration_seed(o.ransac_seed, (uint32_t)iteration);
   // RANSAC constructor: max_num_trials capped by ComputeNumTrials at the
   // assumed min_inlier_ratio over 1e5 samples [upstream optim/ransac.h].
   auto cap = [&](double ratio, int kmin) {
@@ -663,7 +665,8 @@ void xcd_order(std::vector<MatchJob>& jobs, const std::vector<PairDesc>& pds) {
 // Buffers are laid out for the worst case (one match slot per pivot
 // keypoint) so nothing waits for the counts.
 int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
-                  const std::vector<PairSpec>& specs, const uint32_t* given, int64_t given_m) {
+                  const std::vector<PairSpec>& specs, const uint32_t* given,
+                  const int32_t* given_counts) {
   const int64_t P = (int64_t)specs.size();
   bs.P = P;
   bs.verify = false;
@@ -689,9 +692,9 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
     int64_t j = i;
     while (j < P && specs[j].a == a) ++j;
     bool clamp = false;
-    // match slots of every pair of this pivot
-    const int32_t slots = given ? (int32_t)std::max<int64_t>(given_m, 1) : t.ndesc[a];
     for (int64_t k = i; k < j; ++k) {
+      // match slots of the pair: every pivot row, or the given list
+      const int32_t slots = given ? std::max<int32_t>(given_counts[k], 1) : t.ndesc[a];
       const int32_t b = specs[k].b;
       PairDesc& pd = pds[k];
       std::memset(&pd, 0, sizeof(pd));
@@ -794,8 +797,11 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   const size_t s_pairs = align256(NJ * sizeof(MatchJob));
   const size_t s_mo = align256(s_pairs + P * sizeof(PairDesc));
   const size_t s_cnt = align256(s_mo + P * sizeof(int64_t));
-  const size_t s_given = align256(s_cnt + sizeof(int32_t));
-  const size_t s_end = s_given + (given ? (size_t)given_m * sizeof(uint2) : 0);
+  int64_t given_m = 0;  // given matches of all pairs (each list at its pair's slots)
+  if (given)
+    for (int64_t k = 0; k < P; ++k) given_m += given_counts[k];
+  const size_t s_given = align256(s_cnt + P * sizeof(int32_t));
+  const size_t s_end = s_given + (given ? (size_t)mo * sizeof(uint2) : 0);
   SCM_TRY(bs.stage.ensure(s_end));
   uint8_t* st = bs.stage.as<uint8_t>();
   if (NJ) std::memcpy(st, jobs.data(), NJ * sizeof(MatchJob));
@@ -812,12 +818,17 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   SCM_HIP(hipMemcpyAsync(bs.match_off.ptr, st + s_mo, P * sizeof(int64_t), hipMemcpyHostToDevice,
                          sm));
   if (given) {
-    const int32_t gm = (int32_t)given_m;
-    std::memcpy(st + s_cnt, &gm, sizeof(gm));
-    SCM_HIP(hipMemcpyAsync(bs.counts.ptr, st + s_cnt, sizeof(int32_t), hipMemcpyHostToDevice, sm));
+    std::memcpy(st + s_cnt, given_counts, P * sizeof(int32_t));
+    SCM_HIP(hipMemcpyAsync(bs.counts.ptr, st + s_cnt, P * sizeof(int32_t), hipMemcpyHostToDevice,
+                           sm));
     if (given_m > 0) {
-      std::memcpy(st + s_given, given, (size_t)given_m * sizeof(uint2));
-      SCM_HIP(hipMemcpyAsync(bs.matches.ptr, st + s_given, (size_t)given_m * sizeof(uint2),
+      uint2* gd = reinterpret_cast<uint2*>(st + s_given);
+      int64_t src = 0;
+      for (int64_t k = 0; k < P; ++k) {
+        std::memcpy(gd + bs.moff[k], given + 2 * src, (size_t)given_counts[k] * sizeof(uint2));
+        src += given_counts[k];
+      }
+      SCM_HIP(hipMemcpyAsync(bs.matches.ptr, st + s_given, (size_t)mo * sizeof(uint2),
                              hipMemcpyHostToDevice, sm));
     }
   }
@@ -872,7 +883,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
 // EstimateUncalibrated), longest first so the launch tail is short, with the
 // LDS sample buffer sized to the largest match count; finally compacts the
 // matches and F-inlier masks into the mapped result buffer.
-int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
+int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 0) {
   bs.verify = verify;
   if (!bs.pending || bs.P == 0) return SCM_OK;
   const int64_t P = bs.P;
@@ -998,7 +1009,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify) {
     SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
                           bs.xy2.as<double>(), bs.scratch.as<double>(), bs.snaps.as<uint32_t>(),
                           bs.masks.as<uint8_t>(), bs.dvout.as<VerifyOut>(),
-                          make_params(ctx->opts), prof, nullptr, bs.xyf.as<float4>(), rbf, rbh,
+                          make_params(ctx->opts, iteration), prof, nullptr, bs.xyf.as<float4>(), rbf, rbh,
                           sv, bs.sev, &bs.nwin));
   }
   SCM_HIP(hipEventRecord(bs.ev[5], sv));
@@ -1071,9 +1082,9 @@ int collect_batch(scm_context* ctx, BatchSet& bs, BatchView* v) {
 // Both stages of one batch, then its results (single-pair / stencil calls).
 int run_batch(scm_context* ctx, BatchSet& bs, const ImageTable& t,
               const std::vector<PairSpec>& specs, bool verify, const uint32_t* given,
-              int64_t given_m, BatchView* v) {
-  SCM_TRY(enqueue_match(ctx, bs, t, specs, given, given_m));
-  SCM_TRY(enqueue_verify(ctx, bs, verify));
+              const int32_t* given_counts, BatchView* v, int iteration = 0) {
+  SCM_TRY(enqueue_match(ctx, bs, t, specs, given, given_counts));
+  SCM_TRY(enqueue_verify(ctx, bs, verify, iteration));
   return collect_batch(ctx, bs, v);
 }
 
@@ -1182,6 +1193,129 @@ int serialize_rows(scm_context* ctx, const BatchView& v, const std::vector<uint3
     out->row_off.push_back((int64_t)(rstart[r] + 8 + 4 * (pairs_begin[r + 1] - pairs_begin[r])));
   }
   out->size = at;
+  return SCM_OK;
+}
+
+// ---------------------------------------------------------------------------
+// TwoViewGeometry::EstimateMultiple [upstream estimators/two_view_geometry.cc],
+// taken by verifyTwoViewGeometry when multiple_models is set
+// (sequential_matching.cc:94-96):
+//   remaining = matches
+//   loop: g = Estimate(remaining); stop if g.config == DEGENERATE;
+//         keep g unless it is WATERMARK (Options::multiple_ignore_watermark,
+//         COLMAP's default true; the op does not set it);
+//         remaining = ExtractOutlierMatches(remaining, g.inlier_matches)
+//   none kept -> DEGENERATE; one -> that geometry; more -> MULTIPLE with the
+//   kept geometries' inlier matches concatenated (F, H left unset: zeros).
+// The batch's own verification is the first Estimate; every later one runs
+// for all still-active pairs of the batch together as a batch of given
+// match lists on the same set, with the iteration's PRNG seeds
+// (geom::iteration_seed).  One deviation: the reference loops forever when a
+// non-degenerate Estimate removes no match (F failed, H succeeded); here the
+// pair stops.
+struct Geom {
+  int32_t config = 0;
+  double F[9] = {0}, H[9] = {0};
+  std::vector<Match> inliers;
+};
+
+// The Estimate of pair p in view v on the match list `cur` (= the view's
+// matches of p): appends the kept geometry and sets `cur` to the outliers;
+// false when EstimateMultiple stops for the pair.
+bool take_estimate(const scm_matching_options& o, const BatchView& v, int64_t p,
+                   std::vector<Geom>* geoms, std::vector<Match>* cur) {
+  const int32_t n = v.counts[p];
+  const int32_t mni = o.min_num_inliers;
+  if (!v.vout || n < std::max(1, mni)) return false;  // Estimate: DEGENERATE (too few)
+  const VerifyOut& vo = v.vout[p];
+  if (vo.raw_config == SCM_TVG_DEGENERATE || vo.raw_config == 0) return false;
+  const Match* m = v.matches + v.offsets[p];
+  const uint8_t* mk = v.masks + v.offsets[p];
+  const bool f_ok = vo.f_inliers_raw >= 7;  // ExtractInlierMatches of a successful F report
+  Geom g;
+  g.config = vo.raw_config;
+  std::memcpy(g.F, vo.F, sizeof(g.F));
+  std::memcpy(g.H, vo.H, sizeof(g.H));
+  std::vector<Match> out;
+  for (int32_t i = 0; i < n; ++i) {
+    if (f_ok && mk[i]) g.inliers.push_back(m[i]);
+    else out.push_back(m[i]);
+  }
+  const bool removed = !g.inliers.empty();
+  if (g.config != SCM_TVG_WATERMARK) geoms->push_back(std::move(g));
+  cur->swap(out);
+  return removed && (int64_t)cur->size() >= std::max(1, mni);
+}
+
+int estimate_multiple(scm_context* ctx, BatchSet& bs, const BatchView& v0, std::vector<Tvg>* tvgs) {
+  const int64_t P = v0.P;
+  const ImageTable& t = *bs.table;
+  const std::vector<PairSpec> specs = bs.specs;  // bs is reused by the later iterations
+  std::vector<std::vector<Geom>> geoms(P);
+  std::vector<std::vector<Match>> rem(P);
+  std::vector<int64_t> active;
+  for (int64_t p = 0; p < P; ++p)
+    if (take_estimate(ctx->opts, v0, p, &geoms[p], &rem[p])) active.push_back(p);
+  for (int it = 1; !active.empty(); ++it) {
+    std::vector<PairSpec> sp;
+    std::vector<int32_t> cnt;
+    std::vector<Match> all;
+    for (int64_t p : active) {
+      sp.push_back(specs[p]);
+      cnt.push_back((int32_t)rem[p].size());
+      all.insert(all.end(), rem[p].begin(), rem[p].end());
+    }
+    BatchView v;
+    SCM_TRY(run_batch(ctx, bs, t, sp, true, reinterpret_cast<const uint32_t*>(all.data()),
+                      cnt.data(), &v, it));
+    std::vector<int64_t> next;
+    for (size_t q = 0; q < active.size(); ++q)
+      if (take_estimate(ctx->opts, v, (int64_t)q, &geoms[active[q]], &rem[active[q]]))
+        next.push_back(active[q]);
+    active.swap(next);
+  }
+  tvgs->assign(P, Tvg());
+  for (int64_t p = 0; p < P; ++p) {
+    Tvg& tv = (*tvgs)[p];
+    const std::vector<Geom>& g = geoms[p];
+    if (g.size() == 1) {
+      tv.config = g[0].config;
+      std::memcpy(tv.F, g[0].F, sizeof(tv.F));
+      std::memcpy(tv.H, g[0].H, sizeof(tv.H));
+      tv.inlier_matches = g[0].inliers;
+    } else if (g.size() > 1) {
+      tv.config = SCM_TVG_MULTIPLE;
+      for (const Geom& x : g) tv.inlier_matches.insert(tv.inlier_matches.end(), x.inliers.begin(),
+                                                        x.inliers.end());
+    } else {
+      tv.config = SCM_TVG_DEGENERATE;  // none kept
+    }
+    // the op's post-filter (sequential_matching.cc:173-178)
+    if ((int64_t)tv.inlier_matches.size() < (int64_t)ctx->opts.min_num_inliers) tv = Tvg();
+  }
+  return SCM_OK;
+}
+
+// serialize_rows for host geometries (the multiple_models path).
+int serialize_rows_tvg(const std::vector<Tvg>& tv, const std::vector<uint32_t>& pair_ids,
+                       const std::vector<int64_t>& pairs_begin, Packed* out) {
+  const int64_t nrows = (int64_t)pairs_begin.size() - 1;
+  for (int64_t r = 0; r < nrows; ++r) {
+    const int64_t pb = pairs_begin[r], pe = pairs_begin[r + 1];
+    const std::vector<uint8_t> a =
+        id_list_bytes(std::vector<uint32_t>(pair_ids.begin() + pb, pair_ids.begin() + pe));
+    const std::vector<uint8_t> b = tvg_list_bytes(std::vector<Tvg>(tv.begin() + pb, tv.begin() + pe));
+    if (!out->reserve(out->size + a.size() + b.size())) {
+      set_error("output allocation failed");
+      return SCM_E_NOMEM;
+    }
+    out->row_off.push_back((int64_t)out->size);
+    std::memcpy(out->data + out->size, a.data(), a.size());
+    out->size += a.size();
+    out->row_off.push_back((int64_t)out->size);
+    std::memcpy(out->data + out->size, b.data(), b.size());
+    out->size += b.size();
+  }
   return SCM_OK;
 }
 
@@ -1348,7 +1482,6 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
   auto finish = [&](const Batch& b, BatchSet& bs) -> int {
     BatchView v;
     SCM_TRY(collect_batch(ctx, bs, &v));
-    SCM_TRY(serialize_rows(ctx, v, b.pair_ids, b.pairs_begin, out));
     if (keep)
       for (int64_t p = 0; p < v.P; ++p) {
         const int64_t row = b.specs[p].a, o = v.offsets[p];
@@ -1356,7 +1489,12 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
         ctx->last_matches[row - row_begin].push_back(
             {b.specs[p].b - row, std::vector<Match>(v.matches + o, v.matches + o + v.counts[p])});
       }
-    return SCM_OK;
+    if (ctx->opts.multiple_models) {  // the later Estimates reuse bs: v is consumed first
+      std::vector<Tvg> tv;
+      SCM_TRY(estimate_multiple(ctx, bs, v, &tv));
+      return serialize_rows_tvg(tv, b.pair_ids, b.pairs_begin, out);
+    }
+    return serialize_rows(ctx, v, b.pair_ids, b.pairs_begin, out);
   };
   out->row_off.reserve(2 * nr + 1);
   // Three buffer sets: at step k the GPU holds match(k) on the matching
@@ -1367,14 +1505,14 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
     for (size_t k = 0; k < B; ++k) {
       BatchSet& bs = ctx->sets[k % 3];
       if (k >= 3) SCM_TRY(finish(batches[k - 3], bs));
-      SCM_TRY(enqueue_match(ctx, bs, t, batches[k].specs, nullptr, 0));
+      SCM_TRY(enqueue_match(ctx, bs, t, batches[k].specs, nullptr, nullptr));
       SCM_TRY(enqueue_verify(ctx, bs, true));
       if (bs.pending) SCM_HIP(hipStreamWaitEvent(ctx->stream, bs.ev[6], 0));
     }
   } else {
     for (size_t k = 0; k < B; ++k) {
       if (k >= 3) SCM_TRY(finish(batches[k - 3], ctx->sets[(k - 3) % 3]));
-      SCM_TRY(enqueue_match(ctx, ctx->sets[k % 3], t, batches[k].specs, nullptr, 0));
+      SCM_TRY(enqueue_match(ctx, ctx->sets[k % 3], t, batches[k].specs, nullptr, nullptr));
       if (k >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(k - 1) % 3], true));
     }
     if (B >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(B - 1) % 3], true));
@@ -1431,10 +1569,6 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
     o = *opts;
   else
     scm_default_options(&o);
-  if (o.multiple_models) {
-    set_error("multiple_models (TwoViewGeometry::EstimateMultiple) is not supported");
-    return SCM_E_INVALID;
-  }
   scm_context* ctx = new scm_context();
   ctx->device = device_index;
   ctx->opts = o;
@@ -1539,7 +1673,7 @@ int scm_match_pair(scm_context* ctx, const uint8_t* desc1, int64_t n1, const uin
   SCM_TRY(upload_table(ctx, &ctx->scratch_table, rows, true, false));
   BatchSet& bs = ctx->sets[0];
   BatchView v;
-  const int rc = run_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, false, nullptr, 0, &v);
+  const int rc = run_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, false, nullptr, nullptr, &v);
   if (rc != SCM_OK) {
     drain(ctx);
     return rc;
@@ -1583,8 +1717,17 @@ int scm_verify_pair(scm_context* ctx, const float* kp1, int64_t n1, const float*
   SCM_TRY(upload_table(ctx, &ctx->scratch_table, rows, false, true));
   BatchSet& bs = ctx->sets[0];
   BatchView v;
-  const int rc =
-      run_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, true, matches, num_matches, &v);
+  const int32_t gm = (int32_t)num_matches;
+  int rc = run_batch(ctx, bs, ctx->scratch_table, {{0, 1}}, true, matches, &gm, &v);
+  if (rc == SCM_OK && ctx->opts.multiple_models) {
+    std::vector<Tvg> tv;
+    rc = estimate_multiple(ctx, bs, v, &tv);
+    if (rc == SCM_OK) {
+      std::vector<uint8_t> bytes;
+      append_tvg(&bytes, tv[0]);
+      return make_blob(bytes, tvg_out);
+    }
+  }
   if (rc != SCM_OK) {
     drain(ctx);
     return rc;

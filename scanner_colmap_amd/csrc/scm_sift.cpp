@@ -17,6 +17,8 @@
 // same pipeline on the smaller grey image.
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 
@@ -28,7 +30,6 @@ namespace scm {
 namespace {
 
 constexpr int kMaxImageSize = 3200;  // SiftExtractionOptions::max_image_size
-constexpr int kMinImageSize = 16;    // 4 octaves need >= 2 interior pixels in the last
 constexpr int kMaxNumFeatures = 8192;
 constexpr double kPeakThreshold = 0.02 / 3;
 constexpr double kEdgeThreshold = 10.0;
@@ -41,6 +42,7 @@ struct Slot {
   int rtab_w = 0, rtab_h = 0;  // source size the uploaded tables are for
   SiftDev dev{};
   int64_t nel_cap = 0;  // first-octave pixels the workspace holds
+  int cap_scale = 1;    // candidate / keypoint / feature capacities x this (grown on overflow)
   int64_t pending = -1; // frame index whose results are in flight
   int w = 0, h = 0;
 };
@@ -56,6 +58,9 @@ T* carve(uint8_t*& p, size_t n) {
 
 struct SiftState {
   int device = 0;
+  // initial candidate / keypoint / feature capacities (0: sized by the
+  // frame); SCM_SIFT_CAPS=c,k,f sets them (tests: force the overflow path)
+  int caps[3] = {0, 0, 0};
   DevBuf consts;
   SiftConsts c{};
   int widths[6] = {0, 0, 0, 0, 0, 0};
@@ -168,12 +173,21 @@ int bilinear_table(int dst, int src, std::vector<int32_t>* hdr, std::vector<doub
 }
 
 // Workspace of a slot for a frame whose first octave has nel pixels (2w x 2h).
-int ensure_slot(Slot& sl, int w, int h) {
+// Capacities: candidates of one octave, its refined keypoints and their
+// features (<= 2 orientations each), times the slot's cap_scale, which grows
+// whenever a frame overflows them (the frame is then extracted again: the
+// reference has no capacity limit, extraction_op.cc:71-120).
+int ensure_slot(const SiftState* s, Slot& sl, int w, int h) {
   const int64_t ow = 2 * (int64_t)w, oh = 2 * (int64_t)h, nel = ow * oh;
   if (nel <= sl.nel_cap && sl.dev.cnt) return SCM_OK;
-  const int cand_cap = (int)std::min<int64_t>(std::max<int64_t>(65536, nel / 16), 1 << 22);
-  const int key_cap = std::min(cand_cap, 1 << 18);
-  const int feat_cap = 2 * key_cap;
+  const int64_t sc = sl.cap_scale;
+  const int64_t c0 = s->caps[0] ? s->caps[0] : std::min<int64_t>(std::max<int64_t>(65536, nel / 16), 1 << 22);
+  const int64_t k0 = s->caps[1] ? s->caps[1] : std::min<int64_t>(c0, 1 << 18);
+  const int64_t f0 = s->caps[2] ? s->caps[2] : 2 * k0;
+  // every octave pixel of the 3 detection levels is at most one candidate
+  const int cand_cap = (int)std::min<int64_t>(c0 * sc, 3 * nel + 64);
+  const int key_cap = (int)std::min<int64_t>(k0 * sc, cand_cap);
+  const int feat_cap = (int)std::min<int64_t>(f0 * sc, 4 * (int64_t)key_cap);
   const size_t bytes = 18 * (size_t)nel * 4 + 2 * (3 * (size_t)oh + 1) * 4 +
                        (size_t)cand_cap * (16 + 32 + 8) +
                        (size_t)key_cap * (32 + 4 + 16 + 4) +
@@ -288,7 +302,7 @@ int enqueue_frame(SiftState* s, Slot& sl, const scm_frame& f) {
   int w, h;
   fit_size(fw, fh, &w, &h);
   int ch = f.channels;
-  SCM_TRY(ensure_slot(sl, w, h));
+  SCM_TRY(ensure_slot(s, sl, std::max(w, 1), std::max(h, 1)));
   const size_t fb = (size_t)fw * fh * ch;
   SCM_TRY(sl.pin_in.ensure(fb));
   SCM_TRY(sl.frame.ensure(fb));
@@ -303,12 +317,17 @@ int enqueue_frame(SiftState* s, Slot& sl, const scm_frame& f) {
   }
   SiftDev& d = sl.dev;
   int ow = 2 * w, oh = 2 * h, pw = 0, ph = 0;  // this octave's and the previous octave's size
-  for (int o = -1; o < kSiftOctaves - 1; ++o) {
+  // A frame of any size >= 1 x 1 runs, as VLFeat's filter does: octaves too
+  // small for an interior pixel detect nothing, and an octave with no pixel
+  // (width or height >> o == 0) ends the octaves -- VLFeat still steps
+  // through it, on empty images.  (A rescale to a zero size leaves no octave.)
+  for (int o = -1; o < kSiftOctaves - 1 && w > 0 && h > 0; ++o) {
     if (o >= 0) {  // VLFeat octave size: width >> o (width << 1 for o = -1)
       pw = ow;
       ph = oh;
       ow = w >> o;
       oh = h >> o;
+      if (ow == 0 || oh == 0) break;
     }
     const size_t so = (size_t)ow * oh;
     if (o == -1) {
@@ -340,14 +359,14 @@ void put(std::vector<uint8_t>* b, const T& v) {
   b->insert(b->end(), q, q + sizeof(T));
 }
 
-// Wait for a slot's frame and write its three elements.
-int harvest(Slot& sl, uint64_t image_id, scm_blob* kp_out, scm_blob* desc_out, scm_blob* cam_out) {
+// Wait for a slot's frame and write its three elements; *overflow (and
+// nothing written) when the frame exceeded the slot's capacities.
+int harvest(Slot& sl, uint64_t image_id, scm_blob* kp_out, scm_blob* desc_out, scm_blob* cam_out,
+            bool* overflow) {
   SCM_HIP(hipStreamSynchronize(sl.st));
   const SiftCounts cnt = *sl.pin_cnt.as<SiftCounts>();
-  if (cnt.overflow) {
-    set_error("sift: a frame exceeded the extractor's candidate / keypoint capacity");
-    return SCM_E_CAPACITY;
-  }
+  *overflow = cnt.overflow != 0;
+  if (*overflow) return SCM_OK;
   const int nf = cnt.nfeat;
   // COLMAP: keep the coarsest DoG levels; the level whose keypoints first push
   // the count past max_num_features is kept whole.
@@ -406,6 +425,21 @@ int harvest(Slot& sl, uint64_t image_id, scm_blob* kp_out, scm_blob* desc_out, s
 
 }  // namespace
 
+// Harvest of slot sl's frame j; on overflow the slot's capacities grow and the
+// frame is extracted again (synchronously) until it fits.
+int harvest_or_regrow(SiftState* s, Slot& sl, int64_t j, const uint64_t* ids,
+                      const scm_frame* frames, scm_blob* kp_out, scm_blob* desc_out,
+                      scm_blob* cam_out) {
+  for (;;) {
+    bool overflow = false;
+    SCM_TRY(harvest(sl, ids[j], &kp_out[j], &desc_out[j], &cam_out[j], &overflow));
+    if (!overflow) return SCM_OK;
+    sl.cap_scale *= 4;
+    sl.nel_cap = 0;  // re-layout the workspace with the larger capacities
+    SCM_TRY(enqueue_frame(s, sl, frames[j]));
+  }
+}
+
 int sift_extract_frames(SiftState** state, int device, int64_t n, const uint64_t* ids,
                         const scm_frame* frames, scm_blob* kp_out, scm_blob* desc_out,
                         scm_blob* cam_out) {
@@ -415,17 +449,10 @@ int sift_extract_frames(SiftState** state, int device, int64_t n, const uint64_t
   }
   for (int64_t i = 0; i < n; ++i) {
     const scm_frame& f = frames[i];
-    if (!f.data || !(f.channels == 1 || f.channels == 3 || f.channels == 4) ||
-        f.width < kMinImageSize || f.height < kMinImageSize) {
+    if (!f.data || !(f.channels == 1 || f.channels == 3 || f.channels == 4) || f.width < 1 ||
+        f.height < 1) {
       set_error("scm_extract_frames: frame " + std::to_string(i) +
-                " is not a >= 16 x 16 frame of 1, 3 or 4 channels");
-      return SCM_E_INVALID;
-    }
-    int nw, nh;
-    fit_size(f.width, f.height, &nw, &nh);
-    if (nw < kMinImageSize || nh < kMinImageSize) {
-      set_error("scm_extract_frames: frame " + std::to_string(i) +
-                " is below 16 x 16 after the max_image_size rescale");
+                " is not a non-empty frame of 1, 3 or 4 channels");
       return SCM_E_INVALID;
     }
   }
@@ -433,31 +460,45 @@ int sift_extract_frames(SiftState** state, int device, int64_t n, const uint64_t
   if (!*state) {
     std::unique_ptr<SiftState> s(new SiftState());
     s->device = device;
+    if (const char* e = std::getenv("SCM_SIFT_CAPS"))
+      std::sscanf(e, "%d,%d,%d", &s->caps[0], &s->caps[1], &s->caps[2]);
     SCM_TRY(init_state(s.get()));
     *state = s.release();
   }
   SiftState* s = *state;
   for (Slot& sl : s->slots) sl.pending = -1;
+  for (int64_t i = 0; i < n; ++i) kp_out[i] = desc_out[i] = cam_out[i] = scm_blob{nullptr, 0};
   int rc = SCM_OK;
   for (int64_t i = 0; i < n && rc == SCM_OK; ++i) {
     Slot& sl = s->slots[i % kSlots];
     if (sl.pending >= 0) {
       const int64_t j = sl.pending;
       sl.pending = -1;
-      rc = harvest(sl, ids[j], &kp_out[j], &desc_out[j], &cam_out[j]);
+      rc = harvest_or_regrow(s, sl, j, ids, frames, kp_out, desc_out, cam_out);
       if (rc != SCM_OK) break;
     }
     rc = enqueue_frame(s, sl, frames[i]);
     if (rc == SCM_OK) sl.pending = i;
   }
+  // Every slot still holding a frame is drained, on error too (its stream
+  // finishes before the caller's buffers can go away).
   for (int64_t i = std::max<int64_t>(0, n - kSlots); i < n; ++i) {
     Slot& sl = s->slots[i % kSlots];
     if (sl.pending == i) {
       sl.pending = -1;
-      const int r = harvest(sl, ids[i], &kp_out[i], &desc_out[i], &cam_out[i]);
-      if (rc == SCM_OK) rc = r;
+      if (rc == SCM_OK) rc = harvest_or_regrow(s, sl, i, ids, frames, kp_out, desc_out, cam_out);
     }
   }
+  for (Slot& sl : s->slots) {
+    if (sl.st) (void)hipStreamSynchronize(sl.st);
+    sl.pending = -1;
+  }
+  if (rc != SCM_OK)  // no partial output: free what earlier frames produced
+    for (int64_t i = 0; i < n; ++i) {
+      scm_blob_free(&kp_out[i]);
+      scm_blob_free(&desc_out[i]);
+      scm_blob_free(&cam_out[i]);
+    }
   return rc;
 }
 

@@ -297,7 +297,10 @@ __global__ __launch_bounds__(64) void refine_kernel(const float* __restrict__ do
       x += dx;
       y += dy;
       pt = dog + (size_t)x + (size_t)y * w + so * (size_t)(s - kSMin);
-#define AT(ax, ay, as) ((double)*(pt + (ax) + (ptrdiff_t)(ay) * w + (ptrdiff_t)(as) * (ptrdiff_t)so))
+// VLFeat's at() reads vl_sift_pix (float): sums and differences of samples
+// round in float, and only the products with the double literals (0.5, 2.0,
+// 0.25) widen to double -- C's usual arithmetic conversions, kept here.
+#define AT(ax, ay, as) (*(pt + (ax) + (ptrdiff_t)(ay) * w + (ptrdiff_t)(as) * (ptrdiff_t)so))
       Dx = 0.5 * (AT(1, 0, 0) - AT(-1, 0, 0));
       Dy = 0.5 * (AT(0, 1, 0) - AT(0, -1, 0));
       Ds = 0.5 * (AT(0, 0, 1) - AT(0, 0, -1));

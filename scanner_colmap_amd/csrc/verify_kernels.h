@@ -56,7 +56,8 @@ struct VerifyOut {
   int32_t num_inliers;   // F inliers = |inlier_matches| (0 after the post-filter)
   int32_t f_trials, h_trials;
   int32_t f_inliers_raw, h_inliers_raw;
-  int32_t watermark, pad_;
+  int32_t watermark;
+  int32_t raw_config;    // Estimate's configuration before the op's post-filter
   double F[9];
   double H[9];
   // (model, point) residual evaluations the sequential LO-RANSAC scores up to

@@ -1590,6 +1590,7 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
     o->config = keep ? config : 0;
     o->num_inliers = keep ? num_inliers : 0;
     o->watermark = watermark;
+    o->raw_config = config;  // EstimateMultiple (multiple_models) reads the unfiltered result
   }
   if (!keep && lane < 9) {
     o->F[lane] = 0.0;

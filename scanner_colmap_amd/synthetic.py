@@ -185,7 +185,11 @@ def geometry_scene(kind: str, num_matches: int, seed: int, outlier_frac: float =
                      put every inlier "in the border", SURVEY.md §8a a14);
     * "random":      no geometry at all: F and H both find < 15 inliers
                      -> DEGENERATE (1), which the op's post-filter turns into
-                     TwoViewGeometry() (config 0).
+                     TwoViewGeometry() (config 0);
+    * "two_motions": a static 3-D scene (60 % of the matches) and an object
+                     moving on its own (the rest before the outliers): two
+                     epipolar geometries, so EstimateMultiple (multiple_models)
+                     finds both -> MULTIPLE (8); plain Estimate -> UNCALIBRATED.
 
     Returns (kp1 N x 6, kp2 N x 6, matches M x 2 uint32); keypoint order is
     shuffled so the match indices are not the identity."""
@@ -200,17 +204,23 @@ def geometry_scene(kind: str, num_matches: int, seed: int, outlier_frac: float =
         x2 = x1 + np.array([37.5, -12.25])
     elif kind == "random":
         x2 = np.stack([rng.uniform(0, 1920, m), rng.uniform(0, 1080, m)], axis=1)
-    elif kind == "general":
+    elif kind in ("general", "two_motions"):
         X = np.stack([rng.uniform(-4, 4, m), rng.uniform(-2.5, 2.5, m), rng.uniform(6, 20, m)], 1)
         f = 1200.0
 
-        def proj(R, c):
-            Xc = (X - c) @ R.T
+        def proj(R, c, P=None):
+            Xc = ((X if P is None else P) - c) @ R.T
             return np.stack([f * Xc[:, 0] / Xc[:, 2] + 960, f * Xc[:, 1] / Xc[:, 2] + 540], 1)
         a = 0.12
         R2 = np.array([[np.cos(a), 0, np.sin(a)], [0, 1, 0], [-np.sin(a), 0, np.cos(a)]])
         x1 = proj(np.eye(3), np.zeros(3))
         x2 = proj(R2, np.array([1.5, 0.2, 0.3]))
+        if kind == "two_motions":  # the last 40 %: an object rotating and sliding on its own
+            k = int(round(0.6 * m))
+            b = -0.2
+            Rb = np.array([[1, 0, 0], [0, np.cos(b), -np.sin(b)], [0, np.sin(b), np.cos(b)]])
+            Xo = (X[k:] - np.array([0.0, 0.0, 12.0])) @ Rb.T + np.array([-1.2, 0.8, 12.5])
+            x2[k:] = proj(R2, np.array([1.5, 0.2, 0.3]), Xo)
     else:
         raise ValueError(kind)
     x2 = x2 + rng.normal(0, noise_px, x2.shape)

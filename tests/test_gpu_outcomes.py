@@ -57,14 +57,17 @@ def test_execute_stencil_repeated_ids(gpu_ctx):
 
 @pytest.mark.parametrize("kw", [dict(detect_watermark=0), dict(min_num_inliers=40),
                                 dict(max_error=2.0), dict(confidence=0.99, max_num_trials=500),
-                                dict(max_H_inlier_ratio=0.95), dict(ransac_seed=12345)])
+                                dict(max_H_inlier_ratio=0.95), dict(ransac_seed=12345),
+                                dict(multiple_models=1),
+                                dict(multiple_models=1, detect_watermark=0, ransac_seed=7)])
 def test_verify_option_variants(kw):
     o_gpu, o_ref = default_options(), oracle.default_options()
     for k, v in kw.items():
         setattr(o_gpu, k, v)
         setattr(o_ref, k, v)
     with Context(0, o_gpu) as ctx:
-        for kind, m, seed in (("translation", 300, 2), ("planar", 300, 1), ("general", 500, 3)):
+        for kind, m, seed in (("translation", 300, 2), ("planar", 300, 1), ("general", 500, 3),
+                              ("two_motions", 400, 21), ("general", 600, 22)):
             kp1, kp2, mt = geometry_scene(kind, m, seed)
             got = ctx.verify_pair(kp1, kp2, mt, 3, 4)
             assert got == oracle.verify_pair(kp1, kp2, mt, 3, 4, o_ref), (kw, kind)
@@ -92,3 +95,34 @@ def test_pair_with_more_than_65535_matches(gpu_ctx):
     assert got_m.shape == mt.shape and (got_m == mt).all()
     # the row's two_view_geometries element: size_t total, int count, then the TVG
     assert got_tvg[0][12:] == oracle.verify_pair(kp1, kp2, got_m, 3, 4)
+
+
+@pytest.mark.parametrize("batch_pairs", [None, "3"])
+def test_multiple_models_table_path(batch_pairs):
+    """EstimateMultiple (multiple_models) through the table path: every pair
+    of a batch runs its later Estimates together as given-match batches; rows
+    byte-equal to the oracle's, including MULTIPLE (8) rows; small batches put
+    several pipelined batches in flight."""
+    import os
+    scenes = [geometry_scene(k, m, s) for k, m, s in (("two_motions", 400, 21), ("general", 600, 22),
+                                                       ("translation", 300, 2), ("planar", 300, 1),
+                                                       ("two_motions", 300, 23))]
+    imgs = []
+    for i, (kp1, kp2, mt) in enumerate(scenes):
+        d1, d2 = descriptors_for_matches(mt, len(kp1), len(kp2), 40 + i)
+        imgs += [(100 + 2 * i, kp1, d1), (101 + 2 * i, kp2, d2)]
+    ids, kps, descs = table_rows(imgs)
+    o_gpu, o_ref = default_options(), oracle.default_options()
+    o_gpu.multiple_models = o_ref.multiple_models = 1
+    ref = oracle.table_run(ids, kps, descs, 2, 0, len(imgs), o_ref)
+    if batch_pairs:
+        os.environ["SCM_BATCH_PAIRS"] = batch_pairs
+    try:
+        with Context(0, o_gpu) as ctx:
+            ctx.table_load(ids, kps, descs)
+            got = ctx.table_run(2, 0, len(imgs))
+    finally:
+        os.environ.pop("SCM_BATCH_PAIRS", None)
+    assert got == ref
+    configs = [t.config for row in got[1] for t in decode_tvg_list(row)]
+    assert configs.count(8) >= 2

@@ -108,9 +108,32 @@ def test_oversize_frames_rescaled_bit_exact(ctx, h, w, ch, seed):
     assert got[1] == oracle.sift_extract(f[:120, :160], seed + 1)
 
 
-def test_rejects_tiny_frames(ctx):
-    from scanner_colmap_amd import ScmError
-    with pytest.raises(ScmError):
-        ctx.extract_frames([np.zeros((15, 40, 3), np.uint8)])
-    with pytest.raises(ScmError):  # 15 rows become 14 after the max_image_size rescale
-        ctx.extract_frames([np.zeros((15, 3300, 3), np.uint8)])
+@pytest.mark.parametrize("h,w,ch", [(15, 40, 3), (40, 15, 1), (9, 9, 4), (5, 7, 3), (1, 1, 1),
+                                    (1, 200, 3), (16, 17, 3), (15, 3300, 3)])
+def test_tiny_and_thin_frames_bit_exact(ctx, h, w, ch):
+    """Frames VLFeat accepts whose octaves have few or no interior pixels
+    (the reference has no size floor, extraction_op.cc:71-120), including one
+    the max_image_size rescale leaves 14 rows tall: elements byte-equal to
+    the oracle's (no keypoints, or a handful, and the camera)."""
+    f = np.ascontiguousarray(synthetic_frame(max(h, 64), max(w, 64), 70 + h + w, channels=ch)[:h, :w])
+    got = ctx.extract_frames([f], [9])[0]
+    ref = oracle.sift_extract(f, 9)
+    _diff(got, ref, f"{h}x{w}x{ch}")
+    assert got == ref
+
+
+def test_capacity_overflow_regrows(ctx):
+    """Candidate / keypoint / feature capacities far below a frame's needs
+    (SCM_SIFT_CAPS): the overflowing frames are extracted again with larger
+    capacities, never SCM_E_CAPACITY, and every element equals the oracle's."""
+    import os
+    from scanner_colmap_amd import Context
+    frames = [synthetic_frame(240, 320, 90 + i) for i in range(6)]
+    os.environ["SCM_SIFT_CAPS"] = "64,16,16"
+    try:
+        with Context(0) as c2:
+            got = c2.extract_frames(frames, list(range(6)))
+    finally:
+        del os.environ["SCM_SIFT_CAPS"]
+    for i, f in enumerate(frames):
+        assert got[i] == oracle.sift_extract(f, i), i

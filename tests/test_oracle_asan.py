@@ -53,3 +53,21 @@ def test_oracle_table_run_under_asan(tmp_path, n, kpts, overlap, seed):
     ref_ids, ref_tvg = oracle.table_run(ids, kps, descs, overlap, 0, n)
     assert got[0::2] == ref_ids
     assert got[1::2] == ref_tvg
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("w,h,c", [(15, 40, 3), (40, 15, 1), (9, 9, 4), (5, 7, 3), (1, 1, 1),
+                                   (1, 200, 3), (2, 50, 1), (17, 16, 3), (3301, 9, 1)])
+def test_oracle_sift_tiny_and_thin_frames_under_asan(w, h, c):
+    """The SIFT extraction restatement on frames VLFeat accepts but whose
+    octaves have few or no interior pixels (and a frame that the
+    max_image_size rescale makes 1 row tall): no sanitizer report."""
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR, "asan"], check=True)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:abort_on_error=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([DRIVER, "--sift", str(w), str(h), str(c), "7"], env=env,
+                       capture_output=True, text=True, timeout=580)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "runtime error" not in r.stderr and "AddressSanitizer" not in r.stderr, r.stderr[-4000:]
+    nk, nd, nc = map(int, r.stdout.split())
+    assert (nk - 8) % 24 == 0 and nd == 16 + 128 * ((nk - 8) // 24) and nc == 73

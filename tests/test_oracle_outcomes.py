@@ -55,3 +55,51 @@ def test_watermark_off_keeps_planar():
     o.detect_watermark = 0
     kp1, kp2, m = geometry_scene("translation", 300, 2)
     assert oracle.verify_pair_config(kp1, kp2, m, 1, 2, o)[0] == 6
+
+
+# --- EstimateMultiple (multiple_models, sequential_matching.cc:94-96) ----------
+def _multi():
+    o = oracle.default_options()
+    o.multiple_models = 1
+    return o
+
+
+@pytest.mark.parametrize("m,seed", [(400, 21), (300, 23), (600, 22)])
+def test_multiple_models_two_motions(m, seed):
+    """A static scene plus an object moving on its own: plain Estimate keeps the
+    larger motion (UNCALIBRATED); EstimateMultiple estimates again on its
+    outliers, finds the object's epipolar geometry, and returns MULTIPLE (8)
+    with both inlier sets concatenated in estimation order and F = H = 0."""
+    kp1, kp2, mt = geometry_scene("two_motions", m, seed)
+    one = decode_tvg(oracle.verify_pair(kp1, kp2, mt, 3, 4))
+    multi = decode_tvg(oracle.verify_pair(kp1, kp2, mt, 3, 4, _multi()))
+    assert one.config == 3 and multi.config == 8
+    assert not multi.F.any() and not multi.H.any()
+    k = len(one.inlier_matches)
+    # the first estimate is the plain one (iteration seed 0): its inliers lead
+    assert (multi.inlier_matches[:k] == one.inlier_matches).all()
+    rest = multi.inlier_matches[k:]
+    assert len(rest) >= 15
+    # the two inlier sets are disjoint (the second estimate ran on the outliers)
+    a = {tuple(x) for x in one.inlier_matches.tolist()}
+    assert not a & {tuple(x) for x in rest.tolist()}
+    # most of the second set is the object's matches (the last 40 % before
+    # shuffling map to the moving points: match index in the scene order)
+    assert len(rest) >= 0.8 * (m - int(round(0.6 * m)) - int(round(0.2 * m)))
+
+
+def test_multiple_models_single_geometry_equals_estimate():
+    """A planar scene's outliers hold no second geometry: EstimateMultiple keeps
+    one geometry, byte-equal to the plain Estimate."""
+    kp1, kp2, mt = geometry_scene("planar", 300, 1)
+    assert oracle.verify_pair(kp1, kp2, mt, 3, 4, _multi()) == oracle.verify_pair(kp1, kp2, mt, 3, 4)
+
+
+def test_multiple_models_ignores_watermark_geometries():
+    """multiple_ignore_watermark (COLMAP's default): a WATERMARK estimate is
+    not kept, its inliers are still removed; with nothing else to find the
+    pair ends DEGENERATE -> TwoViewGeometry() after the post-filter."""
+    kp1, kp2, mt = geometry_scene("translation", 300, 2)
+    assert decode_tvg(oracle.verify_pair(kp1, kp2, mt, 3, 4)).config == 7
+    t = decode_tvg(oracle.verify_pair(kp1, kp2, mt, 3, 4, _multi()))
+    assert t.config == 0 and len(t.inlier_matches) == 0

@@ -207,5 +207,43 @@ def test_oversize_frame_is_rescaled_before_extraction():
     got = oracle.sift_extract(f, 5)
     assert got == oracle.sift_extract(small[:, :, None], 5)
     assert np.frombuffer(got[2][16:32], np.uint64).tolist() == [nw, nh]  # camera: rescaled size
-    with pytest.raises(ValueError):  # below 16 rows after the rescale
-        oracle.sift_extract(np.zeros((15, 3300, 3), np.uint8))
+    # 14 rows after the rescale: VLFeat runs on it like on any size (no floor)
+    thin = oracle.sift_extract(np.zeros((15, 3300, 3), np.uint8))
+    assert np.frombuffer(thin[2][16:32], np.uint64).tolist() == [3200, 14]
+
+
+def test_refine_terms_round_sums_in_float():
+    """vl_sift_refine_keypoints' at() reads vl_sift_pix (float), so in
+    `Dx = 0.5 * (at(+1,0,0) - at(-1,0,0))` the difference rounds in float and
+    only the product with the double literal widens (C's usual arithmetic
+    conversions; same for the Hessian sums).  Known answer from numpy float32
+    arithmetic on patches where evaluating the sums in double would differ."""
+    import ctypes
+    from oracle import oracle
+    L = oracle.lib()
+    L.oracle_sift_refine_terms.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    rng = np.random.default_rng(5)
+    f = np.float32
+    differs = 0
+    for _ in range(200):
+        p = (rng.uniform(-0.05, 0.05, (3, 3, 3)) * rng.uniform(0.5, 3.0)).astype(np.float32)
+        out = np.zeros(9, np.float64)
+        L.oracle_sift_refine_terms(p.ctypes.data, out.ctypes.data)
+
+        def a(dx, dy, ds):
+            return p[1 + ds, 1 + dy, 1 + dx]
+        ref = [0.5 * np.float64(f(a(1, 0, 0) - a(-1, 0, 0))),
+               0.5 * np.float64(f(a(0, 1, 0) - a(0, -1, 0))),
+               0.5 * np.float64(f(a(0, 0, 1) - a(0, 0, -1))),
+               np.float64(f(a(1, 0, 0) + a(-1, 0, 0))) - 2.0 * np.float64(a(0, 0, 0)),
+               np.float64(f(a(0, 1, 0) + a(0, -1, 0))) - 2.0 * np.float64(a(0, 0, 0)),
+               np.float64(f(a(0, 0, 1) + a(0, 0, -1))) - 2.0 * np.float64(a(0, 0, 0)),
+               0.25 * np.float64(f(f(f(a(1, 1, 0) + a(-1, -1, 0)) - a(-1, 1, 0)) - a(1, -1, 0))),
+               0.25 * np.float64(f(f(f(a(1, 0, 1) + a(-1, 0, -1)) - a(-1, 0, 1)) - a(1, 0, -1))),
+               0.25 * np.float64(f(f(f(a(0, 1, 1) + a(0, -1, -1)) - a(0, -1, 1)) - a(0, 1, -1)))]
+        assert out.tolist() == ref
+        d = np.float64
+        dbl = [0.5 * (d(a(1, 0, 0)) - d(a(-1, 0, 0))),
+               0.25 * (d(a(1, 1, 0)) + d(a(-1, -1, 0)) - d(a(-1, 1, 0)) - d(a(1, -1, 0)))]
+        differs += (dbl[0] != ref[0]) + (dbl[1] != ref[6])
+    assert differs > 50  # the patches do tell float from double sums apart
