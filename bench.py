@@ -30,6 +30,7 @@ METRIC = "image-pairs/s + Gdesc-dist/s, 8192×8192-kpt pairs, 1/2/4/8 GPU"
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (spec)
 I8_DENSE_PEAK_TOPS = 5000.0      # MI355X_MICROARCH.md matrix cores: i8 32x32x32 = 2x the bf16 rate
 FP32_VECTOR_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 (vector, packed)
+HBM_PEAK_GBPS = 8000.0           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 # Reference residual arithmetic (upstream COLMAP estimators): ComputeSquaredSampsonError
 # (F x1, F^T x2, x2^T F x1, e^2 / (4 squares)) and HomographyMatrixEstimator::Residuals
 # (H s, one division, two differences, two squares).
@@ -311,6 +312,20 @@ def pmc_traffic(workload: str, kpts: int, images: int, kernel: str):
     return d, os.path.relpath(files[-1], ROOT)
 
 
+def pmc_sq(kernels: tuple):
+    """MFMA / VALU utilisation of the given kernels from the committed
+    rocprofv3 SQ summary (profiles/rNN_pmc_sq.json, profiles/pmc_sq_summary.py:
+    SQ_INSTS_VALU / SQ_INSTS_MFMA, SQ_VALU_MFMA_BUSY_CYCLES and
+    SQ_ACTIVE_INST_VALU over the chip's SIMD cycles), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_sq.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    out = {k: d[k] for k in kernels if k in d}
+    return (out, os.path.relpath(files[-1], ROOT)) if out else None
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -447,6 +462,17 @@ def main():
         alg_bytes_launch = npairs * steps / launches * 2 * avg_n * 128 * (2 if bf16 else 1)
         pmc = (pmc_traffic(args.workload, kpts, total_images, kernel)
                if world == 1 and not args.images else None)
+        sq = pmc_sq((kernel, "rs_score_kernel<1>", "rs_score_kernel<0>"))
+        launch_s = match_ms * 1e-3 / launches  # average matcher launch (HIP events)
+        hbm = {}
+        if pmc:
+            gbps = pmc[0]["traffic_bytes_per_launch"] / launch_s / 1e9
+            hbm = {"hbm_gbps": round(gbps, 1), "hbm_frac": round(gbps / HBM_PEAK_GBPS, 4)}
+        util = {}
+        if sq and kernel in sq[0]:
+            k = sq[0][kernel]
+            util = {"mfma_busy": round(k["mfma_busy"], 4), "valu_per_mfma": round(k["valu_per_mfma"], 2),
+                    "util_source": f"{sq[1]} (SQ PMC, separate rocprofv3 passes of one bench step)"}
         cpu = parity = None
         if check_pairs:
             if args.no_cpu_baseline:  # parity only, with the oracle's BLAS-dot matcher
@@ -523,6 +549,8 @@ def main():
                 "traffic_source": (f"{pmc[1]}: FETCH_SIZE x2 + WRITE_SIZE per launch, "
                                    f"separate rocprofv3 --pmc passes") if pmc else None,
                 "algorithmic_bytes_per_launch": round(alg_bytes_launch),
+                **hbm,
+                **util,
                 "launches_per_step": round(launches / steps, 2),
                 "wall_achieved": round(wall_tops, 2),
                 "wall_frac": round(wall_tops / peak, 4),
@@ -541,6 +569,11 @@ def main():
                 "frac": (round(score_flops / (score_ms * 1e-3) / 1e12 / FP32_VECTOR_PEAK_TFLOPS, 4)
                          if score_ms > 0 else None),
                 "evals_per_step": {"F": evals_f // steps, "H": evals_h // steps},
+                "valu_active": ({"H": round(sq[0]["rs_score_kernel<1>"]["valu_active_frac_of_simd_cycles"], 4),
+                                 "F": round(sq[0]["rs_score_kernel<0>"]["valu_active_frac_of_simd_cycles"], 4),
+                                 "source": sq[1]}
+                                if sq and "rs_score_kernel<1>" in sq[0] and "rs_score_kernel<0>" in sq[0]
+                                else None),
                 "score_ms_per_step": round(score_ms / steps, 3),
                 "algorithmic": ("reference residual arithmetic per (model, point): Sampson error "
                                 f"{SAMPSON_FLOPS} flops (F), transfer error {TRANSFER_FLOPS} flops (H), "
