@@ -234,7 +234,9 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset,
  * t[2] = RANSAC hypothesis kernels, t[3] = whole run (wall),
  * t[4] = number of descriptor-distance kernel launches of the run,
  * t[5] = inlier-scoring kernels (F + H), t[6] / t[7] = F / H (model, point)
- * residual evaluations of the sequential LO-RANSAC up to its stop. */
+ * residual evaluations of the sequential LO-RANSAC up to its stop;
+ * t[8] / t[9] = host time of the last scm_execute_batch: content keys of its
+ * elements, then the image table (reuse + upload staging). */
 int scm_table_timings(scm_context* ctx, double* t, int32_t n);
 /* Measurement only: serial != 0 runs the following table runs with matching
  * and verification one after the other instead of overlapped (no stage

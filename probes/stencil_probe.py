@@ -34,7 +34,8 @@ def main():
         t = ctx.table_timings()
         walls.append(w)
         print(f"call {r0 // B:3d} wall {w:7.2f} ms match {t['match_ms']:6.2f} finalize "
-              f"{t['finalize_ms']:5.2f} verify {t['verify_ms']:6.2f}", flush=True)
+              f"{t['finalize_ms']:5.2f} verify {t['verify_ms']:6.2f} hash {t['hash_ms']:5.2f} "
+              f"stage {t['stage_ms']:5.2f}", flush=True)
     walls = sorted(walls[1:])
     print(f"median wall {walls[len(walls) // 2]:.2f} ms per call of {B} stencils", flush=True)
     ctx.close()

@@ -19,7 +19,11 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -128,6 +132,121 @@ uint64_t hash_bytes(const uint8_t* p, size_t n, uint64_t seed) {
   h ^= h >> 32;
   return h;
 }
+
+// Content hash of a byte buffer of any size, computed in parallel: the
+// buffer's kHashChunk-byte chunks are hashed independently (hash_bytes, seed
+// mixed with the chunk index) and the hash of their hashes is the content
+// hash (with the length).  Chunk tasks of many buffers run on a WorkerPool.
+constexpr size_t kHashChunk = (size_t)256 << 10;
+inline int64_t hash_chunks(size_t n) { return (int64_t)((n + kHashChunk - 1) / kHashChunk); }
+inline uint64_t hash_chunk(const uint8_t* p, size_t n, int64_t k, uint64_t seed) {
+  const size_t off = (size_t)k * kHashChunk;
+  return hash_bytes(p + off, std::min(kHashChunk, n - off), seed + 0x9E3779B97F4A7C15ULL * (uint64_t)(k + 1));
+}
+inline uint64_t hash_combine_chunks(const uint64_t* h, int64_t m, size_t n, uint64_t seed) {
+  return hash_bytes(reinterpret_cast<const uint8_t*>(h), (size_t)m * sizeof(uint64_t), seed ^ (uint64_t)n);
+}
+
+// Persistent host worker threads (content hashing, upload staging): run()
+// executes f(0 .. n-1) on the workers and the calling thread and returns when
+// all are done; launch() starts them on the workers only and wait() joins
+// (the caller meanwhile drives the GPU).  One job at a time per pool.
+class WorkerPool {
+ public:
+  void start(int workers) {
+    for (int i = 0; i < workers; ++i) th_.emplace_back([this] { loop(); });
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> l(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  void launch(int64_t n, std::function<void(int64_t)> f) {
+    if (th_.empty()) {
+      for (int64_t i = 0; i < n; ++i) f(i);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> l(m_);
+      fn_ = std::move(f);
+      n_ = n;
+      next_.store(0);
+      pending_ = (int)th_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+    busy_ = true;
+  }
+  void wait() {
+    if (!busy_) return;
+    std::unique_lock<std::mutex> l(m_);
+    done_.wait(l, [&] { return pending_ == 0; });
+    fn_ = nullptr;
+    busy_ = false;
+  }
+  void run(int64_t n, std::function<void(int64_t)> f) {
+    if (n <= 1 || th_.empty()) {
+      for (int64_t i = 0; i < n; ++i) f(i);
+      return;
+    }
+    launch(n, std::move(f));
+    work();
+    wait();
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const int64_t i = next_.fetch_add(1);
+      if (i >= n_) return;
+      fn_(i);
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+      std::lock_guard<std::mutex> l(m_);
+      if (--pending_ == 0) done_.notify_all();
+    }
+  }
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  std::function<void(int64_t)> fn_;
+  int64_t n_ = 0;
+  std::atomic<int64_t> next_{0};
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false, busy_ = false;
+};
+
+// Buffers of one execute() element (what Scanner hands over: the same
+// buffers for an element that several stencils or calls share).
+struct Src {
+  const float* kp;
+  int64_t nkp;
+  const uint8_t* desc;
+  int64_t ndesc;
+  bool operator==(const Src& o) const {
+    return kp == o.kp && nkp == o.nkp && desc == o.desc && ndesc == o.ndesc;
+  }
+};
+struct SrcHash {
+  size_t operator()(const Src& s) const {
+    return std::hash<const void*>()(s.desc) ^ (std::hash<const void*>()(s.kp) * 31) ^
+           (size_t)(s.nkp * 0x9E3779B97F4A7C15ULL) ^ (size_t)s.ndesc;
+  }
+};
 
 // Pinned host result buffer: the DMA target of each batch's results.
 struct PinnedOut {
@@ -238,6 +357,7 @@ struct scm_context {
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
   bool score_split = true;  // SCM_SCORE_SPLIT=0: one-pass scoring with every exact test
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
+  double t_hash = 0, t_stage = 0;  // host time of the last execute_batch: content keys, table
   double t_score = 0;                  // scoring kernels (F + H) of the last run
   int64_t evals_f = 0, evals_h = 0;    // their (model, point) evaluations
   int64_t n_match_launches = 0;  // matcher kernel launches of the last table run
@@ -256,6 +376,12 @@ struct scm_context {
   int64_t last_begin = 0, last_end = 0;
   std::vector<std::vector<std::pair<int64_t, std::vector<Match>>>> last_matches;
   SiftState* sift = nullptr;  // SIFT extraction slots (scm_extract_frames), created on first use
+  // Host workers: `pool` for a call's own host work (content keys of new
+  // buffers, upload staging), `vpool` for the speculative key checks that run
+  // while the GPU works (execute_rows).
+  WorkerPool pool, vpool;
+  // Content keys of the previous execute() call's element buffers.
+  std::unordered_map<Src, ImageKey, SrcHash> spec_keys;
 };
 
 namespace {
@@ -369,63 +495,51 @@ int upload_table(scm_context* ctx, ImageTable* t, const std::vector<RowView>& ro
   return SCM_OK;
 }
 
-// Content keys of a call's elements.  Elements that share their buffers
-// (Scanner hands consecutive stencils the same element buffers) are hashed
-// once; distinct buffers are hashed on the context's host threads.
-void hash_elements(scm_context* ctx, const std::vector<RowView>& rows, std::vector<ImageKey>* keys) {
-  const int64_t n = (int64_t)rows.size();
-  keys->assign(n, ImageKey());
-  struct Src {
-    const float* kp;
-    int64_t nkp;
-    const uint8_t* desc;
-    int64_t ndesc;
-    bool operator==(const Src& o) const {
-      return kp == o.kp && nkp == o.nkp && desc == o.desc && ndesc == o.ndesc;
+// Content keys (ImageKey) of a set of elements, hashed chunk-parallel on a
+// WorkerPool: plan(), task(t) for t in [0, ntasks()) (any order, any
+// thread), then key(i) of elems[i].
+struct KeyJob {
+  static constexpr uint64_t kSeedKp = 0x6B70ULL, kSeedDesc = 0x64657363ULL;
+  const std::vector<RowView>* rows = nullptr;
+  std::vector<int64_t> elems;  // row indices
+  std::vector<int64_t> off;    // first chunk of (element i, part: 0 keypoints / 1 descriptors)
+  std::vector<uint64_t> ch;    // chunk hashes
+  int64_t ntasks() const { return off.empty() ? 0 : off.back(); }
+  void plan(const std::vector<RowView>& r, std::vector<int64_t> e) {
+    rows = &r;
+    elems = std::move(e);
+    off.assign(2 * elems.size() + 1, 0);
+    for (size_t i = 0; i < elems.size(); ++i) {
+      const RowView& v = r[elems[i]];
+      off[2 * i + 1] = off[2 * i] + hash_chunks((size_t)v.nkp * 24);
+      off[2 * i + 2] = off[2 * i + 1] + hash_chunks((size_t)v.ndesc * 128);
     }
-  };
-  struct SrcHash {
-    size_t operator()(const Src& s) const {
-      return std::hash<const void*>()(s.desc) ^ (std::hash<const void*>()(s.kp) * 31) ^
-             (size_t)(s.nkp * 0x9E3779B97F4A7C15ULL) ^ (size_t)s.ndesc;
-    }
-  };
-  std::unordered_map<Src, int64_t, SrcHash> first;  // buffers -> first element
-  std::vector<int64_t> of(n), todo;
-  size_t bytes = 0;
-  for (int64_t e = 0; e < n; ++e) {
-    const RowView& r = rows[e];
-    auto it = first.emplace(Src{r.kp, r.nkp, r.desc, r.ndesc}, e).first;
-    of[e] = it->second;
-    if (it->second == e) {
-      todo.push_back(e);
-      bytes += (size_t)r.nkp * 24 + (size_t)r.ndesc * 128;
-    }
+    ch.assign((size_t)ntasks(), 0);
   }
-  auto work = [&](int64_t i) {
-    const RowView& r = rows[todo[i]];
-    ImageKey& k = (*keys)[todo[i]];
-    k.nkp = r.nkp;
-    k.ndesc = r.ndesc;
-    k.hkp = hash_bytes(reinterpret_cast<const uint8_t*>(r.kp), (size_t)r.nkp * 24, 0x6B70ULL);
-    k.hdesc = hash_bytes(r.desc, (size_t)r.ndesc * 128, 0x64657363ULL);
-  };
-  const int64_t nt = (int64_t)todo.size();
-  const int T = (int)std::min<int64_t>(ctx->threads, nt);
-  if (T <= 1 || bytes < ((size_t)4 << 20)) {
-    for (int64_t i = 0; i < nt; ++i) work(i);
-  } else {
-    std::vector<std::thread> ts;
-    for (int t = 0; t < T; ++t)
-      ts.emplace_back([&, t] {
-        for (int64_t i = t; i < nt; i += T) work(i);
-      });
-    for (auto& th : ts) th.join();
+  void task(int64_t t) {
+    const int64_t sl = (int64_t)(std::upper_bound(off.begin(), off.end(), t) - off.begin()) - 1;
+    const RowView& v = (*rows)[elems[sl / 2]];
+    const int64_t k = t - off[sl];
+    ch[t] = sl % 2 == 0
+                ? hash_chunk(reinterpret_cast<const uint8_t*>(v.kp), (size_t)v.nkp * 24, k, kSeedKp)
+                : hash_chunk(v.desc, (size_t)v.ndesc * 128, k, kSeedDesc);
   }
-  for (int64_t e = 0; e < n; ++e) {
-    (*keys)[e] = (*keys)[of[e]];
-    (*keys)[e].id = rows[e].id;
+  ImageKey key(size_t i) const {
+    const RowView& v = (*rows)[elems[i]];
+    ImageKey k;
+    k.id = v.id;
+    k.nkp = v.nkp;
+    k.ndesc = v.ndesc;
+    k.hkp = hash_combine_chunks(ch.data() + off[2 * i], off[2 * i + 1] - off[2 * i],
+                                (size_t)v.nkp * 24, kSeedKp);
+    k.hdesc = hash_combine_chunks(ch.data() + off[2 * i + 1], off[2 * i + 2] - off[2 * i + 1],
+                                  (size_t)v.ndesc * 128, kSeedDesc);
+    return k;
   }
+};
+
+inline bool same_content(const ImageKey& a, const ImageKey& b) {
+  return a.nkp == b.nkp && a.ndesc == b.ndesc && a.hkp == b.hkp && a.hdesc == b.hdesc;
 }
 
 // Table of one execute() call over the call's unique images `rows` (content
@@ -542,26 +656,45 @@ int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows,
     uint8_t* h = ctx->h_stage.as<uint8_t>();
     float2* hk = reinterpret_cast<float2*>(h + koff);
     const size_t nfresh = fresh.size(), k0 = reuse.size();
-    parallel_for(ctx->threads, (int64_t)nfresh, [&](int64_t f) {
+    // Tasks of kStageRows descriptor rows (a new image of 8192 features is
+    // 8 tasks): copy into the staging buffer and the row norms' maximum; an
+    // image's last task also pads its rows and converts its keypoints.
+    constexpr int64_t kStageRows = 1024;
+    std::vector<int64_t> tfirst(nfresh + 1, 0);
+    for (size_t f = 0; f < nfresh; ++f) {
+      const RowView& r = rows[order[k0 + f]];
+      tfirst[f + 1] = tfirst[f] + std::max<int64_t>(1, (r.ndesc + kStageRows - 1) / kStageRows);
+    }
+    std::vector<uint64_t> tmax((size_t)tfirst[nfresh], 0);
+    ctx->pool.run(tfirst[nfresh], [&](int64_t task) {
+      const size_t f = (size_t)(std::upper_bound(tfirst.begin(), tfirst.end(), task) - tfirst.begin()) - 1;
       const int64_t k = (int64_t)(k0 + f);
       const RowView& r = rows[order[k]];
       uint8_t* dst = h + (size_t)(t->desc_row[k] - tail_row) * 128;
-      const size_t nb = (size_t)r.ndesc * 128;
-      if (nb) std::memcpy(dst, r.desc, nb);
-      const size_t padded =
-          (size_t)((r.ndesc + kDescRowAlign - 1) / kDescRowAlign * kDescRowAlign) * 128;
-      std::memset(dst + nb, 0, padded - nb);
+      const int64_t q0 = (task - tfirst[f]) * kStageRows, q1 = std::min(r.ndesc, q0 + kStageRows);
+      if (q1 > q0) std::memcpy(dst + q0 * 128, r.desc + q0 * 128, (size_t)(q1 - q0) * 128);
       uint64_t mx = 0;
-      for (int64_t q = 0; q < r.ndesc; ++q) {
+      for (int64_t q = q0; q < q1; ++q) {
         const uint8_t* d = r.desc + q * 128;
         uint32_t sq = 0;
         for (int j = 0; j < 128; ++j) sq += (uint32_t)d[j] * d[j];
         mx = std::max<uint64_t>(mx, sq);
       }
-      t->max_norm2[k] = mx;
-      float2* kd = hk + (t->kp_off[k] - tail_kp);
-      for (int64_t q = 0; q < r.nkp; ++q) kd[q] = make_float2(r.kp[6 * q], r.kp[6 * q + 1]);
+      tmax[task] = mx;
+      if (task + 1 == tfirst[f + 1]) {
+        const size_t nb = (size_t)r.ndesc * 128;
+        const size_t padded =
+            (size_t)((r.ndesc + kDescRowAlign - 1) / kDescRowAlign * kDescRowAlign) * 128;
+        std::memset(dst + nb, 0, padded - nb);
+        float2* kd = hk + (t->kp_off[k] - tail_kp);
+        for (int64_t q = 0; q < r.nkp; ++q) kd[q] = make_float2(r.kp[6 * q], r.kp[6 * q + 1]);
+      }
     });
+    for (size_t f = 0; f < nfresh; ++f) {
+      uint64_t mx = 0;
+      for (int64_t q = tfirst[f]; q < tfirst[f + 1]; ++q) mx = std::max(mx, tmax[q]);
+      t->max_norm2[k0 + f] = mx;
+    }
     SCM_TRY(t->u8.ensure(koff + kbytes));
     SCM_HIP(hipMemcpyAsync(t->u8.ptr, h, koff + kbytes, hipMemcpyHostToDevice, st));
     if (frows > 0) {
@@ -1576,6 +1709,8 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   int hw = (int)std::thread::hardware_concurrency();
   if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::max(1, std::atoi(e));
   ctx->threads = std::max(1, std::min(16, hw));
+  ctx->pool.start(ctx->threads - 1);
+  ctx->vpool.start(std::max(1, ctx->threads - 1));
   if (const char* e = std::getenv("SCM_SCORE_SPLIT")) ctx->score_split = e[0] != '0';
   if (const char* e = std::getenv("SCM_SERIAL")) ctx->serial = e[0] == '1';
   if (const char* e = std::getenv("SCM_BATCH_PAIRS"))
@@ -1738,25 +1873,57 @@ int scm_verify_pair(scm_context* ctx, const float* kp1, int64_t n1, const float*
   return make_blob(bytes, tvg_out);
 }
 
-int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
-                      const scm_element* image_ids, const scm_element* keypoints,
-                      const scm_element* descriptors, scm_blob* pair_image_ids_out,
-                      scm_blob* tvgs_out) {
-  if (!ctx || batch < 0 || stencil_size < 1 || (batch > 0 && (!pair_image_ids_out || !tvgs_out))) {
-    set_error("invalid arguments");
-    return SCM_E_INVALID;
-  }
-  if (batch == 0) return SCM_OK;
-  SCM_HIP(hipSetDevice(ctx->device));
+}  // extern "C"
+
+namespace {
+
+constexpr int kRetryKeys = 1;  // execute_rows: a speculated content key did not hold
+
+// One execute() call over decoded elements.  Content keys (ImageKey): element
+// buffers the previous call also handed over take that call's keys
+// speculatively and are re-hashed on ctx->vpool while the GPU runs; the
+// results are returned only if every speculated key holds (else kRetryKeys,
+// and the caller runs the call again with every key hashed first).  Buffers
+// new to this call are hashed before anything is enqueued.
+int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
+                 const std::vector<RowView>& rows, bool speculate, scm_blob* pair_image_ids_out,
+                 scm_blob* tvgs_out) {
   const int64_t ne = batch * stencil_size;
-  std::vector<RowView> rows;
-  SCM_TRY(decode_rows(ne, image_ids, keypoints, descriptors, &rows));
+  const auto h0 = std::chrono::steady_clock::now();
+  std::unordered_map<Src, int64_t, SrcHash> first;  // buffers -> first element
+  std::vector<int64_t> of(ne), now_e, spec_e;
+  for (int64_t e = 0; e < ne; ++e) {
+    const RowView& r = rows[e];
+    const Src src{r.kp, r.nkp, r.desc, r.ndesc};
+    auto it = first.emplace(src, e).first;
+    of[e] = it->second;
+    if (it->second == e) (speculate && ctx->spec_keys.count(src) ? spec_e : now_e).push_back(e);
+  }
+  std::vector<ImageKey> ekey(ne);
+  KeyJob now_job;
+  now_job.plan(rows, now_e);
+  ctx->pool.run(now_job.ntasks(), [&](int64_t t) { now_job.task(t); });
+  for (size_t i = 0; i < now_e.size(); ++i) ekey[now_e[i]] = now_job.key(i);
+  for (int64_t e : spec_e) {
+    const RowView& r = rows[e];
+    ekey[e] = ctx->spec_keys[Src{r.kp, r.nkp, r.desc, r.ndesc}];
+  }
+  KeyJob spec_job;
+  spec_job.plan(rows, spec_e);
+  ctx->vpool.launch(spec_job.ntasks(), [&](int64_t t) { spec_job.task(t); });
+  struct Join {
+    WorkerPool& p;
+    ~Join() { p.wait(); }
+  } join{ctx->vpool};
+  for (int64_t e = 0; e < ne; ++e) {
+    ekey[e] = ekey[of[e]];
+    ekey[e].id = rows[e].id;
+  }
+  const auto h1 = std::chrono::steady_clock::now();
   // Unique images of the call, by content (ImageKey): every element is
   // matched with its own bytes, as the reference decodes each stencil
   // element (sequential_matching.cc:115-122); an id that reappears with other
   // bytes is simply another image.
-  std::vector<ImageKey> ekey;
-  hash_elements(ctx, rows, &ekey);
   std::unordered_map<ImageKey, int32_t, ImageKeyHash> uid;
   std::vector<RowView> uniq;
   std::vector<ImageKey> ukeys;
@@ -1770,6 +1937,7 @@ int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
     }
     elem_u[e] = it->second;
   }
+  const int64_t reused0 = ctx->call_reused, uploaded0 = ctx->call_uploaded;
   std::vector<int32_t> uidx;
   int rc = upload_call_table(ctx, uniq, ukeys, &uidx);
   if (rc != SCM_OK) {
@@ -1777,6 +1945,8 @@ int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
     drain(ctx);
     return rc;
   }
+  ctx->t_hash = std::chrono::duration<double, std::milli>(h1 - h0).count();
+  ctx->t_stage = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h1).count();
   const ImageTable& t = ctx->call_tab[ctx->call_cur];
   std::vector<RowPlan> plan(batch);
   std::vector<uint32_t> ids(stencil_size);
@@ -1800,6 +1970,21 @@ int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
     if (!pool_give(pk.data)) std::free(pk.data);
     return rc;
   }
+  ctx->vpool.wait();
+  bool held = true;
+  for (size_t i = 0; i < spec_e.size(); ++i) held = held && same_content(spec_job.key(i), ekey[spec_e[i]]);
+  if (!held) {
+    // A buffer changed since the previous call: nothing of this run is
+    // returned, the cache and the speculation start over.
+    if (!pool_give(pk.data)) std::free(pk.data);
+    ctx->call_cur = -1;
+    ctx->spec_keys.clear();
+    ctx->call_reused = reused0;
+    ctx->call_uploaded = uploaded0;
+    return kRetryKeys;
+  }
+  ctx->spec_keys.clear();
+  for (const auto& f : first) ctx->spec_keys[f.first] = ekey[f.second];
   for (int64_t r = 0; r < batch; ++r) {
     const int64_t a = pk.row_off[2 * r], b = pk.row_off[2 * r + 1], c = pk.row_off[2 * r + 2];
     uint8_t* pa = (uint8_t*)std::malloc((size_t)std::max<int64_t>(b - a, 1));
@@ -1822,6 +2007,28 @@ int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
   }
   if (!pool_give(pk.data)) std::free(pk.data);
   return SCM_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
+                      const scm_element* image_ids, const scm_element* keypoints,
+                      const scm_element* descriptors, scm_blob* pair_image_ids_out,
+                      scm_blob* tvgs_out) {
+  if (!ctx || batch < 0 || stencil_size < 1 || (batch > 0 && (!pair_image_ids_out || !tvgs_out))) {
+    set_error("invalid arguments");
+    return SCM_E_INVALID;
+  }
+  if (batch == 0) return SCM_OK;
+  SCM_HIP(hipSetDevice(ctx->device));
+  const int64_t ne = batch * stencil_size;
+  std::vector<RowView> rows;
+  SCM_TRY(decode_rows(ne, image_ids, keypoints, descriptors, &rows));
+  const int rc = execute_rows(ctx, batch, stencil_size, rows, true, pair_image_ids_out, tvgs_out);
+  if (rc != kRetryKeys) return rc;
+  return execute_rows(ctx, batch, stencil_size, rows, false, pair_image_ids_out, tvgs_out);
 }
 
 int scm_execute_stencil(scm_context* ctx, int64_t stencil_size, const scm_element* image_ids,
@@ -1853,6 +2060,7 @@ int scm_stencil_cache_clear(scm_context* ctx) {
     ctx->call_tab[i].release();
     ctx->call_map[i].clear();
   }
+  ctx->spec_keys.clear();
   return SCM_OK;
 }
 
@@ -2043,10 +2251,10 @@ int scm_table_timings(scm_context* ctx, double* t, int32_t n) {
     set_error("invalid arguments");
     return SCM_E_INVALID;
   }
-  const double v[8] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall,
-                       (double)ctx->n_match_launches, ctx->t_score, (double)ctx->evals_f,
-                       (double)ctx->evals_h};
-  for (int32_t i = 0; i < n && i < 8; ++i) t[i] = v[i];
+  const double v[10] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall,
+                        (double)ctx->n_match_launches, ctx->t_score, (double)ctx->evals_f,
+                        (double)ctx->evals_h, ctx->t_hash, ctx->t_stage};
+  for (int32_t i = 0; i < n && i < 10; ++i) t[i] = v[i];
   return SCM_OK;
 }
 

@@ -21,6 +21,7 @@
 // is bit-identical to the CPU oracle's.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "../../include/scm.h"
 #include "geom_solvers.h"
@@ -768,34 +769,62 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
   return cnt;
 }
 
+// Point loops of the sequential (watermark) LO-RANSAC on the double point
+// arrays: latency-bound on one wave, so each lane keeps kSeqU points' loads in
+// flight; items are consumed in index order per lane (canonical sums keep
+// their order).
+constexpr int kSeqU = 8;
+
 // Residuals of one model over all points into res; returns the inlier count.
 template <int K>
 __device__ int residuals_wave(const double* m, const double* xy1, const double* xy2, int n,
                               double maxr, double* res) {
   int c = 0;
-  for (int i = threadIdx.x; i < n; i += 64) {
-    const double r = residual_pt<K>(m, xy1[2 * i], xy1[2 * i + 1], xy2[2 * i], xy2[2 * i + 1]);
-    res[i] = r;
-    c += (r <= maxr) ? 1 : 0;
+  for (int b = threadIdx.x; b < n; b += 64 * kSeqU) {
+    double a0[kSeqU], a1[kSeqU], b0[kSeqU], b1[kSeqU];
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u) {
+      const int i = min(b + 64 * u, n - 1);
+      a0[u] = xy1[2 * i];
+      a1[u] = xy1[2 * i + 1];
+      b0[u] = xy2[2 * i];
+      b1[u] = xy2[2 * i + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u) {
+      const int i = b + 64 * u;
+      if (i < n) {
+        const double r = residual_pt<K>(m, a0[u], a1[u], b0[u], b1[u]);
+        res[i] = r;
+        c += (r <= maxr) ? 1 : 0;
+      }
+    }
   }
   return wave_sum_i(c);
 }
 
 // InlierSupportMeasurer::Evaluate's residual_sum: inlier residuals summed
-// in index order.  The wave loads 64 residuals at a time; the ordered
+// in index order.  The wave loads 64 x kSeqU residuals at a time; the ordered
 // accumulation runs on values broadcast with v_readlane (every lane computes
 // the same scalar sum).
 __device__ double seq_inlier_sum(const double* res, int n, double maxr) {
   double sum = 0.0;
-  for (int base = 0; base < n; base += 64) {
-    const int i = base + threadIdx.x;
-    const double v = i < n ? res[i] : 1.7976931348623157e308;
-    // Only the inliers contribute: visit them in lane (= index) order.
-    uint64_t bal = __ballot(v <= maxr);
-    while (bal) {
-      const int j = __builtin_ctzll(bal);
-      sum += readlane_d(v, j);
-      bal &= bal - 1;
+  for (int b0 = 0; b0 < n; b0 += 64 * kSeqU) {
+    double v[kSeqU];
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u) {
+      const int i = b0 + 64 * u + (int)threadIdx.x;
+      v[u] = i < n ? res[i] : 1.7976931348623157e308;
+    }
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u) {
+      // Only the inliers contribute: visit them in lane (= index) order.
+      uint64_t bal = __ballot(v[u] <= maxr);
+      while (bal) {
+        const int j = __builtin_ctzll(bal);
+        sum += readlane_d(v[u], j);
+        bal &= bal - 1;
+      }
     }
   }
   return sum;
@@ -806,19 +835,31 @@ __device__ int gather_inliers(const double* res, int n, double maxr, const doubl
                               const double* xy2, double* xin1, double* xin2) {
   const int lane = threadIdx.x;
   int base_out = 0;
-  for (int base = 0; base < n; base += 64) {
-    const int i = base + lane;
-    const bool in = i < n && res[i] <= maxr;
-    const uint64_t bal = __ballot(in);
-    if (in) {
-      const int o = base_out + (int)__builtin_amdgcn_mbcnt_hi(
-                                   (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-      xin1[2 * o] = xy1[2 * i];
-      xin1[2 * o + 1] = xy1[2 * i + 1];
-      xin2[2 * o] = xy2[2 * i];
-      xin2[2 * o + 1] = xy2[2 * i + 1];
+  for (int b0 = 0; b0 < n; b0 += 64 * kSeqU) {
+    double r[kSeqU], a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u) {
+      const int i = b0 + 64 * u + lane, ic = min(i, n - 1);
+      r[u] = i < n ? res[i] : 1.7976931348623157e308;
+      a0[u] = xy1[2 * ic];
+      a1[u] = xy1[2 * ic + 1];
+      c0[u] = xy2[2 * ic];
+      c1[u] = xy2[2 * ic + 1];
     }
-    base_out += __popcll(bal);
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u) {
+      const bool in = r[u] <= maxr;
+      const uint64_t bal = __ballot(in);
+      if (in) {
+        const int o = base_out + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        xin1[2 * o] = a0[u];
+        xin1[2 * o + 1] = a1[u];
+        xin2[2 * o] = c0[u];
+        xin2[2 * o + 1] = c1[u];
+      }
+      base_out += __popcll(bal);
+    }
   }
   return base_out;
 }
@@ -1050,11 +1091,24 @@ __device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const doub
   const int lane = threadIdx.x;
   if (K == KIND_T) {
     double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
-    for (int i = lane; i < n; i += 64) {
-      p0 += xin1[2 * i];
-      p1 += xin1[2 * i + 1];
-      p2 += xin2[2 * i];
-      p3 += xin2[2 * i + 1];
+    for (int b = lane; b < n; b += 64 * kSeqU) {
+      double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
+#pragma unroll
+      for (int u = 0; u < kSeqU; ++u) {
+        const int i = min(b + 64 * u, n - 1);
+        a0[u] = xin1[2 * i];
+        a1[u] = xin1[2 * i + 1];
+        c0[u] = xin2[2 * i];
+        c1[u] = xin2[2 * i + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < kSeqU; ++u)
+        if (b + 64 * u < n) {
+          p0 += a0[u];
+          p1 += a1[u];
+          p2 += c0[u];
+          p3 += c1[u];
+        }
     }
     const double s0 = canon_tree_wave(p0) / (double)n, s1 = canon_tree_wave(p1) / (double)n;
     const double d0 = canon_tree_wave(p2) / (double)n, d1 = canon_tree_wave(p3) / (double)n;
@@ -1539,13 +1593,24 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
       // DetectWatermark with the dummy cameras (width = height = 0): a point
       // is inside the [0,0]x[0,0] box only if it is exactly (0, 0).
       int nb = 0;
-      for (int i = lane; i < n; i += 64) {
-        if (!mask[i]) continue;
-        const bool in1 = xy1[2 * i] >= 0.0 && xy1[2 * i] <= 0.0 && xy1[2 * i + 1] >= 0.0 &&
-                         xy1[2 * i + 1] <= 0.0;
-        const bool in2 = xy2[2 * i] >= 0.0 && xy2[2 * i] <= 0.0 && xy2[2 * i + 1] >= 0.0 &&
-                         xy2[2 * i + 1] <= 0.0;
-        nb += (!in1 && !in2) ? 1 : 0;
+      for (int b = lane; b < n; b += 64 * kSeqU) {
+        uint8_t mk[kSeqU];
+        double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
+#pragma unroll
+        for (int u = 0; u < kSeqU; ++u) {
+          const int i = min(b + 64 * u, n - 1);
+          mk[u] = b + 64 * u < n ? mask[i] : 0;
+          a0[u] = xy1[2 * i];
+          a1[u] = xy1[2 * i + 1];
+          c0[u] = xy2[2 * i];
+          c1[u] = xy2[2 * i + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < kSeqU; ++u) {
+          const bool in1 = a0[u] >= 0.0 && a0[u] <= 0.0 && a1[u] >= 0.0 && a1[u] <= 0.0;
+          const bool in2 = c0[u] >= 0.0 && c0[u] <= 0.0 && c1[u] >= 0.0 && c1[u] <= 0.0;
+          nb += (mk[u] && !in1 && !in2) ? 1 : 0;
+        }
       }
       nb = wave_sum_i(nb);
       const int ni = f_in;
@@ -1558,19 +1623,32 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
         double* tin1 = base;
         double* tin2 = base + 2 * n;
         int w = 0;
-        for (int b0 = 0; b0 < n; b0 += 64) {
-          const int i = b0 + lane;
-          const bool in = i < n && mask[i];
-          const uint64_t bal = __ballot(in);
-          if (in) {
-            const int o2 = w + (int)__builtin_amdgcn_mbcnt_hi(
-                                   (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-            tin1[2 * o2] = xy1[2 * i];
-            tin1[2 * o2 + 1] = xy1[2 * i + 1];
-            tin2[2 * o2] = xy2[2 * i];
-            tin2[2 * o2 + 1] = xy2[2 * i + 1];
+        for (int b0 = 0; b0 < n; b0 += 64 * kSeqU) {
+          uint8_t mk[kSeqU];
+          double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
+#pragma unroll
+          for (int u = 0; u < kSeqU; ++u) {
+            const int i = b0 + 64 * u + lane, ic = min(i, n - 1);
+            mk[u] = i < n ? mask[ic] : 0;
+            a0[u] = xy1[2 * ic];
+            a1[u] = xy1[2 * ic + 1];
+            c0[u] = xy2[2 * ic];
+            c1[u] = xy2[2 * ic + 1];
           }
-          w += __popcll(bal);
+#pragma unroll
+          for (int u = 0; u < kSeqU; ++u) {
+            const bool in = mk[u] != 0;
+            const uint64_t bal = __ballot(in);
+            if (in) {
+              const int o2 = w + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+              tin1[2 * o2] = a0[u];
+              tin1[2 * o2 + 1] = a1[u];
+              tin2[2 * o2] = c0[u];
+              tin2[2 * o2 + 1] = c1[u];
+            }
+            w += __popcll(bal);
+          }
         }
         mt_load(s, ps.state);
         const RansacResult rt = loransac_wave<KIND_T>(s, sidx, tin1, tin2, ni, P.max_trials_T, P,
@@ -1852,6 +1930,145 @@ __device__ __attribute__((always_inline)) void rs_shuffle_body(
       uint32_t* g = pair_sidx(pl);
       for (int i = threadIdx.x; i < pl.n; i += 64) g[i] = lsidx[l * stride + i];
     }
+}
+
+
+// The same window's Shuffle with a whole wave per pair, for small batches
+// (one Scanner stencil: a lane per pair leaves nearly every lane, and the
+// GPU, idle while one pair's chain of kmin dependent LDS round trips per
+// trial runs).  The swap chain is split in time: pass of 64 x kWsC trials,
+// lane L takes trials L*kWsC .. and runs their swaps on symbols -- the
+// position each value had at its chunk's start -- keeping its chunk's
+// touched positions in a per-lane open-addressing table in LDS (key j, symbol
+// at j) and its head (positions 0 .. kmin-1) in registers.  The wave then
+// walks the chunks in order over the real vector: a chunk's samples are the
+// vector at their symbols, and its exit map (every touched position p takes
+// the value at its symbol) moves the vector to the next chunk's start; every
+// read of a step is issued before its writes (one wave: LDS operations
+// complete in order), so the map applies as a permutation.  Same samples and
+// final vector as the sequential chain, bit for bit.
+constexpr int kWsC = 16;               // trials per lane and pass
+constexpr int kWsTab = 256;            // table slots per lane (>= 2 x kmin x kWsC)
+constexpr int kWsPass = 64 * kWsC;     // trials per pass
+constexpr int kWsMaxStride = 32768;    // vector positions staged as uint16
+static_assert(kWsTab == 64 * 4, "phase B reads a chunk's table as one uint4 per lane");
+
+size_t wave_shuffle_lds_bytes(int stride) {
+  return (size_t)64 * kWsTab * 4 + (size_t)kWsPass * 8 * 2 + 64 * 8 * 2 + (size_t)stride * 2;
+}
+
+template <int K>
+__device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
+    const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
+    const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, int bid, int nblk) {
+  constexpr int KM = KindTraits<K>::kmin;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(dyn_lds);            // 64 x kWsTab: (j << 16) | symbol
+  uint16_t* ssym = reinterpret_cast<uint16_t*>(tab + 64 * kWsTab);  // kWsPass x 8 sample symbols
+  uint16_t* hsym = ssym + kWsPass * 8;                               // 64 x 8 head symbols
+  uint16_t* V = hsym + 64 * 8;                                        // the vector
+  const int lane = threadIdx.x;
+  const int na = *nact;
+  for (int a = bid; a < na; a += nblk) {
+    const int q = act[a];
+    const PairSetup ps = pair_at<K>(pairs, q, scratch, snaps, out);
+    uint32_t* g = pair_sidx(ps);
+    const int n = ps.n;
+    for (int i = lane; i < n; i += 64) V[i] = (uint16_t)g[i];
+    uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
+    const int Btot = rst[q].B;
+    for (int p0 = 0; p0 < Btot; p0 += kWsPass) {
+      uint32_t* mt = tab + lane * kWsTab;
+#pragma unroll 4
+      for (int s2 = 0; s2 < kWsTab / 4; ++s2)
+        reinterpret_cast<uint4*>(mt)[s2] = make_uint4(0u, 0u, 0u, 0u);
+      // Phase A: this lane's chunk on symbols.
+      uint32_t R[KM];
+#pragma unroll
+      for (int i = 0; i < KM; ++i) R[i] = (uint32_t)i;
+      const int t0 = p0 + lane * kWsC, t1 = min(t0 + kWsC, Btot);
+      for (int t = t0; t < t1; ++t) {
+        const uint4 w0 = reinterpret_cast<const uint4*>(sq + t * 8)[0];
+        const uint4 w1 = KM > 4 ? reinterpret_cast<const uint4*>(sq + t * 8)[1]
+                                : make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+        for (int i = 0; i < KM; ++i) {  // std::swap(sidx[i], sidx[j])
+          const uint32_t j = wv[i];
+          if (j < (uint32_t)KM) {
+            uint32_t ri = R[i];
+#pragma unroll
+            for (int k = i + 1; k < KM; ++k) {
+              const bool m = j == (uint32_t)k;
+              const uint32_t rk = R[k];
+              R[k] = m ? ri : rk;
+              ri = m ? rk : ri;
+            }
+            R[i] = ri;
+          } else {
+            uint32_t slot = (j * 0x9E3779B1u) >> 24;
+            uint32_t w = mt[slot];
+            while (w != 0u && (w >> 16) != j) {
+              slot = (slot + 1) & (kWsTab - 1);
+              w = mt[slot];
+            }
+            const uint32_t sym = w ? (w & 0xffffu) : j;
+            mt[slot] = (j << 16) | R[i];
+            R[i] = sym;
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < KM; ++i) ssym[(t - p0) * 8 + i] = (uint16_t)R[i];
+      }
+#pragma unroll
+      for (int i = 0; i < KM; ++i) hsym[lane * 8 + i] = (uint16_t)R[i];
+      __syncthreads();
+      // Phase B: the chunks in order over the vector.
+      const int nch = (min(Btot - p0, kWsPass) + kWsC - 1) / kWsC;
+      for (int c = 0; c < nch; ++c) {
+        const int tc = p0 + c * kWsC;
+        uint32_t sv[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int e = lane + 64 * r, i = e & 7;
+          sv[r] = i < KM && tc + (e >> 3) < Btot ? (uint32_t)V[ssym[(c * kWsC + (e >> 3)) * 8 + i]]
+                                                 : 0u;
+        }
+        const uint4 wd = reinterpret_cast<const uint4*>(tab + c * kWsTab)[lane];
+        const uint32_t v0 = wd.x ? V[wd.x & 0xffffu] : 0u, v1 = wd.y ? V[wd.y & 0xffffu] : 0u;
+        const uint32_t v2 = wd.z ? V[wd.z & 0xffffu] : 0u, v3 = wd.w ? V[wd.w & 0xffffu] : 0u;
+        const uint32_t hv = lane < KM ? V[hsym[c * 8 + lane]] : 0u;
+        if (wd.x) V[wd.x >> 16] = (uint16_t)v0;
+        if (wd.y) V[wd.y >> 16] = (uint16_t)v1;
+        if (wd.z) V[wd.z >> 16] = (uint16_t)v2;
+        if (wd.w) V[wd.w >> 16] = (uint16_t)v3;
+        if (lane < KM) V[lane] = (uint16_t)hv;
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+          const int e = lane + 64 * r, i = e & 7, t = tc + (e >> 3);
+          // rows as shuffle_chain writes them: kmin samples (+ a zero pad for F)
+          if (t < Btot && (i < KM || KM > 4)) sq[t * 8 + i] = sv[r];
+        }
+      }
+      __syncthreads();
+    }
+    for (int i = lane; i < n; i += 64) g[i] = V[i];
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(64) void rs_shuffle_wave2_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
+    VerifyRoundBufs rh, int cur, int split) {
+  if ((int)blockIdx.x < split)
+    rs_shuffle_wave_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[cur], rf.nact + cur,
+                                 rf.samp, blockIdx.x, split);
+  else
+    rs_shuffle_wave_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[cur], rh.nact + cur,
+                                 rh.samp, blockIdx.x - split, gridDim.x - split);
 }
 
 
@@ -2546,6 +2763,9 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
 #ifndef SCM_SHUFFLE_LDS_KB
 #define SCM_SHUFFLE_LDS_KB 16
 #endif
+#ifndef SCM_WAVE_SHUFFLE_PAIRS
+#define SCM_WAVE_SHUFFLE_PAIRS 256
+#endif
   // Shuffle blocks: as many pairs per block as fit SCM_SHUFFLE_LDS_KB of LDS sample-index
   // vectors (the swap chains are latency-bound; LDS instead of global memory
   // shortens every step of them).
@@ -2554,6 +2774,15 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   const int sh_ppb =
       sh_stride ? std::max(1, std::min(64, (SCM_SHUFFLE_LDS_KB * 1024) / (2 * sh_stride))) : 1;
   const int sh_blocks = (npairs + sh_ppb - 1) / sh_ppb;
+  // Small batches: a wave per pair (rs_shuffle_wave2_kernel) while the batch
+  // leaves most of the GPU idle under the lane-per-pair chains.
+  static const int wave_pairs = [] {
+    const char* e = getenv("SCM_WAVE_SHUFFLE_PAIRS");
+    return e ? atoi(e) : SCM_WAVE_SHUFFLE_PAIRS;
+  }();
+  const int wave_stride = (max_m + 7) / 8 * 8;
+  const bool wave_sh = npairs <= wave_pairs && wave_stride <= kWsMaxStride;
+  const size_t wave_lds = wave_shuffle_lds_bytes(wave_stride);
   // First window: one round per pair when the batch fills the GPU; a small
   // batch (a single Scanner stencil) starts with wider windows -- its chain of
   // windows is latency-bound, and the speculative rounds past an early stop
@@ -2568,9 +2797,13 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     const int g2 = (f ? sh_blocks : 0) + (h ? sh_blocks : 0), s2 = f ? sh_blocks : 0;
     hipLaunchKernelGGL(rs_draw2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
                        out, rf, rh, cur, W, s1);
-    hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
-                       (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch, snaps,
-                       out, rf, rh, cur, sh_ppb, sh_stride, s2);
+    if (wave_sh)
+      hipLaunchKernelGGL(rs_shuffle_wave2_kernel, dim3(g1), dim3(64), wave_lds, stream, pairs,
+                         scratch, snaps, out, rf, rh, cur, s1);
+    else
+      hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
+                         (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch,
+                         snaps, out, rf, rh, cur, sh_ppb, sh_stride, s2);
     if (f)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(SCM_SOLVE_GRID), dim3(64), 0, stream, pairs, xy1, xy2,
                          rf.rst, rf.act[cur], rf.nact + cur, rf.samp, rf.nmod, rf.fcon, rf.mods,
@@ -2641,6 +2874,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     set_lds_attr(rs_begin2_kernel);
     set_lds_attr(rs_draw2_kernel);
     set_lds_attr(rs_shuffle2_kernel);
+    set_lds_attr(rs_shuffle_wave2_kernel);
     set_lds_attr(rs_replay2_kernel);
     set_lds_attr(verify_final_kernel);
     attr = true;

@@ -128,3 +128,36 @@ def test_execute_batch_id_collisions_per_element(what):
     # the variant really changes the outputs of the rows that use it
     assert ref[1] != oracle.execute_stencil(*([x[:1] + [y] + x[2:] for x, y in
                                                zip(stencils[1], (ids[2], kps[2], descs[2]))]))
+
+
+@pytest.mark.parametrize("what", ["desc", "kp"])
+def test_execute_stencil_buffers_rewritten_in_place(what):
+    """Scanner hands consecutive calls the same element buffers, and a caller
+    may rewrite a buffer in place between calls (same address, same size,
+    other image).  Buffers seen in the previous call take its content keys
+    speculatively while the GPU runs; a key that does not hold must discard
+    the run and give exactly the oracle's rows for the new bytes."""
+    n, K = 6, 4
+    ids, kps, descs = table_rows(Corridor(n, 700, K, seed=71).images())
+    kb = [bytearray(x) for x in kps]
+    db = [bytearray(x) for x in descs]
+    st = (ids[:K], kb[:K], db[:K])
+    with Context(0) as ctx:
+        assert ctx.execute_stencil(*st) == oracle.execute_stencil(ids[:K], kps[:K], descs[:K])
+        # unchanged buffers: every image served from HBM
+        assert ctx.execute_stencil(*st) == oracle.execute_stencil(ids[:K], kps[:K], descs[:K])
+        r0, u0 = ctx.stencil_stats()
+        assert u0 == K and r0 == K
+        kv, dv = _variant(kps[2], descs[2], 72, what)
+        kb[2][:] = kv
+        db[2][:] = dv
+        want = oracle.execute_stencil(ids[:K], [bytes(x) for x in kb[:K]],
+                                      [bytes(x) for x in db[:K]])
+        assert want != oracle.execute_stencil(ids[:K], kps[:K], descs[:K])
+        assert ctx.execute_stencil(*st) == want
+        r1, u1 = ctx.stencil_stats()
+        # the run with the stale key is discarded; the rerun starts from an
+        # empty cache and uploads every image of the stencil once
+        assert u1 - u0 == K and r1 == r0
+        assert ctx.execute_stencil(*st) == want
+        assert ctx.stencil_stats() == (r1 + K, u1)
