@@ -1771,10 +1771,15 @@ void scm_context_destroy(scm_context* ctx) {
                    kind ? "H" : "F", (double)ctx->prof_sum[80 + 4 * kind] / (double)ctx->prof_pairs,
                    (double)ctx->prof_sum[81 + 4 * kind] / (double)ctx->prof_pairs,
                    (double)ctx->prof_sum[82 + 4 * kind] / (double)ctx->prof_pairs);
-    static const char* lnames[] = {"lo_gather", "lo_norm", "lo_ata", "lo_jacobi", "lo_resid",
-                                   "lo_inliers"};
+    static const char* snames[] = {"stage", "phaseA", "phaseB", "writeback", "targets"};
     for (int kind = 0; kind < 2; ++kind)
-      for (int j = 0; j < 6; ++j)
+      for (int j = 0; j < 5; ++j)
+        std::fprintf(stderr, "  shuffle %s %-10s %14.1f\n", kind ? "H" : "F", snames[j],
+                     (double)ctx->prof_sum[60 + 5 * kind + j] / (double)ctx->prof_pairs);
+    static const char* lnames[] = {"lo_gather", "lo_norm", "lo_ata", "lo_jacobi", "lo_resid",
+                                   "lo_inliers", "lo_finish"};
+    for (int kind = 0; kind < 2; ++kind)
+      for (int j = 0; j < 7; ++j)
         std::fprintf(stderr, "  LO %s %-10s %14.1f\n", kind ? "H" : "F", lnames[j],
                      (double)ctx->prof_sum[40 + 10 * kind + j] / (double)ctx->prof_pairs);
   }

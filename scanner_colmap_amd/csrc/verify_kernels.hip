@@ -55,6 +55,9 @@ struct __attribute__((aligned(16))) VerifyLds {
   uint32_t counts[kTrialBatch * 3];
   int32_t nmodels[kTrialBatch];
   uint32_t jbuf[kTrialBatch * 7];  // Shuffle targets of one batch of samples
+  double redd[8];  // cross-wave exchange of the multi-wave replay (NW > 1)
+  double fvec[9];
+  int32_t redi[8];
   int32_t mt_idx;
   int32_t best_n;
   int32_t best_sum_valid;
@@ -93,6 +96,13 @@ enum { PR_SAMPLE = 0, PR_SOLVE, PR_SCORE, PR_CAND, PR_SEQSUM, PR_GATHER, PR_LOES
        PR_SCORE_H, PR_N_HCHUNK, PR_N_HSLOW };
 
 __device__ __forceinline__ void wsync() { __syncthreads(); }  // one wavefront: cheap
+// Barrier of a region one wave runs alone inside a multi-wave block (its LDS
+// operations complete in order; this keeps the compiler from moving them).
+__device__ __forceinline__ void wave_only_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
   const uint64_t u = (uint64_t)__double_as_longlong(v);
@@ -804,28 +814,46 @@ __device__ int residuals_wave(const double* m, const double* xy1, const double* 
 }
 
 // InlierSupportMeasurer::Evaluate's residual_sum: inlier residuals summed
-// in index order.  The wave loads 64 x kSeqU residuals at a time; the ordered
-// accumulation runs on values broadcast with v_readlane (every lane computes
-// the same scalar sum).
-__device__ double seq_inlier_sum(const double* res, int n, double maxr) {
+// in index order.  The wave loads 64 x kSeqU residuals at a time; every lane
+// runs the same ordered chain over the 64 lanes' values, broadcast with
+// v_readlane at fixed lane indices (no per-inlier scan).  A point that is not
+// an inlier contributes -0.0, the exact additive identity (x + -0.0 == x for
+// every x, signed zeros included), so the chain performs exactly the
+// reference's additions.
+__device__ __forceinline__ void seq_inlier_load(const double* res, int n, int b0, double (&x)[4]) {
+  const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = b0 + 64 * u + lane;
+    x[u] = i < n ? res[i] : 1.7976931348623157e308;
+  }
+}
+// A batch of 64 with few inliers visits them by a scan of its ballot; a dense
+// one runs the fixed chain over all 64 lanes with -0.0 for the others.
+__device__ __noinline__ double seq_inlier_sum(const double* res, int n, double maxr) {
   double sum = 0.0;
-  for (int b0 = 0; b0 < n; b0 += 64 * kSeqU) {
-    double v[kSeqU];
+  double cur[4];
+  seq_inlier_load(res, n, 0, cur);
+  for (int b0 = 0; b0 < n; b0 += 256) {
+    double nxt[4];  // the next 256 residuals in flight during this chain
+    seq_inlier_load(res, n, b0 + 256, nxt);
 #pragma unroll
-    for (int u = 0; u < kSeqU; ++u) {
-      const int i = b0 + 64 * u + (int)threadIdx.x;
-      v[u] = i < n ? res[i] : 1.7976931348623157e308;
-    }
+    for (int u = 0; u < 4; ++u) {
+      const bool in = cur[u] <= maxr;
+      uint64_t bal = __ballot(in);
+      if (__popcll(bal) <= 16) {
+        while (bal) {
+          sum += readlane_d(cur[u], __builtin_ctzll(bal));
+          bal &= bal - 1;
+        }
+      } else {
+        const double x = in ? cur[u] : -0.0;
 #pragma unroll
-    for (int u = 0; u < kSeqU; ++u) {
-      // Only the inliers contribute: visit them in lane (= index) order.
-      uint64_t bal = __ballot(v[u] <= maxr);
-      while (bal) {
-        const int j = __builtin_ctzll(bal);
-        sum += readlane_d(v[u], j);
-        bal &= bal - 1;
+        for (int l = 0; l < 64; ++l) sum += readlane_d(x, l);
       }
     }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cur[u] = nxt[u];
   }
   return sum;
 }
@@ -891,10 +919,15 @@ __device__ __forceinline__ void apply_norm_affine(const double* T, double p0, do
   *o1 = T[3] * p0 + T[4] * p1 + T[5];
 }
 
-template <int K>
-__device__ int residuals_f4(const double* m, const float4* xyf, int n, double maxr, double* res) {
+// NW > 1 (multi-wave replay): the waves take alternate blocks of 64 kLoU
+// points; the count is exchanged in redi and every residual is visible to the
+// whole block on return.
+template <int K, int NW = 1>
+__device__ int residuals_f4(const double* m, const float4* xyf, int n, double maxr, double* res,
+                            int32_t* redi = nullptr) {
   int c = 0;
-  for (int b = threadIdx.x; b < n; b += 64 * kLoU) {
+  for (int b = (int)(threadIdx.x >> 6) * 64 * kLoU + (int)(threadIdx.x & 63); b < n;
+       b += 64 * kLoU * NW) {
     float4 v[kLoU];
     load_pts(xyf, b, n, v);
 #pragma unroll
@@ -908,15 +941,28 @@ __device__ int residuals_f4(const double* m, const float4* xyf, int n, double ma
       }
     }
   }
-  return wave_sum_i(c);
+  c = wave_sum_i(c);
+  if (NW == 1) return c;
+  if ((threadIdx.x & 63) == 0) redi[threadIdx.x >> 6] = c;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) t += redi[w];
+  __syncthreads();
+  return t;
 }
 
-// Ordered compaction of the points whose residual is <= maxr into xin.
+// Ordered compaction of the points whose residual is <= maxr into xin.  NW >
+// 1: each round of 64 kLoU NW points gives wave w the w-th block; a prefix of
+// the waves' counts (redi) places its inliers, and xin is visible to the
+// whole block on return.
+template <int NW = 1>
 __device__ int gather_inliers_f4(const double* res, int n, double maxr, const float4* xyf,
-                                 float4* xin) {
-  const int lane = threadIdx.x;
+                                 float4* xin, int32_t* redi = nullptr) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int base_out = 0;
-  for (int b0 = 0; b0 < n; b0 += 64 * kLoU) {
+  for (int r0 = 0; r0 < n; r0 += 64 * kLoU * NW) {
+    const int b0 = r0 + wv * 64 * kLoU;
     float4 v[kLoU];
     double r[kLoU];
     load_pts(xyf, b0 + lane, n, v);
@@ -925,18 +971,37 @@ __device__ int gather_inliers_f4(const double* res, int n, double maxr, const fl
       const int i = b0 + 64 * u + lane;
       r[u] = i < n ? res[i] : 1.7976931348623157e308;
     }
+    uint64_t bal[kLoU];
+    int wc = 0;
 #pragma unroll
     for (int u = 0; u < kLoU; ++u) {
-      const bool in = r[u] <= maxr;
-      const uint64_t bal = __ballot(in);
-      if (in) {
-        const int o = base_out + (int)__builtin_amdgcn_mbcnt_hi(
-                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        xin[o] = v[u];
-      }
-      base_out += __popcll(bal);
+      bal[u] = __ballot(r[u] <= maxr);
+      wc += __popcll(bal[u]);
     }
+    int before = 0, total = wc;
+    if (NW > 1) {
+      if (lane == 0) redi[wv] = wc;
+      __syncthreads();
+      total = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int x = redi[w];
+        before += w < wv ? x : 0;
+        total += x;
+      }
+      __syncthreads();
+    }
+    int o = base_out + before;
+#pragma unroll
+    for (int u = 0; u < kLoU; ++u) {
+      if (r[u] <= maxr)
+        xin[o + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal[u] >> 32),
+                                               __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u))] = v[u];
+      o += __popcll(bal[u]);
+    }
+    base_out += total;
   }
+  if (NW > 1) __syncthreads();
   return base_out;
 }
 
@@ -947,7 +1012,13 @@ __device__ int gather_inliers_f4(const double* res, int n, double maxr, const fl
 // The uniform scalars (pivot reciprocal, trace factor, j*, rank-one test) are
 // evaluated by every lane from broadcast LDS reads.  Returns the unit null
 // vector in f (every lane).
+// SOLO: run by one wave of a multi-wave block (wave-only barriers).
+template <bool SOLO = false>
 __device__ void invsq9_null_wave(const double* ata45, double* A, double* B, double* f) {
+  auto bar = [] {
+    if (SOLO) wave_only_sync();
+    else wsync();
+  };
   const int lane = threadIdx.x;
   const int e0 = lane, e1 = lane + 64;  // e1 valid for lane < 17
   const bool has1 = e1 < 81;
@@ -969,7 +1040,7 @@ __device__ void invsq9_null_wave(const double* ata45, double* A, double* B, doub
     load(e0);
     if (has1) load(e1);
   }
-  wsync();
+  bar();
   const int i0 = e0 / 9, j0 = e0 - 9 * (e0 / 9);
   const int i1 = e1 / 9, j1 = e1 - 9 * (e1 / 9);
 #pragma unroll 1
@@ -977,14 +1048,14 @@ __device__ void invsq9_null_wave(const double* ata45, double* A, double* B, doub
     const double inv = 1.0 / A[k * 9 + k];
     const double n0 = gj9_entry(A[e0], A[i0 * 9 + k], A[k * 9 + j0], inv, i0, j0, k);
     const double n1 = has1 ? gj9_entry(A[e1], A[i1 * 9 + k], A[k * 9 + j1], inv, i1, j1, k) : 0.0;
-    wsync();
+    bar();
     A[e0] = n0;
     if (has1) A[e1] = n1;
-    wsync();
+    bar();
   }
   B[e0] = 0.5 * (A[e0] + A[j0 * 9 + i0]);
   if (has1) B[e1] = 0.5 * (A[e1] + A[j1 * 9 + i1]);
-  wsync();
+  bar();
   int jstar = 0;
   bool done = false;
 #pragma unroll 1
@@ -993,11 +1064,11 @@ __device__ void invsq9_null_wave(const double* ata45, double* A, double* B, doub
     const double q1 = has1 ? sq9_entry(B, i1, j1) : 0.0;
     A[e0] = q0;  // A is free: B holds the iterate
     if (has1) A[e1] = q1;
-    wsync();
+    bar();
     const double ti = sq9_trace_inv(A);
     B[e0] = q0 * ti;
     if (has1) B[e1] = q1 * ti;
-    wsync();
+    bar();
     jstar = sq9_argmax_diag(B);
     if (done) break;
     done = sq + 1 >= kInvSqMin && sq9_rank_one(B, jstar);
@@ -1131,6 +1202,60 @@ __device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const doub
   else homography_finish(f, T1, T2, model);
 }
 
+__device__ __forceinline__ void norm_transforms(double c10, double c11, double c20, double c21,
+                                                double rms1, double rms2, double* T1, double* T2) {
+  const double s1 = sqrt(2.0) / rms1, s2 = sqrt(2.0) / rms2;
+  T1[0] = s1; T1[1] = 0.0; T1[2] = -s1 * c10;
+  T1[3] = 0.0; T1[4] = s1; T1[5] = -s1 * c11;
+  T1[6] = 0.0; T1[7] = 0.0; T1[8] = 1.0;
+  T2[0] = s2; T2[1] = 0.0; T2[2] = -s2 * c20;
+  T2[3] = 0.0; T2[4] = s2; T2[5] = -s2 * c21;
+  T2[6] = 0.0; T2[7] = 0.0; T2[8] = 1.0;
+}
+
+// normalize_pair_f4 with four waves: wave w forms the canonical sum of
+// coordinate w (then waves 0 / 1 the two RMS sums) with the lane mapping of
+// the one-wave version, so every sum is the same.
+__device__ void normalize_pair_f4_w4(const float4* xin, int n, double* T1, double* T2,
+                                     double* redd) {
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  double p = kCanonZero;
+  for (int b = lane; b < n; b += 64 * kLoU) {
+    float4 v[kLoU];
+    load_pts(xin, b, n, v);
+#pragma unroll
+    for (int u = 0; u < kLoU; ++u)
+      if (b + 64 * u < n)
+        p += (double)(wv == 0 ? v[u].x : wv == 1 ? v[u].y : wv == 2 ? v[u].z : v[u].w);
+  }
+  p = canon_tree_wave(p);
+  if (lane == 0) redd[wv] = p;
+  __syncthreads();
+  const double c10 = redd[0] / (double)n, c11 = redd[1] / (double)n;
+  const double c20 = redd[2] / (double)n, c21 = redd[3] / (double)n;
+  __syncthreads();
+  if (wv < 2) {
+    const double ca = wv == 0 ? c10 : c20, cb = wv == 0 ? c11 : c21;
+    p = kCanonZero;
+    for (int b = lane; b < n; b += 64 * kLoU) {
+      float4 v[kLoU];
+      load_pts(xin, b, n, v);
+#pragma unroll
+      for (int u = 0; u < kLoU; ++u)
+        if (b + 64 * u < n) {
+          const double d0 = (double)(wv == 0 ? v[u].x : v[u].z) - ca;
+          const double d1 = (double)(wv == 0 ? v[u].y : v[u].w) - cb;
+          p += d0 * d0 + d1 * d1;
+        }
+    }
+    p = canon_tree_wave(p);
+    if (lane == 0) redd[4 + wv] = p;
+  }
+  __syncthreads();
+  norm_transforms(c10, c11, c20, c21, sqrt(redd[4] / (double)n), sqrt(redd[5] / (double)n), T1, T2);
+  __syncthreads();
+}
+
 // normalize_pair_wave on packed points (canonical sums, same order).
 __device__ void normalize_pair_f4(const float4* xin, int n, double* T1, double* T2) {
   double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
@@ -1173,14 +1298,15 @@ __device__ void normalize_pair_f4(const float4* xin, int n, double* T1, double* 
   T2[6] = 0.0; T2[7] = 0.0; T2[8] = 1.0;
 }
 
-// ata_pass_wave on packed points.
-template <int K, int PASS>
-__device__ __forceinline__ void ata_pass_f4(VerifyLds& s, const float4* xin, int n,
-                                            const double* T1, const double* T2) {
-  const int lane = threadIdx.x;
-  double part[15];
+// ata_pass_wave on packed points: packed entries [K0, K1) of A^T A.
+template <int K, int K0, int K1>
+__device__ __forceinline__ void ata_range_f4(VerifyLds& s, const float4* xin, int n,
+                                             const double* T1, const double* T2) {
+  constexpr int NE = K1 - K0;
+  const int lane = threadIdx.x & 63;
+  double part[NE];
 #pragma unroll
-  for (int k = 0; k < 15; ++k) part[k] = kCanonZero;
+  for (int k = 0; k < NE; ++k) part[k] = kCanonZero;
 #pragma unroll 1
   for (int b = lane; b < n; b += 64 * kLoU) {
     float4 v[kLoU];
@@ -1199,8 +1325,7 @@ __device__ __forceinline__ void ata_pass_f4(VerifyLds& s, const float4* xin, int
       for (int p = 0; p < 9; ++p)
 #pragma unroll
         for (int q = p; q < 9; ++q) {
-          if (k >= 15 * PASS && k < 15 * PASS + 15)
-            part[k - 15 * PASS] = part[k - 15 * PASS] + a[p] * a[q];
+          if (k >= K0 && k < K1) part[k - K0] = part[k - K0] + a[p] * a[q];
           ++k;
         }
       if (K == KIND_H) {
@@ -1209,39 +1334,67 @@ __device__ __forceinline__ void ata_pass_f4(VerifyLds& s, const float4* xin, int
         for (int p = 0; p < 9; ++p)
 #pragma unroll
           for (int q = p; q < 9; ++q) {
-            if (k >= 15 * PASS && k < 15 * PASS + 15)
-              part[k - 15 * PASS] = part[k - 15 * PASS] + c[p] * c[q];
+            if (k >= K0 && k < K1) part[k - K0] = part[k - K0] + c[p] * c[q];
             ++k;
           }
       }
     }
   }
 #pragma unroll
-  for (int k = 0; k < 15; ++k) {
+  for (int k = 0; k < NE; ++k) {
     const double t = canon_tree_wave(part[k]);
-    if (lane == 0) s.ata[15 * PASS + k] = t;
+    if (lane == 0) s.ata[K0 + k] = t;
   }
+}
+template <int K, int PASS>
+__device__ __forceinline__ void ata_pass_f4(VerifyLds& s, const float4* xin, int n,
+                                            const double* T1, const double* T2) {
+  ata_range_f4<K, 15 * PASS, 15 * PASS + 15>(s, xin, n, T1, T2);
 }
 
 // local_estimate_wave (F: 8-point, H: DLT) on packed points.
-template <int K>
+// NW = 4: the coordinate sums and the A^T A entries are split between the
+// waves (each sum whole on one wave), the 9 x 9 null vector runs on wave 0.
+template <int K, int NW = 1>
 __device__ void local_estimate_f4(VerifyLds& s, const float4* xin, int n, double* model,
                                   uint64_t* pl = nullptr) {
+  static_assert(NW == 1 || NW == 4, "one wave or four");
   uint64_t t0 = pl ? __builtin_amdgcn_s_memtime() : 0;
   double T1[9], T2[9];
-  normalize_pair_f4(xin, n, T1, T2);
+  if (NW == 1) normalize_pair_f4(xin, n, T1, T2);
+  else normalize_pair_f4_w4(xin, n, T1, T2, s.redd);
   if (pl && threadIdx.x == 0) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[1] += t - t0; t0 = t; }
-  ata_pass_f4<K, 0>(s, xin, n, T1, T2);
-  ata_pass_f4<K, 1>(s, xin, n, T1, T2);
-  ata_pass_f4<K, 2>(s, xin, n, T1, T2);
+  if (NW == 1) {
+    ata_pass_f4<K, 0>(s, xin, n, T1, T2);
+    ata_pass_f4<K, 1>(s, xin, n, T1, T2);
+    ata_pass_f4<K, 2>(s, xin, n, T1, T2);
+  } else {
+    switch (threadIdx.x >> 6) {
+      case 0: ata_range_f4<K, 0, 12>(s, xin, n, T1, T2); break;
+      case 1: ata_range_f4<K, 12, 24>(s, xin, n, T1, T2); break;
+      case 2: ata_range_f4<K, 24, 35>(s, xin, n, T1, T2); break;
+      default: ata_range_f4<K, 35, 45>(s, xin, n, T1, T2); break;
+    }
+  }
   wsync();
   if (pl && threadIdx.x == 0) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[2] += t - t0; t0 = t; }
   double f[9];
-  invsq9_null_wave(s.ata, s.jA, s.jV, f);
+  if (NW == 1) {
+    invsq9_null_wave(s.ata, s.jA, s.jV, f);
+  } else {
+    if (threadIdx.x < 64) {
+      invsq9_null_wave<true>(s.ata, s.jA, s.jV, f);
+      if (threadIdx.x < 9) s.fvec[threadIdx.x] = f[threadIdx.x];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 9; ++i) f[i] = s.fvec[i];
+  }
   wsync();
-  if (pl && threadIdx.x == 0) pl[3] += __builtin_amdgcn_s_memtime() - t0;
+  if (pl && threadIdx.x == 0) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[3] += t - t0; t0 = t; }
   if (K == KIND_F) fundamental_8pt_finish(f, T1, T2, model);
   else homography_finish(f, T1, T2, model);
+  if (pl && threadIdx.x == 0) pl[6] += __builtin_amdgcn_s_memtime() - t0;
 }
 
 struct RansacResult {
@@ -1551,12 +1704,12 @@ __device__ __forceinline__ PairSetup pair_setup(const VerifyPair* pairs, double*
 }
 
 __device__ __forceinline__ void mt_save(const VerifyLds& s, uint32_t* st) {
-  for (int i = threadIdx.x; i < 624; i += 64) st[i] = s.mt[i];
+  for (int i = threadIdx.x; i < 624; i += blockDim.x) st[i] = s.mt[i];
   if (threadIdx.x == 0) st[624] = (uint32_t)s.mt_idx;
 }
 
 __device__ __forceinline__ void mt_load(VerifyLds& s, const uint32_t* st) {
-  for (int i = threadIdx.x; i < 624; i += 64) s.mt[i] = st[i];
+  for (int i = threadIdx.x; i < 624; i += blockDim.x) s.mt[i] = st[i];
   if (threadIdx.x == 0) s.mt_idx = (int32_t)st[624];
   wsync();
 }
@@ -1718,13 +1871,13 @@ __device__ __forceinline__ uint32_t* pair_sidx(const PairSetup& ps) {
 template <int K>
 __device__ void rs_finish(const PairSetup& ps, const RansacState& st, uint8_t* masks,
                           double maxr) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x;  // block-wide (one or several waves)
   const int n = ps.n;
   if (K == KIND_F) {
     uint8_t* mask = masks + ps.pp.mask_off;
     const double* resb = ps.base + (st.res_sel ? n : 0);
     const bool ok = st.best_n >= KindTraits<K>::kmin;
-    for (int i = lane; i < n; i += 64) mask[i] = (ok && resb[i] <= maxr) ? 1 : 0;
+    for (int i = lane; i < n; i += blockDim.x) mask[i] = (ok && resb[i] <= maxr) ? 1 : 0;
     if (lane < 9) ps.o->F[lane] = st.best_model[lane];
     if (lane == 0) {
       ps.o->f_trials = st.num_trials;
@@ -1950,11 +2103,16 @@ __device__ __attribute__((always_inline)) void rs_shuffle_body(
 constexpr int kWsC = 16;               // trials per lane and pass
 constexpr int kWsTab = 256;            // table slots per lane (>= 2 x kmin x kWsC)
 constexpr int kWsPass = 64 * kWsC;     // trials per pass
+constexpr int kWsRow = 65;             // trial slots per row of ssym (64 lanes + 1: no bank conflicts)
 constexpr int kWsMaxStride = 32768;    // vector positions staged as uint16
 static_assert(kWsTab == 64 * 4, "phase B reads a chunk's table as one uint4 per lane");
 
+// LDS: the lanes' tables, the pass's trial slots (8 uint16: targets, then the
+// sample's symbols), head symbols, the vector plus one dummy entry per lane
+// (the target of the reads and writes of empty table slots: no branches).
 size_t wave_shuffle_lds_bytes(int stride) {
-  return (size_t)64 * kWsTab * 4 + (size_t)kWsPass * 8 * 2 + 64 * 8 * 2 + (size_t)stride * 2;
+  return (size_t)64 * kWsTab * 4 + (size_t)kWsC * kWsRow * 16 + 64 * 8 * 2 +
+         (size_t)(stride + 64) * 2;
 }
 
 template <int K>
@@ -1962,113 +2120,200 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
     const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
-    const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, int bid, int nblk) {
+    const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, uint64_t* __restrict__ prof,
+    int stride, int bid, int nblk) {
   constexpr int KM = KindTraits<K>::kmin;
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-  uint32_t* tab = reinterpret_cast<uint32_t*>(dyn_lds);            // 64 x kWsTab: (j << 16) | symbol
-  uint16_t* ssym = reinterpret_cast<uint16_t*>(tab + 64 * kWsTab);  // kWsPass x 8 sample symbols
-  uint16_t* hsym = ssym + kWsPass * 8;                               // 64 x 8 head symbols
-  uint16_t* V = hsym + 64 * 8;                                        // the vector
+  uint32_t* tab = reinterpret_cast<uint32_t*>(dyn_lds);  // 64 x kWsTab: (j << 16) | symbol
+  // Trial k of lane L's chunk lives in slot k * kWsRow + L (16 bytes).
+  uint4* slots = reinterpret_cast<uint4*>(tab + 64 * kWsTab);
+  uint16_t* hsym = reinterpret_cast<uint16_t*>(slots + kWsC * kWsRow);  // 64 x 8 head symbols
+  uint16_t* V = hsym + 64 * 8;                                           // the vector (+ dummies)
   const int lane = threadIdx.x;
+  const uint32_t dummy = (uint32_t)(stride + lane);
   const int na = *nact;
   for (int a = bid; a < na; a += nblk) {
     const int q = act[a];
     const PairSetup ps = pair_at<K>(pairs, q, scratch, snaps, out);
     uint32_t* g = pair_sidx(ps);
     const int n = ps.n;
-    for (int i = lane; i < n; i += 64) V[i] = (uint16_t)g[i];
+    // Diagnostic phase cycles (SCM_PROFILE=1 only): staging, phase A, phase B, write-back.
+    uint64_t* pc = prof ? prof + (int64_t)q * kVerifyProfSlots + (K == KIND_F ? 60 : 65) : nullptr;
+    uint64_t tp = pc ? __builtin_amdgcn_s_memtime() : 0;
+    auto lap = [&](int k) {
+      if (pc && lane == 0) {
+        const uint64_t t = __builtin_amdgcn_s_memtime();
+        pc[k] += t - tp;
+        tp = t;
+      }
+    };
+    for (int b = lane; b < n; b += 64 * 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = g[min(b + 64 * u, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (b + 64 * u < n) V[b + 64 * u] = (uint16_t)v[u];
+    }
+    __syncthreads();
+    lap(0);
     uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
     const int Btot = rst[q].B;
     for (int p0 = 0; p0 < Btot; p0 += kWsPass) {
-      uint32_t* mt = tab + lane * kWsTab;
-#pragma unroll 4
-      for (int s2 = 0; s2 < kWsTab / 4; ++s2)
-        reinterpret_cast<uint4*>(mt)[s2] = make_uint4(0u, 0u, 0u, 0u);
+      const int np = min(kWsPass, Btot - p0);
+      {
+        uint4* t4 = reinterpret_cast<uint4*>(tab);
+        for (int i = lane; i < 64 * kWsTab / 4; i += 64) t4[i] = make_uint4(0u, 0u, 0u, 0u);
+      }
+      // The pass's targets (drawn by rs_draw into samp) into the trial slots
+      // as uint16 pairs, coalesced.
+      // (All of a lane's loads are issued before the first LDS write: one
+      // memory latency per pass, not one per trial.)
+      {
+        constexpr int U = kWsPass / 64;
+        uint4 a0[U], a1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int idx = min(lane + 64 * u, np - 1);
+          a0[u] = reinterpret_cast<const uint4*>(sq + (p0 + idx) * 8)[0];
+          a1[u] = KM > 4 ? reinterpret_cast<const uint4*>(sq + (p0 + idx) * 8)[1]
+                         : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int idx = lane + 64 * u;
+          if (idx < np)
+            slots[(idx % kWsC) * kWsRow + idx / kWsC] =
+                make_uint4(a0[u].x | (a0[u].y << 16), a0[u].z | (a0[u].w << 16),
+                           a1[u].x | (a1[u].y << 16), a1[u].z | (a1[u].w << 16));
+        }
+      }
+      __syncthreads();
+      lap(4);
       // Phase A: this lane's chunk on symbols.
+      uint32_t* mt = tab + lane * kWsTab;
       uint32_t R[KM];
 #pragma unroll
       for (int i = 0; i < KM; ++i) R[i] = (uint32_t)i;
-      const int t0 = p0 + lane * kWsC, t1 = min(t0 + kWsC, Btot);
-      for (int t = t0; t < t1; ++t) {
-        const uint4 w0 = reinterpret_cast<const uint4*>(sq + t * 8)[0];
-        const uint4 w1 = KM > 4 ? reinterpret_cast<const uint4*>(sq + t * 8)[1]
-                                : make_uint4(0u, 0u, 0u, 0u);
-        const uint32_t wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const int kn = min(kWsC, max(0, np - lane * kWsC));
+      uint4 nx = kn > 0 ? slots[lane] : make_uint4(0u, 0u, 0u, 0u);
+      for (int k = 0; k < kn; ++k) {
+        const uint32_t wv[8] = {nx.x & 0xffffu, nx.x >> 16, nx.y & 0xffffu, nx.y >> 16,
+                                nx.z & 0xffffu, nx.z >> 16, nx.w & 0xffffu, nx.w >> 16};
+        if (k + 1 < kn) nx = slots[(k + 1) * kWsRow + lane];
 #pragma unroll
         for (int i = 0; i < KM; ++i) {  // std::swap(sidx[i], sidx[j])
           const uint32_t j = wv[i];
           if (j < (uint32_t)KM) {
             uint32_t ri = R[i];
 #pragma unroll
-            for (int k = i + 1; k < KM; ++k) {
-              const bool m = j == (uint32_t)k;
-              const uint32_t rk = R[k];
-              R[k] = m ? ri : rk;
+            for (int k2 = i + 1; k2 < KM; ++k2) {
+              const bool m = j == (uint32_t)k2;
+              const uint32_t rk = R[k2];
+              R[k2] = m ? ri : rk;
               ri = m ? rk : ri;
             }
             R[i] = ri;
           } else {
-            uint32_t slot = (j * 0x9E3779B1u) >> 24;
-            uint32_t w = mt[slot];
-            while (w != 0u && (w >> 16) != j) {
-              slot = (slot + 1) & (kWsTab - 1);
-              w = mt[slot];
+            // Buckets of 8 slots (two b128 reads, one round trip), filled
+            // from slot 0 up: j is in its bucket before the first empty slot
+            // or absent; a full bucket continues in the next one.
+            uint32_t b = (j * 0x9E3779B1u) >> 27;
+            uint32_t slot, sym;
+            for (;;) {
+              const uint4 x0 = reinterpret_cast<const uint4*>(mt + b * 8)[0];
+              const uint4 x1 = reinterpret_cast<const uint4*>(mt + b * 8)[1];
+              const uint32_t w[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+              uint32_t stop = 0u;
+#pragma unroll
+              for (int e = 0; e < 8; ++e)
+                stop |= (w[e] == 0u || (w[e] >> 16) == j) ? (1u << e) : 0u;
+              if (stop) {
+                const uint32_t e = (uint32_t)__builtin_ctz(stop);
+                uint32_t we = w[0];
+#pragma unroll
+                for (int e2 = 1; e2 < 8; ++e2) we = e == (uint32_t)e2 ? w[e2] : we;
+                slot = b * 8 + e;
+                sym = we ? (we & 0xffffu) : j;
+                break;
+              }
+              b = (b + 1) & (kWsTab / 8 - 1);
             }
-            const uint32_t sym = w ? (w & 0xffffu) : j;
             mt[slot] = (j << 16) | R[i];
             R[i] = sym;
           }
         }
+        uint32_t o[8];
 #pragma unroll
-        for (int i = 0; i < KM; ++i) ssym[(t - p0) * 8 + i] = (uint16_t)R[i];
+        for (int i = 0; i < 8; ++i) o[i] = i < KM ? R[i] : 0u;
+        slots[k * kWsRow + lane] = make_uint4(o[0] | (o[1] << 16), o[2] | (o[3] << 16),
+                                              o[4] | (o[5] << 16), o[6] | (o[7] << 16));
       }
 #pragma unroll
       for (int i = 0; i < KM; ++i) hsym[lane * 8 + i] = (uint16_t)R[i];
       __syncthreads();
-      // Phase B: the chunks in order over the vector.
-      const int nch = (min(Btot - p0, kWsPass) + kWsC - 1) / kWsC;
-      for (int c = 0; c < nch; ++c) {
-        const int tc = p0 + c * kWsC;
-        uint32_t sv[2];
+      lap(1);
+      // Phase B: the chunks in order over the vector.  Entry e = lane + 64 r
+      // of a chunk's samples is trial e / 8, index e % 8.
+      const int nch = (np + kWsC - 1) / kWsC;
+      const uint16_t* ss = reinterpret_cast<const uint16_t*>(slots);
+      // A chunk's symbols and exit map do not depend on the vector: the next
+      // chunk's are read while this one's vector reads are in flight.
+      auto chunk_syms = [&](int c, uint32_t* sy, uint4* wd, uint32_t* hs) {
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
-          const int e = lane + 64 * r, i = e & 7;
-          sv[r] = i < KM && tc + (e >> 3) < Btot ? (uint32_t)V[ssym[(c * kWsC + (e >> 3)) * 8 + i]]
-                                                 : 0u;
+          const int e = lane + 64 * r, i = e & 7, k = e >> 3;
+          sy[r] = i < KM && c * kWsC + k < np ? (uint32_t)ss[(k * kWsRow + c) * 8 + i] : dummy;
         }
-        const uint4 wd = reinterpret_cast<const uint4*>(tab + c * kWsTab)[lane];
-        const uint32_t v0 = wd.x ? V[wd.x & 0xffffu] : 0u, v1 = wd.y ? V[wd.y & 0xffffu] : 0u;
-        const uint32_t v2 = wd.z ? V[wd.z & 0xffffu] : 0u, v3 = wd.w ? V[wd.w & 0xffffu] : 0u;
-        const uint32_t hv = lane < KM ? V[hsym[c * 8 + lane]] : 0u;
-        if (wd.x) V[wd.x >> 16] = (uint16_t)v0;
-        if (wd.y) V[wd.y >> 16] = (uint16_t)v1;
-        if (wd.z) V[wd.z >> 16] = (uint16_t)v2;
-        if (wd.w) V[wd.w >> 16] = (uint16_t)v3;
-        if (lane < KM) V[lane] = (uint16_t)hv;
+        *wd = reinterpret_cast<const uint4*>(tab + c * kWsTab)[lane];
+        *hs = lane < KM ? (uint32_t)hsym[c * 8 + lane] : dummy;
+      };
+      auto src_of = [&](uint32_t w) { return w ? (w & 0xffffu) : dummy; };
+      auto dst_of = [&](uint32_t w) { return w ? (w >> 16) : dummy; };
+      uint32_t sy[2], hs;
+      uint4 wd;
+      chunk_syms(0, sy, &wd, &hs);
+      for (int c = 0; c < nch; ++c) {
+        const int tc = p0 + c * kWsC;
+        const uint32_t sv0 = V[sy[0]], sv1 = V[sy[1]];
+        const uint32_t v0 = V[src_of(wd.x)], v1 = V[src_of(wd.y)];
+        const uint32_t v2 = V[src_of(wd.z)], v3 = V[src_of(wd.w)];
+        const uint32_t hv = V[hs];
+        const uint32_t d0 = dst_of(wd.x), d1 = dst_of(wd.y), d2 = dst_of(wd.z), d3 = dst_of(wd.w);
+        const uint32_t dh = lane < KM ? (uint32_t)lane : dummy;
+        if (c + 1 < nch) chunk_syms(c + 1, sy, &wd, &hs);
+        V[d0] = (uint16_t)v0;
+        V[d1] = (uint16_t)v1;
+        V[d2] = (uint16_t)v2;
+        V[d3] = (uint16_t)v3;
+        V[dh] = (uint16_t)hv;
+        const uint32_t svr[2] = {sv0, sv1};
 #pragma unroll
         for (int r = 0; r < 2; ++r) {
           const int e = lane + 64 * r, i = e & 7, t = tc + (e >> 3);
           // rows as shuffle_chain writes them: kmin samples (+ a zero pad for F)
-          if (t < Btot && (i < KM || KM > 4)) sq[t * 8 + i] = sv[r];
+          if (t < p0 + np && (i < KM || KM > 4)) sq[t * 8 + i] = i < KM ? svr[r] : 0u;
         }
       }
       __syncthreads();
+      lap(2);
     }
     for (int i = lane; i < n; i += 64) g[i] = V[i];
     __syncthreads();
+    lap(3);
   }
 }
 
 __global__ __launch_bounds__(64) void rs_shuffle_wave2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
-    VerifyRoundBufs rh, int cur, int split) {
+    VerifyRoundBufs rh, int cur, uint64_t* __restrict__ prof, int stride, int split) {
   if ((int)blockIdx.x < split)
     rs_shuffle_wave_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[cur], rf.nact + cur,
-                                 rf.samp, blockIdx.x, split);
+                                 rf.samp, prof, stride, blockIdx.x, split);
   else
     rs_shuffle_wave_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[cur], rh.nact + cur,
-                                 rh.samp, blockIdx.x - split, gridDim.x - split);
+                                 rh.samp, prof, stride, blockIdx.x - split, gridDim.x - split);
 }
 
 
@@ -2410,7 +2655,9 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
 }
 
 // The sequential part of one window, in trial order, for every active pair.
-template <int K>
+// NW waves per pair (4: small batches, see rs_replay2w_kernel): every wave
+// runs the same decisions from the shared LDS state; thread 0 writes it.
+template <int K, int NW = 1>
 __device__ __attribute__((always_inline)) void rs_replay_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
@@ -2424,7 +2671,8 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool t0th = threadIdx.x == 0;
   const double maxr = P.max_residual;
   const int na = *nact;
   for (int a = bid; a < na; a += nblk) {
@@ -2434,7 +2682,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     // whole replay.
     uint64_t* pc = prof ? prof + (int64_t)q * kVerifyProfSlots + (K == KIND_F ? 20 : 30) : nullptr;
     const uint64_t t_enter = pc ? __builtin_amdgcn_s_memtime() : 0;
-    if (pc && lane == 0) pc[0] += 1;
+    if (pc && t0th) pc[0] += 1;
     const PairSetup ps = pair_at<K>(pairs, q, scratch, snaps, out);
     const int n = ps.n;
     double* base = ps.base;
@@ -2447,8 +2695,8 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     const double* mq = mods + (int64_t)q * kWindowTrials * 3 * MS;
     RansacState st = rst[q];
     wsync();
-    if (lane < 9) s.best_model[lane] = st.best_model[lane];
-    if (lane == 0) {
+    if (threadIdx.x < 9) s.best_model[threadIdx.x] = st.best_model[threadIdx.x];
+    if (t0th) {
       s.best_n = st.best_n;
       s.best_sum = st.best_sum;
       s.best_sum_valid = st.best_sum_valid;
@@ -2463,8 +2711,8 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     for (int r0 = 0; r0 < Btot && !abort; r0 += kTrialBatch) {
       const int B = min(kTrialBatch, Btot - r0);
       wsync();
-      for (int i = lane; i < B; i += 64) s.nmodels[i] = nmod[(int64_t)q * kWindowTrials + r0 + i];
-      for (int i = lane; i < B * MM; i += 64)
+      for (int i = threadIdx.x; i < B; i += 64 * NW) s.nmodels[i] = nmod[(int64_t)q * kWindowTrials + r0 + i];
+      for (int i = threadIdx.x; i < B * MM; i += 64 * NW)
         s.counts[i] = cnts[(int64_t)q * kWindowTrials * 3 + r0 * MM + i];
       wsync();
       // Trials of the round in order.  Only two kinds need the sequential
@@ -2502,10 +2750,10 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
 #pragma unroll
               for (int j = 0; j < MS; ++j) mk[j] = src[j];
               double* rt = res[best_sel ^ 1];
-              residuals_f4<K>(mk, xyf, n, maxr, rt);
+              residuals_f4<K, NW>(mk, xyf, n, maxr, rt, s.redi);
               bool better = c > bn;
               double sum = 0.0;
-              if (pc && lane == 0) {
+              if (pc && t0th) {
                 const uint64_t t1 = __builtin_amdgcn_s_memtime();
                 pc[1] += 1;
                 pc[5] += t1 - t0;
@@ -2515,16 +2763,16 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                 sum = seq_inlier_sum(rt, n, maxr);
                 ensure_best_sum(s, res[best_sel], n, maxr);
                 better = sum < s.best_sum;
-                if (pc && lane == 0) {
+                if (pc && t0th) {
                   pc[2] += 1;
                   pc[6] += __builtin_amdgcn_s_memtime() - t0;
                 }
               }
-              if (pc && lane == 0 && better) pc[3] += 1;
+              if (pc && t0th && better) pc[3] += 1;
               const uint64_t t_lo = pc ? __builtin_amdgcn_s_memtime() : 0;
               if (better) {
                 wsync();
-                if (lane == 0) {
+                if (t0th) {
 #pragma unroll
                   for (int j = 0; j < MS; ++j) s.best_model[j] = mk[j];
                   s.best_n = c;
@@ -2536,18 +2784,18 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                 // Recursive local optimisation.
                 if (c > Tr::kmin && c >= Tr::kmin_local) {
                   for (int lt = 0; lt < 10; ++lt) {
-                    if (pc && lane == 0) pc[4] += 1;
+                    if (pc && t0th) pc[4] += 1;
                     uint64_t* pl = pc ? pc + 20 : nullptr;
                     uint64_t tl0 = pl ? __builtin_amdgcn_s_memtime() : 0;
-                    const int ni = gather_inliers_f4(res[best_sel], n, maxr, xyf, xin);
-                    if (pl && lane == 0) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[0] += t - tl0; tl0 = t; pl[5] += ni; }
+                    const int ni = gather_inliers_f4<NW>(res[best_sel], n, maxr, xyf, xin, s.redi);
+                    if (pl && t0th) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[0] += t - tl0; tl0 = t; pl[5] += ni; }
                     double lm[9];
-                    local_estimate_f4<K>(s, xin, ni, lm, pl);
-                    if (pl && lane == 0) tl0 = __builtin_amdgcn_s_memtime();
+                    local_estimate_f4<K, NW>(s, xin, ni, lm, pl);
+                    if (pl && t0th) tl0 = __builtin_amdgcn_s_memtime();
                     const int prev = s.best_n;
                     double* rl = res[best_sel ^ 1];
-                    const int lcn = residuals_f4<K>(lm, xyf, n, maxr, rl);
-                    if (pl && lane == 0) pl[4] += __builtin_amdgcn_s_memtime() - tl0;
+                    const int lcn = residuals_f4<K, NW>(lm, xyf, n, maxr, rl, s.redi);
+                    if (pl && t0th) pl[4] += __builtin_amdgcn_s_memtime() - tl0;
                     bool lbetter = lcn > prev;
                     double lsum = 0.0;
                     if (lcn == prev) {
@@ -2557,7 +2805,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                     }
                     if (lbetter) {
                       wsync();
-                      if (lane == 0) {
+                      if (t0th) {
 #pragma unroll
                         for (int j = 0; j < MS; ++j) s.best_model[j] = lm[j];
                         s.best_n = lcn;
@@ -2574,7 +2822,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                                    num_trials((uint64_t)s.best_n, (uint64_t)n, P.confidence,
                                               P.dyn_num_trials_multiplier, Tr::kmin));
               }
-              if (pc && lane == 0) pc[7] += __builtin_amdgcn_s_memtime() - t_lo;
+              if (pc && t0th) pc[7] += __builtin_amdgcn_s_memtime() - t_lo;
             }
             if (tt >= dyn_max && tt >= P.min_num_trials) {
               abort = true;
@@ -2597,9 +2845,9 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
       // the state before its round, then that round's draws up to it.
       const int w = (abort_trial - trial) / kTrialBatch;
       const uint32_t* snap = wsnap + ((int64_t)q * kMaxWindow + w) * 640;
-      for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
+      for (int i = threadIdx.x; i < 624; i += 64 * NW) s.mt[i] = snap[i];
       wsync();
-      if (lane == 0) {
+      if (t0th) {
         s.mt_idx = (int32_t)snap[624];
         const uint32_t last = (uint32_t)(n - 1);
         for (int b = 0; b <= abort_trial - trial - w * kTrialBatch; ++b)
@@ -2623,10 +2871,10 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
 #pragma unroll
     for (int j = 0; j < 9; ++j) st.best_model[j] = s.best_model[j];
     wsync();
-    if (lane == 0) rst[q] = st;
+    if (t0th) rst[q] = st;
     if (st.done) rs_finish<K>(ps, st, masks, maxr);
-    else if (lane == 0) act_next[atomicAdd(nact_next, 1)] = q;
-    if (pc && lane == 0) {
+    else if (t0th) act_next[atomicAdd(nact_next, 1)] = q;
+    if (pc && t0th) {
       pc[8] += __builtin_amdgcn_s_memtime() - t_enter;
       pc[9] += (uint64_t)Btot;
     }
@@ -2692,6 +2940,23 @@ __global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay2_kernel(
     rs_replay_body<KIND_H>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[cur], rh.nact + cur,
                            rh.act[cur ^ 1], rh.nact + (cur ^ 1), rh.nmod, rh.cnts, rh.mods,
                            rh.wsnap, P, prof, xyf, blockIdx.x - split, gridDim.x - split);
+}
+
+// rs_replay2_kernel with four waves per pair (small batches: the window's
+// sequential decisions are the critical path of one Scanner stencil).
+__global__ __launch_bounds__(256) void rs_replay2w_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
+    VerifyRoundBufs rf, VerifyRoundBufs rh, int cur, VerifyParams P, uint64_t* __restrict__ prof,
+    const float4* __restrict__ xyf, int split) {
+  if ((int)blockIdx.x < split)
+    rs_replay_body<KIND_F, 4>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[cur], rf.nact + cur,
+                              rf.act[cur ^ 1], rf.nact + (cur ^ 1), rf.nmod, rf.cnts, rf.mods,
+                              rf.wsnap, P, prof, xyf, blockIdx.x, split);
+  else
+    rs_replay_body<KIND_H, 4>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[cur], rh.nact + cur,
+                              rh.act[cur ^ 1], rh.nact + (cur ^ 1), rh.nmod, rh.cnts, rh.mods,
+                              rh.wsnap, P, prof, xyf, blockIdx.x - split, gridDim.x - split);
 }
 
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
@@ -2799,7 +3064,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                        out, rf, rh, cur, W, s1);
     if (wave_sh)
       hipLaunchKernelGGL(rs_shuffle_wave2_kernel, dim3(g1), dim3(64), wave_lds, stream, pairs,
-                         scratch, snaps, out, rf, rh, cur, s1);
+                         scratch, snaps, out, rf, rh, cur, prof, wave_stride, s1);
     else
       hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
                          (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch,
@@ -2848,8 +3113,12 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       }
     }
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r + 1], stream);
-    hipLaunchKernelGGL(rs_replay2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
-                       out, masks, rf, rh, cur, P, prof, xyf, s1);
+    if (wave_sh)
+      hipLaunchKernelGGL(rs_replay2w_kernel, dim3(g1), dim3(256), lds, stream, pairs, scratch,
+                         snaps, out, masks, rf, rh, cur, P, prof, xyf, s1);
+    else
+      hipLaunchKernelGGL(rs_replay2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
+                         out, masks, rf, rh, cur, P, prof, xyf, s1);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     covered += W * kTrialBatch;
@@ -2876,6 +3145,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     set_lds_attr(rs_shuffle2_kernel);
     set_lds_attr(rs_shuffle_wave2_kernel);
     set_lds_attr(rs_replay2_kernel);
+    set_lds_attr(rs_replay2w_kernel);
     set_lds_attr(verify_final_kernel);
     attr = true;
   }
