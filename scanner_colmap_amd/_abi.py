@@ -169,18 +169,33 @@ def _blob_bytes(b: Blob) -> bytes:
     return out
 
 
+_U8P = POINTER(c_uint8)
+# Offset of a bytes object's data from its id() (CPython's PyBytesObject
+# layout), measured once: bytes elements -- what Scanner hands over -- are
+# passed by address with no per-element ctypes objects.
+_probe = b"scm"
+_BYTES_OFF = ctypes.cast(c_char_p(_probe), ctypes.c_void_p).value - id(_probe)
+
+
 def _elements(chunks) -> tuple:
-    """Build a ctypes Element array over a list of bytes / numpy buffers
-    (kept alive by the returned tuple)."""
-    keep = []
-    arr = (Element * max(1, len(chunks)))()
+    """An scm_element array over a list of bytes / bytearray / numpy buffers,
+    zero-copy (the buffers are kept alive by the returned tuple): a (pointer,
+    size) uint64 table filled from the bytes objects' own data addresses."""
+    n = len(chunks)
+    tab = np.zeros((max(1, n), 2), dtype=np.uint64)
+    keep = [tab]
     for i, c in enumerate(chunks):
+        if type(c) is bytes:
+            tab[i, 0] = id(c) + _BYTES_OFF
+            tab[i, 1] = len(c)
+            continue
         a = np.frombuffer(c, dtype=np.uint8) if isinstance(c, (bytes, bytearray)) else c
         a = np.ascontiguousarray(a).view(np.uint8).reshape(-1)
         keep.append(a)
-        arr[i].buffer = a.ctypes.data_as(POINTER(c_uint8))
-        arr[i].size = a.nbytes
-    return arr, keep
+        tab[i, 0] = a.ctypes.data
+        tab[i, 1] = a.nbytes
+    keep.append(chunks)
+    return tab.ctypes.data_as(POINTER(Element)), keep
 
 
 class PackedRows:

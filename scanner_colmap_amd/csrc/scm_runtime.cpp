@@ -280,6 +280,12 @@ struct BatchSet {
   // round buffers of the H LO-RANSAC (advanced beside F's, own PRNG stream)
   DevBuf h_rst, h_samp, h_nmod, h_fcon, h_cnts, h_act, h_nact, h_mods, h_wsnap;
   DevBuf ucnt, h_ucnt;  // split scoring: undecided points per model
+  DevBuf wb, wstate, dtrial, h_wb, h_wstate, h_dtrial;  // window trial counts, PRNG states
+  // odd-parity window buffers of small batches (speculative windows, launch_verify)
+  DevBuf o_samp, o_nmod, o_fcon, o_mods, o_cnts, o_ucnt, o_wsnap, o_wb, o_wstate;
+  DevBuf oh_samp, oh_nmod, oh_fcon, oh_mods, oh_cnts, oh_ucnt, oh_wsnap, oh_wb, oh_wstate;
+  hipStream_t rstream = nullptr;  // replay stream of speculative windows
+  hipEvent_t wev[2 * kMaxVerifyWindows] = {};
   HostBuf stage, vstage;
   PinnedOut out;
   size_t off_counts = 0, off_offsets = 0, off_vout = 0, off_matches = 0, off_masks = 0;
@@ -302,7 +308,10 @@ struct BatchSet {
                       &xy1, &xy2, &scratch, &snaps, &masks, &offsets, &match_off, &prof, &xyf, &dvout,
                       &dpack, &dpmask, &rst, &samp, &nmod, &fcon, &cnts, &act, &nact,
                       &mods, &wsnap, &h_rst, &h_samp, &h_nmod, &h_fcon, &h_cnts, &h_act, &h_nact,
-                      &h_mods, &h_wsnap, &ucnt, &h_ucnt})
+                      &h_mods, &h_wsnap, &ucnt, &h_ucnt, &wb, &wstate, &dtrial, &h_wb, &h_wstate,
+                      &h_dtrial, &o_samp, &o_nmod, &o_fcon, &o_mods, &o_cnts, &o_ucnt, &o_wsnap,
+                      &o_wb, &o_wstate, &oh_samp, &oh_nmod, &oh_fcon, &oh_mods, &oh_cnts, &oh_ucnt,
+                      &oh_wsnap, &oh_wb, &oh_wstate})
       b->release();
     stage.release();
     vstage.release();
@@ -312,6 +321,10 @@ struct BatchSet {
       e = nullptr;
     }
     for (auto& e : sev) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+    for (auto& e : wev) {
       if (e) (void)hipEventDestroy(e);
       e = nullptr;
     }
@@ -1101,11 +1114,11 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
     }
     bs.nprof = V;
     SCM_HIP(hipEventRecord(bs.ev[4], sv));
-    // Round buffers per kind (H: one model per hypothesis).
-    auto round_bufs = [&](DevBuf& rst, DevBuf& samp, DevBuf& nmod, DevBuf& fcon, DevBuf& mods,
-                          DevBuf& cnts, DevBuf& ucnt, DevBuf& wsnap, DevBuf& act, DevBuf& nact,
-                          bool split, VerifyRoundBufs* rb) -> int {
-      SCM_TRY(rst.ensure(V * sizeof(RansacState)));
+    // Round buffers per kind (H: one model per hypothesis): the window
+    // buffers of one parity, then the per-pair state.
+    auto window_bufs = [&](DevBuf& samp, DevBuf& nmod, DevBuf& fcon, DevBuf& mods, DevBuf& cnts,
+                           DevBuf& ucnt, DevBuf& wsnap, DevBuf& wb, DevBuf& wstate, bool split,
+                           VerifyRoundBufs* rb) -> int {
       SCM_TRY(samp.ensure(V * kWindowTrials * 8 * sizeof(uint32_t)));
       SCM_TRY(nmod.ensure(V * kWindowTrials * sizeof(int32_t)));
       SCM_TRY(fcon.ensure(V * kWindowTrials * 3 * 12 * sizeof(float)));
@@ -1113,9 +1126,8 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       SCM_TRY(cnts.ensure(V * kWindowTrials * 3 * sizeof(uint32_t)));
       if (split) SCM_TRY(ucnt.ensure(V * kWindowTrials * 3 * sizeof(uint32_t)));
       SCM_TRY(wsnap.ensure(V * kMaxWindow * 640 * sizeof(uint32_t)));
-      SCM_TRY(act.ensure(2 * V * sizeof(int32_t)));
-      SCM_TRY(nact.ensure(2 * sizeof(int32_t)));
-      rb->rst = rst.as<RansacState>();
+      SCM_TRY(wb.ensure(V * sizeof(int32_t)));
+      SCM_TRY(wstate.ensure(V * kVerifyStateWords * sizeof(uint32_t)));
       rb->samp = samp.as<uint32_t>();
       rb->nmod = nmod.as<int32_t>();
       rb->fcon = fcon.as<float>();
@@ -1123,9 +1135,23 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       rb->cnts = cnts.as<uint32_t>();
       rb->ucnt = split ? ucnt.as<uint32_t>() : nullptr;
       rb->wsnap = wsnap.as<uint32_t>();
-      rb->act[0] = act.as<int32_t>();
-      rb->act[1] = act.as<int32_t>() + V;
+      rb->wB = wb.as<int32_t>();
+      rb->wstate = rb->pstate = wstate.as<uint32_t>();
+      return SCM_OK;
+    };
+    auto round_bufs = [&](DevBuf& rst, DevBuf& samp, DevBuf& nmod, DevBuf& fcon, DevBuf& mods,
+                          DevBuf& cnts, DevBuf& ucnt, DevBuf& wsnap, DevBuf& act, DevBuf& nact,
+                          DevBuf& wb, DevBuf& wstate, DevBuf& dtrial, bool split,
+                          VerifyRoundBufs* rb) -> int {
+      SCM_TRY(rst.ensure(V * sizeof(RansacState)));
+      SCM_TRY(window_bufs(samp, nmod, fcon, mods, cnts, ucnt, wsnap, wb, wstate, split, rb));
+      SCM_TRY(act.ensure(3 * V * sizeof(int32_t)));
+      SCM_TRY(nact.ensure(3 * sizeof(int32_t)));
+      SCM_TRY(dtrial.ensure(V * sizeof(int32_t)));
+      rb->rst = rst.as<RansacState>();
+      for (int k = 0; k < 3; ++k) rb->act[k] = act.as<int32_t>() + k * V;
       rb->nact = nact.as<int32_t>();
+      rb->dtrial = dtrial.as<int32_t>();
       return SCM_OK;
     };
     VerifyRoundBufs rbf, rbh;
@@ -1134,16 +1160,39 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
     // (measured per step: F 35.4 + 8.3 ms split vs 40.8 ms one pass; H 138.3 +
     // 4.2 ms vs 153.1 ms).
     SCM_TRY(round_bufs(bs.rst, bs.samp, bs.nmod, bs.fcon, bs.mods, bs.cnts, bs.ucnt, bs.wsnap,
-                       bs.act, bs.nact, false, &rbf));
+                       bs.act, bs.nact, bs.wb, bs.wstate, bs.dtrial, false, &rbf));
     SCM_TRY(round_bufs(bs.h_rst, bs.h_samp, bs.h_nmod, bs.h_fcon, bs.h_mods, bs.h_cnts,
-                       bs.h_ucnt, bs.h_wsnap, bs.h_act, bs.h_nact, ctx->score_split, &rbh));
+                       bs.h_ucnt, bs.h_wsnap, bs.h_act, bs.h_nact, bs.h_wb, bs.h_wstate,
+                       bs.h_dtrial, ctx->score_split, &rbh));
     if (!bs.sev[0])
       for (auto& e : bs.sev) SCM_HIP(hipEventCreate(&e));
+    // Small batches (one Scanner stencil): odd-parity window buffers and a
+    // replay stream, so that the next window's draws and scores overlap the
+    // replay of this one.
+    VerifySpec spec;
+    VerifyRoundBufs rbf1 = rbf, rbh1 = rbh;
+    if (verify_small_batch((int)V, max_m)) {
+      SCM_TRY(window_bufs(bs.o_samp, bs.o_nmod, bs.o_fcon, bs.o_mods, bs.o_cnts, bs.o_ucnt,
+                          bs.o_wsnap, bs.o_wb, bs.o_wstate, false, &rbf1));
+      SCM_TRY(window_bufs(bs.oh_samp, bs.oh_nmod, bs.oh_fcon, bs.oh_mods, bs.oh_cnts, bs.oh_ucnt,
+                          bs.oh_wsnap, bs.oh_wb, bs.oh_wstate, ctx->score_split, &rbh1));
+      if (!bs.rstream)
+        SCM_HIP(hipStreamCreateWithPriority(&bs.rstream, hipStreamNonBlocking,
+                                            stream_priority("SCM_VERIFY_PRIO", true)));
+      if (!bs.wev[0])
+        for (auto& e : bs.wev) SCM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      if (!ctx->serial) {
+        spec.rb_f1 = &rbf1;
+        spec.rb_h1 = &rbh1;
+        spec.rstream = bs.rstream;
+        spec.win_ev = bs.wev;
+      }
+    }
     SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
                           bs.xy2.as<double>(), bs.scratch.as<double>(), bs.snaps.as<uint32_t>(),
                           bs.masks.as<uint8_t>(), bs.dvout.as<VerifyOut>(),
                           make_params(ctx->opts, iteration), prof, nullptr, bs.xyf.as<float4>(), rbf, rbh,
-                          sv, bs.sev, &bs.nwin));
+                          sv, bs.sev, &bs.nwin, &spec));
   }
   SCM_HIP(hipEventRecord(bs.ev[5], sv));
   // Compact matches + F-inlier masks in HBM, then DMA the results into the
@@ -1659,8 +1708,10 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
 // Drains any batch left in flight by an error path.
 void drain(scm_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  for (BatchSet& bs : ctx->sets)
+  for (BatchSet& bs : ctx->sets) {
     if (bs.vstream) (void)hipStreamSynchronize(bs.vstream);
+    if (bs.rstream) (void)hipStreamSynchronize(bs.rstream);
+  }
   for (BatchSet& bs : ctx->sets) bs.pending = bs.posted = false;
 }
 
@@ -1791,8 +1842,10 @@ void scm_context_destroy(scm_context* ctx) {
   for (BatchSet& bs : ctx->sets) bs.release();
   ctx->h_stage.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  for (BatchSet& bs : ctx->sets)
+  for (BatchSet& bs : ctx->sets) {
     if (bs.vstream) (void)hipStreamDestroy(bs.vstream);
+    if (bs.rstream) (void)hipStreamDestroy(bs.rstream);
+  }
   delete ctx;
 }
 

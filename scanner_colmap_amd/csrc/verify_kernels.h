@@ -88,6 +88,11 @@ constexpr int kWindowTrials = kMaxWindow * kTrialBatch;
 // kWindowTrials): rst[V], samp[V][T*8], nmod[V][T], fcon[V][3T][12],
 // mods[V][3T][9], cnts[V][3T], wsnap[V][kMaxWindow][640], act[2][V],
 // nact[2].
+// One window parity's buffers of one RANSAC kind.  The per-window buffers
+// (samp .. wstate) exist twice for small batches, so that the draws, shuffles,
+// solves and scores of window r + 1 can run while window r is replayed
+// (speculative windows, run_windows); rst, dtrial and the active lists are
+// shared by both parities.  Large batches alias both parities.
 struct VerifyRoundBufs {
   RansacState* rst;
   uint32_t* samp;
@@ -97,9 +102,16 @@ struct VerifyRoundBufs {
   uint32_t* cnts;
   uint32_t* ucnt;  // split scoring: undecided points per model [V][3T]
   uint32_t* wsnap;
-  int32_t* act[2];
-  int32_t* nact;
+  int32_t* wB;       // trials of the pair's window
+  uint32_t* wstate;  // PRNG state after the window's draws (kVerifyStateWords per pair)
+  uint32_t* pstate;  // the other parity's wstate: where the window's draws start
+  const uint32_t* pcnts;  // the other parity's cnts and wB (the previous window's, read
+  const int32_t* pwB;     //   by speculative draws to skip pairs certain to stop)
+  int32_t* dtrial;   // trials drawn so far
+  int32_t* act[3];   // active-pair lists (rotating: window r's replay reads r % 3)
+  int32_t* nact;     // their lengths [3]
 };
+constexpr int kVerifyStateWords = 640;
 
 // snaps: kVerifySnapWords uint32 per pair (PRNG states handed between the
 // windowed kernels + the per-round snapshots for the abort rewind).  The F
@@ -109,12 +121,26 @@ struct VerifyRoundBufs {
 // score_ev (optional, 2 * kMaxVerifyWindows events): recorded around each
 // window's scoring kernels; *nwin receives the number of windows launched.
 constexpr int kMaxVerifyWindows = 64;
+// Speculative windows (small batches): rb_f1 / rb_h1 are the odd parity's
+// buffers (nullptr: none), rstream the replay stream and win_ev
+// 2 * kMaxVerifyWindows events (window r's wide kernels done, its replay done).
+struct VerifySpec {
+  const VerifyRoundBufs* rb_f1 = nullptr;
+  const VerifyRoundBufs* rb_h1 = nullptr;
+  hipStream_t rstream = nullptr;
+  hipEvent_t* win_ev = nullptr;
+};
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
                          const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb_f,
                          const VerifyRoundBufs& rb_h, hipStream_t stream,
-                         hipEvent_t* score_ev = nullptr, int* nwin = nullptr);
+                         hipEvent_t* score_ev = nullptr, int* nwin = nullptr,
+                         const VerifySpec* spec = nullptr);
+// Whether launch_verify runs the small-batch kernels (wave-per-pair shuffle,
+// four-wave replay, speculative windows) for a batch of npairs pairs with at
+// most max_m matches.
+bool verify_small_batch(int npairs, int max_m);
 size_t verify_lds_bytes(int max_m);
 constexpr int kVerifyProfSlots = 90;
 

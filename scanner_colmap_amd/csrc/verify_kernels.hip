@@ -1902,7 +1902,8 @@ __device__ __attribute__((always_inline)) void rs_begin_body(
     const VerifyPair* __restrict__ pairs, int npairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
     const float4* __restrict__ xyf_all, RansacState* __restrict__ rst,
-    int32_t* __restrict__ act, int32_t* __restrict__ nact, VerifyParams P, int bid, int nblk) {
+    int32_t* __restrict__ act, int32_t* __restrict__ nact, uint32_t* __restrict__ pstate,
+    int32_t* __restrict__ dtrial, VerifyParams P, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
@@ -1924,9 +1925,11 @@ __device__ __attribute__((always_inline)) void rs_begin_body(
                              : pair_seed_h(P.base_seed, ps.pp.id1, ps.pp.id2));
     wsync();
     mt_save(s, ps.state);
+    mt_save(s, pstate + (int64_t)q * kVerifyStateWords);  // where window 0's draws start
     uint32_t* sidx = pair_sidx(ps);
     for (int i = lane; i < n; i += 64) sidx[i] = (uint32_t)i;
     if (lane == 0) {
+      dtrial[q] = 0;
       RansacState& st = rst[q];
       st.n = n;
       st.max_trials = K == KIND_F ? P.max_trials_F : P.max_trials_H;
@@ -1960,7 +1963,10 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, RansacState* __restrict__ rst,
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
     int32_t* __restrict__ nact_next, uint32_t* __restrict__ samp, uint32_t* __restrict__ cnts,
-    uint32_t* __restrict__ ucnt, uint32_t* __restrict__ wsnap, int W, int bid, int nblk) {
+    uint32_t* __restrict__ ucnt, uint32_t* __restrict__ wsnap, int32_t* __restrict__ wB,
+    const uint32_t* __restrict__ pstate, uint32_t* __restrict__ wstate,
+    int32_t* __restrict__ dtrial, const uint32_t* __restrict__ pcnts,
+    const int32_t* __restrict__ pwB, const VerifyParams& P, bool spec, int W, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
@@ -1971,9 +1977,28 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     const int q = act[a];
     const PairSetup ps = pair_at<K>(pairs, q, scratch, snaps, out);
     const int n = ps.n;
-    const int Btot = min(kTrialBatch * W, rst[q].max_trials - rst[q].trial);
+    // (the trials drawn so far, not the replay's count: this window may be
+    // drawn while the previous one is still replayed)
+    int Btot = max(0, min(kTrialBatch * W, rst[q].max_trials - dtrial[q]));
+    if (spec && Btot > 0) {
+      // Speculative window: skip a pair certain to stop in the previous window.
+      // Its best count after that window is at least every count the window
+      // scored (a model above the best becomes the best; LO only adds), so
+      // its trial bound is at most ComputeNumTrials(cmax); if that bound
+      // falls inside the previous window, the pair aborts there.
+      const int Bp = pwB[q];
+      const uint32_t* pc = pcnts + (int64_t)q * kWindowTrials * 3;
+      uint32_t cm = 0;
+      for (int i = lane; i < Bp * Tr::mm; i += 64) cm = max(cm, pc[i]);
+#pragma unroll
+      for (int d = 32; d >= 1; d >>= 1) cm = max(cm, (uint32_t)__shfl_xor((int)cm, d));
+      const int last = dtrial[q] - 1;  // the previous window's last trial
+      const uint64_t bound = num_trials((uint64_t)cm, (uint64_t)n, P.confidence,
+                                        P.dyn_num_trials_multiplier, Tr::kmin);
+      if (Bp > 0 && last >= P.min_num_trials && (uint64_t)last >= bound) Btot = 0;
+    }
     wsync();
-    mt_load(s, ps.state);
+    mt_load(s, pstate + (int64_t)q * kVerifyStateWords);
     uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
     for (int w = 0; w * kTrialBatch < Btot; ++w) {
       const int B = min(kTrialBatch, Btot - w * kTrialBatch);
@@ -1998,14 +2023,17 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
         sq[(w * kTrialBatch + r / Tr::kmin) * 8 + r % Tr::kmin] = s.jbuf[r];
       wsync();
     }
-    mt_save(s, ps.state);
+    mt_save(s, wstate + (int64_t)q * kVerifyStateWords);
     uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3;
     for (int i = lane; i < Btot * 3; i += 64) cq[i] = 0u;
     if (ucnt) {
       uint32_t* uq = ucnt + (int64_t)q * kWindowTrials * 3;
       for (int i = lane; i < Btot * 3; i += 64) uq[i] = 0u;
     }
-    if (lane == 0) rst[q].B = Btot;
+    if (lane == 0) {
+      wB[q] = Btot;
+      dtrial[q] += Btot;
+    }
   }
 }
 
@@ -2048,7 +2076,7 @@ template <int K>
 __device__ __attribute__((always_inline)) void rs_shuffle_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
-    const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
+    const int32_t* __restrict__ wB, const int32_t* __restrict__ act,
     const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, int ppb, int stride, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   uint16_t* lsidx = reinterpret_cast<uint16_t*>(dyn_lds);
@@ -2072,7 +2100,7 @@ __device__ __attribute__((always_inline)) void rs_shuffle_body(
     constexpr int KM = KindTraits<K>::kmin;
     const int q = act[a0 + threadIdx.x];
     uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
-    const int Btot = rst[q].B;
+    const int Btot = wB[q];
     if (staged) shuffle_chain<KM>(lsidx + threadIdx.x * stride, sq, Btot);
     else shuffle_chain<KM>(pair_sidx(pair_at<K>(pairs, q, scratch, snaps, out)), sq, Btot);
   }
@@ -2119,7 +2147,7 @@ template <int K>
 __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
-    const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
+    const int32_t* __restrict__ wB, const int32_t* __restrict__ act,
     const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, uint64_t* __restrict__ prof,
     int stride, int bid, int nblk) {
   constexpr int KM = KindTraits<K>::kmin;
@@ -2158,7 +2186,7 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
     __syncthreads();
     lap(0);
     uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
-    const int Btot = rst[q].B;
+    const int Btot = wB[q];
     for (int p0 = 0; p0 < Btot; p0 += kWsPass) {
       const int np = min(kWsPass, Btot - p0);
       {
@@ -2307,12 +2335,12 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
 __global__ __launch_bounds__(64) void rs_shuffle_wave2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
-    VerifyRoundBufs rh, int cur, uint64_t* __restrict__ prof, int stride, int split) {
+    VerifyRoundBufs rh, int ain, uint64_t* __restrict__ prof, int stride, int split) {
   if ((int)blockIdx.x < split)
-    rs_shuffle_wave_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[cur], rf.nact + cur,
+    rs_shuffle_wave_body<KIND_F>(pairs, scratch, snaps, out, rf.wB, rf.act[ain], rf.nact + ain,
                                  rf.samp, prof, stride, blockIdx.x, split);
   else
-    rs_shuffle_wave_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[cur], rh.nact + cur,
+    rs_shuffle_wave_body<KIND_H>(pairs, scratch, snaps, out, rh.wB, rh.act[ain], rh.nact + ain,
                                  rh.samp, prof, stride, blockIdx.x - split, gridDim.x - split);
 }
 
@@ -2326,7 +2354,7 @@ template <int K>
 __global__ __launch_bounds__(64) void rs_solve_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
     const double* __restrict__ xy2_all, const RansacState* __restrict__ rst,
-    const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
+    const int32_t* __restrict__ wB, const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
     const uint32_t* __restrict__ samp, int32_t* __restrict__ nmod, float* __restrict__ fcon,
     double* __restrict__ mods, int W, double maxr) {
   using Tr = KindTraits<K>;
@@ -2336,7 +2364,7 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
   for (int it = blockIdx.x; it < na * per; it += gridDim.x) {
     const int q = act[it / per];
     const int h = (it % per) * 64 + threadIdx.x;
-    if (h >= rst[q].B) continue;
+    if (h >= wB[q]) continue;
     const VerifyPair pp = pairs[q];
     const double S = rst[q].S;
     const double* xy1 = xy1_all + pp.pts_off;
@@ -2389,8 +2417,8 @@ constexpr int kScoreTargetItems = SCM_SCORE_ITEMS;  // work items per score laun
 template <int K, bool SPLIT>
 __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     const VerifyPair* __restrict__ pairs, const float4* __restrict__ xyf_all,
-    const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
-    const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
+    const RansacState* __restrict__ rst, const int32_t* __restrict__ wB,
+    const int32_t* __restrict__ act, const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
     const float* __restrict__ fcon, const double* __restrict__ mods,
     uint32_t* __restrict__ cnts, uint32_t* __restrict__ ucnt, int max_chunks, int W, double maxr,
     uint64_t* __restrict__ prof) {
@@ -2419,7 +2447,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     const int n = pp.m;
     const int base = chunk * kScoreChunk;
     if (base >= n) continue;
-    const int Bpair = rst[q].B;
+    const int Bpair = wB[q];
     const int rbeg = ri * rpi * kTrialBatch;
     const int rend = min(Bpair, rbeg + rpi * kTrialBatch);
     if (rbeg >= rend) continue;
@@ -2560,8 +2588,8 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
 template <int K>
 __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
     const VerifyPair* __restrict__ pairs, const float4* __restrict__ xyf_all,
-    const RansacState* __restrict__ rst, const int32_t* __restrict__ act,
-    const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
+    const RansacState* __restrict__ rst, const int32_t* __restrict__ wB,
+    const int32_t* __restrict__ act, const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
     const float* __restrict__ fcon, const double* __restrict__ mods,
     uint32_t* __restrict__ cnts, const uint32_t* __restrict__ ucnt, int max_chunks, int W,
     double maxr) {
@@ -2582,7 +2610,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
     const int n = pp.m;
     const int base = chunk * kScoreChunk;
     if (base >= n) continue;
-    const int Bpair = rst[q].B;
+    const int Bpair = wB[q];
     const uint32_t best0 = (uint32_t)rst[q].best_n;
     const int rbeg = ri * rpi * kTrialBatch;
     const int rend = min(Bpair, rbeg + rpi * kTrialBatch);
@@ -2665,7 +2693,8 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     const int32_t* __restrict__ nact, int32_t* __restrict__ act_next,
     int32_t* __restrict__ nact_next, const int32_t* __restrict__ nmod,
     const uint32_t* __restrict__ cnts, const double* __restrict__ mods,
-    const uint32_t* __restrict__ wsnap, VerifyParams P, uint64_t* __restrict__ prof,
+    const uint32_t* __restrict__ wsnap, const int32_t* __restrict__ wB,
+    const uint32_t* __restrict__ wstate, VerifyParams P, uint64_t* __restrict__ prof,
     const float4* __restrict__ xyf_all, int bid, int nblk) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
@@ -2704,7 +2733,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     int best_sel = st.res_sel;
     int dyn_max = st.dyn_max;
     const int trial = st.trial;
-    const int Btot = st.B;
+    const int Btot = wB[q];
     bool abort = false;
     int abort_trial = -1;
     int64_t evals = st.evals;
@@ -2860,7 +2889,13 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     } else {
       st.trial = trial + Btot;
       st.num_trials = st.trial;
-      if (st.trial >= st.max_trials) st.done = 1;
+      if (st.trial >= st.max_trials) {
+        st.done = 1;
+        // the stream continues (H: the watermark RANSAC) from the state after
+        // the last window's draws
+        const uint32_t* ws = wstate + (int64_t)q * kVerifyStateWords;
+        for (int i = threadIdx.x; i < 625; i += blockDim.x) ps.state[i] = ws[i];
+      }
     }
     st.dyn_max = dyn_max;
     st.evals = evals;
@@ -2895,51 +2930,53 @@ __global__ __launch_bounds__(64) void rs_begin2_kernel(
     int split) {
   if ((int)blockIdx.x < split)
     rs_begin_body<KIND_F>(pairs, npairs, scratch, snaps, out, masks, xyf, rf.rst, rf.act[0],
-                          rf.nact, P, blockIdx.x, split);
+                          rf.nact, rf.pstate, rf.dtrial, P, blockIdx.x, split);
   else
     rs_begin_body<KIND_H>(pairs, npairs, scratch, snaps, out, masks, xyf, rh.rst, rh.act[0],
-                          rh.nact, P, blockIdx.x - split, gridDim.x - split);
+                          rh.nact, rh.pstate, rh.dtrial, P, blockIdx.x - split, gridDim.x - split);
 }
 
 __global__ __launch_bounds__(64) void rs_draw2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
-    VerifyRoundBufs rh, int cur, int W, int split) {
+    VerifyRoundBufs rh, int ain, int aclr, VerifyParams P, int spec, int W, int split) {
   if ((int)blockIdx.x < split)
-    rs_draw_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[cur], rf.nact + cur,
-                         rf.nact + (cur ^ 1), rf.samp, rf.cnts, rf.ucnt, rf.wsnap, W, blockIdx.x,
+    rs_draw_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[ain], rf.nact + ain,
+                         rf.nact + aclr, rf.samp, rf.cnts, rf.ucnt, rf.wsnap, rf.wB, rf.pstate,
+                         rf.wstate, rf.dtrial, rf.pcnts, rf.pwB, P, spec != 0, W, blockIdx.x,
                          split);
   else
-    rs_draw_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[cur], rh.nact + cur,
-                         rh.nact + (cur ^ 1), rh.samp, rh.cnts, rh.ucnt, rh.wsnap, W,
+    rs_draw_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[ain], rh.nact + ain,
+                         rh.nact + aclr, rh.samp, rh.cnts, rh.ucnt, rh.wsnap, rh.wB, rh.pstate,
+                         rh.wstate, rh.dtrial, rh.pcnts, rh.pwB, P, spec != 0, W,
                          blockIdx.x - split, gridDim.x - split);
 }
 
 __global__ __launch_bounds__(64) void rs_shuffle2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
-    VerifyRoundBufs rh, int cur, int ppb, int stride, int split) {
+    VerifyRoundBufs rh, int ain, int ppb, int stride, int split) {
   if ((int)blockIdx.x < split)
-    rs_shuffle_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[cur], rf.nact + cur,
+    rs_shuffle_body<KIND_F>(pairs, scratch, snaps, out, rf.wB, rf.act[ain], rf.nact + ain,
                             rf.samp, ppb, stride, blockIdx.x, split);
   else
-    rs_shuffle_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[cur], rh.nact + cur,
+    rs_shuffle_body<KIND_H>(pairs, scratch, snaps, out, rh.wB, rh.act[ain], rh.nact + ain,
                             rh.samp, ppb, stride, blockIdx.x - split, gridDim.x - split);
 }
 
 __global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
-    VerifyRoundBufs rf, VerifyRoundBufs rh, int cur, VerifyParams P, uint64_t* __restrict__ prof,
-    const float4* __restrict__ xyf, int split) {
+    VerifyRoundBufs rf, VerifyRoundBufs rh, int ain, int aout, VerifyParams P,
+    uint64_t* __restrict__ prof, const float4* __restrict__ xyf, int split) {
   if ((int)blockIdx.x < split)
-    rs_replay_body<KIND_F>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[cur], rf.nact + cur,
-                           rf.act[cur ^ 1], rf.nact + (cur ^ 1), rf.nmod, rf.cnts, rf.mods,
-                           rf.wsnap, P, prof, xyf, blockIdx.x, split);
+    rs_replay_body<KIND_F>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[ain], rf.nact + ain,
+                           rf.act[aout], rf.nact + aout, rf.nmod, rf.cnts, rf.mods,
+                           rf.wsnap, rf.wB, rf.wstate, P, prof, xyf, blockIdx.x, split);
   else
-    rs_replay_body<KIND_H>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[cur], rh.nact + cur,
-                           rh.act[cur ^ 1], rh.nact + (cur ^ 1), rh.nmod, rh.cnts, rh.mods,
-                           rh.wsnap, P, prof, xyf, blockIdx.x - split, gridDim.x - split);
+    rs_replay_body<KIND_H>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[ain], rh.nact + ain,
+                           rh.act[aout], rh.nact + aout, rh.nmod, rh.cnts, rh.mods,
+                           rh.wsnap, rh.wB, rh.wstate, P, prof, xyf, blockIdx.x - split, gridDim.x - split);
 }
 
 // rs_replay2_kernel with four waves per pair (small batches: the window's
@@ -2947,16 +2984,16 @@ __global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay2_kernel(
 __global__ __launch_bounds__(256) void rs_replay2w_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
-    VerifyRoundBufs rf, VerifyRoundBufs rh, int cur, VerifyParams P, uint64_t* __restrict__ prof,
-    const float4* __restrict__ xyf, int split) {
+    VerifyRoundBufs rf, VerifyRoundBufs rh, int ain, int aout, VerifyParams P,
+    uint64_t* __restrict__ prof, const float4* __restrict__ xyf, int split) {
   if ((int)blockIdx.x < split)
-    rs_replay_body<KIND_F, 4>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[cur], rf.nact + cur,
-                              rf.act[cur ^ 1], rf.nact + (cur ^ 1), rf.nmod, rf.cnts, rf.mods,
-                              rf.wsnap, P, prof, xyf, blockIdx.x, split);
+    rs_replay_body<KIND_F, 4>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[ain], rf.nact + ain,
+                              rf.act[aout], rf.nact + aout, rf.nmod, rf.cnts, rf.mods,
+                              rf.wsnap, rf.wB, rf.wstate, P, prof, xyf, blockIdx.x, split);
   else
-    rs_replay_body<KIND_H, 4>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[cur], rh.nact + cur,
-                              rh.act[cur ^ 1], rh.nact + (cur ^ 1), rh.nmod, rh.cnts, rh.mods,
-                              rh.wsnap, P, prof, xyf, blockIdx.x - split, gridDim.x - split);
+    rs_replay_body<KIND_H, 4>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[ain], rh.nact + ain,
+                              rh.act[aout], rh.nact + aout, rh.nmod, rh.cnts, rh.mods,
+                              rh.wsnap, rh.wB, rh.wstate, P, prof, xyf, blockIdx.x - split, gridDim.x - split);
 }
 
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
@@ -3014,22 +3051,46 @@ void set_lds_attr(F f) {
                             160 * 1024);
 }
 
+#ifndef SCM_WAVE_SHUFFLE_PAIRS
+#define SCM_WAVE_SHUFFLE_PAIRS 256
+#endif
+// Small batches: a wave per pair (rs_shuffle_wave2_kernel), four waves per
+// pair in the replay, speculative windows -- while the batch leaves most of
+// the GPU idle, latency decides.
+int wave_pairs_limit() {
+  static const int v = [] {
+    const char* e = getenv("SCM_WAVE_SHUFFLE_PAIRS");
+    return e ? atoi(e) : SCM_WAVE_SHUFFLE_PAIRS;
+  }();
+  return v;
+}
+
 // Windows of both RANSAC kinds (W = 1, 2, 4, ..., kMaxWindow rounds) until
 // each kind's trial cap: draw / shuffle / replay as dual-kind launches, the
 // wide solve and score kernels per kind.  Kernels of windows with no active
 // pair exit at once.
+//
+// Window r uses the parity r & 1 buffers (rb[r & 1]) and the active lists in
+// rotation: its replay reads list r % 3 (the pairs still running) and writes
+// list (r + 1) % 3.  Speculative schedule (spec: small batches with odd-parity
+// buffers and a replay stream): the draws, shuffles, solves and scores of
+// window r + 1 run on `stream` while window r is replayed on `rstream`; they
+// take the pairs that were running at the start of window r (list (r - 1) %
+// 3 after its replay -- that replay, two windows back, is waited for), so a
+// pair that stops in window r has had one window drawn and scored in vain, and
+// nothing else changes: the draws count their own trials (dtrial), read and
+// write their parity's PRNG state, and the replay alone decides the pair's
+// state, output and final PRNG state.
 hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, const double* xy2,
                        double* scratch, uint32_t* snaps, uint8_t* masks, VerifyOut* out,
-                       const VerifyParams& P, const float4* xyf, const VerifyRoundBufs& rf,
-                       const VerifyRoundBufs& rh, int max_chunks, int max_m, uint64_t* prof,
-                       hipStream_t stream, hipEvent_t* score_ev, int* nwin) {
+                       const VerifyParams& P, const float4* xyf, const VerifyRoundBufs* rfp,
+                       const VerifyRoundBufs* rhp, int max_chunks, int max_m, uint64_t* prof,
+                       hipStream_t stream, hipEvent_t* score_ev, int* nwin, bool spec,
+                       hipStream_t rstream, hipEvent_t* win_ev) {
   const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
   const int gw = npairs < kPairGrid ? npairs : kPairGrid;
 #ifndef SCM_SHUFFLE_LDS_KB
 #define SCM_SHUFFLE_LDS_KB 16
-#endif
-#ifndef SCM_WAVE_SHUFFLE_PAIRS
-#define SCM_WAVE_SHUFFLE_PAIRS 256
 #endif
   // Shuffle blocks: as many pairs per block as fit SCM_SHUFFLE_LDS_KB of LDS sample-index
   // vectors (the swap chains are latency-bound; LDS instead of global memory
@@ -3039,14 +3100,8 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   const int sh_ppb =
       sh_stride ? std::max(1, std::min(64, (SCM_SHUFFLE_LDS_KB * 1024) / (2 * sh_stride))) : 1;
   const int sh_blocks = (npairs + sh_ppb - 1) / sh_ppb;
-  // Small batches: a wave per pair (rs_shuffle_wave2_kernel) while the batch
-  // leaves most of the GPU idle under the lane-per-pair chains.
-  static const int wave_pairs = [] {
-    const char* e = getenv("SCM_WAVE_SHUFFLE_PAIRS");
-    return e ? atoi(e) : SCM_WAVE_SHUFFLE_PAIRS;
-  }();
   const int wave_stride = (max_m + 7) / 8 * 8;
-  const bool wave_sh = npairs <= wave_pairs && wave_stride <= kWsMaxStride;
+  const bool wave_sh = verify_small_batch(npairs, max_m);
   const size_t wave_lds = wave_shuffle_lds_bytes(wave_stride);
   // First window: one round per pair when the batch fills the GPU; a small
   // batch (a single Scanner stencil) starts with wider windows -- its chain of
@@ -3056,43 +3111,50 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   while (W < kMaxWindow && (int64_t)npairs * 2 * W <= 1024) W *= 2;
   int covered = 0, r = 0;
   while (covered < P.max_trials_F || covered < P.max_trials_H) {
-    const int cur = r & 1;
+    const VerifyRoundBufs& rf = rfp[r & 1];
+    const VerifyRoundBufs& rh = rhp[r & 1];
+    // lists: the replay's input and output, the wide kernels' input
+    const int lin = r % 3, lout = (r + 1) % 3;
+    const int lw = spec && r > 0 ? (r - 1) % 3 : lin;
+    if (spec && r >= 2 && r - 2 < kMaxVerifyWindows)
+      (void)hipStreamWaitEvent(stream, win_ev[2 * (r - 2) + 1], 0);
     const bool f = covered < P.max_trials_F, h = covered < P.max_trials_H;
     const int g1 = (f ? gw : 0) + (h ? gw : 0), s1 = f ? gw : 0;
     const int g2 = (f ? sh_blocks : 0) + (h ? sh_blocks : 0), s2 = f ? sh_blocks : 0;
     hipLaunchKernelGGL(rs_draw2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
-                       out, rf, rh, cur, W, s1);
+                       out, rf, rh, lw, lout, P, (spec && r > 0) ? 1 : 0, W, s1);
     if (wave_sh)
       hipLaunchKernelGGL(rs_shuffle_wave2_kernel, dim3(g1), dim3(64), wave_lds, stream, pairs,
-                         scratch, snaps, out, rf, rh, cur, prof, wave_stride, s1);
+                         scratch, snaps, out, rf, rh, lw, prof, wave_stride, s1);
     else
       hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
                          (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch,
-                         snaps, out, rf, rh, cur, sh_ppb, sh_stride, s2);
+                         snaps, out, rf, rh, lw, sh_ppb, sh_stride, s2);
     if (f)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(SCM_SOLVE_GRID), dim3(64), 0, stream, pairs, xy1, xy2,
-                         rf.rst, rf.act[cur], rf.nact + cur, rf.samp, rf.nmod, rf.fcon, rf.mods,
+                         rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.samp, rf.nmod, rf.fcon, rf.mods,
                          W, P.max_residual);
     if (h)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_H>, dim3(SCM_SOLVE_GRID), dim3(64), 0, stream, pairs, xy1, xy2,
-                         rh.rst, rh.act[cur], rh.nact + cur, rh.samp, rh.nmod, rh.fcon, rh.mods,
+                         rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.samp, rh.nmod, rh.fcon, rh.mods,
                          W, P.max_residual);
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r], stream);
     // Scoring per kind: split (filter counts + undecided counts, then exact
     // tests only for the models that can reach the best; the runtime's
     // choice for H) or one pass with the exact tests of every undecided point
-    // (round buffers without ucnt; F).
+    // (round buffers without ucnt; F).  (Speculative windows: the best a model
+    // must reach may lag one window behind -- only more exact recounts.)
     if (f) {
       if (rf.ucnt) {
         hipLaunchKernelGGL((rs_score_kernel<KIND_F, true>), dim3(8192), dim3(kScoreThreads), 0,
-                           stream, pairs, xyf, rf.rst, rf.act[cur], rf.nact + cur, rf.nmod, rf.fcon,
+                           stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
                            rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual, prof);
         hipLaunchKernelGGL(rs_exact_kernel<KIND_F>, dim3(8192), dim3(kScoreThreads), 0, stream,
-                           pairs, xyf, rf.rst, rf.act[cur], rf.nact + cur, rf.nmod, rf.fcon,
+                           pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
                            rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual);
       } else {
         hipLaunchKernelGGL((rs_score_kernel<KIND_F, false>), dim3(8192), dim3(kScoreThreads), 0,
-                           stream, pairs, xyf, rf.rst, rf.act[cur], rf.nact + cur, rf.nmod, rf.fcon,
+                           stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
                            rf.mods, rf.cnts, nullptr, max_chunks, W, P.max_residual, prof);
       }
     }
@@ -3101,42 +3163,55 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       // exact recount: it takes the one-pass kernel (exact tests inline).
       if (rh.ucnt && r > 0) {
         hipLaunchKernelGGL((rs_score_kernel<KIND_H, true>), dim3(8192), dim3(kScoreThreads), 0,
-                           stream, pairs, xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon,
+                           stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod, rh.fcon,
                            rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, prof);
         hipLaunchKernelGGL(rs_exact_kernel<KIND_H>, dim3(8192), dim3(kScoreThreads), 0, stream,
-                           pairs, xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon,
+                           pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod, rh.fcon,
                            rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual);
       } else {
         hipLaunchKernelGGL((rs_score_kernel<KIND_H, false>), dim3(8192), dim3(kScoreThreads), 0,
-                           stream, pairs, xyf, rh.rst, rh.act[cur], rh.nact + cur, rh.nmod, rh.fcon,
+                           stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod, rh.fcon,
                            rh.mods, rh.cnts, nullptr, max_chunks, W, P.max_residual, prof);
       }
     }
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r + 1], stream);
+    hipStream_t rs = stream;
+    if (spec && r < kMaxVerifyWindows) {
+      (void)hipEventRecord(win_ev[2 * r], stream);
+      (void)hipStreamWaitEvent(rstream, win_ev[2 * r], 0);
+      rs = rstream;
+    }
     if (wave_sh)
-      hipLaunchKernelGGL(rs_replay2w_kernel, dim3(g1), dim3(256), lds, stream, pairs, scratch,
-                         snaps, out, masks, rf, rh, cur, P, prof, xyf, s1);
+      hipLaunchKernelGGL(rs_replay2w_kernel, dim3(g1), dim3(256), lds, rs, pairs, scratch,
+                         snaps, out, masks, rf, rh, lin, lout, P, prof, xyf, s1);
     else
-      hipLaunchKernelGGL(rs_replay2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
-                         out, masks, rf, rh, cur, P, prof, xyf, s1);
+      hipLaunchKernelGGL(rs_replay2_kernel, dim3(g1), dim3(64), lds, rs, pairs, scratch, snaps,
+                         out, masks, rf, rh, lin, lout, P, prof, xyf, s1);
+    if (spec && r < kMaxVerifyWindows) (void)hipEventRecord(win_ev[2 * r + 1], rstream);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     covered += W * kTrialBatch;
     W = W * 2 > kMaxWindow ? kMaxWindow : W * 2;
     ++r;
+    if (spec && r >= kMaxVerifyWindows) spec = false;  // out of events: the rest in order
   }
+  if (spec && r > 0) (void)hipStreamWaitEvent(stream, win_ev[2 * (r - 1) + 1], 0);
   if (nwin) *nwin = r < kMaxVerifyWindows ? r : kMaxVerifyWindows;
   return hipSuccess;
 }
 
 }  // namespace
 
+bool verify_small_batch(int npairs, int max_m) {
+  return npairs <= wave_pairs_limit() && (max_m + 7) / 8 * 8 <= kWsMaxStride;
+}
+
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
                          VerifyOut* out, const VerifyParams& params, uint64_t* prof,
                          const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb_f,
                          const VerifyRoundBufs& rb_h, hipStream_t stream, hipEvent_t* score_ev,
-                         int* nwin) {
+                         int* nwin, const VerifySpec* spec) {
   if (npairs <= 0) return hipSuccess;
   static bool attr = false;
   if (!attr) {
@@ -3153,14 +3228,28 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   const int gw = npairs < kPairGrid ? npairs : kPairGrid;
   const int max_chunks = (max_m + kScoreChunk - 1) / kScoreChunk;
   hipError_t err;
+  // Parity buffers: the odd ones from spec, else both parities alias (the
+  // windows then run strictly in order on one stream).
+  const bool sp = spec && spec->rb_f1 && spec->rb_h1 && spec->rstream && spec->win_ev &&
+                  verify_small_batch(npairs, max_m);
+  VerifyRoundBufs rfp[2] = {rb_f, sp ? *spec->rb_f1 : rb_f};
+  VerifyRoundBufs rhp[2] = {rb_h, sp ? *spec->rb_h1 : rb_h};
+  for (VerifyRoundBufs* b : {&rfp[0], &rfp[1], &rhp[0], &rhp[1]}) {
+    const VerifyRoundBufs& o = b == &rfp[0] ? rfp[1] : b == &rfp[1] ? rfp[0]
+                             : b == &rhp[0] ? rhp[1] : rhp[0];
+    b->pstate = o.wstate;
+    b->pcnts = o.cnts;
+    b->pwB = o.wB;
+  }
   // LORANSAC<7-pt, 8-pt> (F, then its inlier masks) and LORANSAC<H, H>, each
   // on its own PRNG stream, advanced together window by window.
-  if ((err = hipMemsetAsync(rb_f.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
-  if ((err = hipMemsetAsync(rb_h.nact, 0, 2 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  if ((err = hipMemsetAsync(rb_f.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  if ((err = hipMemsetAsync(rb_h.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
   hipLaunchKernelGGL(rs_begin2_kernel, dim3(2 * gw), dim3(64), kVerifyLdsHead, stream, pairs,
-                     npairs, scratch, snaps, out, masks, xyf, rb_f, rb_h, params, gw);
-  if ((err = run_windows(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf, rb_f,
-                         rb_h, max_chunks, max_m, prof, stream, score_ev, nwin)) != hipSuccess)
+                     npairs, scratch, snaps, out, masks, xyf, rfp[0], rhp[0], params, gw);
+  if ((err = run_windows(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf, rfp,
+                         rhp, max_chunks, max_m, prof, stream, score_ev, nwin, sp,
+                         sp ? spec->rstream : stream, sp ? spec->win_ev : nullptr)) != hipSuccess)
     return err;
   hipLaunchKernelGGL(verify_final_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
                      xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
