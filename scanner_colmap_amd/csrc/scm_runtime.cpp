@@ -1818,10 +1818,11 @@ void scm_context_destroy(scm_context* ctx) {
         std::fprintf(stderr, "  replay %s %-10s %14.1f\n", kind ? "H" : "F", rnames[j],
                      (double)ctx->prof_sum[20 + 10 * kind + j] / (double)ctx->prof_pairs);
     for (int kind = 0; kind < 2; ++kind)
-      std::fprintf(stderr, "  score %s chunk_models %14.1f slow %14.1f exact %14.1f\n",
+      std::fprintf(stderr, "  score %s chunk_models %14.1f slow %14.1f exact %14.1f item_cycles %14.1f\n",
                    kind ? "H" : "F", (double)ctx->prof_sum[80 + 4 * kind] / (double)ctx->prof_pairs,
                    (double)ctx->prof_sum[81 + 4 * kind] / (double)ctx->prof_pairs,
-                   (double)ctx->prof_sum[82 + 4 * kind] / (double)ctx->prof_pairs);
+                   (double)ctx->prof_sum[82 + 4 * kind] / (double)ctx->prof_pairs,
+                   (double)ctx->prof_sum[83 + 4 * kind] / (double)ctx->prof_pairs);
     static const char* snames[] = {"stage", "phaseA", "phaseB", "writeback", "targets"};
     for (int kind = 0; kind < 2; ++kind)
       for (int j = 0; j < 5; ++j)

@@ -184,7 +184,7 @@ __device__ __forceinline__ uint32_t mt_temper(uint32_t y) {
 // [454,624) the new words k-227 of phase two (k = 623 also reads the new
 // word 0) -- exactly the values the sequential loop in mt_next sees.
 __device__ void mt_twist_wave(VerifyLds& s) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;  // (several waves: each computes the same words)
   const int bounds[4] = {0, 227, 454, 624};
 #pragma unroll
   for (int ph = 0; ph < 3; ++ph) {
@@ -217,7 +217,7 @@ __device__ void mt_twist_wave(VerifyLds& s) {
 // batch serially.  Draw r's target index goes to s.jbuf[r].
 template <int KMIN>
 __device__ bool draw_targets_wave(VerifyLds& s, int D, uint32_t n) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;  // (several waves: each computes the same draws)
   const int idx0 = s.mt_idx;
   const int avail = 624 - idx0;
   uint32_t outv[KMIN];
@@ -476,13 +476,14 @@ constexpr int kDeferCap = 256;
 struct DeferQ {
   uint32_t* q;  // LDS: model << 16 | point offset within the chunk
   int n;        // entries queued (wave-uniform)
+  int cap = kDeferCap;
 };
 
 // Queue the undecided lanes um of point slot p for model m; false when the
 // queue is full (the caller then tests them at once).
 __device__ __forceinline__ bool defer_push(DeferQ* d, uint64_t um, int p, int m) {
   const int c = __popcll(um);
-  if (d->n + c > kDeferCap) return false;
+  if (d->n + c > d->cap) return false;
   const uint32_t lane = threadIdx.x;
   if (um & (1ull << lane)) {
     const int pos = d->n + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(um >> 32),
@@ -786,11 +787,14 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
 constexpr int kSeqU = 8;
 
 // Residuals of one model over all points into res; returns the inlier count.
-template <int K>
+// NW > 1: the waves take alternate blocks of 64 kSeqU points; the count is
+// exchanged in redi and every residual is visible to the block on return.
+template <int K, int NW = 1>
 __device__ int residuals_wave(const double* m, const double* xy1, const double* xy2, int n,
-                              double maxr, double* res) {
+                              double maxr, double* res, int32_t* redi = nullptr) {
   int c = 0;
-  for (int b = threadIdx.x; b < n; b += 64 * kSeqU) {
+  for (int b = (int)(threadIdx.x >> 6) * 64 * kSeqU + (int)(threadIdx.x & 63); b < n;
+       b += 64 * kSeqU * NW) {
     double a0[kSeqU], a1[kSeqU], b0[kSeqU], b1[kSeqU];
 #pragma unroll
     for (int u = 0; u < kSeqU; ++u) {
@@ -810,7 +814,15 @@ __device__ int residuals_wave(const double* m, const double* xy1, const double* 
       }
     }
   }
-  return wave_sum_i(c);
+  c = wave_sum_i(c);
+  if (NW == 1) return c;
+  if ((threadIdx.x & 63) == 0) redi[threadIdx.x >> 6] = c;
+  __syncthreads();
+  int t = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) t += redi[w];
+  __syncthreads();
+  return t;
 }
 
 // InlierSupportMeasurer::Evaluate's residual_sum: inlier residuals summed
@@ -858,12 +870,17 @@ __device__ __noinline__ double seq_inlier_sum(const double* res, int n, double m
   return sum;
 }
 
-// Ordered compaction of the points whose residual is <= maxr.
+// Ordered compaction of the points whose residual is <= maxr.  NW > 1: wave
+// w takes the w-th block of each round, a prefix of the waves' counts (redi)
+// places its inliers; the output is visible to the block on return.
+template <int NW = 1>
 __device__ int gather_inliers(const double* res, int n, double maxr, const double* xy1,
-                              const double* xy2, double* xin1, double* xin2) {
-  const int lane = threadIdx.x;
+                              const double* xy2, double* xin1, double* xin2,
+                              int32_t* redi = nullptr) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int base_out = 0;
-  for (int b0 = 0; b0 < n; b0 += 64 * kSeqU) {
+  for (int r0 = 0; r0 < n; r0 += 64 * kSeqU * NW) {
+    const int b0 = r0 + wv * 64 * kSeqU;
     double r[kSeqU], a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
 #pragma unroll
     for (int u = 0; u < kSeqU; ++u) {
@@ -874,21 +891,42 @@ __device__ int gather_inliers(const double* res, int n, double maxr, const doubl
       c0[u] = xy2[2 * ic];
       c1[u] = xy2[2 * ic + 1];
     }
+    uint64_t bal[kSeqU];
+    int wc = 0;
 #pragma unroll
     for (int u = 0; u < kSeqU; ++u) {
-      const bool in = r[u] <= maxr;
-      const uint64_t bal = __ballot(in);
-      if (in) {
-        const int o = base_out + (int)__builtin_amdgcn_mbcnt_hi(
-                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-        xin1[2 * o] = a0[u];
-        xin1[2 * o + 1] = a1[u];
-        xin2[2 * o] = c0[u];
-        xin2[2 * o + 1] = c1[u];
-      }
-      base_out += __popcll(bal);
+      bal[u] = __ballot(r[u] <= maxr);
+      wc += __popcll(bal[u]);
     }
+    int before = 0, total = wc;
+    if (NW > 1) {
+      if (lane == 0) redi[wv] = wc;
+      __syncthreads();
+      total = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) {
+        const int x = redi[w];
+        before += w < wv ? x : 0;
+        total += x;
+      }
+      __syncthreads();
+    }
+    int o = base_out + before;
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u) {
+      if (r[u] <= maxr) {
+        const int oo = o + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal[u] >> 32),
+                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
+        xin1[2 * oo] = a0[u];
+        xin1[2 * oo + 1] = a1[u];
+        xin2[2 * oo] = c0[u];
+        xin2[2 * oo + 1] = c1[u];
+      }
+      o += __popcll(bal[u]);
+    }
+    base_out += total;
   }
+  if (NW > 1) __syncthreads();
   return base_out;
 }
 
@@ -1156,10 +1194,37 @@ __device__ __forceinline__ void ata_pass_wave(VerifyLds& s, const double* xin1,
   }
 }
 
-template <int K>
+// NW = 4 (KIND_T only): wave w forms the canonical sum of coordinate w with
+// the one-wave lane mapping (the same sums), exchanged in s.redd.
+template <int K, int NW = 1>
 __device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const double* xin2, int n,
                                     double* model) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  if (K == KIND_T && NW > 1) {
+    const int wv = threadIdx.x >> 6;
+    const double* src = wv < 2 ? xin1 : xin2;
+    const int c = wv & 1;
+    double p = kCanonZero;
+    if (wv < 4) {
+      for (int b = lane; b < n; b += 64 * kSeqU) {
+        double a[kSeqU];
+#pragma unroll
+        for (int u = 0; u < kSeqU; ++u) a[u] = src[2 * min(b + 64 * u, n - 1) + c];
+#pragma unroll
+        for (int u = 0; u < kSeqU; ++u)
+          if (b + 64 * u < n) p += a[u];
+      }
+      p = canon_tree_wave(p);
+      if (lane == 0) s.redd[wv] = p;
+    }
+    __syncthreads();
+    const double s0 = s.redd[0] / (double)n, s1 = s.redd[1] / (double)n;
+    const double d0 = s.redd[2] / (double)n, d1 = s.redd[3] / (double)n;
+    __syncthreads();
+    model[0] = d0 - s0;
+    model[1] = d1 - s1;
+    return;
+  }
   if (K == KIND_T) {
     double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
     for (int b = lane; b < n; b += 64 * kSeqU) {
@@ -1421,7 +1486,9 @@ __device__ void ensure_best_sum(VerifyLds& s, const double* res_best, int n, dou
 // res0 / res1: residual buffers (n doubles each); xin1 / xin2 inlier gather
 // buffers (2n doubles each); snap: 625-word PRNG snapshot (global).  The
 // best model ends in s.best_model.
-template <int K>
+// NW waves (4: small batches, verify_final_kernel<4>; KIND_T): every wave runs
+// the same decisions; the point loops split as in the windowed replay.
+template <int K, int NW = 1>
 __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& s, uint32_t* sidx, const double* xy1,
                                       const double* xy2, int n, int max_trials,
                                       const VerifyParams P, double* res0, double* res1,
@@ -1429,18 +1496,20 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                                       double* mbuf, Prof pf) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool t0th = threadIdx.x == 0;
+  constexpr int BS = 64 * NW;
   const double maxr = P.max_residual;
   RansacResult out = {0, 0, 0, 0};
-  if (lane < 9) s.best_model[lane] = 0.0;  // report.model when no model is found
-  if (lane == 0) {
+  if (threadIdx.x < 9) s.best_model[threadIdx.x] = 0.0;  // report.model when no model is found
+  if (t0th) {
     s.best_n = 0;
     s.best_sum = 1.7976931348623157e308;  // Support() default: DBL_MAX
     s.best_sum_valid = 1;
   }
   wsync();
   if (n < Tr::kmin) return out;
-  for (int i = lane; i < n; i += 64) sidx[i] = (uint32_t)i;
+  for (int i = threadIdx.x; i < n; i += BS) sidx[i] = (uint32_t)i;
   double* res[2] = {res0, res1};
   int best_sel = 0;
   int dyn_max = max_trials;
@@ -1455,15 +1524,15 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
     pf.count(PR_N_BATCH);
     // -- snapshot the PRNG (global), draw B samples (Shuffle of the persistent
     //    index vector, RandomSampler::Sample).
-    for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
-    if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
+    for (int i = threadIdx.x; i < 624; i += BS) snap[i] = s.mt[i];
+    if (t0th) snap[624] = (uint32_t)s.mt_idx;
     wsync();
     if (draw_targets_wave<Tr::kmin>(s, B * Tr::kmin, (uint32_t)n)) {
-      if (lane == 0) shuffle_batch_lane0<Tr::kmin>(s, sidx, B);
+      if (t0th) shuffle_batch_lane0<Tr::kmin>(s, sidx, B);
     } else {  // a draw may need rejection sampling: serial replay from the snapshot
-      for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
+      for (int i = threadIdx.x; i < 624; i += BS) s.mt[i] = snap[i];
       wsync();
-      if (lane == 0) {
+      if (t0th) {
         s.mt_idx = (int32_t)snap[624];
         const uint32_t last = (uint32_t)(n - 1);
         for (int b = 0; b < B; ++b)
@@ -1476,12 +1545,12 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
           }
       }
     }
-    for (int i = lane; i < kTrialBatch * 3; i += 64) s.counts[i] = 0u;
+    for (int i = threadIdx.x; i < kTrialBatch * 3; i += BS) s.counts[i] = 0u;
     wsync();
     pf.lap(PR_SAMPLE);
     // -- solve the B minimal samples, one lane each; models go to the pair's
     //    model buffer (global, L1/L2-resident), counts of models to LDS.
-    if (lane < B) {
+    if ((int)threadIdx.x < B) {  // wave 0
       double a[2 * 7], b[2 * 7];
 #pragma unroll
       for (int i = 0; i < Tr::kmin; ++i) {
@@ -1520,7 +1589,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
         for (int j = 0; j < MS; ++j) m[k][j] = 0.0;
     }
     constexpr int PC = 8;  // points per lane per chunk
-    for (int base = 0; base < n; base += 64 * PC) {
+    for (int base = (int)(threadIdx.x >> 6) * 64 * PC; base < n; base += 64 * PC * NW) {
       double pa0[PC], pa1[PC], pb0[PC], pb1[PC];
       bool ok[PC];
 #pragma unroll
@@ -1549,7 +1618,10 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
               else in = residual_pt<K>(mk, pa0[p], pa1[p], pb0[p], pb1[p]) <= maxr;
               c += __popcll(__ballot(ok[p] && in));
             }
-            if (lane == 0) s.counts[t * MM + k] += (uint32_t)c;
+            if (lane == 0) {
+              if (NW == 1) s.counts[t * MM + k] += (uint32_t)c;
+              else atomicAdd(&s.counts[t * MM + k], (uint32_t)c);
+            }
           }
         }
       }
@@ -1573,7 +1645,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
             pf.lap(PR_OTHER);
             pf.count(PR_N_CAND);
             double* rt = res[best_sel ^ 1];
-            residuals_wave<K>(mk, xy1, xy2, n, maxr, rt);
+            residuals_wave<K, NW>(mk, xy1, xy2, n, maxr, rt, s.redi);
             pf.lap(PR_CAND);
             bool better = c > bn;
             double sum = 0.0;
@@ -1586,7 +1658,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
             }
             if (better) {
               wsync();
-              if (lane == 0) {
+              if (t0th) {
 #pragma unroll
                 for (int j = 0; j < MS; ++j) s.best_model[j] = mk[j];
                 s.best_n = c;
@@ -1600,14 +1672,15 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                 for (int lt = 0; lt < 10; ++lt) {
                   pf.lap(PR_OTHER);
                   pf.count(PR_N_LO);
-                  const int ni = gather_inliers(res[best_sel], n, maxr, xy1, xy2, xin1, xin2);
+                  const int ni =
+                      gather_inliers<NW>(res[best_sel], n, maxr, xy1, xy2, xin1, xin2, s.redi);
                   pf.lap(PR_GATHER);
                   double lm[9];
-                  local_estimate_wave<K>(s, xin1, xin2, ni, lm);
+                  local_estimate_wave<K, NW>(s, xin1, xin2, ni, lm);
                   pf.lap(PR_LOEST);
                   const int prev = s.best_n;
                   double* rl = res[best_sel ^ 1];
-                  const int lc = residuals_wave<K>(lm, xy1, xy2, n, maxr, rl);
+                  const int lc = residuals_wave<K, NW>(lm, xy1, xy2, n, maxr, rl, s.redi);
                   pf.lap(PR_LORES);
                   bool lbetter = lc > prev;
                   double lsum = 0.0;
@@ -1620,7 +1693,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                   }
                   if (lbetter) {
                     wsync();
-                    if (lane == 0) {
+                    if (t0th) {
 #pragma unroll
                       for (int j = 0; j < MS; ++j) s.best_model[j] = lm[j];
                       s.best_n = lc;
@@ -1648,9 +1721,9 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
     if (abort) {
       // Rewind the PRNG to the state right after trial abort_trial's sample.
       wsync();
-      for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
+      for (int i = threadIdx.x; i < 624; i += BS) s.mt[i] = snap[i];
       wsync();
-      if (lane == 0) {
+      if (t0th) {
         s.mt_idx = (int32_t)snap[624];
         const uint32_t last = (uint32_t)(n - 1);
         for (int b = 0; b <= abort_trial - trial; ++b)
@@ -1714,7 +1787,10 @@ __device__ __forceinline__ void mt_load(VerifyLds& s, const uint32_t* st) {
   wsync();
 }
 
-__global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
+// NW waves per pair (4 for small batches: the watermark LO-RANSAC is on the
+// critical path of one Scanner stencil).
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void verify_final_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
     const double* __restrict__ xy2_all, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, const uint8_t* __restrict__ masks,
@@ -1725,7 +1801,7 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
   Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
   pf.start();
   const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
-  const int n = ps.n, lane = threadIdx.x;
+  const int n = ps.n, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   uint32_t* sidx = reinterpret_cast<uint32_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
   if (!(n >= P.min_num_inliers && n > 0)) return;
   const double* xy1 = xy1_all + ps.pp.pts_off;
@@ -1746,7 +1822,7 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
       // DetectWatermark with the dummy cameras (width = height = 0): a point
       // is inside the [0,0]x[0,0] box only if it is exactly (0, 0).
       int nb = 0;
-      for (int b = lane; b < n; b += 64 * kSeqU) {
+      for (int b = wv * 64 * kSeqU + lane; b < n; b += 64 * kSeqU * NW) {
         uint8_t mk[kSeqU];
         double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
 #pragma unroll
@@ -1766,6 +1842,14 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
         }
       }
       nb = wave_sum_i(nb);
+      if (NW > 1) {
+        if (lane == 0) s.redi[wv] = nb;
+        __syncthreads();
+        nb = 0;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) nb += s.redi[w];
+        __syncthreads();
+      }
       const int ni = f_in;
       const double bratio = (double)nb / (double)ni;
       if (!(bratio < P.watermark_min_inlier_ratio)) {
@@ -1776,7 +1860,8 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
         double* tin1 = base;
         double* tin2 = base + 2 * n;
         int w = 0;
-        for (int b0 = 0; b0 < n; b0 += 64 * kSeqU) {
+        for (int r0 = 0; r0 < n; r0 += 64 * kSeqU * NW) {
+          const int b0 = r0 + wv * 64 * kSeqU;
           uint8_t mk[kSeqU];
           double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
 #pragma unroll
@@ -1788,23 +1873,44 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
             c0[u] = xy2[2 * ic];
             c1[u] = xy2[2 * ic + 1];
           }
+          uint64_t bal[kSeqU];
+          int wc = 0;
 #pragma unroll
           for (int u = 0; u < kSeqU; ++u) {
-            const bool in = mk[u] != 0;
-            const uint64_t bal = __ballot(in);
-            if (in) {
-              const int o2 = w + (int)__builtin_amdgcn_mbcnt_hi(
-                                     (uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+            bal[u] = __ballot(mk[u] != 0);
+            wc += __popcll(bal[u]);
+          }
+          int before = 0, total = wc;
+          if (NW > 1) {
+            if (lane == 0) s.redi[wv] = wc;
+            __syncthreads();
+            total = 0;
+#pragma unroll
+            for (int q = 0; q < NW; ++q) {
+              const int x = s.redi[q];
+              before += q < wv ? x : 0;
+              total += x;
+            }
+            __syncthreads();
+          }
+          int o = w + before;
+#pragma unroll
+          for (int u = 0; u < kSeqU; ++u) {
+            if (mk[u]) {
+              const int o2 = o + (int)__builtin_amdgcn_mbcnt_hi(
+                                     (uint32_t)(bal[u] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
               tin1[2 * o2] = a0[u];
               tin1[2 * o2 + 1] = a1[u];
               tin2[2 * o2] = c0[u];
               tin2[2 * o2 + 1] = c1[u];
             }
-            w += __popcll(bal);
+            o += __popcll(bal[u]);
           }
+          w += total;
         }
+        if (NW > 1) __syncthreads();
         mt_load(s, ps.state);
-        const RansacResult rt = loransac_wave<KIND_T>(s, sidx, tin1, tin2, ni, P.max_trials_T, P,
+        const RansacResult rt = loransac_wave<KIND_T, NW>(s, sidx, tin1, tin2, ni, P.max_trials_T, P,
                                                       base + 4 * n, base + 5 * n, base + 6 * n,
                                                       base + 8 * n, ps.snap, base + 10 * n, pf);
         const double iratio = (double)rt.num_inliers / (double)ni;
@@ -1817,15 +1923,15 @@ __global__ __launch_bounds__(kVerifyThreads) void verify_final_kernel(
   }
   // Post-filter (sequential_matching.cc:173-178): TwoViewGeometry().
   const bool keep = num_inliers >= mni;
-  if (lane == 0) {
+  if (threadIdx.x == 0) {
     o->config = keep ? config : 0;
     o->num_inliers = keep ? num_inliers : 0;
     o->watermark = watermark;
     o->raw_config = config;  // EstimateMultiple (multiple_models) reads the unfiltered result
   }
-  if (!keep && lane < 9) {
-    o->F[lane] = 0.0;
-    o->H[lane] = 0.0;
+  if (!keep && threadIdx.x < 9) {
+    o->F[threadIdx.x] = 0.0;
+    o->H[threadIdx.x] = 0.0;
   }
 }
 
@@ -2409,12 +2515,18 @@ constexpr int kScoreThreads = 64;
 #endif
 constexpr int kScorePch = SCM_SCORE_PCH;  // points per lane
 constexpr int kScoreChunk = kScoreThreads * kScorePch;
+#ifndef SCM_SCORE_PCH_SMALL
+#define SCM_SCORE_PCH_SMALL 4
+#endif
+constexpr int kScorePchSmall = SCM_SCORE_PCH_SMALL;  // small batches: points per lane
 #ifndef SCM_SCORE_ITEMS
 #define SCM_SCORE_ITEMS 65536  // 16K / 32K / 131K / 262K items: -1.5 to -6 % (profiles/r02_j_*vbench.log)
 #endif
 constexpr int kScoreTargetItems = SCM_SCORE_ITEMS;  // work items per score launch
 
-template <int K, bool SPLIT>
+// PCH: points per lane of a work item (kScorePch; small batches take more,
+// so that each model's constants and loop overhead serve more points).
+template <int K, bool SPLIT, int PCH = kScorePch>
 __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     const VerifyPair* __restrict__ pairs, const float4* __restrict__ xyf_all,
     const RansacState* __restrict__ rst, const int32_t* __restrict__ wB,
@@ -2426,7 +2538,8 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
   constexpr int MM = Tr::mm, MS = Tr::ms;
   __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * MM][12];
   __shared__ int32_t lnm[kTrialBatch];
-  __shared__ uint32_t ldq[SPLIT ? 1 : kDeferCap];         // deferred exact tests (defer_push)
+  constexpr int CH = kScoreThreads * PCH, QCAP = kDeferCap * (PCH / 8 > 1 ? PCH / 8 : 1);
+  __shared__ uint32_t ldq[SPLIT ? 1 : QCAP];         // deferred exact tests (defer_push)
   __shared__ uint32_t ldc[SPLIT ? 1 : kTrialBatch * MM];  // their inliers per model of the round
   const int lane = threadIdx.x;
   const int na = *nact;
@@ -2445,16 +2558,17 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     const int chunk = rem / nri, ri = rem - (rem / nri) * nri;
     const VerifyPair pp = pairs[q];
     const int n = pp.m;
-    const int base = chunk * kScoreChunk;
+    const int base = chunk * CH;
     if (base >= n) continue;
     const int Bpair = wB[q];
     const int rbeg = ri * rpi * kTrialBatch;
     const int rend = min(Bpair, rbeg + rpi * kTrialBatch);
     if (rbeg >= rend) continue;
     const float4* xyf = xyf_all + pp.pts_off / 2;
-    f32x2 x0[kScorePch / 2], x1[kScorePch / 2], y0[kScorePch / 2], y1[kScorePch / 2];
+    const uint64_t t_item = prof ? __builtin_amdgcn_s_memtime() : 0;
+    f32x2 x0[PCH / 2], x1[PCH / 2], y0[PCH / 2], y1[PCH / 2];
 #pragma unroll
-    for (int qq = 0; qq < kScorePch / 2; ++qq) {
+    for (int qq = 0; qq < PCH / 2; ++qq) {
       const int i0 = base + (2 * qq) * 64 + lane, i1 = i0 + 64;
       const float4 v0 = i0 < n ? xyf[i0] : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 v1 = i1 < n ? xyf[i1] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -2467,7 +2581,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
         y1[qq] *= dsc;
       }
     }
-    const bool full = base + kScoreChunk <= n;
+    const bool full = base + CH <= n;
     for (int r0 = rbeg; r0 < rend; r0 += kTrialBatch) {
       const int B = min(kTrialBatch, rend - r0);
       __syncthreads();
@@ -2482,7 +2596,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
         for (int i = lane; i < B * MM; i += kScoreThreads) ldc[i] = 0;
       __syncthreads();
       const double* mb = mods + ((int64_t)q * kWindowTrials * 3 + r0 * MM) * MS;
-      DeferQ dq{ldq, 0};
+      DeferQ dq{ldq, 0, QCAP};
       int nslow = 0;
       uint32_t c0 = 0, c1 = 0, c2 = 0;  // lane t: counts of hypothesis t's models
       uint32_t u0 = 0, u1 = 0, u2 = 0;  // SPLIT: lane t: their undecided points
@@ -2494,8 +2608,8 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
 #pragma unroll
           for (int k = 0; k < NM; ++k) f[k] = h_filter_load(&lc[min(t + k, B - 1)][0]);
           int uc[NM];
-          if (full) score_h_notout_n<kScorePch, true, NM>(f, x0, x1, y0, y1, n, base, uc);
-          else score_h_notout_n<kScorePch, false, NM>(f, x0, x1, y0, y1, n, base, uc);
+          if (full) score_h_notout_n<PCH, true, NM>(f, x0, x1, y0, y1, n, base, uc);
+          else score_h_notout_n<PCH, false, NM>(f, x0, x1, y0, y1, n, base, uc);
 #pragma unroll
           for (int k = 0; k < NM; ++k)
             if (t + k < B && lane == t + k) u0 += (uint32_t)uc[k];
@@ -2508,24 +2622,24 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
           int c, u = 0;
           if (K == KIND_F) {
             const FFilt f = f_filter_load(&lc[m][0], maxrf);
-            c = full ? score_f_chunk<kScorePch, true, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
+            c = full ? score_f_chunk<PCH, true, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
                                                              base, maxr, &nslow,
                                                              SPLIT ? nullptr : &dq, m, &u)
-                     : score_f_chunk<kScorePch, false, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
+                     : score_f_chunk<PCH, false, SPLIT>(f, mb + m * MS, x0, x1, y0, y1, n,
                                                               base, maxr, &nslow,
                                                               SPLIT ? nullptr : &dq, m, &u);
           } else {
             const HFilt f = h_filter_load(&lc[m][0]);
             if (SPLIT) {  // points not surely outside (bound); exact counts in rs_exact_kernel
               c = 0;
-              u = full ? score_h_chunk<kScorePch, true, true>(f, mb + m * MS, xyf, x0, x1, y0, y1,
+              u = full ? score_h_chunk<PCH, true, true>(f, mb + m * MS, xyf, x0, x1, y0, y1,
                                                               n, base, maxr, &nslow)
-                       : score_h_chunk<kScorePch, false, true>(f, mb + m * MS, xyf, x0, x1, y0,
+                       : score_h_chunk<PCH, false, true>(f, mb + m * MS, xyf, x0, x1, y0,
                                                                y1, n, base, maxr, &nslow);
             } else {
-              c = full ? score_h_chunk<kScorePch, true>(f, mb + m * MS, xyf, x0, x1, y0, y1, n,
+              c = full ? score_h_chunk<PCH, true>(f, mb + m * MS, xyf, x0, x1, y0, y1, n,
                                                         base, maxr, &nslow, &dq, m)
-                       : score_h_chunk<kScorePch, false>(f, mb + m * MS, xyf, x0, x1, y0, y1, n,
+                       : score_h_chunk<PCH, false>(f, mb + m * MS, xyf, x0, x1, y0, y1, n,
                                                          base, maxr, &nslow, &dq, m);
             }
           }
@@ -2571,6 +2685,10 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
         if (MM > 2 && u2) atomicAdd(&uq[lane * MM + 2], u2);
       }
     }
+    if (prof && lane == 0)  // diagnostics: cycles of the pair's score items
+      atomicAdd(reinterpret_cast<unsigned long long*>(prof + (int64_t)q * kVerifyProfSlots +
+                                                      (K == KIND_F ? 83 : 87)),
+                (unsigned long long)(__builtin_amdgcn_s_memtime() - t_item));
   }
 }
 
@@ -3103,6 +3221,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   const int wave_stride = (max_m + 7) / 8 * 8;
   const bool wave_sh = verify_small_batch(npairs, max_m);
   const size_t wave_lds = wave_shuffle_lds_bytes(wave_stride);
+  const int max_chunks_s = (max_m + kScoreThreads * kScorePchSmall - 1) / (kScoreThreads * kScorePchSmall);
   // First window: one round per pair when the batch fills the GPU; a small
   // batch (a single Scanner stencil) starts with wider windows -- its chain of
   // windows is latency-bound, and the speculative rounds past an early stop
@@ -3149,29 +3268,48 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
         hipLaunchKernelGGL((rs_score_kernel<KIND_F, true>), dim3(8192), dim3(kScoreThreads), 0,
                            stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
                            rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual, prof);
+
         hipLaunchKernelGGL(rs_exact_kernel<KIND_F>, dim3(8192), dim3(kScoreThreads), 0, stream,
                            pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
                            rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual);
       } else {
-        hipLaunchKernelGGL((rs_score_kernel<KIND_F, false>), dim3(8192), dim3(kScoreThreads), 0,
-                           stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
-                           rf.mods, rf.cnts, nullptr, max_chunks, W, P.max_residual, prof);
+        if (wave_sh)
+          hipLaunchKernelGGL((rs_score_kernel<KIND_F, false, kScorePchSmall>), dim3(8192),
+                             dim3(kScoreThreads), 0, stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw],
+                             rf.nact + lw, rf.nmod, rf.fcon, rf.mods, rf.cnts, nullptr, max_chunks_s,
+                             W, P.max_residual, prof);
+        else
+          hipLaunchKernelGGL((rs_score_kernel<KIND_F, false>), dim3(8192), dim3(kScoreThreads), 0,
+                             stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod,
+                             rf.fcon, rf.mods, rf.cnts, nullptr, max_chunks, W, P.max_residual, prof);
       }
     }
     if (h) {
       // The first window starts from best 0, where every model would need the
       // exact recount: it takes the one-pass kernel (exact tests inline).
       if (rh.ucnt && r > 0) {
-        hipLaunchKernelGGL((rs_score_kernel<KIND_H, true>), dim3(8192), dim3(kScoreThreads), 0,
-                           stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod, rh.fcon,
-                           rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, prof);
+        if (wave_sh)
+          hipLaunchKernelGGL((rs_score_kernel<KIND_H, true, kScorePchSmall>), dim3(8192),
+                             dim3(kScoreThreads), 0, stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw],
+                             rh.nact + lw, rh.nmod, rh.fcon, rh.mods, rh.cnts, rh.ucnt, max_chunks_s,
+                             W, P.max_residual, prof);
+        else
+          hipLaunchKernelGGL((rs_score_kernel<KIND_H, true>), dim3(8192), dim3(kScoreThreads), 0,
+                             stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod,
+                             rh.fcon, rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, prof);
         hipLaunchKernelGGL(rs_exact_kernel<KIND_H>, dim3(8192), dim3(kScoreThreads), 0, stream,
                            pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod, rh.fcon,
                            rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual);
       } else {
-        hipLaunchKernelGGL((rs_score_kernel<KIND_H, false>), dim3(8192), dim3(kScoreThreads), 0,
-                           stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod, rh.fcon,
-                           rh.mods, rh.cnts, nullptr, max_chunks, W, P.max_residual, prof);
+        if (wave_sh)
+          hipLaunchKernelGGL((rs_score_kernel<KIND_H, false, kScorePchSmall>), dim3(8192),
+                             dim3(kScoreThreads), 0, stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw],
+                             rh.nact + lw, rh.nmod, rh.fcon, rh.mods, rh.cnts, nullptr, max_chunks_s,
+                             W, P.max_residual, prof);
+        else
+          hipLaunchKernelGGL((rs_score_kernel<KIND_H, false>), dim3(8192), dim3(kScoreThreads), 0,
+                             stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod,
+                             rh.fcon, rh.mods, rh.cnts, nullptr, max_chunks, W, P.max_residual, prof);
       }
     }
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r + 1], stream);
@@ -3221,7 +3359,8 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     set_lds_attr(rs_shuffle_wave2_kernel);
     set_lds_attr(rs_replay2_kernel);
     set_lds_attr(rs_replay2w_kernel);
-    set_lds_attr(verify_final_kernel);
+    set_lds_attr(verify_final_kernel<1>);
+    set_lds_attr(verify_final_kernel<4>);
     attr = true;
   }
   const size_t lds = sizeof(VerifyLds);
@@ -3251,8 +3390,12 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
                          rhp, max_chunks, max_m, prof, stream, score_ev, nwin, sp,
                          sp ? spec->rstream : stream, sp ? spec->win_ev : nullptr)) != hipSuccess)
     return err;
-  hipLaunchKernelGGL(verify_final_kernel, dim3(npairs), dim3(kVerifyThreads), lds, stream, pairs,
-                     xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
+  if (verify_small_batch(npairs, max_m))
+    hipLaunchKernelGGL(verify_final_kernel<4>, dim3(npairs), dim3(256), lds, stream, pairs, xy1,
+                       xy2, scratch, snaps, masks, out, params, prof, counts);
+  else
+    hipLaunchKernelGGL(verify_final_kernel<1>, dim3(npairs), dim3(kVerifyThreads), lds, stream,
+                       pairs, xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
   return hipGetLastError();
 }
 
