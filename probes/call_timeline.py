@@ -1,5 +1,5 @@
 """Diagnostics: the kernel/copy timeline of one drop-in call from a rocprofv3
-kernel trace (calls delimited by verify_final_kernel).
+kernel trace (a call = from its matcher launch to the next call's).
 usage: python probes/call_timeline.py TRACE.csv [CALL]"""
 import csv
 import sys
@@ -7,8 +7,8 @@ import sys
 r = list(csv.DictReader(open(sys.argv[1])))
 r.sort(key=lambda x: int(x['Start_Timestamp']))
 call = int(sys.argv[2]) if len(sys.argv) > 2 else 4
-idx = [i for i, x in enumerate(r) if 'verify_final' in x['Kernel_Name']]
-a, b = idx[call] + 1, idx[call + 1] + 1
+idx = [i for i, x in enumerate(r) if 'match_g8_kernel' in x['Kernel_Name']]
+a, b = idx[call], idx[call + 1]
 t0 = int(r[a]['Start_Timestamp'])
 prev_end = t0
 busy = 0

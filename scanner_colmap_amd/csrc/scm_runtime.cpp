@@ -284,8 +284,10 @@ struct BatchSet {
   // odd-parity window buffers of small batches (speculative windows, launch_verify)
   DevBuf o_samp, o_nmod, o_fcon, o_mods, o_cnts, o_ucnt, o_wsnap, o_wb, o_wstate;
   DevBuf oh_samp, oh_nmod, oh_fcon, oh_mods, oh_cnts, oh_ucnt, oh_wsnap, oh_wb, oh_wstate;
-  hipStream_t rstream = nullptr;  // replay stream of speculative windows
+  hipStream_t rstream = nullptr;  // replay stream of speculative windows (another set's vstream)
+  hipStream_t fstream = nullptr;  // early verify_final pass of small batches (the third set's)
   hipEvent_t wev[2 * kMaxVerifyWindows] = {};
+  hipEvent_t fev = nullptr;
   HostBuf stage, vstage;
   PinnedOut out;
   size_t off_counts = 0, off_offsets = 0, off_vout = 0, off_matches = 0, off_masks = 0;
@@ -328,6 +330,8 @@ struct BatchSet {
       if (e) (void)hipEventDestroy(e);
       e = nullptr;
     }
+    if (fev) (void)hipEventDestroy(fev);
+    fev = nullptr;
   }
 };
 
@@ -820,8 +824,14 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   bs.pending = false;
   bs.table = &t;
   bs.specs = specs;
-  for (auto& e : bs.ev)
-    if (!e) SCM_HIP(hipEventCreate(&e));
+  // Events 3 and 6 are waited for by the host before it reads pinned memory
+  // (system-scope release); the others only time stages or order the
+  // device's own streams (a device-scope release: no system-scope cache
+  // writeback at each record, tens of microseconds on the small-batch path).
+  for (int i = 0; i < 7; ++i)
+    if (!bs.ev[i])
+      SCM_HIP(hipEventCreateWithFlags(&bs.ev[i], i == 3 || i == 6 ? hipEventDefault
+                                                                  : hipEventReleaseToDevice));
   if (P == 0) return SCM_OK;
   std::vector<PairDesc> pds(P);
   std::vector<MatchJob> jobs, jobs_clamp;
@@ -1165,7 +1175,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
                        bs.h_ucnt, bs.h_wsnap, bs.h_act, bs.h_nact, bs.h_wb, bs.h_wstate,
                        bs.h_dtrial, ctx->score_split, &rbh));
     if (!bs.sev[0])
-      for (auto& e : bs.sev) SCM_HIP(hipEventCreate(&e));
+      for (auto& e : bs.sev) SCM_HIP(hipEventCreateWithFlags(&e, hipEventReleaseToDevice));
     // Small batches (one Scanner stencil): odd-parity window buffers and a
     // replay stream, so that the next window's draws and scores overlap the
     // replay of this one.
@@ -1176,16 +1186,28 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
                           bs.o_wsnap, bs.o_wb, bs.o_wstate, false, &rbf1));
       SCM_TRY(window_bufs(bs.oh_samp, bs.oh_nmod, bs.oh_fcon, bs.oh_mods, bs.oh_cnts, bs.oh_ucnt,
                           bs.oh_wsnap, bs.oh_wb, bs.oh_wstate, ctx->score_split, &rbh1));
-      if (!bs.rstream)
-        SCM_HIP(hipStreamCreateWithPriority(&bs.rstream, hipStreamNonBlocking,
-                                            stream_priority("SCM_VERIFY_PRIO", true)));
+      // The replay stream and the early-final stream are the other two batch
+      // sets' verification streams: a process has few hardware queues
+      // (GPU_MAX_HW_QUEUES, 4 by default) and streams beyond them share one,
+      // serialising their work; these three are created on distinct queues.
+      // (A small batch's neighbours have nothing pending on the drop-in path;
+      // sharing a stream with a pending batch only adds ordering.)
+      const int si = (int)(&bs - ctx->sets);
+      bs.rstream = ctx->sets[(si + 1) % 3].vstream;
+      bs.fstream = ctx->sets[(si + 2) % 3].vstream;
       if (!bs.wev[0])
-        for (auto& e : bs.wev) SCM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (auto& e : bs.wev)
+          SCM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice));
+
+      if (!bs.fev)
+        SCM_HIP(hipEventCreateWithFlags(&bs.fev, hipEventDisableTiming | hipEventReleaseToDevice));
       if (!ctx->serial) {
         spec.rb_f1 = &rbf1;
         spec.rb_h1 = &rbh1;
         spec.rstream = bs.rstream;
         spec.win_ev = bs.wev;
+        spec.fstream = bs.fstream;
+        spec.fin_ev = bs.fev;
       }
     }
     SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
@@ -1708,10 +1730,8 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
 // Drains any batch left in flight by an error path.
 void drain(scm_context* ctx) {
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-  for (BatchSet& bs : ctx->sets) {
+  for (BatchSet& bs : ctx->sets)
     if (bs.vstream) (void)hipStreamSynchronize(bs.vstream);
-    if (bs.rstream) (void)hipStreamSynchronize(bs.rstream);
-  }
   for (BatchSet& bs : ctx->sets) bs.pending = bs.posted = false;
 }
 
@@ -1843,10 +1863,8 @@ void scm_context_destroy(scm_context* ctx) {
   for (BatchSet& bs : ctx->sets) bs.release();
   ctx->h_stage.release();
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
-  for (BatchSet& bs : ctx->sets) {
+  for (BatchSet& bs : ctx->sets)
     if (bs.vstream) (void)hipStreamDestroy(bs.vstream);
-    if (bs.rstream) (void)hipStreamDestroy(bs.rstream);
-  }
   delete ctx;
 }
 

@@ -124,11 +124,15 @@ constexpr int kMaxVerifyWindows = 64;
 // Speculative windows (small batches): rb_f1 / rb_h1 are the odd parity's
 // buffers (nullptr: none), rstream the replay stream and win_ev
 // 2 * kMaxVerifyWindows events (window r's wide kernels done, its replay done).
+// fstream / fin_ev: the early verify_final pass (pairs whose F and H are both
+// done once H's last window is replayed) runs there beside the later windows.
 struct VerifySpec {
   const VerifyRoundBufs* rb_f1 = nullptr;
   const VerifyRoundBufs* rb_h1 = nullptr;
   hipStream_t rstream = nullptr;
   hipEvent_t* win_ev = nullptr;
+  hipStream_t fstream = nullptr;
+  hipEvent_t fin_ev = nullptr;
 };
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,

@@ -1795,9 +1795,28 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
     const double* __restrict__ xy2_all, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, const uint8_t* __restrict__ masks,
     VerifyOut* __restrict__ out, VerifyParams P, uint64_t* __restrict__ prof,
-    const int32_t* __restrict__ counts) {
+    const int32_t* __restrict__ counts, RansacState* __restrict__ rstF,
+    const RansacState* __restrict__ rstH, int phase) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
+  // phase 1 (early, small batches): only pairs whose F and H RANSACs are both
+  // done (read once, by thread 0: the replay of other pairs is still
+  // running), marked in rstF[q].pad_; phase 2: the rest; phase 0: every pair.
+  if (phase != 0) {
+    if (threadIdx.x == 0) {
+      const int q0 = blockIdx.x;
+      const int fd = *reinterpret_cast<volatile const int32_t*>(&rstF[q0].done);
+      const int hd = *reinterpret_cast<volatile const int32_t*>(&rstH[q0].done);
+      const int mk = *reinterpret_cast<volatile const int32_t*>(&rstF[q0].pad_);
+      s.redi[7] = phase == 1 ? (fd && hd) : !mk;
+      __threadfence();
+    }
+    __syncthreads();
+    const bool go = s.redi[7] != 0;
+    __syncthreads();
+    if (!go) return;
+    if (phase == 1 && threadIdx.x == 0) rstF[blockIdx.x].pad_ = 1;
+  }
   Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
   pf.start();
   const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
@@ -2249,28 +2268,69 @@ size_t wave_shuffle_lds_bytes(int stride) {
          (size_t)(stride + 64) * 2;
 }
 
-template <int K>
+// DRAW: the window's draws (rs_draw_body's work: RandomSampler targets from
+// the pair's PRNG stream, round snapshots for the abort rewind, the trial
+// counts) happen here too, straight into the trial slots in LDS -- one launch
+// and no round trip of the targets through memory (small batches).
+constexpr size_t kWsDrawHead = (kVerifyLdsHead + 15) / 16 * 16;
+struct WsDraw {
+  RansacState* rst;
+  int32_t* nact_next;
+  uint32_t* cnts;
+  uint32_t* ucnt;
+  uint32_t* wsnap;
+  const uint32_t* pstate;
+  uint32_t* wstate;
+  int32_t* dtrial;
+  const uint32_t* pcnts;
+  const int32_t* pwB;
+  int spec, W;
+};
+
+template <int K, bool DRAW = false>
 __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
-    const int32_t* __restrict__ wB, const int32_t* __restrict__ act,
+    int32_t* __restrict__ wB, const int32_t* __restrict__ act,
     const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, uint64_t* __restrict__ prof,
-    int stride, int bid, int nblk) {
+    int stride, int bid, int nblk, const WsDraw& dr = WsDraw{}, const VerifyParams* Pp = nullptr) {
   constexpr int KM = KindTraits<K>::kmin;
+  using Tr = KindTraits<K>;
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-  uint32_t* tab = reinterpret_cast<uint32_t*>(dyn_lds);  // 64 x kWsTab: (j << 16) | symbol
+  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);  // DRAW: the PRNG state
+  uint32_t* tab = reinterpret_cast<uint32_t*>(dyn_lds + (DRAW ? kWsDrawHead : 0));  // 64 x kWsTab: (j << 16) | symbol
   // Trial k of lane L's chunk lives in slot k * kWsRow + L (16 bytes).
   uint4* slots = reinterpret_cast<uint4*>(tab + 64 * kWsTab);
   uint16_t* hsym = reinterpret_cast<uint16_t*>(slots + kWsC * kWsRow);  // 64 x 8 head symbols
   uint16_t* V = hsym + 64 * 8;                                           // the vector (+ dummies)
   const int lane = threadIdx.x;
   const uint32_t dummy = (uint32_t)(stride + lane);
+  if (DRAW && bid == 0 && lane == 0) *dr.nact_next = 0;
   const int na = *nact;
   for (int a = bid; a < na; a += nblk) {
     const int q = act[a];
     const PairSetup ps = pair_at<K>(pairs, q, scratch, snaps, out);
     uint32_t* g = pair_sidx(ps);
     const int n = ps.n;
+    int Bdraw = 0;
+    if (DRAW) {  // as rs_draw_body
+      const VerifyParams& P = *Pp;
+      Bdraw = max(0, min(kTrialBatch * dr.W, dr.rst[q].max_trials - dr.dtrial[q]));
+      if (dr.spec && Bdraw > 0) {
+        const int Bp = dr.pwB[q];
+        const uint32_t* pc2 = dr.pcnts + (int64_t)q * kWindowTrials * 3;
+        uint32_t cm = 0;
+        for (int i = lane; i < Bp * Tr::mm; i += 64) cm = max(cm, pc2[i]);
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) cm = max(cm, (uint32_t)__shfl_xor((int)cm, d));
+        const int last = dr.dtrial[q] - 1;
+        const uint64_t bound = num_trials((uint64_t)cm, (uint64_t)n, P.confidence,
+                                          P.dyn_num_trials_multiplier, Tr::kmin);
+        if (Bp > 0 && last >= P.min_num_trials && (uint64_t)last >= bound) Bdraw = 0;
+      }
+      wsync();
+      mt_load(s, dr.pstate + (int64_t)q * kVerifyStateWords);
+    }
     // Diagnostic phase cycles (SCM_PROFILE=1 only): staging, phase A, phase B, write-back.
     uint64_t* pc = prof ? prof + (int64_t)q * kVerifyProfSlots + (K == KIND_F ? 60 : 65) : nullptr;
     uint64_t tp = pc ? __builtin_amdgcn_s_memtime() : 0;
@@ -2292,7 +2352,7 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
     __syncthreads();
     lap(0);
     uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
-    const int Btot = wB[q];
+    const int Btot = DRAW ? Bdraw : wB[q];
     for (int p0 = 0; p0 < Btot; p0 += kWsPass) {
       const int np = min(kWsPass, Btot - p0);
       {
@@ -2303,7 +2363,37 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
       // as uint16 pairs, coalesced.
       // (All of a lane's loads are issued before the first LDS write: one
       // memory latency per pass, not one per trial.)
-      {
+      if (DRAW) {
+        // The pass's rounds of 64 draws: snapshot, targets into the slots.
+        for (int w0 = 0; w0 * kTrialBatch < np; ++w0) {
+          const int B = min(kTrialBatch, np - w0 * kTrialBatch);
+          const int wg = p0 / kTrialBatch + w0;  // round of the window
+          uint32_t* snap = dr.wsnap + ((int64_t)q * kMaxWindow + wg) * 640;
+          for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
+          if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
+          wsync();
+          if (!draw_targets_wave<KM>(s, B * KM, (uint32_t)n)) {
+            for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
+            wsync();
+            if (lane == 0) {
+              s.mt_idx = (int32_t)snap[624];
+              const uint32_t last = (uint32_t)(n - 1);
+              for (int r = 0; r < B * KM; ++r) s.jbuf[r] = uniform_u32(s, (uint32_t)(r % KM), last);
+            }
+          }
+          wsync();
+          if (lane < B) {
+            uint32_t tg[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) tg[i] = i < KM ? s.jbuf[lane * KM + i] : 0u;
+            const int idx = w0 * kTrialBatch + lane;
+            slots[(idx % kWsC) * kWsRow + idx / kWsC] =
+                make_uint4(tg[0] | (tg[1] << 16), tg[2] | (tg[3] << 16), tg[4] | (tg[5] << 16),
+                           tg[6] | (tg[7] << 16));
+          }
+          wsync();
+        }
+      } else {
         constexpr int U = kWsPass / 64;
         uint4 a0[U], a1[U];
 #pragma unroll
@@ -2433,6 +2523,19 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
       lap(2);
     }
     for (int i = lane; i < n; i += 64) g[i] = V[i];
+    if (DRAW) {
+      mt_save(s, dr.wstate + (int64_t)q * kVerifyStateWords);
+      uint32_t* cq = dr.cnts + (int64_t)q * kWindowTrials * 3;
+      for (int i = lane; i < Btot * 3; i += 64) cq[i] = 0u;
+      if (dr.ucnt) {
+        uint32_t* uq = dr.ucnt + (int64_t)q * kWindowTrials * 3;
+        for (int i = lane; i < Btot * 3; i += 64) uq[i] = 0u;
+      }
+      if (lane == 0) {
+        wB[q] = Btot;
+        dr.dtrial[q] += Btot;
+      }
+    }
     __syncthreads();
     lap(3);
   }
@@ -2450,6 +2553,27 @@ __global__ __launch_bounds__(64) void rs_shuffle_wave2_kernel(
                                  rh.samp, prof, stride, blockIdx.x - split, gridDim.x - split);
 }
 
+
+// Draws and Shuffle of a window in one launch (small batches).
+__global__ __launch_bounds__(64) void rs_drawshuffle_wave2_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
+    VerifyRoundBufs rh, int ain, int aclr, VerifyParams P, int spec, int W,
+    uint64_t* __restrict__ prof, int stride, int split) {
+  if ((int)blockIdx.x < split) {
+    const WsDraw d{rf.rst, rf.nact + aclr, rf.cnts, rf.ucnt, rf.wsnap, rf.pstate, rf.wstate,
+                   rf.dtrial, rf.pcnts, rf.pwB, spec, W};
+    rs_shuffle_wave_body<KIND_F, true>(pairs, scratch, snaps, out, rf.wB, rf.act[ain],
+                                       rf.nact + ain, rf.samp, prof, stride, blockIdx.x, split, d,
+                                       &P);
+  } else {
+    const WsDraw d{rh.rst, rh.nact + aclr, rh.cnts, rh.ucnt, rh.wsnap, rh.pstate, rh.wstate,
+                   rh.dtrial, rh.pcnts, rh.pwB, spec, W};
+    rs_shuffle_wave_body<KIND_H, true>(pairs, scratch, snaps, out, rh.wB, rh.act[ain],
+                                       rh.nact + ain, rh.samp, prof, stride, blockIdx.x - split,
+                                       gridDim.x - split, d, &P);
+  }
+}
 
 // Minimal solvers, one thread per hypothesis of the window, plus the fp32
 // filter constants of every model.
@@ -3023,10 +3147,13 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     st.best_sum_valid = s.best_sum_valid;
 #pragma unroll
     for (int j = 0; j < 9; ++j) st.best_model[j] = s.best_model[j];
+    // The pair's outputs first, then its state: a reader that sees done
+    // (the early verify_final pass) sees the outputs too.
+    if (st.done) rs_finish<K>(ps, st, masks, maxr);
+    __threadfence();
     wsync();
     if (t0th) rst[q] = st;
-    if (st.done) rs_finish<K>(ps, st, masks, maxr);
-    else if (t0th) act_next[atomicAdd(nact_next, 1)] = q;
+    if (!st.done && t0th) act_next[atomicAdd(nact_next, 1)] = q;
     if (pc && t0th) {
       pc[8] += __builtin_amdgcn_s_memtime() - t_enter;
       pc[9] += (uint64_t)Btot;
@@ -3204,7 +3331,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                        const VerifyParams& P, const float4* xyf, const VerifyRoundBufs* rfp,
                        const VerifyRoundBufs* rhp, int max_chunks, int max_m, uint64_t* prof,
                        hipStream_t stream, hipEvent_t* score_ev, int* nwin, bool spec,
-                       hipStream_t rstream, hipEvent_t* win_ev) {
+                       hipStream_t rstream, hipEvent_t* win_ev, int* last_h) {
   const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
   const int gw = npairs < kPairGrid ? npairs : kPairGrid;
 #ifndef SCM_SHUFFLE_LDS_KB
@@ -3238,17 +3365,20 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     if (spec && r >= 2 && r - 2 < kMaxVerifyWindows)
       (void)hipStreamWaitEvent(stream, win_ev[2 * (r - 2) + 1], 0);
     const bool f = covered < P.max_trials_F, h = covered < P.max_trials_H;
+    if (h && last_h) *last_h = r;
     const int g1 = (f ? gw : 0) + (h ? gw : 0), s1 = f ? gw : 0;
     const int g2 = (f ? sh_blocks : 0) + (h ? sh_blocks : 0), s2 = f ? sh_blocks : 0;
-    hipLaunchKernelGGL(rs_draw2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
-                       out, rf, rh, lw, lout, P, (spec && r > 0) ? 1 : 0, W, s1);
-    if (wave_sh)
-      hipLaunchKernelGGL(rs_shuffle_wave2_kernel, dim3(g1), dim3(64), wave_lds, stream, pairs,
-                         scratch, snaps, out, rf, rh, lw, prof, wave_stride, s1);
-    else
+    if (wave_sh) {
+      hipLaunchKernelGGL(rs_drawshuffle_wave2_kernel, dim3(g1), dim3(64), kWsDrawHead + wave_lds,
+                         stream, pairs, scratch, snaps, out, rf, rh, lw, lout, P,
+                         (spec && r > 0) ? 1 : 0, W, prof, wave_stride, s1);
+    } else {
+      hipLaunchKernelGGL(rs_draw2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
+                         out, rf, rh, lw, lout, P, (spec && r > 0) ? 1 : 0, W, s1);
       hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
                          (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch,
                          snaps, out, rf, rh, lw, sh_ppb, sh_stride, s2);
+    }
     if (f)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(SCM_SOLVE_GRID), dim3(64), 0, stream, pairs, xy1, xy2,
                          rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.samp, rf.nmod, rf.fcon, rf.mods,
@@ -3357,6 +3487,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     set_lds_attr(rs_draw2_kernel);
     set_lds_attr(rs_shuffle2_kernel);
     set_lds_attr(rs_shuffle_wave2_kernel);
+    set_lds_attr(rs_drawshuffle_wave2_kernel);
     set_lds_attr(rs_replay2_kernel);
     set_lds_attr(rs_replay2w_kernel);
     set_lds_attr(verify_final_kernel<1>);
@@ -3370,7 +3501,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   // Parity buffers: the odd ones from spec, else both parities alias (the
   // windows then run strictly in order on one stream).
   const bool sp = spec && spec->rb_f1 && spec->rb_h1 && spec->rstream && spec->win_ev &&
-                  verify_small_batch(npairs, max_m);
+                  spec->fstream && spec->fin_ev && verify_small_batch(npairs, max_m);
   VerifyRoundBufs rfp[2] = {rb_f, sp ? *spec->rb_f1 : rb_f};
   VerifyRoundBufs rhp[2] = {rb_h, sp ? *spec->rb_h1 : rb_h};
   for (VerifyRoundBufs* b : {&rfp[0], &rfp[1], &rhp[0], &rhp[1]}) {
@@ -3386,16 +3517,34 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   if ((err = hipMemsetAsync(rb_h.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
   hipLaunchKernelGGL(rs_begin2_kernel, dim3(2 * gw), dim3(64), kVerifyLdsHead, stream, pairs,
                      npairs, scratch, snaps, out, masks, xyf, rfp[0], rhp[0], params, gw);
+  int last_h = -1;
   if ((err = run_windows(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf, rfp,
                          rhp, max_chunks, max_m, prof, stream, score_ev, nwin, sp,
-                         sp ? spec->rstream : stream, sp ? spec->win_ev : nullptr)) != hipSuccess)
+                         sp ? spec->rstream : stream, sp ? spec->win_ev : nullptr, &last_h)) !=
+      hipSuccess)
     return err;
-  if (verify_small_batch(npairs, max_m))
+  if (sp && last_h >= 0 && last_h < kMaxVerifyWindows) {
+    // Configuration + watermark of the pairs done when H's last window is
+    // replayed (typically all but the far pairs' F), beside the later windows;
+    // then the rest after the last window.
+    (void)hipStreamWaitEvent(spec->fstream, spec->win_ev[2 * last_h + 1], 0);
+    hipLaunchKernelGGL(verify_final_kernel<4>, dim3(npairs), dim3(256), lds, spec->fstream, pairs,
+                       xy1, xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst,
+                       rb_h.rst, 1);
+    (void)hipEventRecord(spec->fin_ev, spec->fstream);
+    (void)hipStreamWaitEvent(stream, spec->fin_ev, 0);
     hipLaunchKernelGGL(verify_final_kernel<4>, dim3(npairs), dim3(256), lds, stream, pairs, xy1,
-                       xy2, scratch, snaps, masks, out, params, prof, counts);
-  else
+                       xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,
+                       2);
+  } else if (verify_small_batch(npairs, max_m)) {
+    hipLaunchKernelGGL(verify_final_kernel<4>, dim3(npairs), dim3(256), lds, stream, pairs, xy1,
+                       xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,
+                       0);
+  } else {
     hipLaunchKernelGGL(verify_final_kernel<1>, dim3(npairs), dim3(kVerifyThreads), lds, stream,
-                       pairs, xy1, xy2, scratch, snaps, masks, out, params, prof, counts);
+                       pairs, xy1, xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst,
+                       rb_h.rst, 0);
+  }
   return hipGetLastError();
 }
 
