@@ -3148,9 +3148,10 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
 #pragma unroll
     for (int j = 0; j < 9; ++j) st.best_model[j] = s.best_model[j];
     // The pair's outputs first, then its state: a reader that sees done
-    // (the early verify_final pass) sees the outputs too.
+    // (the early verify_final pass of small batches, NW > 1) sees the
+    // outputs too.
     if (st.done) rs_finish<K>(ps, st, masks, maxr);
-    __threadfence();
+    if (NW > 1) __threadfence();
     wsync();
     if (t0th) rst[q] = st;
     if (!st.done && t0th) act_next[atomicAdd(nact_next, 1)] = q;
