@@ -173,7 +173,11 @@ int scm_execute_stencil(scm_context* ctx, int64_t stencil_size,
  * the keypoint and descriptor bytes), never by id alone: PrepareImage ids
  * are per-instance counters (prepare_image.cc:11-20), so one id may name two
  * images, and every element is matched with its own bytes as the reference
- * decodes them (sequential_matching.cc:115-122). */
+ * decodes them (sequential_matching.cc:115-122).  Element buffers the
+ * previous call also handed over (same addresses and sizes) take that call's
+ * content keys at once and are re-hashed while the GPU runs; if a buffer was
+ * rewritten in place the run is discarded and the call runs again with every
+ * key hashed first, so the outputs always follow the bytes. */
 int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
                       const scm_element* image_ids,
                       const scm_element* keypoints,
