@@ -114,10 +114,12 @@ std::vector<uint8_t> tvg_list_bytes(const std::vector<Tvg>& list);
 std::vector<uint8_t> id_list_bytes(const std::vector<uint32_t>& ids);
 
 // GPU SIFT extraction (scm_sift.cpp): per-context state, created on first use.
+// streams: kSiftSlotStreams streams the slots borrow (nullptr: their own).
+constexpr int kSiftSlotStreams = 4;
 struct SiftState;
 void sift_state_destroy(SiftState* s);
-int sift_extract_frames(SiftState** state, int device, int64_t n, const uint64_t* ids,
-                        const scm_frame* frames, scm_blob* kp_out, scm_blob* desc_out,
-                        scm_blob* cam_out);
+int sift_extract_frames(SiftState** state, int device, const hipStream_t* streams, int64_t n,
+                        const uint64_t* ids, const scm_frame* frames, scm_blob* kp_out,
+                        scm_blob* desc_out, scm_blob* cam_out);
 
 }  // namespace scm

@@ -2240,8 +2240,13 @@ int scm_extract_frames(scm_context* ctx, int64_t n, const uint64_t* image_ids,
     set_error("null context");
     return SCM_E_INVALID;
   }
-  return sift_extract_frames(&ctx->sift, ctx->device, n, image_ids, frames, keypoints_out,
-                             descriptors_out, cameras_out);
+  // the slots run on the context's four streams (one hardware queue each);
+  // SCM_SIFT_OWN_STREAMS=1 gives them streams of their own
+  const char* own = std::getenv("SCM_SIFT_OWN_STREAMS");
+  const hipStream_t lent[kSiftSlotStreams] = {ctx->stream, ctx->sets[0].vstream,
+                                              ctx->sets[1].vstream, ctx->sets[2].vstream};
+  return sift_extract_frames(&ctx->sift, ctx->device, own && own[0] == '1' ? nullptr : lent, n,
+                             image_ids, frames, keypoints_out, descriptors_out, cameras_out);
 }
 
 int scm_set_serial(scm_context* ctx, int32_t serial) {

@@ -33,7 +33,7 @@ constexpr int kMaxImageSize = 3200;  // SiftExtractionOptions::max_image_size
 constexpr int kMaxNumFeatures = 8192;
 constexpr double kPeakThreshold = 0.02 / 3;
 constexpr double kEdgeThreshold = 10.0;
-constexpr int kSlots = 4;
+constexpr int kSlots = kSiftSlotStreams;
 
 struct Slot {
   hipStream_t st = nullptr;
@@ -65,6 +65,7 @@ struct SiftState {
   SiftConsts c{};
   int widths[6] = {0, 0, 0, 0, 0, 0};
   Slot slots[kSlots];
+  bool own_streams = false;  // slot streams created here (else the context's, borrowed)
 };
 
 void sift_state_destroy(SiftState* s) {
@@ -73,7 +74,7 @@ void sift_state_destroy(SiftState* s) {
   for (Slot& sl : s->slots) {
     if (sl.st) {
       (void)hipStreamSynchronize(sl.st);
-      (void)hipStreamDestroy(sl.st);
+      if (s->own_streams) (void)hipStreamDestroy(sl.st);
     }
     sl.frame.release();
     sl.rs.release();
@@ -104,7 +105,7 @@ int gauss_taps(double sigma, float* g) {
   return W;
 }
 
-int init_state(SiftState* s) {
+int init_state(SiftState* s, const hipStream_t* streams) {
   // VLFeat: sigmak = 2^(1/S), sigma0 = 1.6 sigmak, dsigma0 = sigma0 sqrt(1 - 1/sigmak^2),
   // first level of the first octave: sd = sqrt(sa^2 - sb^2), sa = sigma0 sigmak^-1,
   // sb = 0.5 * 2^1; level s: dsigma0 sigmak^s.
@@ -126,7 +127,14 @@ int init_state(SiftState* s) {
   SCM_HIP(hipMemcpy(s->c.taps, taps.data(), tb, hipMemcpyHostToDevice));
   SCM_HIP(hipMemcpy(s->c.widths, s->widths, sizeof(s->widths), hipMemcpyHostToDevice));
   SCM_HIP(hipMemcpy(s->c.expn, expn, eb, hipMemcpyHostToDevice));
-  for (Slot& sl : s->slots) SCM_HIP(hipStreamCreateWithFlags(&sl.st, hipStreamNonBlocking));
+  // The slots run on the context's streams when it lends them: each of those
+  // has a hardware queue of its own, while streams created past
+  // GPU_MAX_HW_QUEUES share queues, and frames on one queue serialise.
+  s->own_streams = streams == nullptr;
+  for (int i = 0; i < kSlots; ++i) {
+    if (streams) s->slots[i].st = streams[i];
+    else SCM_HIP(hipStreamCreateWithFlags(&s->slots[i].st, hipStreamNonBlocking));
+  }
   return SCM_OK;
 }
 
@@ -440,9 +448,9 @@ int harvest_or_regrow(SiftState* s, Slot& sl, int64_t j, const uint64_t* ids,
   }
 }
 
-int sift_extract_frames(SiftState** state, int device, int64_t n, const uint64_t* ids,
-                        const scm_frame* frames, scm_blob* kp_out, scm_blob* desc_out,
-                        scm_blob* cam_out) {
+int sift_extract_frames(SiftState** state, int device, const hipStream_t* streams, int64_t n,
+                        const uint64_t* ids, const scm_frame* frames, scm_blob* kp_out,
+                        scm_blob* desc_out, scm_blob* cam_out) {
   if (n < 0 || (n > 0 && (!ids || !frames || !kp_out || !desc_out || !cam_out))) {
     set_error("scm_extract_frames: null argument");
     return SCM_E_INVALID;
@@ -462,7 +470,7 @@ int sift_extract_frames(SiftState** state, int device, int64_t n, const uint64_t
     s->device = device;
     if (const char* e = std::getenv("SCM_SIFT_CAPS"))
       std::sscanf(e, "%d,%d,%d", &s->caps[0], &s->caps[1], &s->caps[2]);
-    SCM_TRY(init_state(s.get()));
+    SCM_TRY(init_state(s.get(), streams));
     *state = s.release();
   }
   SiftState* s = *state;

@@ -448,11 +448,17 @@ __global__ void gradient_kernel(const float* __restrict__ lev, float2* __restric
 }
 
 // vl_sift_calc_keypoint_orientations, one wave per keypoint.  The window's
-// samples are visited 64 at a time in VLFeat's (ys, xs) order: each lane
-// prepares one sample (mod * wgt) and marks it in its bin's 64-bit sample
-// mask, then lane b < 36 adds its bin's samples in mask-bit (= sample) order
-// -- the same double additions in the same order as the serial histogram.
-// Smoothing and peak search by lane 0.
+// samples are visited 64 at a time in VLFeat's (ys, xs) order: lane j
+// prepares sample j of the chunk (mod * wgt) and writes it into column j of
+// its bin's row of a zero-filled bin-major LDS table; lane b < 36 then adds
+// row b over all 64 columns in order.  Each sample reaches one bin and every
+// value is >= +0, so the added zeros leave the double sums unchanged -- the
+// serial histogram's additions in its order.  The six smoothing passes read
+// only the previous pass's bins (new[b] = (old[b-1] + old[b] + old[b+1]) / 3,
+// circular), so lane b computes bin b; the peaks are the first two set bits
+// of a ballot in bin order (VLFeat keeps up to 4, COLMAP uses 2).
+constexpr int kOriRow = 66;  // doubles per bin row (64 samples + pad)
+
 __global__ __launch_bounds__(64) void orient_kernel(const float2* __restrict__ grad, int w, int h,
                                                     const SiftKey* __restrict__ keys,
                                                     SiftCounts* __restrict__ cnt,
@@ -460,15 +466,17 @@ __global__ __launch_bounds__(64) void orient_kernel(const float2* __restrict__ g
                                                     double* __restrict__ ang,
                                                     const double* __restrict__ expn, int octave) {
   constexpr int nbins = 36;
-  __shared__ unsigned long long smask[nbins];  // per bin: the chunk's samples adding to it
-  __shared__ double sval[64];
+  __shared__ __attribute__((aligned(16))) double s_v[nbins * kOriRow];
+  __shared__ double s_expn[257];
   __shared__ double hist[nbins];
   const int lane = threadIdx.x;
+  for (int b = lane; b < nbins * kOriRow; b += 64) s_v[b] = 0.0;
+  for (int b = lane; b < 257; b += 64) s_expn[b] = expn[b];
+  __syncthreads();
   const int n = cnt->nkey;
   const double xper = ldexp(1.0, octave);
   const size_t so = (size_t)w * h;
-  if (lane < nbins) smask[lane] = 0;
-  __syncthreads();
+  const double2* row = reinterpret_cast<const double2*>(s_v + min(lane, nbins - 1) * kOriRow);
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const SiftKey k = keys[i];
     const double x = k.x / xper, y = k.y / xper, sigma = k.sigma / xper;
@@ -477,6 +485,8 @@ __global__ __launch_bounds__(64) void orient_kernel(const float2* __restrict__ g
     const int W = max((int)floor(3.0 * sigmaw), 1);
     const bool valid =
         !(xi < 0 || xi > w - 1 || yi < 0 || yi > h - 1 || si < kSMin + 1 || si > kSMax - 2);
+    int nu = 0;
+    double out0 = 0.0, out1 = 0.0;
     if (valid) {
       const int ys0 = max(-W, -yi), ys1 = min(W, h - 1 - yi);
       const int xs0 = max(-W, -xi), xs1 = min(W, w - 1 - xi);
@@ -485,71 +495,75 @@ __global__ __launch_bounds__(64) void orient_kernel(const float2* __restrict__ g
       double acc = 0.0;
       for (int t0 = 0; t0 < total; t0 += 64) {
         const int t = t0 + lane;
-        int bin = -1;
-        double v = 0.0;
+        int p = -1;
         if (t < total) {
           const int ys = ys0 + t / ncols, xs = xs0 + t % ncols;
           const double dx = (double)(xi + xs) - x, dy = (double)(yi + ys) - y;
           const double r2 = dx * dx + dy * dy;
           if (r2 < W * W + 0.6) {
-            const double wgt = fast_expn(expn, r2 / (2 * sigmaw * sigmaw));
+            const double wgt = fast_expn(s_expn, r2 / (2 * sigmaw * sigmaw));
             const float2 g = pt[xs + (ptrdiff_t)ys * w];
             const double mod = g.x, an = g.y;
-            bin = (int)floor(nbins * an / (2 * kPi)) % nbins;
-            v = mod * wgt;
+            const int bin = (int)floor(nbins * an / (2 * kPi)) % nbins;
+            p = bin * kOriRow + lane;
+            s_v[p] = mod * wgt;
           }
         }
-        sval[lane] = v;
-        if (bin >= 0) atomicOr(&smask[bin], 1ull << lane);
         __syncthreads();
         if (lane < nbins) {
-          uint64_t m = smask[lane];
-          while (m) {  // this bin's samples of the chunk, in order
-            acc += sval[__builtin_ctzll(m)];
-            m &= m - 1;
+#pragma unroll
+          for (int q = 0; q < 32; ++q) {
+            const double2 u = row[q];
+            acc += u.x;
+            acc += u.y;
           }
         }
         __syncthreads();
-        if (lane < nbins) smask[lane] = 0;
+        if (p >= 0) s_v[p] = 0.0;
       }
-      if (lane < nbins) hist[lane] = acc;
+      // six smoothing passes, bin b on lane b
+      double hb = acc;
+      for (int iter = 0; iter < 6; ++iter) {
+        if (lane < nbins) hist[lane] = hb;
+        __syncthreads();
+        if (lane < nbins) {
+          const double hm = hist[(lane + nbins - 1) % nbins], hp = hist[(lane + 1) % nbins];
+          hb = (hm + hb + hp) / 3.0;
+        }
+        __syncthreads();
+      }
+      if (lane < nbins) hist[lane] = hb;
+      __syncthreads();
+      double maxh = 0;
+      for (int b = 0; b < nbins; ++b) maxh = fmax(maxh, hist[b]);
+      bool peak = false;
+      double th = 0.0;
+      if (lane < nbins) {
+        const double h0 = hb, hm = hist[(lane + nbins - 1) % nbins], hp = hist[(lane + 1) % nbins];
+        if (h0 > 0.8 * maxh && h0 > hm && h0 > hp) {
+          const double di = -0.5 * (hp - hm) / (hp + hm - 2 * h0);
+          th = 2 * kPi * (lane + di + 0.5) / nbins;
+          peak = true;
+        }
+      }
+      uint64_t m = __ballot(peak);
+      if (m) {
+        out0 = __shfl(th, __builtin_ctzll(m));
+        m &= m - 1;
+        nu = 1;
+        if (m) {
+          out1 = __shfl(th, __builtin_ctzll(m));
+          nu = 2;
+        }
+      }
       __syncthreads();
     }
     if (lane == 0) {
-      int na = 0;
-      double out[4] = {0, 0, 0, 0};
-      if (valid) {
-        double hs[nbins];
-        for (int b = 0; b < nbins; ++b) hs[b] = hist[b];
-        for (int iter = 0; iter < 6; ++iter) {
-          double prev = hs[nbins - 1];
-          const double first = hs[0];
-          int b;
-          for (b = 0; b < nbins - 1; ++b) {
-            const double nh = (prev + hs[b] + hs[(b + 1) % nbins]) / 3.0;
-            prev = hs[b];
-            hs[b] = nh;
-          }
-          hs[b] = (prev + hs[b] + first) / 3.0;
-        }
-        double maxh = 0;
-        for (int b = 0; b < nbins; ++b) maxh = fmax(maxh, hs[b]);
-        for (int b = 0; b < nbins; ++b) {
-          const double h0 = hs[b], hm = hs[(b - 1 + nbins) % nbins], hp = hs[(b + 1 + nbins) % nbins];
-          if (h0 > 0.8 * maxh && h0 > hm && h0 > hp) {
-            const double di = -0.5 * (hp - hm) / (hp + hm - 2 * h0);
-            out[na++] = 2 * kPi * (b + di + 0.5) / nbins;
-            if (na == 4) break;
-          }
-        }
-      }
-      const int nu = min(na, 2);
       nori[i] = nu;
-      ang[2 * i] = out[0];
-      ang[2 * i + 1] = out[1];
+      ang[2 * i] = out0;
+      ang[2 * i + 1] = out1;
       if (nu) atomicAdd(&cnt->level_feats[(octave + 1) * 3 + si], nu);
     }
-    __syncthreads();
   }
 }
 
@@ -604,13 +618,21 @@ __device__ void descriptor_finish(float a0, float a1, float* __restrict__ sh, fl
 }
 
 // vl_sift_calc_keypoint_descriptor + the COLMAP conversions, one wave per
-// keypoint (its <= 2 orientations in turn).  The sample rectangle is visited
-// 64 samples at a time in VLFeat's (dyi, dxi) order: each lane prepares one
-// sample (win * mod, bins and fractional offsets) and marks it in the 64-bit
-// sample masks of the (up to 8) bins it reaches, then lane L accumulates bins
-// L and L + 64 over their samples in mask-bit (= sample) order.  A sample
-// reaches a bin through at most one corner, so every bin sees VLFeat's float
-// additions in VLFeat's order.
+// (keypoint, orientation).  The sample rectangle is visited 64 samples at a
+// time in VLFeat's (dyi, dxi) order: lane j prepares sample j of the chunk
+// and keeps its (up to 8) bin weights.  The samples that reach a bin keep
+// their order as columns 0 .. k-1 (ballot rank), 32 at a time: each writes
+// its weights into its column of a bin-major LDS table whose other entries
+// are zero, and lane L adds rows L and L + 64 over the used columns in order.
+// A sample reaches a bin through at most one corner and every weight is >= +0
+// (win * mod * |.| * |.| * |.|), so the added zeros leave the sums unchanged:
+// every bin sees VLFeat's float additions in VLFeat's order.  Rows of
+// kDescRow floats are read as float2 (34: the 32 lanes of a read fall on
+// distinct bank pairs); the writers zero their entries again after each pass,
+// and unused corners write to a dummy slot (no branches).  20 KB of LDS per
+// wave: 2 waves per SIMD.
+constexpr int kDescRow = 34;
+
 __global__ __launch_bounds__(64) void descriptor_kernel(
     const float2* __restrict__ grad, int w, int h, const SiftKey* __restrict__ keys,
     SiftCounts* __restrict__ cnt, const int32_t* __restrict__ nori, const double* __restrict__ ang,
@@ -618,107 +640,147 @@ __global__ __launch_bounds__(64) void descriptor_kernel(
     uint8_t* __restrict__ desc, int32_t* __restrict__ stale, const double* __restrict__ expn,
     int feat_cap, int octave) {
   constexpr int NBP = 4, NBO = 8;
-  __shared__ float s_wm[64], s_rx[64], s_ry[64], s_rt[64];
-  __shared__ int s_b[64];  // binx + 3 | (biny + 3) << 8 | bint << 16 (bint in 0 .. 8)
-  __shared__ unsigned long long s_mask[128];  // per bin: the chunk's samples adding to it
-  __shared__ float sh[129];
+  constexpr int kDummy = 128 * kDescRow;  // 32 dummy floats, then the finish's 129
+  __shared__ __attribute__((aligned(16))) float s_v[128 * kDescRow + 32 + 129];
+  __shared__ double s_expn[257];
+  float* sh = s_v + kDummy + 32;
   const int lane = threadIdx.x;
-  const int bt0 = lane & 7, bx0 = (lane >> 3) & 3, by0 = lane >> 5, by1 = 2 + (lane >> 5);
-  const int n = cnt->nkey;
-  s_mask[lane] = 0;
-  s_mask[lane + 64] = 0;
+  for (int b = lane; b < 128 * kDescRow; b += 64) s_v[b] = 0.0f;
+  for (int b = lane; b < 257; b += 64) s_expn[b] = expn[b];
   __syncthreads();
+  const int n = cnt->nkey;
   const double xper = ldexp(1.0, octave);
   const size_t so = (size_t)w * h;
-  for (int i = blockIdx.x; i < n; i += gridDim.x) {
+  const float2* r0 = reinterpret_cast<const float2*>(s_v + lane * kDescRow);
+  const float2* r1 = reinterpret_cast<const float2*>(s_v + (lane + 64) * kDescRow);
+  for (int it = blockIdx.x; it < 2 * n; it += gridDim.x) {
+    const int i = it >> 1, o = it & 1;
+    if (o >= nori[i]) continue;
     const SiftKey k = keys[i];
-    const int nu = nori[i];
-    for (int o = 0; o < nu; ++o) {
-      const int fi = koff[i] + o;
-      if (fi >= feat_cap) {
-        if (lane == 0) cnt->overflow = 1;
-        break;
+    const int fi = koff[i] + o;
+    if (fi >= feat_cap) {
+      if (lane == 0) cnt->overflow = 1;
+      continue;
+    }
+    const double angle0 = ang[2 * i + o];
+    if (lane == 0) feat[fi] = SiftFeat{k.x + 0.5f, k.y + 0.5f, k.sigma, (float)angle0};
+    const double x = k.x / xper, y = k.y / xper, sigma = k.sigma / xper;
+    const int xi = (int)(x + 0.5), yi = (int)(y + 0.5), si = k.is;
+    if (xi < 0 || xi >= w || yi < 0 || yi >= h - 1 || si < kSMin + 1 || si > kSMax - 2) {
+      // vl_sift_calc_keypoint_descriptor returns before writing: COLMAP
+      // re-normalises the previous descriptor's buffer (fixup_kernel)
+      if (lane == 0) {
+        stale[fi] = 1;
+        atomicAdd(&cnt->nstale, 1);
       }
-      const double angle0 = ang[2 * i + o];
-      if (lane == 0) feat[fi] = SiftFeat{k.x + 0.5f, k.y + 0.5f, k.sigma, (float)angle0};
-      const double x = k.x / xper, y = k.y / xper, sigma = k.sigma / xper;
-      const int xi = (int)(x + 0.5), yi = (int)(y + 0.5), si = k.is;
-      if (xi < 0 || xi >= w || yi < 0 || yi >= h - 1 || si < kSMin + 1 || si > kSMax - 2) {
-        // vl_sift_calc_keypoint_descriptor returns before writing: COLMAP
-        // re-normalises the previous descriptor's buffer (fixup_kernel)
-        if (lane == 0) {
-          stale[fi] = 1;
-          atomicAdd(&cnt->nstale, 1);
+      continue;
+    }
+    if (lane == 0) stale[fi] = 0;
+    const double st0 = sin(angle0), ct0 = cos(angle0);
+    const double SBP = 3.0 * sigma + kEpsD;
+    const int W = (int)floor(sqrt(2.0) * SBP * (NBP + 1) / 2.0 + 0.5);
+    const int dy0 = max(-W, 1 - yi), dy1 = min(W, h - yi - 2);
+    const int dx0 = max(-W, 1 - xi), dx1 = min(W, w - xi - 2);
+    const int ncols = dx1 - dx0 + 1, nrows = dy1 - dy0 + 1;
+    const int total = (ncols > 0 && nrows > 0) ? ncols * nrows : 0;
+    const float2* pt = grad + so * (size_t)(si - kSMin - 1) + (size_t)yi * w + xi;
+    float a0 = 0.0f, a1 = 0.0f;
+    // the lane's sample t = t0 + lane as (row, column) of the rectangle,
+    // stepped by 64 per chunk; the next chunk's gradient is loaded while this
+    // chunk is summed
+    const int step_r = total ? 64 / ncols : 0, step_c = total ? 64 % ncols : 0;
+    int cr = total ? lane / ncols : 0, cc = total ? lane % ncols : 0;
+    float2 gn = make_float2(0.0f, 0.0f);
+    if (lane < total) gn = pt[dx0 + cc + (ptrdiff_t)(dy0 + cr) * w];
+    for (int t0 = 0; t0 < total; t0 += 64) {
+      const int t = t0 + lane;
+      const float2 g = gn;
+      const int dyi = dy0 + cr, dxi = dx0 + cc;
+      cr += step_r;
+      cc += step_c;
+      if (cc >= ncols) {
+        cc -= ncols;
+        ++cr;
+      }
+      if (t + 64 < total) gn = pt[dx0 + cc + (ptrdiff_t)(dy0 + cr) * w];
+      float wv[8];
+      int bin[8];  // -1: the corner is outside the 4 x 4 grid
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        wv[c] = 0.0f;
+        bin[c] = -1;
+      }
+      bool reach = false;
+      if (t < total) {
+        const float mod = g.x, angle = g.y;
+        const float theta = mod_2pi_f((float)(angle - angle0));
+        const float dx = (float)(xi + dxi - x);
+        const float dy = (float)(yi + dyi - y);
+        const float nx = (float)((ct0 * dx + st0 * dy) / SBP);
+        const float ny = (float)((-st0 * dx + ct0 * dy) / SBP);
+        const float nt = (float)(NBO * theta / (2 * kPi));
+        const float wsigma = 2.0f;
+        const float win = (float)fast_expn(s_expn, (nx * nx + ny * ny) / (2.0 * wsigma * wsigma));
+        const int binx = (int)floorf((float)(nx - 0.5));
+        const int biny = (int)floorf((float)(ny - 0.5));
+        const int bint = (int)floorf(nt);
+        const float wm = win * mod;
+        const float rx = (float)(nx - (binx + 0.5));
+        const float ry = (float)(ny - (biny + 0.5));
+        const float rt = nt - bint;
+#pragma unroll
+        for (int dbinx = 0; dbinx < 2; ++dbinx)
+#pragma unroll
+          for (int dbiny = 0; dbiny < 2; ++dbiny)
+#pragma unroll
+            for (int dbint = 0; dbint < 2; ++dbint) {
+              const int c = dbinx * 4 + dbiny * 2 + dbint;
+              const bool in = binx + dbinx >= -(NBP / 2) && binx + dbinx < (NBP / 2) &&
+                              biny + dbiny >= -(NBP / 2) && biny + dbiny < (NBP / 2);
+              wv[c] = wm * fabsf(1 - dbinx - rx) * fabsf(1 - dbiny - ry) * fabsf(1 - dbint - rt);
+              bin[c] = in ? ((bint + dbint) % NBO) + (biny + dbiny + NBP / 2) * NBO * NBP +
+                                (binx + dbinx + NBP / 2) * NBO
+                          : -1;
+              reach |= in;
+            }
+      }
+      // the reaching samples as columns 0 .. k-1 in sample order
+      const uint64_t rm = __ballot(reach);
+      const int kk = __popcll(rm);
+      const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(rm >> 32),
+                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)rm, 0));
+      for (int c0 = 0; c0 < kk; c0 += 32) {
+        const bool mine = reach && rank >= c0 && rank < c0 + 32;
+        const int colp = rank - c0;
+        int pos[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          pos[c] = (mine && bin[c] >= 0) ? bin[c] * kDescRow + colp : kDummy + (lane & 31);
+          s_v[pos[c]] = wv[c];
         }
-        continue;
-      }
-      if (lane == 0) stale[fi] = 0;
-      const double st0 = sin(angle0), ct0 = cos(angle0);
-      const double SBP = 3.0 * sigma + kEpsD;
-      const int W = (int)floor(sqrt(2.0) * SBP * (NBP + 1) / 2.0 + 0.5);
-      const int dy0 = max(-W, 1 - yi), dy1 = min(W, h - yi - 2);
-      const int dx0 = max(-W, 1 - xi), dx1 = min(W, w - xi - 2);
-      const int ncols = dx1 - dx0 + 1, nrows = dy1 - dy0 + 1;
-      const int total = (ncols > 0 && nrows > 0) ? ncols * nrows : 0;
-      const float2* pt = grad + so * (size_t)(si - kSMin - 1) + (size_t)yi * w + xi;
-      float a0 = 0.0f, a1 = 0.0f;
-      for (int t0 = 0; t0 < total; t0 += 64) {
-        const int t = t0 + lane;
-        if (t < total) {
-          const int dyi = dy0 + t / ncols, dxi = dx0 + t % ncols;
-          const float2 g = pt[dxi + (ptrdiff_t)dyi * w];
-          const float mod = g.x, angle = g.y;
-          const float theta = mod_2pi_f((float)(angle - angle0));
-          const float dx = (float)(xi + dxi - x);
-          const float dy = (float)(yi + dyi - y);
-          const float nx = (float)((ct0 * dx + st0 * dy) / SBP);
-          const float ny = (float)((-st0 * dx + ct0 * dy) / SBP);
-          const float nt = (float)(NBO * theta / (2 * kPi));
-          const float wsigma = 2.0f;
-          const float win = (float)fast_expn(expn, (nx * nx + ny * ny) / (2.0 * wsigma * wsigma));
-          const int binx = (int)floorf((float)(nx - 0.5));
-          const int biny = (int)floorf((float)(ny - 0.5));
-          const int bint = (int)floorf(nt);
-          s_wm[lane] = win * mod;
-          s_rx[lane] = (float)(nx - (binx + 0.5));
-          s_ry[lane] = (float)(ny - (biny + 0.5));
-          s_rt[lane] = nt - bint;
-          // corners binx + {0, 1} etc. (binx + 3 >= 0 for every sample that
-          // reaches bin -2); mark the sample in each reachable bin's mask
-          s_b[lane] = (binx + 3) | ((biny + 3) << 8) | (bint << 16);
-          for (int dbinx = 0; dbinx < 2; ++dbinx)
-            for (int dbiny = 0; dbiny < 2; ++dbiny)
-              for (int dbint = 0; dbint < 2; ++dbint)
-                if (binx + dbinx >= -(NBP / 2) && binx + dbinx < (NBP / 2) &&
-                    biny + dbiny >= -(NBP / 2) && biny + dbiny < (NBP / 2))
-                  atomicOr(&s_mask[((bint + dbint) % NBO) + (biny + dbiny + NBP / 2) * NBO * NBP +
-                                   (binx + dbinx + NBP / 2) * NBO],
-                           1ull << lane);
+        __syncthreads();
+        const int ng = min(kk - c0, 32);  // columns of this pass
+        for (int q = 0; q < ng; q += 8) {
+          float2 u[4], v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            u[e] = r0[q / 2 + e];
+            v[e] = r1[q / 2 + e];
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            a0 += u[e].x;
+            a1 += v[e].x;
+            a0 += u[e].y;
+            a1 += v[e].y;
+          }
         }
         __syncthreads();
 #pragma unroll
-        for (int q = 0; q < 2; ++q) {
-          uint64_t m = s_mask[lane + 64 * q];
-          const int byq = q ? by1 : by0;
-          float a = q ? a1 : a0;
-          while (m) {  // this bin's samples of the chunk, in sample order
-            const int j = __builtin_ctzll(m);
-            m &= m - 1;
-            const int sb = s_b[j];
-            const int dbx = bx0 + 1 - (sb & 0xFF), dby = byq + 1 - ((sb >> 8) & 0xFF);
-            const int dbt = (bt0 - (sb >> 16)) & 7;
-            a += s_wm[j] * fabsf(1 - dbx - s_rx[j]) * fabsf(1 - dby - s_ry[j]) *
-                 fabsf(1 - dbt - s_rt[j]);
-          }
-          if (q) a1 = a;
-          else a0 = a;
-        }
-        __syncthreads();
-        s_mask[lane] = 0;
-        s_mask[lane + 64] = 0;
+        for (int c = 0; c < 8; ++c) s_v[pos[c]] = 0.0f;
       }
-      descriptor_finish(a0, a1, sh, descf + (size_t)fi * 128, desc + (size_t)fi * 128);
     }
+    descriptor_finish(a0, a1, sh, descf + (size_t)fi * 128, desc + (size_t)fi * 128);
   }
 }
 

@@ -549,9 +549,6 @@ __device__ __forceinline__ int score_h_chunk(const HFilt& f, const double* mk, c
     um[2 * q + 1] = u1;
     any |= u0 | u1;
   }
-#ifdef SCM_DIAG_SCORE_NOSLOW
-  any = 0;  // diagnostics only: undecided points counted as outliers
-#endif
   if (nsure) *nsure = cnt;
   if (any) {  // rare: exact test of the undecided points only (queued when dq)
     ++*nslow;
@@ -744,9 +741,6 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
     um[2 * q + 1] = u1;
     any |= u0 | u1;
   }
-#ifdef SCM_DIAG_SCORE_NOSLOW
-  any = 0;  // diagnostics only: undecided points counted as outliers
-#endif
   if (UND) {
     int u = 0;
 #pragma unroll
