@@ -265,7 +265,7 @@ def extraction_bench(ctx, frames: int, height: int, width: int, check: bool, cpu
            "ms_per_frame": round(dt / frames * 1e3, 3),
            "features_per_frame": round(sum(len(decode_keypoints(o[0])) for o in out) / frames, 1),
            "inputs": "host frame buffers (PCIe inside the timed region)",
-           "dominant_kernel": "descriptor_kernel (profiles/r02_sift_kernel_stats.csv)"}
+           "dominant_kernel": "descriptor_kernel (profiles/r03_sift_kernel_stats.csv)"}
     if check or cpu:
         from oracle import oracle
     if check:

@@ -3,8 +3,9 @@
 // integration/op_cpp/extraction_op.cc:70-121) behind scm_extract_frames.
 //
 // Per frame: upload (pinned staging), grey + 2x upsampling, the six Gaussian
-// levels of each of the 4 octaves, detection / refinement, orientations and
-// descriptors (sift_kernels.hip), then the counts and the features come back
+// levels of each of the 4 octaves, detection / refinement and gradients per
+// octave, then orientations and descriptors of every octave's keypoints in one
+// launch each (sift_kernels.hip), then the counts and the features come back
 // and the host writes the three io.cc elements: COLMAP's DoG-level selection
 // of max_num_features (ExtractSiftFeaturesCPU keeps the coarsest levels whose
 // keypoint count first exceeds it), FeatureKeypoint(x, y, scale, orientation)
@@ -181,10 +182,11 @@ int bilinear_table(int dst, int src, std::vector<int32_t>* hdr, std::vector<doub
 }
 
 // Workspace of a slot for a frame whose first octave has nel pixels (2w x 2h).
-// Capacities: candidates of one octave, its refined keypoints and their
-// features (<= 2 orientations each), times the slot's cap_scale, which grows
-// whenever a frame overflows them (the frame is then extracted again: the
-// reference has no capacity limit, extraction_op.cc:71-120).
+// Capacities: candidates of one octave, the frame's refined keypoints (every
+// octave's) and their features (<= 2 orientations each), times the slot's
+// cap_scale, which grows whenever a frame overflows them (the frame is then
+// extracted again: the reference has no capacity limit,
+// extraction_op.cc:71-120).
 int ensure_slot(const SiftState* s, Slot& sl, int w, int h) {
   const int64_t ow = 2 * (int64_t)w, oh = 2 * (int64_t)h, nel = ow * oh;
   if (nel <= sl.nel_cap && sl.dev.cnt) return SCM_OK;
@@ -194,9 +196,14 @@ int ensure_slot(const SiftState* s, Slot& sl, int w, int h) {
   const int64_t f0 = s->caps[2] ? s->caps[2] : 2 * k0;
   // every octave pixel of the 3 detection levels is at most one candidate
   const int cand_cap = (int)std::min<int64_t>(c0 * sc, 3 * nel + 64);
-  const int key_cap = (int)std::min<int64_t>(k0 * sc, cand_cap);
+  // every octave's keypoints: at most 3 per pixel of each octave (<= 4 nel in all)
+  const int key_cap = (int)std::min<int64_t>(k0 * sc, 4 * nel + 64);
   const int feat_cap = (int)std::min<int64_t>(f0 * sc, 4 * (int64_t)key_cap);
-  const size_t bytes = 18 * (size_t)nel * 4 + 2 * (3 * (size_t)oh + 1) * 4 +
+  // every octave's gradient planes stay until the frame's describe launches
+  // (octave sizes nel, nel / 4, <= nel / 16, <= nel / 64)
+  const size_t ngrad = 3 * ((size_t)nel + nel / 4 + nel / 16 + nel / 64 + 64);
+  const size_t bytes = 12 * (size_t)nel * 4 + ngrad * 8 + 4 * 256 +
+                       2 * (3 * (size_t)oh + 1) * 4 +
                        (size_t)cand_cap * (16 + 32 + 8) +
                        (size_t)key_cap * (32 + 4 + 16 + 4) +
                        (size_t)feat_cap * (16 + 512 + 128 + 4) + 64 * 256;
@@ -207,7 +214,7 @@ int ensure_slot(const SiftState* s, Slot& sl, int w, int h) {
   d.levels = carve<float>(p, kSiftLevels * (size_t)nel);
   d.temp = carve<float>(p, (size_t)nel);
   d.dog = carve<float>(p, kSiftDogLevels * (size_t)nel);
-  d.grad = carve<float2>(p, 3 * (size_t)nel);
+  d.grad = carve<float2>(p, ngrad);
   d.rowcnt = carve<int32_t>(p, 3 * (size_t)oh + 1);
   d.rowoff = carve<int32_t>(p, 3 * (size_t)oh + 1);
   d.cand = carve<SiftCand>(p, cand_cap);
@@ -324,6 +331,8 @@ int enqueue_frame(SiftState* s, Slot& sl, const scm_frame& f) {
     ch = 1;
   }
   SiftDev& d = sl.dev;
+  SiftOctaves oct{};
+  float2* grad = d.grad;
   int ow = 2 * w, oh = 2 * h, pw = 0, ph = 0;  // this octave's and the previous octave's size
   // A frame of any size >= 1 x 1 runs, as VLFeat's filter does: octaves too
   // small for an interior pixel detect nothing, and an octave with no pixel
@@ -339,8 +348,8 @@ int enqueue_frame(SiftState* s, Slot& sl, const scm_frame& f) {
     }
     const size_t so = (size_t)ow * oh;
     if (o == -1) {
-      SCM_HIP(sift_upsample(src, w, h, ch, d.levels, st));
-      SCM_HIP(sift_smooth(d.levels, d.levels, d.temp, ow, oh, s->c, 0, s->widths[0], st));
+      SCM_HIP(sift_upsample(src, w, h, ch, d.temp, st));
+      SCM_HIP(sift_smooth(d.temp, d.levels, d.dog, nullptr, ow, oh, s->c, 0, s->widths[0], st));
     } else {
       // copy_and_downsample of level s_best = 2 (index 3) of the previous
       // octave: every other pixel; no extra smoothing (sa == sb).  The source
@@ -348,11 +357,17 @@ int enqueue_frame(SiftState* s, Slot& sl, const scm_frame& f) {
       SCM_HIP(sift_downsample(d.levels + 3 * (size_t)pw * ph, pw, d.levels, ow, oh, st));
     }
     for (int l = 1; l < kSiftLevels; ++l)
-      SCM_HIP(sift_smooth(d.levels + (l - 1) * so, d.levels + l * so, d.temp, ow, oh, s->c, l,
-                          s->widths[l], st));
+      SCM_HIP(sift_smooth(d.levels + (l - 1) * so, d.levels + l * so, d.temp,
+                          d.dog + (l - 1) * so, ow, oh, s->c, l, s->widths[l], st));
     SCM_HIP(sift_octave_detect(d, s->c, ow, oh, o, kPeakThreshold, kEdgeThreshold, st));
-    SCM_HIP(sift_octave_describe(d, s->c, ow, oh, o, st));
+    SCM_HIP(sift_octave_gradient(d, grad, ow, oh, st));
+    oct.grad[o + 1] = grad;
+    oct.w[o + 1] = ow;
+    oct.h[o + 1] = oh;
+    grad += 3 * so;
   }
+  // orientations and descriptors of every octave's keypoints at once
+  SCM_HIP(sift_describe(d, s->c, oct, st));
   SCM_HIP(sift_fixup(d, st));
   SCM_TRY(sl.pin_cnt.ensure(sizeof(SiftCounts)));
   SCM_HIP(hipMemcpyAsync(sl.pin_cnt.ptr, d.cnt, sizeof(SiftCounts), hipMemcpyDeviceToHost, st));

@@ -10,18 +10,21 @@
 // so the keypoints and descriptors are the oracle's bit for bit:
 //   * Gaussian smoothing: vl_imconvcol_vf's sum over the window in ascending
 //     source order (multiply, then add, float), vertical pass first, edge
-//     samples repeated (VL_PAD_BY_CONTINUITY); one output per thread, the
-//     window staged in LDS (HBM-bound: one read and one write per pass);
+//     samples repeated (VL_PAD_BY_CONTINUITY); both passes and the DoG
+//     difference in one kernel per level (smooth_vh_kernel: the input window
+//     and the intermediate tile in LDS, register-blocked runs of outputs);
 //   * detection in VLFeat's scan order (s, y, x) by per-row counts, one
 //     exclusive scan and an ordered write (ballot prefix within each wave);
 //   * refinement one thread per candidate; orientation histograms and
-//     descriptors one wave per keypoint: the window's samples are prepared 64
-//     at a time (one per lane) and each histogram bin is owned by one lane,
-//     which adds the chunk's contributions in VLFeat's sample order -- the
-//     reference's serial float / double sums, bit for bit, with 64-way
-//     parallelism per keypoint.
+//     descriptors one wave per keypoint (and orientation), over every
+//     octave's keypoints in one launch each: the window's samples are
+//     prepared 64 at a time (one per lane), written into a zero-filled
+//     bin-major LDS table, and each histogram bin is owned by one lane, which
+//     adds its row in VLFeat's sample order -- the reference's serial float /
+//     double sums, bit for bit, with 64-way parallelism per keypoint.
 // Layout: one image slot holds the first octave's six levels (the largest),
-// later octaves reuse the same buffers at their smaller size.
+// later octaves reuse the same buffers at their smaller size; the gradient
+// planes of every octave stay until the frame's describe launches.
 #include "sift_kernels.h"
 
 namespace scm {
@@ -157,17 +160,114 @@ __global__ __launch_bounds__(256) void smooth_h_kernel(const float* __restrict__
   }
 }
 
+// The same two passes fused for the widths the filter uses (W = 5, 7, 8, 10,
+// 13): one workgroup per 64 x 64 output tile stages the (64 + 2W)^2 input
+// window (edges clamped) in LDS, runs the vertical pass over the window's
+// 64 + 2W columns (kSmoothVR rows per thread), then -- in the same LDS, once
+// the window is consumed -- the horizontal pass (kSmoothR outputs per
+// thread), and writes the level plus, when dog is given, the DoG level
+// out - in (the difference dog_kernel took; the centre inputs are kept in
+// registers).  Each thread's outputs come from a run of samples in
+// registers, taps in scalar registers: every output is the same
+// multiply-then-add sequence in ascending source order as the two-kernel
+// path, and the intermediate level never goes to HBM.  in and out must differ
+// (the window is read while other tiles write).  The horizontal pass reads
+// lane = row (odd pitch: no bank conflicts); results leave through LDS for
+// coalesced stores.
+constexpr int kSmoothR = 16, kSmoothVR = 32;
+
+template <int W>
+__global__ __launch_bounds__(256) void smooth_vh_kernel(const float* __restrict__ in,
+                                                        float* __restrict__ out,
+                                                        float* __restrict__ dog, int w, int h,
+                                                        const float* __restrict__ taps) {
+  constexpr int N = 2 * W + 1, R = kSmoothR, VR = kSmoothVR, C = 64 + 2 * W;  // window side
+  constexpr int PM = C | 1;  // pitch of the intermediate and output tiles (odd)
+  static_assert(64 * PM <= C * C, "the intermediate tile reuses the window's LDS");
+  __shared__ float lds[C * C];
+  const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 64;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < C * C; i += 256) {
+    const int r = i / C, c = i - r * C;
+    const int yy = min(max(y0 - W + r, 0), h - 1), xx = min(max(x0 - W + c, 0), w - 1);
+    lds[i] = in[(size_t)yy * w + xx];
+  }
+  float g[N];
+#pragma unroll
+  for (int k = 0; k < N; ++k) g[k] = taps[k];
+  __syncthreads();
+  float ctr[16];  // the inputs at this thread's 16 output pixels (tile element tid + 256 m)
+  if (dog) {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int i = tid + 256 * m;
+      ctr[m] = lds[((i >> 6) + W) * C + (i & 63) + W];
+    }
+  }
+  // vertical pass: column c, rows yl0 .. yl0 + VR - 1 of the tile
+  const bool vt = tid < C * (64 / VR);
+  const int c = tid % C, yl0 = (tid / C) * VR;
+  float vacc[VR];
+  if (vt) {
+    float v[VR + 2 * W];
+#pragma unroll
+    for (int j = 0; j < VR + 2 * W; ++j) v[j] = lds[(yl0 + j) * C + c];
+#pragma unroll
+    for (int r = 0; r < VR; ++r) vacc[r] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+#pragma unroll
+      for (int r = 0; r < VR; ++r) vacc[r] += v[r + k] * g[2 * W - k];
+  }
+  __syncthreads();
+  if (vt) {
+#pragma unroll
+    for (int r = 0; r < VR; ++r) lds[(yl0 + r) * PM + c] = vacc[r];
+  }
+  __syncthreads();
+  // horizontal pass: row, outputs xs .. xs + R - 1
+  const int row = tid & 63, xs = (tid >> 6) * R;
+  float acc[R];
+  {
+    float v[R + 2 * W];
+#pragma unroll
+    for (int j = 0; j < R + 2 * W; ++j) v[j] = lds[row * PM + xs + j];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < N; ++k)
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] += v[r + k] * g[2 * W - k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < R; ++r) lds[row * PM + xs + r] = acc[r];
+  __syncthreads();
+  const int nr = min(64, h - y0), nc = min(64, w - x0);
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int i = tid + 256 * m, r = i >> 6, cc = i & 63;
+    if (r < nr && cc < nc) {
+      const float o = lds[r * PM + cc];
+      const size_t at = (size_t)(y0 + r) * w + x0 + cc;
+      out[at] = o;
+      if (dog) dog[at] = o - ctr[m];
+    }
+  }
+}
+
+// DoG level of the two-kernel path: dog = a - b.
+__global__ void sub_kernel(const float* __restrict__ a, const float* __restrict__ b,
+                           float* __restrict__ dog, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    dog[i] = a[i] - b[i];
+}
+
 __global__ void downsample_kernel(const float* __restrict__ in, int w_in, float* __restrict__ out,
                                   int w, int h) {
   const int x = blockIdx.x * blockDim.x + threadIdx.x, y = blockIdx.y;
   if (x < w) out[(size_t)y * w + x] = in[(size_t)(2 * y) * w_in + 2 * x];
-}
-
-__global__ void dog_kernel(const float* __restrict__ lev, float* __restrict__ dog, size_t so) {
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < so;
-       i += (size_t)gridDim.x * blockDim.x)
-#pragma unroll
-    for (int l = 0; l < kSiftDogLevels; ++l) dog[l * so + i] = lev[(l + 1) * so + i] - lev[l * so + i];
 }
 
 // vl_sift_detect's 26-neighbour strict extremum test at DoG level s.
@@ -459,12 +559,12 @@ __global__ void gradient_kernel(const float* __restrict__ lev, float2* __restric
 // of a ballot in bin order (VLFeat keeps up to 4, COLMAP uses 2).
 constexpr int kOriRow = 66;  // doubles per bin row (64 samples + pad)
 
-__global__ __launch_bounds__(64) void orient_kernel(const float2* __restrict__ grad, int w, int h,
+__global__ __launch_bounds__(64) void orient_kernel(SiftOctaves oct,
                                                     const SiftKey* __restrict__ keys,
                                                     SiftCounts* __restrict__ cnt,
                                                     int32_t* __restrict__ nori,
                                                     double* __restrict__ ang,
-                                                    const double* __restrict__ expn, int octave) {
+                                                    const double* __restrict__ expn) {
   constexpr int nbins = 36;
   __shared__ __attribute__((aligned(16))) double s_v[nbins * kOriRow];
   __shared__ double s_expn[257];
@@ -474,11 +574,13 @@ __global__ __launch_bounds__(64) void orient_kernel(const float2* __restrict__ g
   for (int b = lane; b < 257; b += 64) s_expn[b] = expn[b];
   __syncthreads();
   const int n = cnt->nkey;
-  const double xper = ldexp(1.0, octave);
-  const size_t so = (size_t)w * h;
   const double2* row = reinterpret_cast<const double2*>(s_v + min(lane, nbins - 1) * kOriRow);
   for (int i = blockIdx.x; i < n; i += gridDim.x) {
     const SiftKey k = keys[i];
+    const int octave = k.o, w = oct.w[octave + 1], h = oct.h[octave + 1];
+    const float2* __restrict__ grad = oct.grad[octave + 1];
+    const double xper = ldexp(1.0, octave);
+    const size_t so = (size_t)w * h;
     const double x = k.x / xper, y = k.y / xper, sigma = k.sigma / xper;
     const int xi = (int)(x + 0.5), yi = (int)(y + 0.5), si = k.is;
     const double sigmaw = 1.5 * sigma;
@@ -634,11 +736,11 @@ __device__ void descriptor_finish(float a0, float a1, float* __restrict__ sh, fl
 constexpr int kDescRow = 34;
 
 __global__ __launch_bounds__(64) void descriptor_kernel(
-    const float2* __restrict__ grad, int w, int h, const SiftKey* __restrict__ keys,
-    SiftCounts* __restrict__ cnt, const int32_t* __restrict__ nori, const double* __restrict__ ang,
+    SiftOctaves oct, const SiftKey* __restrict__ keys, SiftCounts* __restrict__ cnt,
+    const int32_t* __restrict__ nori, const double* __restrict__ ang,
     const int32_t* __restrict__ koff, SiftFeat* __restrict__ feat, float* __restrict__ descf,
     uint8_t* __restrict__ desc, int32_t* __restrict__ stale, const double* __restrict__ expn,
-    int feat_cap, int octave) {
+    int feat_cap) {
   constexpr int NBP = 4, NBO = 8;
   constexpr int kDummy = 128 * kDescRow;  // 32 dummy floats, then the finish's 129
   __shared__ __attribute__((aligned(16))) float s_v[128 * kDescRow + 32 + 129];
@@ -649,8 +751,6 @@ __global__ __launch_bounds__(64) void descriptor_kernel(
   for (int b = lane; b < 257; b += 64) s_expn[b] = expn[b];
   __syncthreads();
   const int n = cnt->nkey;
-  const double xper = ldexp(1.0, octave);
-  const size_t so = (size_t)w * h;
   const float2* r0 = reinterpret_cast<const float2*>(s_v + lane * kDescRow);
   const float2* r1 = reinterpret_cast<const float2*>(s_v + (lane + 64) * kDescRow);
   for (int it = blockIdx.x; it < 2 * n; it += gridDim.x) {
@@ -664,6 +764,10 @@ __global__ __launch_bounds__(64) void descriptor_kernel(
     }
     const double angle0 = ang[2 * i + o];
     if (lane == 0) feat[fi] = SiftFeat{k.x + 0.5f, k.y + 0.5f, k.sigma, (float)angle0};
+    const int w = oct.w[k.o + 1], h = oct.h[k.o + 1];
+    const float2* __restrict__ grad = oct.grad[k.o + 1];
+    const double xper = ldexp(1.0, k.o);
+    const size_t so = (size_t)w * h;
     const double x = k.x / xper, y = k.y / xper, sigma = k.sigma / xper;
     const int xi = (int)(x + 0.5), yi = (int)(y + 0.5), si = k.is;
     if (xi < 0 || xi >= w || yi < 0 || yi >= h - 1 || si < kSMin + 1 || si > kSMax - 2) {
@@ -681,69 +785,107 @@ __global__ __launch_bounds__(64) void descriptor_kernel(
     const int W = (int)floor(sqrt(2.0) * SBP * (NBP + 1) / 2.0 + 0.5);
     const int dy0 = max(-W, 1 - yi), dy1 = min(W, h - yi - 2);
     const int dx0 = max(-W, 1 - xi), dx1 = min(W, w - xi - 2);
-    const int ncols = dx1 - dx0 + 1, nrows = dy1 - dy0 + 1;
-    const int total = (ncols > 0 && nrows > 0) ? ncols * nrows : 0;
+    const int ncols = dx1 - dx0 + 1, nrows = max(dy1 - dy0 + 1, 0);
     const float2* pt = grad + so * (size_t)(si - kSMin - 1) + (size_t)yi * w + xi;
     float a0 = 0.0f, a1 = 0.0f;
-    // the lane's sample t = t0 + lane as (row, column) of the rectangle,
-    // stepped by 64 per chunk; the next chunk's gradient is loaded while this
-    // chunk is summed
-    const int step_r = total ? 64 / ncols : 0, step_c = total ? 64 % ncols : 0;
-    int cr = total ? lane / ncols : 0, cc = total ? lane % ncols : 0;
-    float2 gn = make_float2(0.0f, 0.0f);
-    if (lane < total) gn = pt[dx0 + cc + (ptrdiff_t)(dy0 + cr) * w];
-    for (int t0 = 0; t0 < total; t0 += 64) {
-      const int t = t0 + lane;
-      const float2 g = gn;
-      const int dyi = dy0 + cr, dxi = dx0 + cc;
-      cr += step_r;
-      cc += step_c;
-      if (cc >= ncols) {
-        cc -= ncols;
-        ++cr;
-      }
-      if (t + 64 < total) gn = pt[dx0 + cc + (ptrdiff_t)(dy0 + cr) * w];
-      float wv[8];
-      int bin[8];  // -1: the corner is outside the 4 x 4 grid
+    // Only samples that can reach the 4 x 4 grid are visited: per row of the
+    // rectangle, the dxi interval where |nx| and |ny| <= 2.5 (binx =
+    // floor(nx - 0.5) in -3 .. 1, likewise biny), widened by a pixel on each
+    // side and clipped to the rectangle.  Every skipped sample reaches no bin
+    // and the visited ones keep VLFeat's (dyi, dxi) order.  Row r's
+    // (first dxi - dx0) << 16 | length sits in rtab (the finish's scratch).
+    int* rtab = reinterpret_cast<int*>(sh);
+    const bool rag = nrows <= 129;
+    int total = 0;
+    if (ncols > 0 && nrows > 0) {
+      if (rag) {
+        const double B = 2.5 * SBP * (1.0 + 1e-6) + 1e-3;
+        for (int rr = lane; rr < nrows; rr += 64) {
+          const double dy = (double)(yi + dy0 + rr) - y;
+          double lo = -1e6, hi = 1e6;  // dx = xi + dxi - x
+          // |ct0 dx + st0 dy| <= B and |-st0 dx + ct0 dy| <= B
+          const double ca[2] = {ct0, -st0}, cb[2] = {st0 * dy, ct0 * dy};
 #pragma unroll
-      for (int c = 0; c < 8; ++c) {
-        wv[c] = 0.0f;
-        bin[c] = -1;
-      }
-      bool reach = false;
-      if (t < total) {
-        const float mod = g.x, angle = g.y;
-        const float theta = mod_2pi_f((float)(angle - angle0));
-        const float dx = (float)(xi + dxi - x);
-        const float dy = (float)(yi + dyi - y);
-        const float nx = (float)((ct0 * dx + st0 * dy) / SBP);
-        const float ny = (float)((-st0 * dx + ct0 * dy) / SBP);
-        const float nt = (float)(NBO * theta / (2 * kPi));
-        const float wsigma = 2.0f;
-        const float win = (float)fast_expn(s_expn, (nx * nx + ny * ny) / (2.0 * wsigma * wsigma));
-        const int binx = (int)floorf((float)(nx - 0.5));
-        const int biny = (int)floorf((float)(ny - 0.5));
-        const int bint = (int)floorf(nt);
-        const float wm = win * mod;
-        const float rx = (float)(nx - (binx + 0.5));
-        const float ry = (float)(ny - (biny + 0.5));
-        const float rt = nt - bint;
-#pragma unroll
-        for (int dbinx = 0; dbinx < 2; ++dbinx)
-#pragma unroll
-          for (int dbiny = 0; dbiny < 2; ++dbiny)
-#pragma unroll
-            for (int dbint = 0; dbint < 2; ++dbint) {
-              const int c = dbinx * 4 + dbiny * 2 + dbint;
-              const bool in = binx + dbinx >= -(NBP / 2) && binx + dbinx < (NBP / 2) &&
-                              biny + dbiny >= -(NBP / 2) && biny + dbiny < (NBP / 2);
-              wv[c] = wm * fabsf(1 - dbinx - rx) * fabsf(1 - dbiny - ry) * fabsf(1 - dbint - rt);
-              bin[c] = in ? ((bint + dbint) % NBO) + (biny + dbiny + NBP / 2) * NBO * NBP +
-                                (binx + dbinx + NBP / 2) * NBO
-                          : -1;
-              reach |= in;
+          for (int e = 0; e < 2; ++e) {
+            if (fabs(ca[e]) < 1e-9) {
+              if (fabs(cb[e]) > B) hi = -1e6;
+            } else {
+              const double u = (-B - cb[e]) / ca[e], v = (B - cb[e]) / ca[e];
+              lo = fmax(lo, fmin(u, v));
+              hi = fmin(hi, fmax(u, v));
             }
+          }
+          int l = dx0, len = 0;
+          if (lo <= hi) {
+            l = max(dx0, (int)floor(lo + x - xi) - 1);
+            len = max(0, min(dx1, (int)ceil(hi + x - xi) + 1) - l + 1);
+          }
+          rtab[rr] = ((l - dx0) << 16) | len;
+          total += len;
+        }
+#pragma unroll
+        for (int m = 32; m > 0; m >>= 1) total += __shfl_xor(total, m);
+      } else {
+        total = ncols * nrows;
       }
+    }
+    __syncthreads();
+    auto row_len = [&](int r) { return rag ? (rtab[r] & 0xFFFF) : ncols; };
+    auto row_lo = [&](int r) { return rag ? dx0 + (rtab[r] >> 16) : dx0; };
+    // the lane's sample t = t0 + lane as (row, column), stepped by 64 per
+    // chunk; the next chunk's gradient is loaded while this chunk is summed
+    int r = 0, c = lane;
+    auto advance = [&]() {
+      while (r < nrows && c >= row_len(r)) {
+        c -= row_len(r);
+        ++r;
+      }
+    };
+    if (total > 0) advance();
+    float2 gn = make_float2(0.0f, 0.0f);
+    if (total > 0 && r < nrows) gn = pt[row_lo(r) + c + (ptrdiff_t)(dy0 + r) * w];
+    for (int t0 = 0; t0 < total; t0 += 64) {
+      const bool valid = r < nrows;
+      const int dyi = dy0 + r, dxi = valid ? row_lo(r) + c : dx0;
+      const float2 g = gn;
+      c += 64;
+      advance();
+      gn = r < nrows ? pt[row_lo(r) + c + (ptrdiff_t)(dy0 + r) * w] : make_float2(0.0f, 0.0f);
+      // every lane prepares its sample (lanes past the rectangle's end see a
+      // zero gradient and reach nothing)
+      float wv[8];
+      int row[8];  // LDS row offset of the corner's bin, -1 outside the 4 x 4 grid
+      const float mod = g.x, angle = g.y;
+      const float theta = mod_2pi_f((float)(angle - angle0));
+      const float dx = (float)(xi + dxi - x);
+      const float dy = (float)(yi + dyi - y);
+      const float nx = (float)((ct0 * dx + st0 * dy) / SBP);
+      const float ny = (float)((-st0 * dx + ct0 * dy) / SBP);
+      const float nt = (float)(NBO * theta / (2 * kPi));
+      const float wsigma = 2.0f;
+      const float win = (float)fast_expn(s_expn, (nx * nx + ny * ny) / (2.0 * wsigma * wsigma));
+      const int binx = (int)floorf((float)(nx - 0.5));
+      const int biny = (int)floorf((float)(ny - 0.5));
+      const int bint = (int)floorf(nt);  // 0 .. 8: nt is in [0, 8]
+      const float wm = win * mod;
+      const float rx = (float)(nx - (binx + 0.5));
+      const float ry = (float)(ny - (biny + 0.5));
+      const float rt = nt - bint;
+      bool reach = false;
+#pragma unroll
+      for (int dbinx = 0; dbinx < 2; ++dbinx)
+#pragma unroll
+        for (int dbiny = 0; dbiny < 2; ++dbiny)
+#pragma unroll
+          for (int dbint = 0; dbint < 2; ++dbint) {
+            const int c = dbinx * 4 + dbiny * 2 + dbint;
+            const int bx = binx + dbinx + NBP / 2, by = biny + dbiny + NBP / 2;
+            const bool in = valid && (unsigned)bx < (unsigned)NBP && (unsigned)by < (unsigned)NBP;
+            wv[c] = wm * fabsf(1 - dbinx - rx) * fabsf(1 - dbiny - ry) * fabsf(1 - dbint - rt);
+            row[c] = in ? __mul24(((bint + dbint) & (NBO - 1)) + by * NBO * NBP + bx * NBO, kDescRow)
+                        : -1;
+            reach |= in;
+          }
       // the reaching samples as columns 0 .. k-1 in sample order
       const uint64_t rm = __ballot(reach);
       const int kk = __popcll(rm);
@@ -755,7 +897,7 @@ __global__ __launch_bounds__(64) void descriptor_kernel(
         int pos[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          pos[c] = (mine && bin[c] >= 0) ? bin[c] * kDescRow + colp : kDummy + (lane & 31);
+          pos[c] = (mine && row[c] >= 0) ? row[c] + colp : kDummy + (lane & 31);
           s_v[pos[c]] = wv[c];
         }
         __syncthreads();
@@ -842,12 +984,31 @@ hipError_t sift_rescale_cols(const uint8_t* src, int cols, int sh, uint8_t* dst,
   return hipGetLastError();
 }
 
-hipError_t sift_smooth(const float* in, float* out, float* tmp, int w, int h, const SiftConsts& c,
-                       int tap_set, int W, hipStream_t st) {
+hipError_t sift_smooth(const float* in, float* out, float* tmp, float* dog, int w, int h,
+                       const SiftConsts& c, int tap_set, int W, hipStream_t st) {
   const float* taps = c.taps + tap_set * kSiftMaxTaps;
+  const dim3 tiles(blocks_for(w, 64), blocks_for(h, 64));
+  switch (W) {
+#define SCM_SMOOTH_CASE(WW)                                                       \
+  case WW:                                                                        \
+    smooth_vh_kernel<WW><<<tiles, 256, 0, st>>>(in, out, dog, w, h, taps);        \
+    return hipGetLastError();
+    SCM_SMOOTH_CASE(5)
+    SCM_SMOOTH_CASE(7)
+    SCM_SMOOTH_CASE(8)
+    SCM_SMOOTH_CASE(10)
+    SCM_SMOOTH_CASE(13)
+#undef SCM_SMOOTH_CASE
+    default:
+      break;
+  }
   smooth_v_kernel<<<dim3(blocks_for(w, kVTile), blocks_for(h, kVTile)), 256, 0, st>>>(in, tmp, w, h,
                                                                                      taps, W);
   smooth_h_kernel<<<dim3(blocks_for(w, kHTile), h), 256, 0, st>>>(tmp, out, w, h, taps, W);
+  if (dog) {
+    const size_t n = (size_t)w * h;
+    sub_kernel<<<min(4096, blocks_for(n, 256)), 256, 0, st>>>(out, in, dog, n);
+  }
   return hipGetLastError();
 }
 
@@ -858,9 +1019,7 @@ hipError_t sift_downsample(const float* in, int w_in, float* out, int w, int h, 
 
 hipError_t sift_octave_detect(const SiftDev& d, const SiftConsts& c, int w, int h, int octave,
                               double tp, double te, hipStream_t st) {
-  (void)c;
-  const size_t so = (size_t)w * h;
-  dog_kernel<<<min(4096, blocks_for(so, 256)), 256, 0, st>>>(d.levels, d.dog, so);
+  (void)c;  // the DoG levels come from sift_smooth
   detect_count_kernel<<<dim3(h, 3), 256, 0, st>>>(d.dog, w, h, tp, d.rowcnt);
   // rowoff[3h] = total (the candidate count), written by the scan's total
   scan_kernel<<<1, 1024, 0, st>>>(d.rowcnt, d.rowoff, nullptr, 3 * h, 3 * h, d.rowoff + 3 * h,
@@ -870,22 +1029,27 @@ hipError_t sift_octave_detect(const SiftDev& d, const SiftConsts& c, int w, int 
   const double sigma0 = 1.6 * pow(2.0, 1.0 / kS);
   refine_kernel<<<kGrid, 64, 0, st>>>(d.dog, w, h, d.cand, d.cnt, d.ktmp, d.flag, tp, te, sigma0,
                                       octave);
-  scan_kernel<<<1, 1024, 0, st>>>(d.flag, d.foff, &d.cnt->ncand, 0, d.cand_cap, d.rowcnt, nullptr);
-  set_count_kernel<<<1, 1, 0, st>>>(d.cnt, d.rowcnt, 1, d.key_cap);
+  // positions in the frame's key list: after the earlier octaves' keypoints
+  scan_kernel<<<1, 1024, 0, st>>>(d.flag, d.foff, &d.cnt->ncand, 0, d.cand_cap, d.rowcnt,
+                                  &d.cnt->keys_run);
+  set_count_kernel<<<1, 1, 0, st>>>(d.cnt, &d.cnt->keys_run, 1, d.key_cap);
   compact_keys_kernel<<<kGrid, 64, 0, st>>>(d.ktmp, d.flag, d.foff, d.cnt, d.keys, d.key_cap,
                                             octave);
   return hipGetLastError();
 }
 
-hipError_t sift_octave_describe(const SiftDev& d, const SiftConsts& c, int w, int h, int octave,
-                                hipStream_t st) {
-  gradient_kernel<<<dim3(blocks_for(w, 256), h, 3), 256, 0, st>>>(d.levels, d.grad, w, h);
-  orient_kernel<<<4 * kGrid, 64, 0, st>>>(d.grad, w, h, d.keys, d.cnt, d.nori, d.ang, c.expn, octave);
+hipError_t sift_octave_gradient(const SiftDev& d, float2* grad, int w, int h, hipStream_t st) {
+  gradient_kernel<<<dim3(blocks_for(w, 256), h, 3), 256, 0, st>>>(d.levels, grad, w, h);
+  return hipGetLastError();
+}
+
+hipError_t sift_describe(const SiftDev& d, const SiftConsts& c, const SiftOctaves& oct,
+                         hipStream_t st) {
+  orient_kernel<<<4 * kGrid, 64, 0, st>>>(oct, d.keys, d.cnt, d.nori, d.ang, c.expn);
   scan_kernel<<<1, 1024, 0, st>>>(d.nori, d.koff, &d.cnt->nkey, 0, d.key_cap, nullptr,
                                   &d.cnt->nfeat);
-  descriptor_kernel<<<4 * kGrid, 64, 0, st>>>(d.grad, w, h, d.keys, d.cnt, d.nori, d.ang, d.koff,
-                                          d.feat, d.descf, d.desc, d.stale, c.expn, d.feat_cap,
-                                          octave);
+  descriptor_kernel<<<4 * kGrid, 64, 0, st>>>(oct, d.keys, d.cnt, d.nori, d.ang, d.koff, d.feat,
+                                              d.descf, d.desc, d.stale, c.expn, d.feat_cap);
   return hipGetLastError();
 }
 
