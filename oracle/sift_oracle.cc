@@ -46,6 +46,10 @@
 // orientation check), and COLMAP then re-normalises the descriptor buffer of
 // the previous keypoint (L1-root of an L1-rooted vector); the very first
 // buffer is uninitialised in the reference, zeros here.
+// Third-party algorithms restated (test oracle): VLFeat's SIFT (vl/sift.c,
+// vl/mathop.h; A. Vedaldi and B. Fulkerson, BSD licence) and FreeImage 3.17's
+// bilinear rescale (Resize.cpp; FreeImage Public License), as COLMAP 3.4 calls
+// them -- written from their published algorithms, no source copied.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>

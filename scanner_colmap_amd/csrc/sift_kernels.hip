@@ -25,6 +25,12 @@
 // Layout: one image slot holds the first octave's six levels (the largest),
 // later octaves reuse the same buffers at their smaller size; the gradient
 // planes of every octave stay until the frame's describe launches.
+// Third-party algorithms restated here (bit-exactness needs their constants
+// and operation order): VLFeat's SIFT (vl/sift.c, vl/mathop.h; A. Vedaldi and
+// B. Fulkerson, BSD licence) and FreeImage 3.17's bilinear rescale
+// (Source/FreeImageToolkit/Resize.cpp; FreeImage Public License), as COLMAP
+// 3.4 calls them.  The code is written from their published algorithms; no
+// source of theirs is copied.
 #include "sift_kernels.h"
 
 namespace scm {
