@@ -272,9 +272,9 @@ typedef struct scm_frame {
  * as VLFeat's filter does (octaves too small for an interior pixel detect
  * nothing); a frame that overflows the workspace's keypoint capacities grows
  * them and runs again (the reference has no capacity limit).  SCM_E_INVALID:
- * a null argument, an empty frame or a channel count other than 1, 3, 4.  The frames run on the
- * context's four streams, in stream order with its other calls; on any error
- * no output blob stays allocated. */
+ * a null argument, an empty frame or a channel count other than 1, 3, 4.
+ * The frames run on the context's four streams, in stream order with its
+ * other calls; on any error no output blob stays allocated. */
 int scm_extract_frames(scm_context* ctx, int64_t n, const uint64_t* image_ids,
                        const scm_frame* frames, scm_blob* keypoints_out,
                        scm_blob* descriptors_out, scm_blob* cameras_out);
