@@ -15,5 +15,6 @@ wait
 for spec in "$@"; do
   name=${spec%%:*}
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o probes/build/libscm_$name.so \
-    probes/build/match_$name.o $O/verify_kernels.o $O/scm_runtime.o $O/scm_codec.o
+    probes/build/match_$name.o $O/verify_kernels.o $O/sift_kernels.o $O/scm_runtime.o \
+    $O/scm_codec.o $O/scm_sift.o
 done

@@ -451,8 +451,12 @@ __device__ __forceinline__ uint32_t merge_second_values(uint32_t b1a, uint32_t b
 // (B2' << 3) | wave of B1.
 // ===========================================================================
 constexpr int kG8T = 4;                                        // tiles per barrier group
-constexpr int kG8Q = 4;                                        // groups in the LDS ring
+#ifndef SCM_G8_Q
+#define SCM_G8_Q 4
+#endif
+constexpr int kG8Q = SCM_G8_Q;                                 // groups in the LDS ring (DMA kG8Q - 1 ahead)
 constexpr int kG8Stages = kG8T * kG8Q;                         // 16 x 8 KiB of B tiles
+static_assert(kG8Q >= 3, "the ring holds the group in use, the next, and one in flight");
 constexpr int kG8CscGroups = 3;                                // column partials of 3 groups
 constexpr int kG8CbOff = kG8Stages * kTile8Bytes;              // column sums, 64 int32 per stage
 constexpr int kG8MetaOff = kG8CbOff + kG8Stages * kTile8Cols * 4;  // colpart index per tile
@@ -497,7 +501,7 @@ __device__ __forceinline__ void g8_wait_vm(int n) {
 // stage g mod kG8Stages), read one step ahead of their use.
 __device__ __forceinline__ void g8_next(const uint8_t* lds, int g, int r, int h, i32x4 (&bf)[4],
                                         uint32_t& cb0, uint32_t& cb1) {
-  const int stage = g & (kG8Stages - 1);
+  const int stage = g % kG8Stages;
   load_bfrag8(lds + stage * kTile8Bytes, r, h, bf);
   const int32_t* cbs = reinterpret_cast<const int32_t*>(lds + kG8CbOff + stage * kTile8Cols * 4);
   cb0 = (uint32_t)cbs[r];
@@ -641,7 +645,7 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
   auto dma_group = [&](int grp) {
 #pragma unroll 1
     for (int i = 0; i < kG8T; ++i) {
-      g8_stage(desc8 + fb * 128, csum + fb, ft, (grp * kG8T + i) & (kG8Stages - 1), wave, lane, lds);
+      g8_stage(desc8 + fb * 128, csum + fb, ft, (grp * kG8T + i) % kG8Stages, wave, lane, lds);
       if (++ft == fn) {
         if (fp + 1 < job.npairs) {
           ++fp;
@@ -679,7 +683,7 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
   i32x16 acc = chain8(afrag[0], bf0, ra[0]);
 
   for (int g = 0; g < G; ++g) {
-    const int stage = g & (kG8Stages - 1);
+    const int stage = g % kG8Stages;
     const uint8_t* cur = lds + stage * kTile8Bytes;
     const uint32_t cb0 = cbn0, cb1 = cbn1;  // read with the tile's c0 fragments
     if (tid == 0) meta[stage] = cpi + (int64_t)t * kTile8Cols;
@@ -715,9 +719,13 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
       // must be done: younger are group m + 2's DMA and the merge stores of
       // barriers m - 2 and m - 1 (wave w merges at barrier j when
       // ((j - 1) & 1) == w / 4); after a row flush (many stores) drain.
+      // (kG8Q - 3 groups of DMA younger than group m + 1's; the merges of
+      // the last kG8Q - 2 barriers.)
       const int half = wave >> 2;
-      const int st = (m >= 3 && (((m - 3) & 1) == half)) + (m >= 2 && (((m - 2) & 1) == half));
-      g8_wait_vm(g - flushed <= 2 * kG8T ? 0 : kG8T * gpt + st);
+      int st = 0;
+#pragma unroll
+      for (int j = 1; j <= kG8Q - 2; ++j) st += (m - j >= 1 && (((m - j - 1) & 1) == half));
+      g8_wait_vm(g - flushed <= 2 * kG8T ? 0 : (kG8Q - 3) * kG8T * gpt + st);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       dma_group(m + kG8Q - 1);
@@ -725,7 +733,7 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
         const int tg = (m - 1) * kG8T + (wave & (kG8T - 1));
         const uint32_t* src =
             csc + (((m - 1) % kG8CscGroups) * kG8T + (wave & (kG8T - 1))) * kMatch8Waves * kTile8Cols;
-        g8_merge(src + lane, colpart + meta[tg & (kG8Stages - 1)] + lane);
+        g8_merge(src + lane, colpart + meta[tg % kG8Stages] + lane);
       }
       g8_next(lds, g + 1, r, h, bf0, cbn0, cbn1);
     }
@@ -763,7 +771,7 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
   if (tg < G) {
     const uint32_t* src = csc + (((tg / kG8T) % kG8CscGroups) * kG8T + (tg & (kG8T - 1))) *
                                     kMatch8Waves * kTile8Cols;
-    g8_merge(src + lane, colpart + meta[tg & (kG8Stages - 1)] + lane);
+    g8_merge(src + lane, colpart + meta[tg % kG8Stages] + lane);
   }
 }
 

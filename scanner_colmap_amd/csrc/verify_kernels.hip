@@ -2644,8 +2644,13 @@ constexpr int kScoreTargetItems = SCM_SCORE_ITEMS;  // work items per score laun
 
 // PCH: points per lane of a work item (kScorePch; small batches take more,
 // so that each model's constants and loop overhead serve more points).
+#ifdef SCM_SCORE_WPE
+#define SCM_SCORE_ATTR __attribute__((amdgpu_waves_per_eu(SCM_SCORE_WPE)))
+#else
+#define SCM_SCORE_ATTR
+#endif
 template <int K, bool SPLIT, int PCH = kScorePch>
-__global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
+__global__ __launch_bounds__(kScoreThreads) SCM_SCORE_ATTR void rs_score_kernel(
     const VerifyPair* __restrict__ pairs, const float4* __restrict__ xyf_all,
     const RansacState* __restrict__ rst, const int32_t* __restrict__ wB,
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
