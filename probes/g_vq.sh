@@ -1,5 +1,8 @@
-# A/B of verifier occupancy variants (short benches, alternating order).
+# A/B of verifier scoring variants (short benches, alternating order) + the
+# verification GPU tests on the variant.
 set -e
 R=$GRAFT_REPO_ROOT
 cd $R
-bash probes/g_vbench.sh r03_vq vbase hm2w6 w5 hm3w5 rp3 rp4 vbase hm2w6 w5 hm3w5 rp3 rp4
+mkdir -p gpurun_out/r03_vc
+SCM_LIB=probes/build/libscm_vcnt.so timeout -k 10 400 python -u -m pytest tests/test_gpu_outcomes.py tests/test_gpu_verify.py tests/test_gpu_stencil.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/r03_vc/tests.log 2>&1
+bash probes/g_vbench.sh r03_vc vbase vcnt vbase vcnt

@@ -597,6 +597,42 @@ __device__ __forceinline__ void score_h_notout_n(const HFilt* f, const f32x2* s0
   }
 }
 
+// The same bounds as per-lane counts (SCM_SCORE_VCNT): lane L counts, per
+// model, its own points not surely outside (v_cmp + carry-in add, no
+// ballot / scalar popcount per compare); the caller sums the lanes.
+template <int PCH, bool FULL, int NM>
+__device__ __forceinline__ void score_h_notout_lanes(const HFilt* f, const f32x2* s0,
+                                                     const f32x2* s1, const f32x2* d0,
+                                                     const f32x2* d1, int n, int base,
+                                                     uint32_t* c) {
+#pragma unroll
+  for (int k = 0; k < NM; ++k) c[k] = 0u;
+  const int lane = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < PCH / 2; ++q) {
+    if (!FULL && base + 128 * q >= n) continue;
+    f32x2 d[NM];
+#pragma unroll
+    for (int k = 0; k < NM; ++k) d[k] = h_filter_pair(f[k], s0[q], s1[q], d0[q], d1[q]);
+    if (FULL) {
+      // d <= M  <=>  d - M+ < 0 with M+ the next float above M (d is finite:
+      // h_filter_consts guards overflow), read as the difference's sign bit
+#pragma unroll
+      for (int k = 0; k < NM; ++k) {
+        const float mp = __int_as_float(__float_as_int(f[k].p8m.y) + 1);
+        const f32x2 t = d[k] - f32x2(mp);
+        c[k] += (__float_as_uint(t.x) >> 31) + (__float_as_uint(t.y) >> 31);
+      }
+    } else {
+      const bool ok0 = base + 128 * q + lane < n;
+      const bool ok1 = base + 128 * q + 64 + lane < n;
+#pragma unroll
+      for (int k = 0; k < NM; ++k)
+        c[k] += (uint32_t)(ok0 && d[k].x <= f[k].p8m.y) + (uint32_t)(ok1 && d[k].y <= f[k].p8m.y);
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Packed-fp32 Sampson inlier filter (FundamentalMatrix*Estimator::Residuals,
 // SURVEY.md §8a a12) with exact fp64 fallback.  With U = F x1 (rows 0..2),
@@ -2631,6 +2667,9 @@ constexpr int kScoreThreads = 64;
 #ifndef SCM_SCORE_PCH
 #define SCM_SCORE_PCH 8
 #endif
+#ifndef SCM_SCORE_VCNT
+#define SCM_SCORE_VCNT 0  // H split pass: per-lane counts summed through LDS once per round
+#endif
 constexpr int kScorePch = SCM_SCORE_PCH;  // points per lane
 constexpr int kScoreChunk = kScoreThreads * kScorePch;
 #ifndef SCM_SCORE_PCH_SMALL
@@ -2661,6 +2700,8 @@ __global__ __launch_bounds__(kScoreThreads) SCM_SCORE_ATTR void rs_score_kernel(
   constexpr int MM = Tr::mm, MS = Tr::ms;
   __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * MM][12];
   __shared__ int32_t lnm[kTrialBatch];
+  // SCM_SCORE_VCNT: per-lane counts of model pairs (2t, 2t + 1) as two u16 halves
+  __shared__ uint32_t lcnt[(K == KIND_H && SPLIT && SCM_SCORE_VCNT) ? kTrialBatch / 2 * 64 : 1];
   constexpr int CH = kScoreThreads * PCH, QCAP = kDeferCap * (PCH / 8 > 1 ? PCH / 8 : 1);
   __shared__ uint32_t ldq[SPLIT ? 1 : QCAP];         // deferred exact tests (defer_push)
   __shared__ uint32_t ldc[SPLIT ? 1 : kTrialBatch * MM];  // their inliers per model of the round
@@ -2726,6 +2767,28 @@ __global__ __launch_bounds__(kScoreThreads) SCM_SCORE_ATTR void rs_score_kernel(
       if (K == KIND_H && SPLIT && SCM_SCORE_HM > 1) {
         // H split pass: SCM_SCORE_HM models per iteration (one model per hypothesis)
         constexpr int NM = SCM_SCORE_HM;
+#if SCM_SCORE_VCNT
+        static_assert(NM % 2 == 0, "model pairs per LDS word");
+        for (int t = 0; t < B; t += NM) {
+          HFilt f[NM];
+#pragma unroll
+          for (int k = 0; k < NM; ++k) f[k] = h_filter_load(&lc[min(t + k, B - 1)][0]);
+          uint32_t cv[NM];  // <= PCH each
+          if (full) score_h_notout_lanes<PCH, true, NM>(f, x0, x1, y0, y1, n, base, cv);
+          else score_h_notout_lanes<PCH, false, NM>(f, x0, x1, y0, y1, n, base, cv);
+#pragma unroll
+          for (int k = 0; k < NM; k += 2) lcnt[((t + k) >> 1) * 64 + lane] = cv[k] | (cv[k + 1] << 16);
+        }
+        __syncthreads();
+        if (lane < B) {  // sum of the 64 lanes' halves (each <= 64 PCH: no carry across)
+          const uint32_t* row = lcnt + (lane >> 1) * 64;
+          uint32_t sum = 0u;
+#pragma unroll 16
+          for (int j = 0; j < 64; ++j) sum += row[(j + lane) & 63];
+          u0 += (lane & 1) ? (sum >> 16) : (sum & 0xFFFFu);
+        }
+        if (false)
+#endif
         for (int t = 0; t < B; t += NM) {
           HFilt f[NM];
 #pragma unroll
