@@ -330,6 +330,7 @@ __device__ __forceinline__ bool sampson_inlier(const double* F, double x1_0, dou
 }
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float readlane_f(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
@@ -594,42 +595,6 @@ __device__ __forceinline__ void score_h_notout_n(const HFilt* f, const f32x2* s0
     for (int k = 0; k < NM; ++k)
       c[k] += __popcll(__ballot(d[k].x <= f[k].p8m.y) & ok0) +
               __popcll(__ballot(d[k].y <= f[k].p8m.y) & ok1);
-  }
-}
-
-// The same bounds as per-lane counts (SCM_SCORE_VCNT): lane L counts, per
-// model, its own points not surely outside (v_cmp + carry-in add, no
-// ballot / scalar popcount per compare); the caller sums the lanes.
-template <int PCH, bool FULL, int NM>
-__device__ __forceinline__ void score_h_notout_lanes(const HFilt* f, const f32x2* s0,
-                                                     const f32x2* s1, const f32x2* d0,
-                                                     const f32x2* d1, int n, int base,
-                                                     uint32_t* c) {
-#pragma unroll
-  for (int k = 0; k < NM; ++k) c[k] = 0u;
-  const int lane = threadIdx.x;
-#pragma unroll
-  for (int q = 0; q < PCH / 2; ++q) {
-    if (!FULL && base + 128 * q >= n) continue;
-    f32x2 d[NM];
-#pragma unroll
-    for (int k = 0; k < NM; ++k) d[k] = h_filter_pair(f[k], s0[q], s1[q], d0[q], d1[q]);
-    if (FULL) {
-      // d <= M  <=>  d - M+ < 0 with M+ the next float above M (d is finite:
-      // h_filter_consts guards overflow), read as the difference's sign bit
-#pragma unroll
-      for (int k = 0; k < NM; ++k) {
-        const float mp = __int_as_float(__float_as_int(f[k].p8m.y) + 1);
-        const f32x2 t = d[k] - f32x2(mp);
-        c[k] += (__float_as_uint(t.x) >> 31) + (__float_as_uint(t.y) >> 31);
-      }
-    } else {
-      const bool ok0 = base + 128 * q + lane < n;
-      const bool ok1 = base + 128 * q + 64 + lane < n;
-#pragma unroll
-      for (int k = 0; k < NM; ++k)
-        c[k] += (uint32_t)(ok0 && d[k].x <= f[k].p8m.y) + (uint32_t)(ok1 && d[k].y <= f[k].p8m.y);
-    }
   }
 }
 
@@ -2667,8 +2632,8 @@ constexpr int kScoreThreads = 64;
 #ifndef SCM_SCORE_PCH
 #define SCM_SCORE_PCH 8
 #endif
-#ifndef SCM_SCORE_VCNT
-#define SCM_SCORE_VCNT 0  // H split pass: per-lane counts summed through LDS once per round
+#ifndef SCM_SCORE_MFMA
+#define SCM_SCORE_MFMA 0  // H split pass: the three affine forms of 8 models x 32 points per f32 MFMA
 #endif
 constexpr int kScorePch = SCM_SCORE_PCH;  // points per lane
 constexpr int kScoreChunk = kScoreThreads * kScorePch;
@@ -2700,8 +2665,6 @@ __global__ __launch_bounds__(kScoreThreads) SCM_SCORE_ATTR void rs_score_kernel(
   constexpr int MM = Tr::mm, MS = Tr::ms;
   __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * MM][12];
   __shared__ int32_t lnm[kTrialBatch];
-  // SCM_SCORE_VCNT: per-lane counts of model pairs (2t, 2t + 1) as two u16 halves
-  __shared__ uint32_t lcnt[(K == KIND_H && SPLIT && SCM_SCORE_VCNT) ? kTrialBatch / 2 * 64 : 1];
   constexpr int CH = kScoreThreads * PCH, QCAP = kDeferCap * (PCH / 8 > 1 ? PCH / 8 : 1);
   __shared__ uint32_t ldq[SPLIT ? 1 : QCAP];         // deferred exact tests (defer_push)
   __shared__ uint32_t ldc[SPLIT ? 1 : kTrialBatch * MM];  // their inliers per model of the round
@@ -2767,27 +2730,66 @@ __global__ __launch_bounds__(kScoreThreads) SCM_SCORE_ATTR void rs_score_kernel(
       if (K == KIND_H && SPLIT && SCM_SCORE_HM > 1) {
         // H split pass: SCM_SCORE_HM models per iteration (one model per hypothesis)
         constexpr int NM = SCM_SCORE_HM;
-#if SCM_SCORE_VCNT
-        static_assert(NM % 2 == 0, "model pairs per LDS word");
-        for (int t = 0; t < B; t += NM) {
-          HFilt f[NM];
+#if SCM_SCORE_MFMA
+        // Full chunks: q_k = h'_k0 s0 + h'_k1 s1 + h'_k2 of 8 models x 32 points
+        // per v_mfma_f32_32x32x2f32 (row 8k + model, column = point; the K = 2
+        // operands are s0, s1 and the C operand the constant terms).  An MFMA
+        // rounds like an fmaf chain, inside h_filter_consts' bound for q
+        // (3.01u A'); w, lhs and diff as h_filter_pair, two models per packed
+        // op.  Lane (point r, half h) holds models 4h .. 4h + 3 of the tile.
+        if (full) {
+          constexpr int NT = CH / 32;  // point tiles
+          float bv[NT], e0[NT], e1[NT];
+          const int r = lane & 31, h = lane >> 5;
 #pragma unroll
-          for (int k = 0; k < NM; ++k) f[k] = h_filter_load(&lc[min(t + k, B - 1)][0]);
-          uint32_t cv[NM];  // <= PCH each
-          if (full) score_h_notout_lanes<PCH, true, NM>(f, x0, x1, y0, y1, n, base, cv);
-          else score_h_notout_lanes<PCH, false, NM>(f, x0, x1, y0, y1, n, base, cv);
+          for (int j = 0; j < NT; ++j) {
+            const float4 v = xyf[base + 32 * j + r];
+            bv[j] = h ? v.y : v.x;
+            e0[j] = -(v.z * dsc.x);  // -d' (exact negation; w enters squared)
+            e1[j] = -(v.w * dsc.x);
+          }
+          for (int mt = 0; mt * 8 < B; ++mt) {
+            const int row = lane & 31, krow = row >> 3;
+            const float a = krow < 3 ? lc[min(mt * 8 + (row & 7), B - 1)][3 * krow + h] : 0.0f;
+            f32x16 cm;
 #pragma unroll
-          for (int k = 0; k < NM; k += 2) lcnt[((t + k) >> 1) * 64 + lane] = cv[k] | (cv[k + 1] << 16);
-        }
-        __syncthreads();
-        if (lane < B) {  // sum of the 64 lanes' halves (each <= 64 PCH: no carry across)
-          const uint32_t* row = lcnt + (lane >> 1) * 64;
-          uint32_t sum = 0u;
-#pragma unroll 16
-          for (int j = 0; j < 64; ++j) sum += row[(j + lane) & 63];
-          u0 += (lane & 1) ? (sum >> 16) : (sum & 0xFFFFu);
-        }
-        if (false)
+            for (int i = 0; i < 16; ++i) {
+              const int k = i >> 2, mdl = min(mt * 8 + 4 * h + (i & 3), B - 1);
+              cm[i] = k < 3 ? lc[mdl][3 * k + 2] : 0.0f;
+            }
+            const f32x2 mg0 = f32x2{lc[min(mt * 8 + 4 * h, B - 1)][9], lc[min(mt * 8 + 4 * h + 1, B - 1)][9]};
+            const f32x2 mg1 = f32x2{lc[min(mt * 8 + 4 * h + 2, B - 1)][9], lc[min(mt * 8 + 4 * h + 3, B - 1)][9]};
+            uint32_t cnt[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cnt[k] = 0u;
+#pragma unroll
+            for (int j = 0; j < NT; ++j) {
+              const f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv[j], cm, 0, 0, 0);
+              const f32x2 dd0 = f32x2(e0[j]), dd1 = f32x2(e1[j]);
+#pragma unroll
+              for (int cp = 0; cp < 2; ++cp) {
+                const f32x2 q0 = f32x2{acc[2 * cp], acc[2 * cp + 1]};
+                const f32x2 q1 = f32x2{acc[4 + 2 * cp], acc[5 + 2 * cp]};
+                const f32x2 q2 = f32x2{acc[8 + 2 * cp], acc[9 + 2 * cp]};
+                // -w_j = q_j - d'_j q_2 and -diff = q_2^2 - lhs: the same
+                // roundings as h_filter_pair up to sign
+                const f32x2 w0 = __builtin_elementwise_fma(dd0, q2, q0);
+                const f32x2 w1 = __builtin_elementwise_fma(dd1, q2, q1);
+                const f32x2 lhs = __builtin_elementwise_fma(w0, w0, w1 * w1);
+                const f32x2 ndiff = __builtin_elementwise_fma(q2, q2, -lhs);
+                const f32x2 M = cp ? mg1 : mg0;
+                const uint64_t bx = __ballot(ndiff.x >= -M.x), by = __ballot(ndiff.y >= -M.y);
+                // one count for the models of both halves (c and 4 + c): their
+                // sum bounds each (a looser bound only adds exact recounts)
+                cnt[2 * cp] += __popcll(bx);
+                cnt[2 * cp + 1] += __popcll(by);
+              }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+              if (lane == mt * 8 + k) u0 += cnt[k & 3];
+          }
+        } else
 #endif
         for (int t = 0; t < B; t += NM) {
           HFilt f[NM];
