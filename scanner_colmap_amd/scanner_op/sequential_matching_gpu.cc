@@ -110,7 +110,19 @@ REGISTER_OP(SequentialMatchingGPU)
     .output("two_view_geometries")
     .protobuf_name("SequentialMatchingArgs");
 
+// Placement: the kernel holds a GPU (config.devices[0] is the GPU Scanner
+// assigned to this pipeline instance), but every column stays in host
+// memory -- execute() hands the element bytes to scm_execute_batch, which
+// stages them into its own HBM image cache, and the outputs are
+// new_buffer(CPU_DEVICE) elements.  Without these declarations Scanner's
+// evaluator would move the inputs to the GPU before execute() and treat the
+// outputs as device buffers.
 REGISTER_KERNEL(SequentialMatchingGPU, SequentialMatchingGPUKernel)
     .device(scanner::DeviceType::GPU)
+    .input_device("image_ids", scanner::DeviceType::CPU)
+    .input_device("keypoints", scanner::DeviceType::CPU)
+    .input_device("descriptors", scanner::DeviceType::CPU)
+    .output_device("pair_image_ids", scanner::DeviceType::CPU)
+    .output_device("two_view_geometries", scanner::DeviceType::CPU)
     .batch()
     .num_devices(1);

@@ -73,6 +73,16 @@ REGISTER_OP(SiftExtractionGPU)
     .output("cameras")
     .protobuf_name("siftExtractionArgs");
 
+// Placement: a GPU kernel whose columns all stay in host memory -- the frame
+// is read as host bytes (check_frame(CPU_DEVICE, ...) above) and uploaded by
+// scm_extract_frames, the outputs are new_buffer(CPU_DEVICE) elements.
+// Without these declarations Scanner's evaluator would hand execute() the
+// frame in device memory and treat the outputs as device buffers.
 REGISTER_KERNEL(SiftExtractionGPU, SiftExtractionGPUKernel)
     .device(scanner::DeviceType::GPU)
+    .input_device("image_ids", scanner::DeviceType::CPU)
+    .input_device("frames", scanner::DeviceType::CPU)
+    .output_device("keypoints", scanner::DeviceType::CPU)
+    .output_device("descriptors", scanner::DeviceType::CPU)
+    .output_device("cameras", scanner::DeviceType::CPU)
     .num_devices(1);

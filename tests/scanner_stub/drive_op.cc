@@ -28,6 +28,20 @@ static bool read_file(const std::string& path, std::vector<scanner::u8>* out) {
 }
 
 int main(int argc, char** argv) {
+  // drive_op --placements OP: print the kernel's device and every column's
+  // placement ("input <col> CPU|GPU", "output <col> CPU|GPU").
+  if (argc == 3 && std::string(argv[1]) == "--placements") {
+    auto k = scanner::kernel_registry().find(argv[2]);
+    if (k == scanner::kernel_registry().end()) return 2;
+    const scanner::OpInfo& op = scanner::op_registry()[argv[2]];
+    auto name = [](scanner::DeviceType d) { return d == scanner::DeviceType::CPU ? "CPU" : "GPU"; };
+    std::printf("kernel %s\n", name(k->second.device));
+    for (const auto& c : op.inputs)
+      std::printf("input %s %s\n", c.c_str(), name(scanner::input_placement(k->second, c)));
+    for (const auto& c : op.outputs)
+      std::printf("output %s %s\n", c.c_str(), name(scanner::output_placement(k->second, c)));
+    return 0;
+  }
   if (argc < 4) {
     std::fprintf(stderr, "usage: %s OP DIR K [DEVICE]\n", argv[0]);
     return 2;
@@ -41,6 +55,15 @@ int main(int argc, char** argv) {
     return 2;
   }
   const scanner::OpInfo& info = scanner::op_registry()[op];
+  // Column placement: the inputs below are host buffers and the outputs are
+  // freed as host buffers, which is what a Scanner worker does only for
+  // CPU-placed columns (KernelBuilder::input_device / output_device).
+  const std::string misplaced = scanner::first_non_cpu_column(info, it->second);
+  if (!misplaced.empty()) {
+    std::fprintf(stderr, "op %s: %s is not placed on the CPU device\n", op.c_str(),
+                 misplaced.c_str());
+    return 3;
+  }
   scanner::KernelConfig config;
   config.devices.push_back({it->second.device, device});
   read_file(dir + "/args", &config.args);

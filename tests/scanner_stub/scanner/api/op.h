@@ -23,6 +23,12 @@ struct KernelInfo {
   DeviceType device = DeviceType::CPU;
   bool batch = false;
   int num_devices = 1;
+  // Column placement (Scanner KernelBuilder::input_device / output_device):
+  // a column listed here lives on that device whatever the kernel's own
+  // device is; an unlisted column lives on the kernel's device.  Scanner's
+  // evaluator copies an input column to that device before execute() and
+  // treats an output column's buffers as allocated there.
+  std::map<std::string, DeviceType> input_devices, output_devices;
   std::function<StenciledBatchedKernel*(const KernelConfig&)> make;  // stenciled / batched kernels
   std::function<Kernel*(const KernelConfig&)> make_plain;            // scanner::Kernel
 };
@@ -69,7 +75,39 @@ struct KernelBuilder {
   KernelBuilder& device(DeviceType d) { info->device = d; return *this; }
   KernelBuilder& batch() { info->batch = true; return *this; }
   KernelBuilder& num_devices(int n) { info->num_devices = n; return *this; }
+  KernelBuilder& input_device(const std::string& col, DeviceType d) {
+    info->input_devices[col] = d;
+    return *this;
+  }
+  KernelBuilder& output_device(const std::string& col, DeviceType d) {
+    info->output_devices[col] = d;
+    return *this;
+  }
 };
+
+// Where a Scanner worker places a kernel's column: the declared device, else
+// the kernel's own device.
+inline DeviceType input_placement(const KernelInfo& k, const std::string& col) {
+  auto it = k.input_devices.find(col);
+  return it == k.input_devices.end() ? k.device : it->second;
+}
+inline DeviceType output_placement(const KernelInfo& k, const std::string& col) {
+  auto it = k.output_devices.find(col);
+  return it == k.output_devices.end() ? k.device : it->second;
+}
+
+// The drivers hand every column over in host memory and free every output
+// with delete_buffer(CPU_DEVICE, ...), so -- as under a real Scanner worker,
+// which would move a GPU-placed column to device memory -- a kernel whose
+// columns are not all CPU-placed cannot run here.  Returns the first such
+// column ("" when every column is on the CPU).
+inline std::string first_non_cpu_column(const OpInfo& op, const KernelInfo& k) {
+  for (const auto& c : op.inputs)
+    if (input_placement(k, c) != DeviceType::CPU) return "input " + c;
+  for (const auto& c : op.outputs)
+    if (output_placement(k, c) != DeviceType::CPU) return "output " + c;
+  return "";
+}
 }  // namespace scanner
 
 #define SCANNER_STUB_CAT2(a, b) a##b

@@ -103,6 +103,54 @@ def test_exhaustive_shape():
     assert len(configs) == 780
 
 
+def test_exhaustive_full_size_config4():
+    """Config 4 at its own size: the bench's south-building-synth workload
+    (128 images x 8192 keypoints, exhaustive: stencil range(0, 128), every
+    one of the 8,128 pairs on one GPU through the HIP table path).
+    Every row's pair ids follow the stencil rule of
+    sequential_matching.cc:139-146 (feature_matching.py:43 with K = N); a
+    fixed sample of pairs -- pivot row 0's first and last 8 neighbours, all
+    of row 63, rows 120-126 -- has raw matches bit-exact and TwoViewGeometry
+    bytes equal to the CPU oracle's."""
+    from scanner_colmap_amd.codecs import decode_pair_ids, split_tvg_list
+    n, k = 128, 8192
+    imgs = Corridor(n, k, n, seed=20253).images()
+    ids, kps, descs = table_rows(imgs)
+    sample = {0: list(range(1, 9)) + list(range(120, 128)), 63: list(range(64, 128))}
+    for r in range(120, 127):
+        sample[r] = list(range(r + 1, 128))
+    with Context(0) as ctx:
+        ctx.table_load(ids, kps, descs)
+        for r in sample:
+            ctx.add_keep_matches_range(r, r + 1)
+        got_ids, got_tvg = ctx.table_run(n, 0, n)
+        got_m = {(r, s): ctx.table_matches(r, s - r) for r in sample for s in sample[r]}
+        ctx.set_keep_matches(False)
+    assert len(got_ids) == n and len(got_tvg) == n
+    for r in range(n):
+        assert decode_pair_ids(got_ids[r]) == [imgs[s][0] for s in range(r + 1, n)], r
+    assert sum(len(decode_pair_ids(b)) for b in got_ids) == n * (n - 1) // 2
+
+    def one(job):
+        r, s = job
+        m = oracle.match_pair_fast(imgs[r][2], imgs[s][2])
+        return m, oracle.verify_pair(imgs[r][1], imgs[s][1], m, imgs[r][0], imgs[s][0])
+
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = [(r, s) for r in sample for s in sample[r]]
+    with ThreadPoolExecutor(max_workers=THREADS) as ex:
+        ref = dict(zip(jobs, ex.map(one, jobs)))
+    for r in sample:
+        row = split_tvg_list(got_tvg[r])
+        assert len(row) == n - 1 - r
+        for s in sample[r]:
+            m, tvg = ref[(r, s)]
+            g = got_m[(r, s)]
+            assert g.shape == m.shape and (g == m).all(), (r, s)
+            assert row[s - r - 1] == tvg, (r, s)
+    assert len(jobs) == 16 + 64 + 28
+
+
 def test_k50_shape_many_batches():
     """Config 5 shape (4096 kpts, overlap 50): 64 images (1,911 pairs) in
     batches of 400 pairs, so several batches are in flight at once."""

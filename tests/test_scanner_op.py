@@ -39,6 +39,51 @@ def test_op_compiles_against_scanner_api_and_links(tmp_path):
     _build_driver(tmp_path)
 
 
+def _placements(exe, op):
+    r = subprocess.run([str(exe), "--placements", op], capture_output=True, text=True, check=True)
+    return [tuple(line.split()) for line in r.stdout.splitlines()]
+
+
+def test_op_declares_cpu_placed_columns(tmp_path):
+    """A GPU kernel whose columns are host bytes must say so
+    (KernelBuilder::input_device / output_device): otherwise a Scanner
+    worker would move the inputs to the GPU before execute() and treat the
+    outputs as device buffers.  Every column of SequentialMatchingGPU is
+    CPU-placed; the kernel itself holds a GPU."""
+    exe = _build_driver(tmp_path)
+    assert _placements(exe, "SequentialMatchingGPU") == [
+        ("kernel", "GPU"),
+        ("input", "image_ids", "CPU"), ("input", "keypoints", "CPU"),
+        ("input", "descriptors", "CPU"),
+        ("output", "pair_image_ids", "CPU"), ("output", "two_view_geometries", "CPU")]
+
+
+def test_driver_refuses_gpu_placed_columns(tmp_path):
+    """The stub driver refuses a GPU kernel that leaves a column on the GPU
+    (it would receive host pointers where Scanner hands device pointers)."""
+    src = tmp_path / "bad_op.cc"
+    src.write_text("""
+#include "scanner/api/kernel.h"
+#include "scanner/api/op.h"
+class BadKernel : public scanner::StenciledBatchedKernel {
+ public:
+  explicit BadKernel(const scanner::KernelConfig& c) : scanner::StenciledBatchedKernel(c) {}
+  void execute(const scanner::StenciledBatchedElements&, scanner::BatchedElements&) override {}
+};
+REGISTER_OP(BadOp).stencil().input("image_ids").output("out");
+REGISTER_KERNEL(BadOp, BadKernel).device(scanner::DeviceType::GPU)
+    .output_device("out", scanner::DeviceType::CPU);
+""")
+    exe = tmp_path / "drive_bad"
+    subprocess.run(["g++", "-std=c++17", "-O2", "-Wall", "-Werror", "-I", STUB,
+                    os.path.join(STUB, "drive_op.cc"), str(src), "-o", str(exe)], check=True)
+    d = tmp_path / "io"
+    d.mkdir()
+    (d / "in_0_0").write_bytes(b"\0" * 8)
+    r = subprocess.run([str(exe), "BadOp", str(d), "1"], capture_output=True, text=True)
+    assert r.returncode == 3 and "input image_ids is not placed on the CPU device" in r.stderr
+
+
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")
 def test_op_aborts_without_gpu(tmp_path):
     """No CPU fallback: the kernel constructor aborts the worker (the
@@ -158,6 +203,16 @@ def _write_frames(d, frames, ids):
 
 def test_sift_op_compiles_against_scanner_api_and_links(tmp_path):
     _build_frame_driver(tmp_path)
+
+
+def test_sift_op_declares_cpu_placed_columns(tmp_path):
+    """SiftExtractionGPU reads the frame as host bytes (check_frame with
+    CPU_DEVICE) and writes host outputs: every column is CPU-placed."""
+    exe = _build_frame_driver(tmp_path)
+    assert _placements(exe, "SiftExtractionGPU") == [
+        ("kernel", "GPU"), ("input", "image_ids", "CPU"), ("input", "frames", "CPU"),
+        ("output", "keypoints", "CPU"), ("output", "descriptors", "CPU"),
+        ("output", "cameras", "CPU")]
 
 
 @pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="a GPU is visible")
