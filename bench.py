@@ -232,6 +232,7 @@ def stencil_bench(ctx, src, overlap: int, rows: int, batches: list) -> dict:
         calls = [stencils(r0, min(rows, r0 + b)) for r0 in range(0, rows, b)]
         ctx.execute_batch(calls[0])  # warm-up (buffers, cache)
         r0_, u0_ = ctx.stencil_stats()
+        s0_ = ctx.stencil_spec_stats()
         t0 = time.perf_counter()
         npairs = 0
         for c in calls:
@@ -239,9 +240,12 @@ def stencil_bench(ctx, src, overlap: int, rows: int, batches: list) -> dict:
             npairs += sum(int(np.frombuffer(x[:8], np.uint64)[0]) for x in a)
         dt = time.perf_counter() - t0
         r1_, u1_ = ctx.stencil_stats()
+        s1_ = ctx.stencil_spec_stats()
         res[f"batch{b}"] = {"pairs_per_s": round(npairs / dt, 1), "ms_per_call": round(dt / len(calls) * 1e3, 2),
                             "calls": len(calls), "pairs": npairs,
-                            "images_uploaded": u1_ - u0_, "images_reused": r1_ - r0_}
+                            "images_uploaded": u1_ - u0_, "images_reused": r1_ - r0_,
+                            "keys_speculated": s1_[0] - s0_[0], "speculation_refused": s1_[1] - s0_[1],
+                            "calls_rerun": s1_[2] - s0_[2]}
     return res
 
 

@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SCM_ABI_VERSION 4
+#define SCM_ABI_VERSION 5
 
 enum {
   SCM_OK = 0,
@@ -175,9 +175,10 @@ int scm_execute_stencil(scm_context* ctx, int64_t stencil_size,
  * images, and every element is matched with its own bytes as the reference
  * decodes them (sequential_matching.cc:115-122).  Element buffers the
  * previous call also handed over (same addresses and sizes) take that call's
- * content keys at once and are re-hashed while the GPU runs; if a buffer was
- * rewritten in place the run is discarded and the call runs again with every
- * key hashed first, so the outputs always follow the bytes. */
+ * content keys at once (when a sample of their words is unchanged) and are
+ * re-hashed while the GPU runs; if a buffer was rewritten in place the run is
+ * discarded and the call runs again with every key hashed first, so the
+ * outputs always follow the bytes. */
 int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
                       const scm_element* image_ids,
                       const scm_element* keypoints,
@@ -185,6 +186,15 @@ int scm_execute_batch(scm_context* ctx, int64_t batch, int64_t stencil_size,
                       scm_blob* pair_image_ids_out, scm_blob* tvgs_out);
 /* Images the execute() cache reused / uploaded so far (cumulative). */
 int scm_stencil_stats(scm_context* ctx, int64_t* reused, int64_t* uploaded);
+/* Content-key speculation of scm_execute_batch so far (cumulative): elements
+ * whose buffers took the previous call's key while the GPU ran; elements whose
+ * buffers the previous call also handed over but whose sampled words changed
+ * (a recycled buffer holding another image: hashed before the run instead);
+ * calls whose speculated key did not hold (buffer rewritten in place with
+ * its sampled words unchanged) and ran again -- the image cache is kept, so
+ * the rerun uploads only the changed images.  Diagnostics (bench, tests). */
+int scm_stencil_spec_stats(scm_context* ctx, int64_t* speculated, int64_t* rejected,
+                           int64_t* retried);
 /* Drops the execute() image cache (Scanner Kernel::reset(), called when a
  * kernel instance starts on a new stream of rows): the next call uploads
  * every image it needs.  Never needed for correctness -- the cache is keyed

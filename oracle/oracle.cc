@@ -37,6 +37,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 #include <random>
 #include <vector>
 
@@ -244,6 +245,30 @@ size_t compute_num_trials(size_t num_inliers, size_t num_samples,
                                        multiplier, kmin);
 }
 
+// The RANSAC constructor's cap on max_num_trials [upstream optim/ransac.h]:
+// ComputeNumTrials(min_inlier_ratio * 1e5, 1e5) with the host libm
+// (std::pow, std::log, std::ceil) and static_cast<size_t> as gcc emits it on
+// x86-64 for out-of-range values.
+size_t constructor_num_trials(double min_inlier_ratio, double confidence, double multiplier,
+                              int kmin) {
+  auto cast = [](double v) -> size_t {
+    if (!(v < 9223372036854775808.0)) {
+      if (!(v < 18446744073709551616.0)) return v == v ? 0 : (size_t)1 << 63;
+      return (size_t)(int64_t)(v - 9223372036854775808.0) ^ ((size_t)1 << 63);
+    }
+    if (!(v > -9223372036854775808.0)) return (size_t)1 << 63;
+    return (size_t)(int64_t)v;
+  };
+  const size_t kNumSamples = 100000;
+  const size_t num_inliers = cast(min_inlier_ratio * kNumSamples);
+  const double inlier_ratio = num_inliers / static_cast<double>(kNumSamples);
+  const double nom = 1 - confidence;
+  if (nom <= 0) return std::numeric_limits<size_t>::max();
+  const double denom = 1 - std::pow(inlier_ratio, kmin);
+  if (denom <= 0) return 1;
+  return cast(std::ceil(std::log(nom) / std::log(denom) * multiplier));
+}
+
 using Model = std::vector<double>;  // 9 (F, H) or 2 (translation) doubles
 
 // Estimator policies.  kind: 0 = F (7-pt min / 8-pt local), 1 = H, 2 = T.
@@ -338,13 +363,9 @@ Report loransac(int kind, const RansacOptions& opt_in,
   const int kmin = min_samples(kind, false);
   const int kmin_local = min_samples(kind, true);
   RansacOptions opt = opt_in;
-  {
-    const size_t kNumSamples = 100000;
-    const size_t dyn = compute_num_trials(
-        static_cast<size_t>(opt.min_inlier_ratio * kNumSamples), kNumSamples,
-        opt.confidence, opt.dyn_num_trials_multiplier, kmin);
-    opt.max_num_trials = std::min<size_t>(opt.max_num_trials, dyn);
-  }
+  opt.max_num_trials = std::min<size_t>(
+      opt.max_num_trials, constructor_num_trials(opt.min_inlier_ratio, opt.confidence,
+                                                 opt.dyn_num_trials_multiplier, kmin));
   Report report;
   const size_t num_samples = X.size() / 2;
   if (num_samples < (size_t)kmin) return report;

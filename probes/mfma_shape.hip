@@ -1,0 +1,111 @@
+// Diagnostics (not product): chip-wide i8 MFMA throughput of the two gfx950
+// shapes the matcher could use, v_mfma_i32_32x32x32_i8 and
+// v_mfma_i32_16x16x64_i8, on random operands (power, hence the clock, depends
+// on the data), 8 waves per CU, every CU busy.  Prints TOP/s and the
+// effective shader clock (s_memtime cycles per wave / wall time).
+// Build: hipcc -O3 --offload-arch=gfx950 probes/mfma_shape.hip -o probes/build/mfma_shape
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int kIter = 4096;
+
+// MODE 0: 32x32x32, 4 accumulators (16 MFMAs per iteration: a 64-row x 64-col tile, K = 128)
+// MODE 1: 16x16x64, 16 accumulators (32 MFMAs per iteration: the same tile and K)
+template <int MODE>
+__global__ __launch_bounds__(512) void shape_kernel(const i32x4* __restrict__ src, int* out,
+                                                    long long* cyc) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  i32x4 a[4], b[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    a[q] = src[(tid * 8 + q) & 0xFFFFF];
+    b[q] = src[(tid * 8 + 4 + q) & 0xFFFFF];
+  }
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  int sink = 0;
+  if (MODE == 0) {
+    i32x16 acc[4] = {};
+    for (int it = 0; it < kIter; ++it) {
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc[s] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[(q + s) & 3], b[q], acc[s], 0, 0, 0);
+    }
+#pragma unroll
+    for (int s = 0; s < 4; ++s)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sink ^= acc[s][i];
+  } else {
+    i32x4 acc[16] = {};
+    for (int it = 0; it < kIter; ++it) {
+#pragma unroll
+      for (int s = 0; s < 16; ++s)
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+          acc[s] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[(2 * q + s) & 3], b[(s + q) & 3],
+                                                         acc[s], 0, 0, 0);
+    }
+#pragma unroll
+    for (int s = 0; s < 16; ++s)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sink ^= acc[s][i];
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  out[tid] = sink;
+  if ((threadIdx.x & 63) == 0) cyc[tid >> 6] = t1 - t0;
+}
+
+template <int MODE>
+static void run(const i32x4* src, int* out, long long* cyc, int blocks) {
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  shape_kernel<MODE><<<blocks, 512>>>(src, out, cyc);  // warm
+  hipDeviceSynchronize();
+  hipEventRecord(e0);
+  shape_kernel<MODE><<<blocks, 512>>>(src, out, cyc);
+  hipEventRecord(e1);
+  hipEventSynchronize(e1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, e0, e1);
+  const int waves = blocks * 8;
+  long long* h = (long long*)malloc(waves * sizeof(long long));
+  hipMemcpy(h, cyc, waves * sizeof(long long), hipMemcpyDeviceToHost);
+  double mean = 0;
+  for (int i = 0; i < waves; ++i) mean += (double)h[i];
+  mean /= waves;
+  free(h);
+  // ops per wave per iteration: 64 rows x 64 cols x 128 K x 2
+  const double ops = (double)waves * kIter * 64.0 * 64.0 * 128.0 * 2.0;
+  // s_memtime ticks at a fixed 100 MHz reference on gfx950? report cycles as counted
+  printf("%s: %.3f ms, %.1f TOP/s (%.3f of 5000), wave ticks %.0f, ticks/ms %.0f\n",
+         MODE == 0 ? "32x32x32_i8" : "16x16x64_i8", ms, ops / (ms * 1e-3) / 1e12,
+         ops / (ms * 1e-3) / 1e12 / 5000.0, mean, mean / ms);
+}
+
+int main() {
+  const size_t n = 1 << 20;
+  i32x4* src;
+  int* out;
+  long long* cyc;
+  hipMalloc(&src, n * sizeof(i32x4));
+  i32x4* h = (i32x4*)malloc(n * sizeof(i32x4));
+  srand(1);
+  for (size_t i = 0; i < n; ++i)
+    for (int k = 0; k < 4; ++k) h[i][k] = (rand() << 16) ^ rand();
+  hipMemcpy(src, h, n * sizeof(i32x4), hipMemcpyHostToDevice);
+  const int blocks = 256 * 4;
+  hipMalloc(&out, (size_t)blocks * 512 * sizeof(int));
+  hipMalloc(&cyc, (size_t)blocks * 8 * sizeof(long long));
+  for (int rep = 0; rep < 2; ++rep) {
+    run<0>(src, out, cyc, blocks);
+    run<1>(src, out, cyc, blocks);
+  }
+  return 0;
+}

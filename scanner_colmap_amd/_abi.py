@@ -33,7 +33,7 @@ EXPORTS = (
     "scm_parse_args", "scm_pair_seed", "scm_blob_free",
     "scm_context_create", "scm_context_destroy", "scm_match_pair",
     "scm_verify_pair", "scm_execute_stencil", "scm_execute_batch", "scm_stencil_stats",
-    "scm_stencil_cache_clear",
+    "scm_stencil_spec_stats", "scm_stencil_cache_clear",
     "scm_table_load",
     "scm_table_run", "scm_table_run_packed", "scm_set_keep_matches",
     "scm_set_keep_matches_range", "scm_add_keep_matches_range",
@@ -113,6 +113,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                       POINTER(Element), POINTER(Element),
                                       POINTER(Blob), POINTER(Blob)]
     lib.scm_stencil_stats.argtypes = [c_void_p, POINTER(c_int64), POINTER(c_int64)]
+    lib.scm_stencil_spec_stats.argtypes = [c_void_p, POINTER(c_int64), POINTER(c_int64),
+                                           POINTER(c_int64)]
     lib.scm_stencil_cache_clear.argtypes = [c_void_p]
     lib.scm_table_load.argtypes = [c_void_p, c_int64, POINTER(Element),
                                    POINTER(Element), POINTER(Element)]
@@ -313,6 +315,13 @@ class Context:
         r, u = c_int64(), c_int64()
         _check(self._lib.scm_stencil_stats(self._ptr, byref(r), byref(u)))
         return r.value, u.value
+
+    def stencil_spec_stats(self) -> tuple[int, int, int]:
+        """(elements speculated, speculations refused by the sampled words,
+        calls run again because a speculated key did not hold) so far."""
+        a, b, c = c_int64(), c_int64(), c_int64()
+        _check(self._lib.scm_stencil_spec_stats(self._ptr, byref(a), byref(b), byref(c)))
+        return a.value, b.value, c.value
 
     def stencil_cache_clear(self) -> None:
         """Drop the execute() HBM image cache (Scanner Kernel::reset())."""

@@ -248,6 +248,36 @@ struct SrcHash {
   }
 };
 
+// Sampled fingerprint of an element's bytes: 64 8-byte words at offsets
+// i * stride (stride = ((n - 8) / 64) rounded down to a multiple of 8) and the
+// last 8 bytes of each buffer, or the whole buffer when it is under 520 bytes.
+// ~130 loads: cheap enough to check before the GPU run whether a buffer the
+// previous call also handed over (same address and size) still holds the
+// same image.  A recycled buffer that now holds another image differs in
+// these words; only an in-place rewrite that leaves every sampled word alone
+// gets past it, and the full content hash checked after the run catches that.
+uint64_t sample_words(const uint8_t* p, size_t n, uint64_t h) {
+  if (n < 520) return hash_bytes(p, n, h);
+  const size_t stride = ((n - 8) / 64) & ~(size_t)7;
+  auto mix = [](uint64_t a, uint64_t w) {
+    a ^= w * 0x9E3779B185EBCA87ULL;
+    return ((a << 29) | (a >> 35)) * 0xC2B2AE3D27D4EB4FULL;
+  };
+  for (size_t i = 0; i < 64; ++i) {
+    uint64_t w;
+    std::memcpy(&w, p + i * stride, 8);
+    h = mix(h, w);
+  }
+  uint64_t w;
+  std::memcpy(&w, p + n - 8, 8);
+  return mix(h, w) ^ n;
+}
+
+struct SpecKey {
+  ImageKey key;  // content key the buffers held in the previous call
+  uint64_t fp;   // their sampled fingerprint then
+};
+
 // Pinned host result buffer: the DMA target of each batch's results.
 struct PinnedOut {
   void* host = nullptr;
@@ -398,7 +428,8 @@ struct scm_context {
   // while the GPU works (execute_rows).
   WorkerPool pool, vpool;
   // Content keys of the previous execute() call's element buffers.
-  std::unordered_map<Src, ImageKey, SrcHash> spec_keys;
+  std::unordered_map<Src, SpecKey, SrcHash> spec_keys;
+  int64_t spec_elems = 0, spec_rejected = 0, spec_retries = 0;  // scm_stencil_spec_stats
 };
 
 namespace {
@@ -564,9 +595,11 @@ inline bool same_content(const ImageKey& a, const ImageKey& b) {
 // ImageKey) are copied device-to-device, the rest are staged, uploaded and
 // converted in one tail range.  Layout: reused images first (in their old
 // order, so consecutive ones coalesce into single copies), then new ones.
-// (*idx)[i] = table index of rows[i].
+// (*idx)[i] = table index of rows[i]; (*uploaded)[i] = rows[i] was staged
+// from its host bytes (not copied from the previous table).
 int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows,
-                      const std::vector<ImageKey>& keys, std::vector<int32_t>* idx) {
+                      const std::vector<ImageKey>& keys, std::vector<int32_t>* idx,
+                      std::vector<char>* uploaded) {
   const int nxt = ctx->call_cur < 0 ? 0 : 1 - ctx->call_cur;
   const ImageTable* old = ctx->call_cur < 0 ? nullptr : &ctx->call_tab[ctx->call_cur];
   const std::unordered_map<ImageKey, int32_t, ImageKeyHash>* omap =
@@ -589,6 +622,8 @@ int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows,
     }
     (from[i] >= 0 ? reuse : fresh).push_back(i);
   }
+  uploaded->assign(n, 0);
+  for (int64_t i : fresh) (*uploaded)[i] = 1;
   std::stable_sort(reuse.begin(), reuse.end(),
                    [&](int64_t a, int64_t b) { return from[a] < from[b]; });
   std::vector<int64_t> order = reuse;
@@ -732,6 +767,31 @@ int upload_call_table(scm_context* ctx, const std::vector<RowView>& rows,
   return SCM_OK;
 }
 
+// static_cast<size_t>(v) as gcc emits it on x86-64 (cvttsd2si, with the
+// 2^63 offset branch for large values): -inf / negative -> 2^63, >= 2^64 and
+// +inf -> 0, NaN -> 2^63.
+uint64_t size_t_cast_x86(double v) {
+  if (!(v < 9223372036854775808.0)) {
+    if (!(v < 18446744073709551616.0)) return v == v ? 0 : 1ull << 63;
+    return (uint64_t)(int64_t)(v - 9223372036854775808.0) ^ (1ull << 63);
+  }
+  if (!(v > -9223372036854775808.0)) return 1ull << 63;
+  return (uint64_t)(int64_t)v;
+}
+
+// RANSAC::ComputeNumTrials [upstream optim/ransac.h] with the host libm, as
+// the RANSAC constructor evaluates it for its max_num_trials cap (host only:
+// the per-trial dynamic bound on the device uses geom::num_trials).
+uint64_t num_trials_libm(uint64_t num_inliers, uint64_t num_samples, double confidence,
+                         double multiplier, int kmin) {
+  const double inlier_ratio = (double)num_inliers / (double)num_samples;
+  const double nom = 1.0 - confidence;
+  if (nom <= 0.0) return ~0ull;  // std::numeric_limits<size_t>::max()
+  const double denom = 1.0 - std::pow(inlier_ratio, kmin);
+  if (denom <= 0.0) return 1;
+  return size_t_cast_x86(std::ceil(std::log(nom) / std::log(denom) * multiplier));
+}
+
 // `iteration` > 0: the k-th Estimate of TwoViewGeometry::EstimateMultiple
 // (multiple_models), whose PRNG streams start from geom::iteration_seed.
 VerifyParams make_params(const scm_matching_options& o, int iteration = 0) {
@@ -749,11 +809,12 @@ VerifyParams make_params(const scm_matching_options& o, int iteration = 0) {
   p.detect_watermark = o.detect_watermark;
   p.base_seed = geom::iteration_seed(o.ransac_seed, (uint32_t)iteration);
   // RANSAC constructor: max_num_trials capped by ComputeNumTrials at the
-  // assumed min_inlier_ratio over 1e5 samples [upstream optim/ransac.h].
+  // assumed min_inlier_ratio over 1e5 samples [upstream optim/ransac.h],
+  // evaluated with the host libm as the constructor does.
   auto cap = [&](double ratio, int kmin) {
     const uint64_t kNumSamples = 100000;
-    const uint64_t dyn = geom::num_trials((uint64_t)(ratio * (double)kNumSamples), kNumSamples,
-                                          o.confidence, o.dyn_num_trials_multiplier, kmin);
+    const uint64_t dyn = num_trials_libm(size_t_cast_x86(ratio * (double)kNumSamples), kNumSamples,
+                                         o.confidence, o.dyn_num_trials_multiplier, kmin);
     const uint64_t m = std::min<uint64_t>((uint64_t)std::max(0, o.max_num_trials), dyn);
     return (int32_t)std::min<uint64_t>(m, 0x7FFFFFFF);
   };
@@ -1448,6 +1509,13 @@ bool take_estimate(const scm_matching_options& o, const BatchView& v, int64_t p,
   const bool removed = !g.inliers.empty();
   if (g.config != SCM_TVG_WATERMARK) geoms->push_back(std::move(g));
   cur->swap(out);
+  // The oracle (verify_pair_multiple, oracle.cc) runs the next Estimate and
+  // stops on its DEGENERATE result; stopping here when fewer than
+  // min_num_inliers (or no) matches remain is the same decision only because
+  // Estimate returns DEGENERATE for such a list before any RANSAC
+  // (TwoViewGeometry::Estimate's size guard, oracle.cc verify_pair
+  // `matches.size() < min_num_inliers`, and the `n < max(1, mni)` test at the
+  // top of this function).  A change to that guard must change this stop.
   return removed && (int64_t)cur->size() >= std::max(1, mni);
 }
 
@@ -1956,6 +2024,12 @@ namespace {
 
 constexpr int kRetryKeys = 1;  // execute_rows: a speculated content key did not hold
 
+// Sampled fingerprint of an element's keypoint and descriptor buffers.
+uint64_t fingerprint(const RowView& r) {
+  const uint64_t h = sample_words(reinterpret_cast<const uint8_t*>(r.kp), (size_t)r.nkp * 24, 0x6670ULL);
+  return sample_words(r.desc, (size_t)r.ndesc * 128, h);
+}
+
 // One execute() call over decoded elements.  Content keys (ImageKey): element
 // buffers the previous call also handed over take that call's keys
 // speculatively and are re-hashed on ctx->vpool while the GPU runs; the
@@ -1974,8 +2048,15 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
     const Src src{r.kp, r.nkp, r.desc, r.ndesc};
     auto it = first.emplace(src, e).first;
     of[e] = it->second;
-    if (it->second == e) (speculate && ctx->spec_keys.count(src) ? spec_e : now_e).push_back(e);
+    if (it->second != e) continue;
+    // Speculate only on buffers whose sampled words still match (a recycled
+    // buffer that now holds another image is hashed now instead).
+    auto sp = speculate ? ctx->spec_keys.find(src) : ctx->spec_keys.end();
+    const bool spec = sp != ctx->spec_keys.end() && sp->second.fp == fingerprint(r);
+    if (sp != ctx->spec_keys.end() && !spec) ++ctx->spec_rejected;
+    (spec ? spec_e : now_e).push_back(e);
   }
+  ctx->spec_elems += (int64_t)spec_e.size();
   std::vector<ImageKey> ekey(ne);
   KeyJob now_job;
   now_job.plan(rows, now_e);
@@ -1983,7 +2064,7 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
   for (size_t i = 0; i < now_e.size(); ++i) ekey[now_e[i]] = now_job.key(i);
   for (int64_t e : spec_e) {
     const RowView& r = rows[e];
-    ekey[e] = ctx->spec_keys[Src{r.kp, r.nkp, r.desc, r.ndesc}];
+    ekey[e] = ctx->spec_keys[Src{r.kp, r.nkp, r.desc, r.ndesc}].key;
   }
   KeyJob spec_job;
   spec_job.plan(rows, spec_e);
@@ -2016,7 +2097,8 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
   }
   const int64_t reused0 = ctx->call_reused, uploaded0 = ctx->call_uploaded;
   std::vector<int32_t> uidx;
-  int rc = upload_call_table(ctx, uniq, ukeys, &uidx);
+  std::vector<char> uploaded;
+  int rc = upload_call_table(ctx, uniq, ukeys, &uidx, &uploaded);
   if (rc != SCM_OK) {
     ctx->call_cur = -1;  // the cache may be half written
     drain(ctx);
@@ -2051,17 +2133,26 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
   bool held = true;
   for (size_t i = 0; i < spec_e.size(); ++i) held = held && same_content(spec_job.key(i), ekey[spec_e[i]]);
   if (!held) {
-    // A buffer changed since the previous call: nothing of this run is
-    // returned, the cache and the speculation start over.
+    // A buffer was rewritten in place since the previous call (its sampled
+    // words unchanged): nothing of this run is returned and the call runs
+    // again with every key hashed.  The image cache stays: an entry copied
+    // from the previous table holds the bytes its key names.  Only an entry
+    // staged from a wrong-keyed buffer (its key not resident) would name
+    // other bytes, and those entries are dropped.
     if (!pool_give(pk.data)) std::free(pk.data);
-    ctx->call_cur = -1;
+    auto& cmap = ctx->call_map[ctx->call_cur];
+    for (size_t i = 0; i < spec_e.size(); ++i) {
+      const int32_t u = elem_u[spec_e[i]];
+      if (uploaded[u] && !same_content(spec_job.key(i), ekey[spec_e[i]])) cmap.erase(ukeys[u]);
+    }
     ctx->spec_keys.clear();
     ctx->call_reused = reused0;
     ctx->call_uploaded = uploaded0;
+    ++ctx->spec_retries;
     return kRetryKeys;
   }
   ctx->spec_keys.clear();
-  for (const auto& f : first) ctx->spec_keys[f.first] = ekey[f.second];
+  for (const auto& f : first) ctx->spec_keys[f.first] = SpecKey{ekey[f.second], fingerprint(rows[f.second])};
   for (int64_t r = 0; r < batch; ++r) {
     const int64_t a = pk.row_off[2 * r], b = pk.row_off[2 * r + 1], c = pk.row_off[2 * r + 2];
     uint8_t* pa = (uint8_t*)std::malloc((size_t)std::max<int64_t>(b - a, 1));
@@ -2122,6 +2213,18 @@ int scm_stencil_stats(scm_context* ctx, int64_t* reused, int64_t* uploaded) {
   }
   *reused = ctx->call_reused;
   *uploaded = ctx->call_uploaded;
+  return SCM_OK;
+}
+
+int scm_stencil_spec_stats(scm_context* ctx, int64_t* speculated, int64_t* rejected,
+                           int64_t* retried) {
+  if (!ctx || !speculated || !rejected || !retried) {
+    set_error("invalid arguments");
+    return SCM_E_INVALID;
+  }
+  *speculated = ctx->spec_elems;
+  *rejected = ctx->spec_rejected;
+  *retried = ctx->spec_retries;
   return SCM_OK;
 }
 

@@ -43,7 +43,8 @@ struct Slot {
   int rtab_w = 0, rtab_h = 0;  // source size the uploaded tables are for
   SiftDev dev{};
   int64_t nel_cap = 0;  // first-octave pixels the workspace holds
-  int cap_scale = 1;    // candidate / keypoint / feature capacities x this (grown on overflow)
+  int64_t cap_scale = 1;  // candidate / keypoint / feature capacities x this (grown on overflow)
+  bool caps_at_bound = false;  // every capacity at its hard per-frame bound (no overflow possible)
   int64_t pending = -1; // frame index whose results are in flight
   int w = 0, h = 0;
 };
@@ -195,10 +196,10 @@ int ensure_slot(const SiftState* s, Slot& sl, int w, int h) {
   const int64_t k0 = s->caps[1] ? s->caps[1] : std::min<int64_t>(c0, 1 << 18);
   const int64_t f0 = s->caps[2] ? s->caps[2] : 2 * k0;
   // every octave pixel of the 3 detection levels is at most one candidate
-  const int cand_cap = (int)std::min<int64_t>(c0 * sc, 3 * nel + 64);
+  const int cand_cap = (int)std::min<int64_t>({c0 * sc, 3 * nel + 64, INT32_MAX});
   // every octave's keypoints: at most 3 per pixel of each octave (<= 4 nel in all)
-  const int key_cap = (int)std::min<int64_t>(k0 * sc, 4 * nel + 64);
-  const int feat_cap = (int)std::min<int64_t>(f0 * sc, 4 * (int64_t)key_cap);
+  const int key_cap = (int)std::min<int64_t>({k0 * sc, 4 * nel + 64, INT32_MAX});
+  const int feat_cap = (int)std::min<int64_t>({f0 * sc, 4 * (int64_t)key_cap, INT32_MAX});
   // every octave's gradient planes stay until the frame's describe launches
   // (octave sizes nel, nel / 4, <= nel / 16, <= nel / 64)
   const size_t ngrad = 3 * ((size_t)nel + nel / 4 + nel / 16 + nel / 64 + 64);
@@ -238,6 +239,9 @@ int ensure_slot(const SiftState* s, Slot& sl, int w, int h) {
     return SCM_E_INVALID;
   }
   sl.nel_cap = nel;
+  sl.caps_at_bound = cand_cap == std::min<int64_t>(INT32_MAX, 3 * nel + 64) &&
+                     key_cap == std::min<int64_t>(INT32_MAX, 4 * nel + 64) &&
+                     feat_cap == std::min<int64_t>(INT32_MAX, 4 * (int64_t)key_cap);
   return SCM_OK;
 }
 
@@ -448,16 +452,25 @@ int harvest(Slot& sl, uint64_t image_id, scm_blob* kp_out, scm_blob* desc_out, s
 
 }  // namespace
 
-// Harvest of slot sl's frame j; on overflow the slot's capacities grow and the
-// frame is extracted again (synchronously) until it fits.
+// Harvest of slot sl's frame j; on overflow the slot's capacities grow 4x and
+// the frame is extracted again (synchronously) until it fits.  The capacities
+// reach their hard bounds (ensure_slot: one candidate per detection-level
+// pixel, three keypoints per octave pixel, four features per keypoint) after
+// at most ~12 regrowths; an overflow at those bounds is an internal error.
+// The enlarged workspace stays with the slot (it is reused by later frames).
 int harvest_or_regrow(SiftState* s, Slot& sl, int64_t j, const uint64_t* ids,
                       const scm_frame* frames, scm_blob* kp_out, scm_blob* desc_out,
                       scm_blob* cam_out) {
-  for (;;) {
+  for (int regrow = 0;; ++regrow) {
     bool overflow = false;
     SCM_TRY(harvest(sl, ids[j], &kp_out[j], &desc_out[j], &cam_out[j], &overflow));
     if (!overflow) return SCM_OK;
-    sl.cap_scale *= 4;
+    if (sl.caps_at_bound || regrow >= 16) {
+      set_error("scm_extract_frames: frame " + std::to_string(j) +
+                " overflows the SIFT capacities at their upper bounds");
+      return SCM_E_CAPACITY;
+    }
+    sl.cap_scale = std::min<int64_t>(sl.cap_scale * 4, (int64_t)1 << 40);
     sl.nel_cap = 0;  // re-layout the workspace with the larger capacities
     SCM_TRY(enqueue_frame(s, sl, frames[j]));
   }

@@ -130,13 +130,54 @@ def test_execute_batch_id_collisions_per_element(what):
                                                zip(stencils[1], (ids[2], kps[2], descs[2]))]))
 
 
+def _sampled(n):
+    """Bytes of an n-byte buffer that the speculation fingerprint reads
+    (scm_runtime.cpp sample_words): 64 8-byte words at i * stride, stride =
+    ((n - 8) // 64) rounded down to a multiple of 8, and the last 8 bytes."""
+    m = np.zeros(n, bool)
+    if n < 520:
+        m[:] = True
+        return m
+    stride = ((n - 8) // 64) & ~7
+    for i in range(64):
+        m[i * stride:i * stride + 8] = True
+    m[n - 8:] = True
+    return m
+
+
+def _unsampled_variant(kp, desc, seed, what):
+    """Same id and counts, other bytes, every sampled word unchanged."""
+    rng = np.random.default_rng(seed)
+    d = np.frombuffer(desc, np.uint8).copy()
+    k = np.frombuffer(kp, np.uint8).copy()
+    if what == "desc":
+        body = d[16:]
+        free = np.flatnonzero(~_sampled(len(body)))
+        pick = free[rng.random(len(free)) < 0.5]
+        body[pick] = body[rng.permutation(pick)]
+    else:
+        body = k[8:]
+        m = _sampled(len(body)).reshape(-1, 24)[:, :8].any(axis=1)  # x, y of keypoint q
+        xy = body.view(np.float32).reshape(-1, 6)
+        rows = np.flatnonzero(~m)
+        xy[rows, :2] += rng.normal(0, 3.0, size=(len(rows), 2)).astype(np.float32)
+    assert (np.frombuffer(desc, np.uint8)[16:][_sampled(len(d) - 16)] == d[16:][_sampled(len(d) - 16)]).all()
+    assert (np.frombuffer(kp, np.uint8)[8:][_sampled(len(k) - 8)] == k[8:][_sampled(len(k) - 8)]).all()
+    return k.tobytes(), d.tobytes()
+
+
 @pytest.mark.parametrize("what", ["desc", "kp"])
-def test_execute_stencil_buffers_rewritten_in_place(what):
+@pytest.mark.parametrize("sampled", [True, False])
+def test_execute_stencil_buffers_rewritten_in_place(what, sampled):
     """Scanner hands consecutive calls the same element buffers, and a caller
-    may rewrite a buffer in place between calls (same address, same size,
-    other image).  Buffers seen in the previous call take its content keys
-    speculatively while the GPU runs; a key that does not hold must discard
-    the run and give exactly the oracle's rows for the new bytes."""
+    (or a recycling allocator) may put another image into a buffer between
+    calls (same address, same size, other bytes).  A buffer seen in the
+    previous call takes its content key speculatively while the GPU runs only
+    if a sample of its words is unchanged; a rewrite that changes sampled
+    words is hashed before the run (no rerun, one upload), and one that leaves
+    them alone is caught by the full hash after the run: the run is discarded
+    and the call runs again, keeping the image cache (again one upload).
+    Either way the rows are exactly the oracle's for the new bytes."""
     n, K = 6, 4
     ids, kps, descs = table_rows(Corridor(n, 700, K, seed=71).images())
     kb = [bytearray(x) for x in kps]
@@ -144,11 +185,13 @@ def test_execute_stencil_buffers_rewritten_in_place(what):
     st = (ids[:K], kb[:K], db[:K])
     with Context(0) as ctx:
         assert ctx.execute_stencil(*st) == oracle.execute_stencil(ids[:K], kps[:K], descs[:K])
-        # unchanged buffers: every image served from HBM
+        # unchanged buffers: every image served from HBM, every key speculated
         assert ctx.execute_stencil(*st) == oracle.execute_stencil(ids[:K], kps[:K], descs[:K])
         r0, u0 = ctx.stencil_stats()
         assert u0 == K and r0 == K
-        kv, dv = _variant(kps[2], descs[2], 72, what)
+        s0 = ctx.stencil_spec_stats()
+        assert s0 == (K, 0, 0)
+        kv, dv = (_variant if sampled else _unsampled_variant)(kps[2], descs[2], 72, what)
         kb[2][:] = kv
         db[2][:] = dv
         want = oracle.execute_stencil(ids[:K], [bytes(x) for x in kb[:K]],
@@ -156,8 +199,41 @@ def test_execute_stencil_buffers_rewritten_in_place(what):
         assert want != oracle.execute_stencil(ids[:K], kps[:K], descs[:K])
         assert ctx.execute_stencil(*st) == want
         r1, u1 = ctx.stencil_stats()
-        # the run with the stale key is discarded; the rerun starts from an
-        # empty cache and uploads every image of the stencil once
-        assert u1 - u0 == K and r1 == r0
+        s1 = ctx.stencil_spec_stats()
+        # the changed image is the only upload; the cache survives a rerun
+        assert u1 - u0 == 1 and r1 - r0 == K - 1
+        if sampled:
+            assert s1 == (s0[0] + K - 1, 1, 0)
+        else:
+            assert s1 == (s0[0] + K, 0, 1)
         assert ctx.execute_stencil(*st) == want
         assert ctx.stencil_stats() == (r1 + K, u1)
+
+
+def test_execute_stencil_recycled_buffers():
+    """A recycling allocator: the buffer of the image that leaves the stencil
+    receives the image that enters it (same address, same size, other bytes)
+    on every call.  The sampled words refuse the stale key before the run, so
+    no call runs twice, each call uploads only its new image, and every row is
+    the oracle's."""
+    n, K = 12, 4
+    ids, kps, descs = table_rows(Corridor(n, 600, K, seed=74).images())
+    assert len({len(x) for x in kps}) == 1 and len({len(x) for x in descs}) == 1
+    kb = [bytearray(kps[i]) for i in range(K)]
+    db = [bytearray(descs[i]) for i in range(K)]
+    slot = list(range(K))  # slot[s] = buffer holding stencil entry s
+    with Context(0) as ctx:
+        for r in range(n - K + 1):
+            if r > 0:  # image r - 1 leaves, image r + K - 1 enters its buffer
+                b = slot.pop(0)
+                kb[b][:] = kps[r + K - 1]
+                db[b][:] = descs[r + K - 1]
+                slot.append(b)
+            st = (ids[r:r + K], [kb[b] for b in slot], [db[b] for b in slot])
+            assert ctx.execute_stencil(*st) == oracle.execute_stencil(ids[r:r + K], kps[r:r + K],
+                                                                      descs[r:r + K]), r
+        spec, refused, rerun = ctx.stencil_spec_stats()
+        reused, uploaded = ctx.stencil_stats()
+    assert rerun == 0
+    assert refused == n - K  # one recycled buffer per call after the first
+    assert uploaded == K + (n - K) and reused == (n - K) * (K - 1)
