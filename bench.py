@@ -407,12 +407,15 @@ def main():
     last = {}
 
     def step():
-        packed, _ = plan.step(ctx, device=device)
+        # N > 1: the step's io.cc rows travel to rank 0 on the plan's gather
+        # thread while the next step computes (drained before the clock stops)
+        packed, _ = plan.step(ctx, device=device, background=world > 1, keep=False)
         last["packed"] = packed
         return ctx.table_timings()
 
     for _ in range(args.warmup):
         step()
+    plan.drain()
     if world > 1:
         dist.barrier()
     if torch.cuda.is_available():
@@ -433,6 +436,9 @@ def main():
         evals_f += tm["evals_f"]
         evals_h += tm["evals_h"]
         launches += tm["match_launches"]
+    t_tail = time.perf_counter()
+    plan.drain()  # the last steps' gathers: the exposed tail of the overlapped gather
+    gather_tail_ms = (time.perf_counter() - t_tail) * 1e3
     if world > 1:
         dist.barrier()
     if torch.cuda.is_available():
@@ -591,6 +597,13 @@ def main():
             "stage_ms_per_step": {"match": round(match_ms / steps, 3),
                                   "finalize": round(final_ms / steps, 3),
                                   "verify": round(verify_ms / steps, 3)},
+            "gather": ({"how": ("each step's packed io.cc rows (offsets + bytes, two P2P messages per "
+                                "rank) gathered to rank 0 on a background thread while the next step "
+                                "computes; the last ones drained inside the timed region"),
+                        "backend": args.dist_backend,
+                        "avg_gather_ms": (round(float(np.mean(plan.gatherer.ms)), 2)
+                                          if plan.gatherer and plan.gatherer.ms else None),
+                        "tail_ms_rank0": round(gather_tail_ms, 2)} if world > 1 else None),
             "cpu_baseline": cpu,
             "parity": parity,
             "drop_in": drop_in,

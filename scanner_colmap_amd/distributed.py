@@ -9,8 +9,6 @@ RCCL over xGMI when the process group is `nccl`, gloo on CPU in the tests.
 """
 from __future__ import annotations
 
-import struct
-
 import numpy as np
 
 
@@ -45,93 +43,147 @@ def table_range(row_begin: int, row_end: int, num_rows: int, overlap: int) -> tu
     return row_begin, min(num_rows, row_end + overlap - 1)
 
 
-def pack_rows(pair_blobs: list[bytes], tvg_blobs: list[bytes]) -> bytes:
-    parts = [struct.pack("<Q", len(pair_blobs))]
-    for a, b in zip(pair_blobs, tvg_blobs):
-        parts.append(struct.pack("<QQ", len(a), len(b)))
-        parts.append(a)
-        parts.append(b)
-    return b"".join(parts)
+class _Staging:
+    """Persistent transfer buffers of the nccl gather (grown, never shrunk):
+    a pinned host buffer and a device buffer for the sender's H2D hop, and a
+    ring of two pinned host buffers for rank 0's D2H (a gather's views stay
+    valid until the gather after next)."""
+
+    def __init__(self):
+        self.pin = None
+        self.dev = None
+        self.ring = [None, None]
+        self.k = 0
+
+    @staticmethod
+    def _grow(buf, n, **kw):
+        import torch
+        if buf is None or buf.numel() < n:
+            buf = torch.empty(max(n, 1 << 20), dtype=torch.uint8, **kw)
+        return buf
+
+    def send_buffers(self, n, device):
+        self.pin = self._grow(self.pin, n, pin_memory=True)
+        self.dev = self._grow(self.dev, n, device=device)
+        return self.pin, self.dev
+
+    def recv_host(self, n):
+        self.k ^= 1
+        self.ring[self.k] = self._grow(self.ring[self.k], n, pin_memory=True)
+        return self.ring[self.k]
 
 
-def unpack_rows(buf: bytes) -> tuple[list[bytes], list[bytes]]:
-    (n,) = struct.unpack_from("<Q", buf, 0)
-    off = 8
-    pa, pb = [], []
-    for _ in range(n):
-        la, lb = struct.unpack_from("<QQ", buf, off)
-        off += 16
-        pa.append(bytes(buf[off:off + la]))
-        off += la
-        pb.append(bytes(buf[off:off + lb]))
-        off += lb
-    return pa, pb
+def gather_packed(offsets: np.ndarray, data: np.ndarray, device=None, staging=None):
+    """Gather every rank's scm_table_run_packed output (element offsets and
+    packed element bytes) to rank 0: a list of (offsets int64 array, data
+    uint8 array) per rank on rank 0, None elsewhere.
 
-
-def pack_packed(offsets: np.ndarray, data: np.ndarray) -> np.ndarray:
-    """Payload of one rank's scm_table_run_packed output: element count,
-    the 2n+1 element offsets, then the packed element bytes."""
-    offs = np.ascontiguousarray(offsets, dtype=np.int64)
-    head = np.array([offs.size], dtype=np.int64)
-    return np.concatenate([head.view(np.uint8), offs.view(np.uint8),
-                           np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)])
-
-
-def unpack_packed(buf) -> tuple[list[bytes], list[bytes]]:
-    """Inverse of pack_packed, split into (pair_image_ids, tvgs) rows."""
-    b = np.frombuffer(buf, dtype=np.uint8) if isinstance(buf, (bytes, bytearray)) else buf
-    (n,) = b[:8].view(np.int64)
-    offs = b[8:8 + 8 * n].view(np.int64)
-    data = b[8 + 8 * n:]
-    rows = (n - 1) // 2
-    pa = [data[offs[2 * r]:offs[2 * r + 1]].tobytes() for r in range(rows)]
-    pb = [data[offs[2 * r + 1]:offs[2 * r + 2]].tobytes() for r in range(rows)]
-    return pa, pb
-
-
-def gather_to_root(payload, device=None) -> list[bytes] | None:
-    """Gather every rank's byte payload (bytes or a uint8 numpy array) to
-    rank 0 (None elsewhere).
-
-    Sizes are exchanged with an all_gather of one int64 per rank; then ONE
-    batch_isend_irecv group moves every rank's exact payload to rank 0 (no
-    padding): rank r > 0 posts its send, rank 0 posts all receives at once into
-    views of one flat buffer.  On the `nccl` backend (RCCL over xGMI) the
-    group is device-resident end to end -- each sender stages its payload once
-    host -> device (the library's io.cc rows live in pinned host memory), each
-    peer's bytes travel over its own xGMI link to GPU 0, and rank 0 copies the
-    flat buffer to the host once; on gloo the same group runs on CPU tensors."""
+    Sizes travel in one all_gather (two int64 per rank); then ONE
+    batch_isend_irecv group moves each rank's offsets and bytes to rank 0 as
+    two messages (no packing copy), rank 0 posting every receive at once into
+    slices of one flat buffer.  On `nccl` (RCCL over xGMI) a sender stages its
+    bytes into a persistent pinned buffer and one H2D copy, each peer's bytes
+    travel over its own xGMI link to GPU 0, and rank 0 makes one D2H copy into
+    a pinned ring buffer; the per-rank results are views into it.  On gloo the
+    same group runs on CPU tensors with no staging."""
     import torch
     import torch.distributed as dist
 
     world = dist.get_world_size()
     rank = dist.get_rank()
     dev = device if device is not None else torch.device("cpu")
-    src = (np.frombuffer(payload, dtype=np.uint8) if isinstance(payload, (bytes, bytearray))
-           else np.ascontiguousarray(payload, dtype=np.uint8).reshape(-1))
-    n = torch.tensor([src.size], dtype=torch.int64, device=dev)
-    sizes = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(world)]
-    dist.all_gather(sizes, n)
-    sizes = [int(s.item()) for s in sizes]
+    on_gpu = dev.type != "cpu"
+    offs = np.ascontiguousarray(offsets, dtype=np.int64).reshape(-1)
+    dat = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+    ob = offs.view(np.uint8)
+    meta = torch.tensor([[ob.size, dat.size]], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros(1, 2, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(sizes, meta)
+    sizes = [tuple(int(x) for x in t.cpu().view(-1)) for t in sizes]
     if rank != 0:
-        if sizes[rank]:
-            host = torch.from_numpy(src if src.flags.writeable else src.copy())
-            t = host.to(dev, non_blocking=False) if dev.type != "cpu" else host
-            for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, t, 0)]):
-                w.wait()
+        no, nd = sizes[rank]
+        if no + nd == 0:
+            return None
+        if on_gpu:
+            pin, dbuf = (staging or _Staging()).send_buffers(no + nd, dev)
+            hp = pin.numpy()
+            hp[:no] = ob
+            hp[no:no + nd] = dat
+            dbuf[:no + nd].copy_(pin[:no + nd], non_blocking=True)
+            t_o, t_d = dbuf[:no], dbuf[no:no + nd]
+        else:
+            t_o, t_d = torch.from_numpy(ob), torch.from_numpy(dat if dat.flags.writeable else dat.copy())
+        ops = [dist.P2POp(dist.isend, t, 0) for t in (t_o, t_d) if t.numel()]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
         return None
-    offs = np.concatenate([[0], np.cumsum(sizes[1:])]).astype(np.int64)
-    flat = torch.empty(int(offs[-1]), dtype=torch.uint8, device=dev)
-    ops = [dist.P2POp(dist.irecv, flat[int(offs[r - 1]):int(offs[r])], r)
-           for r in range(1, world) if sizes[r]]
+    starts = np.concatenate([[0], np.cumsum([a + b for a, b in sizes[1:]])]).astype(np.int64)
+    total = int(starts[-1])
+    flat = torch.empty(total, dtype=torch.uint8, device=dev)
+    ops = []
+    for r in range(1, world):
+        a, no, nd = int(starts[r - 1]), sizes[r][0], sizes[r][1]
+        if no:
+            ops.append(dist.P2POp(dist.irecv, flat[a:a + no], r))
+        if nd:
+            ops.append(dist.P2POp(dist.irecv, flat[a + no:a + no + nd], r))
     if ops:
         for w in dist.batch_isend_irecv(ops):
             w.wait()
-    host = flat.cpu().numpy() if dev.type != "cpu" else flat.numpy()
-    out = [src.tobytes()]
+    if on_gpu and total:
+        host_t = (staging or _Staging()).recv_host(total)
+        host_t[:total].copy_(flat)
+        host = host_t.numpy()
+    else:
+        host = flat.numpy()
+    out = [(offs, dat)]
     for r in range(1, world):
-        out.append(host[int(offs[r - 1]):int(offs[r])].tobytes())
+        a, no, nd = int(starts[r - 1]), sizes[r][0], sizes[r][1]
+        out.append((host[a:a + no].view(np.int64), host[a + no:a + no + nd]))
     return out
+
+
+class Gatherer:
+    """Runs gather_packed on a background thread, one gather at a time in step
+    order, so that step k's rows travel to rank 0 while step k + 1 computes.
+    At most two gathers are outstanding (submit waits for the older one)."""
+
+    def __init__(self, device=None):
+        from concurrent.futures import ThreadPoolExecutor
+        self.device = device
+        self.pool = ThreadPoolExecutor(max_workers=1)
+        self.pending = []
+        self.done = []  # results of the gathers already waited for, in step order
+        self.staging = _Staging()
+        self.ms = []  # duration of each gather (ms)
+
+    def _run(self, packed):
+        import time
+        if self.device is not None and self.device.type == "cuda":
+            import torch
+            torch.cuda.set_device(self.device)
+        t0 = time.perf_counter()
+        out = gather_packed(packed.offsets, packed.data, self.device, self.staging)
+        self.ms.append((time.perf_counter() - t0) * 1e3)
+        return out
+
+    def submit(self, packed, keep: bool = True):
+        while len(self.pending) >= 2:
+            f, k = self.pending.pop(0)
+            r = f.result()
+            if k:
+                self.done.append(r)
+        self.pending.append((self.pool.submit(self._run, packed), keep))
+
+    def drain(self) -> list:
+        """Wait for every outstanding gather; the kept results in step order
+        (rank 0's (offsets, data) views stay valid until two more gathers ran)."""
+        for f, k in self.pending:
+            r = f.result()
+            if k:
+                self.done.append(r)
+        out, self.done, self.pending = self.done, [], []
+        return out
 
 
 class ShardPlan:
@@ -153,6 +205,7 @@ class ShardPlan:
         self.row_begin, self.row_end = shard_rows(self.total_images, overlap, world, rank)
         self.table_begin, self.table_end = table_range(self.row_begin, self.row_end,
                                                        self.total_images, overlap)
+        self.gatherer = None
 
     @property
     def local_rows(self) -> tuple[int, int]:
@@ -162,28 +215,40 @@ class ShardPlan:
     def pairs(self) -> int:
         return int(pairs_per_row(self.total_images, self.overlap)[self.row_begin:self.row_end].sum())
 
-    def step(self, runner, device=None):
+    def step(self, runner, device=None, background: bool = False, keep: bool = True):
         """One pass of the op over this rank's rows: `runner.table_run_packed`
         (the scm_table_run_packed binding, or a stand-in with the same
         result shape), then for world > 1 the gather of the packed io.cc rows
         to rank 0.  Returns (this rank's packed rows, the gathered per-rank
-        payloads on rank 0 / None)."""
+        (offsets, data) on rank 0 / None).  With `background` the gather runs
+        on the plan's Gatherer thread while the caller goes on (the next
+        step's compute), the second value is None, and drain() returns the
+        gathered results (`keep` False: the result is dropped once done, as
+        the bench does)."""
         lb, le = self.local_rows
         packed = runner.table_run_packed(self.overlap, lb, le)
         gathered = None
         if self.world > 1:
-            gathered = gather_to_root(pack_packed(packed.offsets, packed.data), device=device)
+            if background:
+                if self.gatherer is None:
+                    self.gatherer = Gatherer(device)
+                self.gatherer.submit(packed, keep)
+            else:
+                gathered = gather_packed(packed.offsets, packed.data, device)
         return packed, gathered
+
+    def drain(self) -> list:
+        """Wait for the background gathers; rank 0: their results in step order."""
+        return self.gatherer.drain() if self.gatherer is not None else []
 
 
 def merge_gathered(payloads: list) -> tuple[list[bytes], list[bytes]]:
-    """Rank 0: concatenate the gathered per-rank packed rows in rank order
-    (= pivot-row order) into (pair_image_ids rows, two_view_geometries rows)."""
+    """Rank 0: concatenate the gathered per-rank packed rows (gather_packed's
+    (offsets, data) pairs) in rank order (= pivot-row order) into
+    (pair_image_ids rows, two_view_geometries rows)."""
     rows_a, rows_b = [], []
-    for p in payloads:
-        if len(p) == 0:
-            continue
-        a, b = unpack_packed(p)
-        rows_a += a
-        rows_b += b
+    for offs, data in payloads:
+        for r in range((len(offs) - 1) // 2):
+            rows_a.append(data[offs[2 * r]:offs[2 * r + 1]].tobytes())
+            rows_b.append(data[offs[2 * r + 1]:offs[2 * r + 2]].tobytes())
     return rows_a, rows_b

@@ -29,13 +29,17 @@ def test_shard_rows_partition(n, K, world):
         assert ta == a and tb == min(n, b + K - 1)
 
 
-def test_pack_unpack_packed():
+def test_merge_gathered():
+    """Rank 0's per-rank (offsets, packed bytes) payloads -> the two output
+    columns' rows in rank order; empty ranks contribute nothing."""
     rows_a = [b"\x01\x00\x00\x00\x00\x00\x00\x00\x05\x00\x00\x00", b"\x00" * 8]
     rows_b = [b"abc" * 5, b"\x0c" + b"\x00" * 11]
     data = b"".join(x for pair in zip(rows_a, rows_b) for x in pair)
-    offs = np.cumsum([0] + [len(x) for pair in zip(rows_a, rows_b) for x in pair])
-    payload = sd.pack_packed(offs, np.frombuffer(data, np.uint8))
-    assert sd.unpack_packed(payload.tobytes()) == (rows_a, rows_b)
+    offs = np.cumsum([0] + [len(x) for pair in zip(rows_a, rows_b) for x in pair]).astype(np.int64)
+    empty = (np.zeros(1, np.int64), np.zeros(0, np.uint8))
+    got = sd.merge_gathered([(offs[:3], np.frombuffer(data, np.uint8)[:offs[2]]), empty,
+                             (offs[2:] - offs[2], np.frombuffer(data, np.uint8)[offs[2]:])])
+    assert got == (rows_a, rows_b)
 
 
 def _free_port():
@@ -66,7 +70,7 @@ class _OracleRunner:
         return _P()
 
 
-def _rank_main(rank, world, port, n, K, scaling, q):
+def _rank_main(rank, world, port, n, K, scaling, q, background=False, steps=1):
     import torch.distributed as dist
 
     from oracle import oracle
@@ -78,15 +82,25 @@ def _rank_main(rank, world, port, n, K, scaling, q):
     try:
         # bench.py's own sharding and step: ShardPlan -> table slice with the
         # halo -> runner.table_run_packed over the local rows -> P2P gather
+        # (synchronous, or on the plan's background thread over several steps)
         plan = sd.ShardPlan(n, K, world, rank, scaling)
         c = Corridor(plan.total_images, 400, K, seed=53)
         runner = _OracleRunner(*table_rows(c.images(plan.table_begin, plan.table_end)))
-        _, got = plan.step(runner)
+        results = []
+        for _ in range(steps):
+            _, got = plan.step(runner, background=background)
+            results.append(got)
+        if background:
+            assert results == [None] * steps
+            results = plan.drain()
         if rank == 0:
-            rows_a, rows_b = sd.merge_gathered(got)
             ids, kps, descs = table_rows(c.images())
             ref = oracle.table_run(ids, kps, descs, K, 0, plan.total_images)
-            q.put((rows_a == ref[0], rows_b == ref[1], len(rows_a), plan.total_images))
+            ok = [sd.merge_gathered(g) == (ref[0], ref[1]) for g in results]
+            rows_a, _ = sd.merge_gathered(results[-1])
+            q.put((all(ok) and len(ok) == steps, True, len(rows_a), plan.total_images))
+        else:
+            assert all(g is None for g in results)
     finally:
         dist.destroy_process_group()
 
@@ -110,19 +124,27 @@ def test_gloo_shard_step_world2(n, K, scaling):
     assert total == (n if scaling == "strong" else n * world)
 
 
+def _payload(rank, n):
+    rng = np.random.default_rng(rank)
+    data = rng.integers(0, 256, n, dtype=np.uint8)
+    cuts = np.sort(rng.integers(0, n + 1, 4)) if n else np.zeros(4, np.int64)
+    return np.concatenate([[0], cuts, [n]]).astype(np.int64), data
+
+
 def _gather_main(rank, world, port, sizes, q):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        rng = np.random.default_rng(rank)
-        payload = rng.integers(0, 256, sizes[rank], dtype=np.uint8)
-        got = sd.gather_to_root(payload if rank % 2 else payload.tobytes())
+        offs, data = _payload(rank, sizes[rank])
+        got = sd.gather_packed(offs, data)
         if rank == 0:
-            ref = [np.random.default_rng(r).integers(0, 256, sizes[r], dtype=np.uint8).tobytes()
-                   for r in range(world)]
-            q.put(got == ref)
+            ok = len(got) == world
+            for r in range(world):
+                ro, rd = _payload(r, sizes[r])
+                ok = ok and (got[r][0] == ro).all() and got[r][1].tobytes() == rd.tobytes()
+            q.put(bool(ok))
         else:
             q.put(got is None)
     finally:
@@ -131,8 +153,9 @@ def _gather_main(rank, world, port, sizes, q):
 
 @pytest.mark.parametrize("sizes", [[5, 0, 70000, 1], [0, 0, 0, 0], [0, 3, 0, 12345]])
 def test_gloo_gather_world4_uneven_and_empty(sizes):
-    """gather_to_root (one batch_isend_irecv group) at world 4: empty payloads
-    on any rank (rank 0 included), uneven sizes, bytes and numpy inputs."""
+    """gather_packed (one batch_isend_irecv group, offsets and bytes as two
+    messages per rank) at world 4: empty payloads on any rank (rank 0
+    included), uneven sizes."""
     world = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -144,6 +167,25 @@ def test_gloo_gather_world4_uneven_and_empty(sizes):
         p.join(timeout=120)
     assert [p.exitcode for p in procs] == [0] * world
     assert all(q.get(timeout=5) for _ in range(world))
+
+
+def test_gloo_background_gather_world2():
+    """The bench's overlapped form: three steps whose gathers run on the
+    plan's background thread while the next step computes; drain() returns
+    every step's gathered rows, each equal to a one-rank run."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, 7, 4, "strong", q, True, 3))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert [p.exitcode for p in procs] == [0, 0]
+    ok, _, nrows, total = q.get(timeout=5)
+    assert ok and nrows == total == 7
 
 
 @pytest.mark.parametrize("n,K,scaling", [(6, 4, "strong"), (3, 5, "weak")])
