@@ -300,6 +300,15 @@ def cpu_model() -> str:
     return "unknown"
 
 
+def lib_sha16() -> str:
+    """sha256[:16] of the libscm.so this process loads (PMC summaries record
+    the hash of the library they profiled; a summary of another build is
+    reported as stale, never as this run's figures)."""
+    import hashlib
+    from scanner_colmap_amd._abi import LIB_PATH
+    return hashlib.sha256(open(LIB_PATH, "rb").read()).hexdigest()[:16]
+
+
 def pmc_traffic(workload: str, kpts: int, images: int, kernel: str):
     """HBM bytes per matcher launch from the committed rocprofv3 PMC summary
     of this workload (profiles/rNN_pmc_match.json, profiles/pmc_summary.py),
@@ -327,6 +336,8 @@ def pmc_sq(kernels: tuple):
         return None
     d = json.load(open(files[-1]))
     out = {k: d[k] for k in kernels if k in d}
+    if out:
+        out["lib_sha16"] = d.get("lib_sha16")
     return (out, os.path.relpath(files[-1], ROOT)) if out else None
 
 
@@ -475,14 +486,32 @@ def main():
         sq = pmc_sq((kernel, "rs_score_kernel<1>", "rs_score_kernel<0>"))
         launch_s = match_ms * 1e-3 / launches  # average matcher launch (HIP events)
         hbm = {}
+        util = {}
+        stale = {}
+        loaded_sha = lib_sha16()
         if pmc:
             gbps = pmc[0]["traffic_bytes_per_launch"] / launch_s / 1e9
             hbm = {"hbm_gbps": round(gbps, 1), "hbm_frac": round(gbps / HBM_PEAK_GBPS, 4)}
-        util = {}
+            if pmc[0].get("lib_sha16") != loaded_sha:
+                stale["traffic"] = round(pmc[0]["traffic_bytes_per_launch"])
+                stale["traffic_source"] = pmc[1]
+                stale.update(hbm)
+                stale["traffic_lib_sha16"] = pmc[0].get("lib_sha16")
+                hbm = {}
+                pmc = None
         if sq and kernel in sq[0]:
             k = sq[0][kernel]
             util = {"mfma_busy": round(k["mfma_busy"], 4), "valu_per_mfma": round(k["valu_per_mfma"], 2),
                     "util_source": f"{sq[1]} (SQ PMC, separate rocprofv3 passes of one bench step)"}
+            if sq[0].get("lib_sha16") != loaded_sha:
+                stale.update(util)
+                stale["util_lib_sha16"] = sq[0].get("lib_sha16")
+                util = {}
+                sq = None
+        if stale:
+            stale["loaded_lib_sha16"] = loaded_sha
+            stale["note"] = ("committed PMC summaries of another libscm.so build: not this run's "
+                             "kernels, kept only for reference")
         cpu = parity = None
         if check_pairs:
             if args.no_cpu_baseline:  # parity only, with the oracle's BLAS-dot matcher
@@ -561,6 +590,7 @@ def main():
                 "algorithmic_bytes_per_launch": round(alg_bytes_launch),
                 **hbm,
                 **util,
+                **({"stale_profile": stale} if stale else {}),
                 "launches_per_step": round(launches / steps, 2),
                 "wall_achieved": round(wall_tops, 2),
                 "wall_frac": round(wall_tops / peak, 4),

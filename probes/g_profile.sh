@@ -7,6 +7,7 @@ R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/$S
 mkdir -p $O
 cd $R
+sha256sum scanner_colmap_amd/lib/libscm.so | cut -c1-16 > $O/lib_sha16
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
 fi

@@ -24,11 +24,21 @@ DEFAULT = {
 }
 
 
+def lib_sha(v):
+    """bench.py uses a summary only when this hash equals the loaded library's."""
+    import os
+    if v and os.path.exists(v):
+        return open(v).read().split()[0][:16]
+    return v
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("out_json")
     ap.add_argument("dirs", nargs="+")
     ap.add_argument("--kernel", action="append", default=[])
+    ap.add_argument("--lib-sha16", default=None,
+                    help="sha256[:16] of the libscm.so the profiled run loaded (or a file holding it)")
     a = ap.parse_args()
     kernels = dict(k.split("=", 1) for k in a.kernel) if a.kernel else DEFAULT
     out = {}
@@ -61,8 +71,11 @@ def main():
                                   "active_inst_any": per.get("SQ_ACTIVE_INST_ANY", 0.0) / w}
                                  if w else None),
         }
+    out["lib_sha16"] = lib_sha(a.lib_sha16)
     json.dump(out, open(a.out_json, "w"), indent=1)
     for k, v in out.items():
+        if not isinstance(v, dict):
+            continue
         print(k, v["dispatches"], {x: v[x] for x in ("valu_per_mfma", "mfma_busy",
                                                      "valu_active_frac_of_simd_cycles")})
 

@@ -25,6 +25,14 @@ def per_dispatch(path, kernel, counter):
     return [vals[k] for k in sorted(vals)]
 
 
+def lib_sha(v):
+    """bench.py uses a summary only when this hash equals the loaded library's."""
+    import os
+    if v and os.path.exists(v):
+        return open(v).read().split()[0][:16]
+    return v
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("fetch_csv")
@@ -33,6 +41,8 @@ def main():
     ap.add_argument("--kernel", default="match_tiles_i8_kernel")
     ap.add_argument("--workload", default="synth-1000x8192-k20")
     ap.add_argument("--pairs-per-step", type=int, default=18810)
+    ap.add_argument("--lib-sha16", default=None,
+                    help="sha256[:16] of the libscm.so the profiled run loaded (or a file holding it)")
     a = ap.parse_args()
     fetch = per_dispatch(a.fetch_csv, a.kernel, "FETCH_SIZE")
     write = per_dispatch(a.write_csv, a.kernel, "WRITE_SIZE")
@@ -51,6 +61,7 @@ def main():
         "fetch_bytes_per_dispatch": fb,
         "write_bytes_per_dispatch": wb,
         "note": "FETCH_SIZE x2 (gfx950 half-count) + WRITE_SIZE, KiB -> bytes; one bench step",
+        "lib_sha16": lib_sha(a.lib_sha16),
     }
     json.dump(out, open(a.out_json, "w"), indent=1)
     print(json.dumps({k: v for k, v in out.items() if not k.endswith("dispatch")}))
