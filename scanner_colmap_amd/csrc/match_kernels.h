@@ -9,10 +9,9 @@ namespace scm {
 constexpr int kMatchWaves = 8;                   // waves per workgroup
 constexpr int kMatchThreads = kMatchWaves * 64;  // 512
 constexpr int kRowsPerBlock = kMatchWaves * 64;  // pivot rows per workgroup
-#ifndef SCM_MATCH8_WAVES
-#define SCM_MATCH8_WAVES 8  // 4 (256-row jobs, two workgroups per CU): +5% isolated, no gain beside verification
-#endif
-constexpr int kMatch8Waves = SCM_MATCH8_WAVES;   // i8 kernel: waves per workgroup
+// i8 kernel: waves per workgroup (4 = 256-row jobs, two workgroups per CU:
+// +5 % isolated, no gain beside verification)
+constexpr int kMatch8Waves = 8;
 constexpr int kMatch8Threads = kMatch8Waves * 64;
 constexpr int kRowsPerBlock8 = kMatch8Waves * 64;
 constexpr int kTileBytes = 32 * 256;             // bf16 kernel: 32 descriptors per LDS tile

@@ -451,10 +451,8 @@ __device__ __forceinline__ uint32_t merge_second_values(uint32_t b1a, uint32_t b
 // (B2' << 3) | wave of B1.
 // ===========================================================================
 constexpr int kG8T = 4;                                        // tiles per barrier group
-#ifndef SCM_G8_Q
-#define SCM_G8_Q 4
-#endif
-constexpr int kG8Q = SCM_G8_Q;                                 // groups in the LDS ring (DMA kG8Q - 1 ahead)
+// groups in the LDS ring (DMA kG8Q - 1 ahead; 3 measured equal, profiles/r03_q3_vbench.log)
+constexpr int kG8Q = 4;
 constexpr int kG8Stages = kG8T * kG8Q;                         // 16 x 8 KiB of B tiles
 static_assert(kG8Q >= 3, "the ring holds the group in use, the next, and one in flight");
 constexpr int kG8CscGroups = 3;                                // column partials of 3 groups

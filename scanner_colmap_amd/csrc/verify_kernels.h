@@ -78,10 +78,7 @@ struct RansacState {
 };
 
 // Windowed verifier: up to kMaxWindow rounds of kTrialBatch hypotheses.
-#ifndef SCM_MAX_WINDOW
-#define SCM_MAX_WINDOW 32  // 16: -1.3 %, 64: -1 % (bench, s35)
-#endif
-constexpr int kMaxWindow = SCM_MAX_WINDOW;
+constexpr int kMaxWindow = 32;  // rounds per window at most (16: -1.3 %, 64: -1 %, bench s35)
 constexpr int kWindowTrials = kMaxWindow * kTrialBatch;
 
 // Device buffers of the windowed verifier (V = pairs of a batch, T =

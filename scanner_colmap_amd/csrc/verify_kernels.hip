@@ -65,9 +65,6 @@ struct __attribute__((aligned(16))) VerifyLds {
   // Tail: the sequential LO-RANSAC of verify_final_kernel only (the watermark).
   uint32_t samples[kTrialBatch][8];
 };
-#ifndef SCM_REPLAY_ATTR
-#define SCM_REPLAY_ATTR
-#endif
 constexpr size_t kVerifyLdsHead = __builtin_offsetof(VerifyLds, samples);
 
 // ---------------------------------------------------------------------------
@@ -2159,7 +2156,7 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
 
 // RandomSampler::Sample's Shuffle for every trial of the window: the swap
 // chain of one pair is sequential, so each lane runs one pair's chain; the
-// pairs' sample-index vectors are staged in LDS (SCM_SHUFFLE_LDS_KB per
+// pairs' sample-index vectors are staged in LDS (kShuffleLdsKb per
 // block) so that every swap costs one LDS round trip.  The targets drawn by
 // rs_draw_kernel are read from samp and replaced by the trial's sample.
 // One pair's swap chain over Btot trials: the trial's kmin targets are read
@@ -2572,9 +2569,7 @@ __global__ __launch_bounds__(64) void rs_drawshuffle_wave2_kernel(
 
 // Minimal solvers, one thread per hypothesis of the window, plus the fp32
 // filter constants of every model.
-#ifndef SCM_SOLVE_GRID
-#define SCM_SOLVE_GRID 4096  // 1024 / 2048 / 3072: equal or slower (profiles/r02_m_solve_vbench.log)
-#endif
+constexpr int kSolveGrid = 4096;  // 1024 / 2048 / 3072: equal or slower (profiles/r02_m_solve_vbench.log)
 template <int K>
 __global__ __launch_bounds__(64) void rs_solve_kernel(
     const VerifyPair* __restrict__ pairs, const double* __restrict__ xy1_all,
@@ -2625,36 +2620,20 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
 // the filter constants of one round at a time are broadcast from LDS and
 // lane t accumulates the count of hypothesis t of the round.
 constexpr int kScoreThreads = 64;
-#ifndef SCM_SCORE_HM
-#define SCM_SCORE_HM 4  // H split pass: models per loop iteration (1: the generic loop; 2, 3: -0.5 %)
-#endif
+// H split pass: models per loop iteration (2, 3: -0.5 %; 6, 8: no change,
+// profiles/r03_hm_score_models_vbench.log)
+constexpr int kScoreHm = 4;
 
-#ifndef SCM_SCORE_PCH
-#define SCM_SCORE_PCH 8
-#endif
-#ifndef SCM_SCORE_MFMA
-#define SCM_SCORE_MFMA 0  // H split pass: the three affine forms of 8 models x 32 points per f32 MFMA
-#endif
-constexpr int kScorePch = SCM_SCORE_PCH;  // points per lane
+constexpr int kScorePch = 8;  // points per lane
 constexpr int kScoreChunk = kScoreThreads * kScorePch;
-#ifndef SCM_SCORE_PCH_SMALL
-#define SCM_SCORE_PCH_SMALL 4
-#endif
-constexpr int kScorePchSmall = SCM_SCORE_PCH_SMALL;  // small batches: points per lane
-#ifndef SCM_SCORE_ITEMS
-#define SCM_SCORE_ITEMS 65536  // 16K / 32K / 131K / 262K items: -1.5 to -6 % (profiles/r02_j_*vbench.log)
-#endif
-constexpr int kScoreTargetItems = SCM_SCORE_ITEMS;  // work items per score launch
+constexpr int kScorePchSmall = 4;  // small batches: points per lane
+// work items per score launch (16K / 32K / 131K / 262K: -1.5 to -6 %, profiles/r02_j_*vbench.log)
+constexpr int kScoreTargetItems = 65536;
 
 // PCH: points per lane of a work item (kScorePch; small batches take more,
 // so that each model's constants and loop overhead serve more points).
-#ifdef SCM_SCORE_WPE
-#define SCM_SCORE_ATTR __attribute__((amdgpu_waves_per_eu(SCM_SCORE_WPE)))
-#else
-#define SCM_SCORE_ATTR
-#endif
 template <int K, bool SPLIT, int PCH = kScorePch>
-__global__ __launch_bounds__(kScoreThreads) SCM_SCORE_ATTR void rs_score_kernel(
+__global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     const VerifyPair* __restrict__ pairs, const float4* __restrict__ xyf_all,
     const RansacState* __restrict__ rst, const int32_t* __restrict__ wB,
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
@@ -2727,70 +2706,9 @@ __global__ __launch_bounds__(kScoreThreads) SCM_SCORE_ATTR void rs_score_kernel(
       int nslow = 0;
       uint32_t c0 = 0, c1 = 0, c2 = 0;  // lane t: counts of hypothesis t's models
       uint32_t u0 = 0, u1 = 0, u2 = 0;  // SPLIT: lane t: their undecided points
-      if (K == KIND_H && SPLIT && SCM_SCORE_HM > 1) {
-        // H split pass: SCM_SCORE_HM models per iteration (one model per hypothesis)
-        constexpr int NM = SCM_SCORE_HM;
-#if SCM_SCORE_MFMA
-        // Full chunks: q_k = h'_k0 s0 + h'_k1 s1 + h'_k2 of 8 models x 32 points
-        // per v_mfma_f32_32x32x2f32 (row 8k + model, column = point; the K = 2
-        // operands are s0, s1 and the C operand the constant terms).  An MFMA
-        // rounds like an fmaf chain, inside h_filter_consts' bound for q
-        // (3.01u A'); w, lhs and diff as h_filter_pair, two models per packed
-        // op.  Lane (point r, half h) holds models 4h .. 4h + 3 of the tile.
-        if (full) {
-          constexpr int NT = CH / 32;  // point tiles
-          float bv[NT], e0[NT], e1[NT];
-          const int r = lane & 31, h = lane >> 5;
-#pragma unroll
-          for (int j = 0; j < NT; ++j) {
-            const float4 v = xyf[base + 32 * j + r];
-            bv[j] = h ? v.y : v.x;
-            e0[j] = -(v.z * dsc.x);  // -d' (exact negation; w enters squared)
-            e1[j] = -(v.w * dsc.x);
-          }
-          for (int mt = 0; mt * 8 < B; ++mt) {
-            const int row = lane & 31, krow = row >> 3;
-            const float a = krow < 3 ? lc[min(mt * 8 + (row & 7), B - 1)][3 * krow + h] : 0.0f;
-            f32x16 cm;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-              const int k = i >> 2, mdl = min(mt * 8 + 4 * h + (i & 3), B - 1);
-              cm[i] = k < 3 ? lc[mdl][3 * k + 2] : 0.0f;
-            }
-            const f32x2 mg0 = f32x2{lc[min(mt * 8 + 4 * h, B - 1)][9], lc[min(mt * 8 + 4 * h + 1, B - 1)][9]};
-            const f32x2 mg1 = f32x2{lc[min(mt * 8 + 4 * h + 2, B - 1)][9], lc[min(mt * 8 + 4 * h + 3, B - 1)][9]};
-            uint32_t cnt[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cnt[k] = 0u;
-#pragma unroll
-            for (int j = 0; j < NT; ++j) {
-              const f32x16 acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, bv[j], cm, 0, 0, 0);
-              const f32x2 dd0 = f32x2(e0[j]), dd1 = f32x2(e1[j]);
-#pragma unroll
-              for (int cp = 0; cp < 2; ++cp) {
-                const f32x2 q0 = f32x2{acc[2 * cp], acc[2 * cp + 1]};
-                const f32x2 q1 = f32x2{acc[4 + 2 * cp], acc[5 + 2 * cp]};
-                const f32x2 q2 = f32x2{acc[8 + 2 * cp], acc[9 + 2 * cp]};
-                // -w_j = q_j - d'_j q_2 and -diff = q_2^2 - lhs: the same
-                // roundings as h_filter_pair up to sign
-                const f32x2 w0 = __builtin_elementwise_fma(dd0, q2, q0);
-                const f32x2 w1 = __builtin_elementwise_fma(dd1, q2, q1);
-                const f32x2 lhs = __builtin_elementwise_fma(w0, w0, w1 * w1);
-                const f32x2 ndiff = __builtin_elementwise_fma(q2, q2, -lhs);
-                const f32x2 M = cp ? mg1 : mg0;
-                const uint64_t bx = __ballot(ndiff.x >= -M.x), by = __ballot(ndiff.y >= -M.y);
-                // one count for the models of both halves (c and 4 + c): their
-                // sum bounds each (a looser bound only adds exact recounts)
-                cnt[2 * cp] += __popcll(bx);
-                cnt[2 * cp + 1] += __popcll(by);
-              }
-            }
-#pragma unroll
-            for (int k = 0; k < 8; ++k)
-              if (lane == mt * 8 + k) u0 += cnt[k & 3];
-          }
-        } else
-#endif
+      if (K == KIND_H && SPLIT) {
+        // H split pass: kScoreHm models per iteration (one model per hypothesis)
+        constexpr int NM = kScoreHm;
         for (int t = 0; t < B; t += NM) {
           HFilt f[NM];
 #pragma unroll
@@ -3274,7 +3192,7 @@ __global__ __launch_bounds__(64) void rs_shuffle2_kernel(
                             rh.samp, ppb, stride, blockIdx.x - split, gridDim.x - split);
 }
 
-__global__ __launch_bounds__(64) SCM_REPLAY_ATTR void rs_replay2_kernel(
+__global__ __launch_bounds__(64) void rs_replay2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
     VerifyRoundBufs rf, VerifyRoundBufs rh, int ain, int aout, VerifyParams P,
@@ -3350,10 +3268,7 @@ namespace {
 
 // Blocks of the wave-per-pair kernels (rs_begin / rs_draw / rs_replay) per
 // kind; pairs beyond it are taken in grid-stride order.
-#ifndef SCM_PAIR_GRID
-#define SCM_PAIR_GRID 4096  // 2048: -1 %, 16384 (a block per pair): +0.4 %, within noise (profiles/r02_o_pairgrid_vbench.log)
-#endif
-constexpr int kPairGrid = SCM_PAIR_GRID;
+constexpr int kPairGrid = 4096;  // 2048: -1 %, 16384 (a block per pair): +0.4 %, within noise (profiles/r02_o_pairgrid_vbench.log)
 
 template <typename F>
 void set_lds_attr(F f) {
@@ -3361,16 +3276,14 @@ void set_lds_attr(F f) {
                             160 * 1024);
 }
 
-#ifndef SCM_WAVE_SHUFFLE_PAIRS
-#define SCM_WAVE_SHUFFLE_PAIRS 256
-#endif
+constexpr int kWaveShufflePairs = 256;
 // Small batches: a wave per pair (rs_shuffle_wave2_kernel), four waves per
 // pair in the replay, speculative windows -- while the batch leaves most of
 // the GPU idle, latency decides.
 int wave_pairs_limit() {
   static const int v = [] {
     const char* e = getenv("SCM_WAVE_SHUFFLE_PAIRS");
-    return e ? atoi(e) : SCM_WAVE_SHUFFLE_PAIRS;
+    return e ? atoi(e) : kWaveShufflePairs;
   }();
   return v;
 }
@@ -3399,16 +3312,14 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                        hipStream_t rstream, hipEvent_t* win_ev, int* last_h) {
   const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
   const int gw = npairs < kPairGrid ? npairs : kPairGrid;
-#ifndef SCM_SHUFFLE_LDS_KB
-#define SCM_SHUFFLE_LDS_KB 16
-#endif
-  // Shuffle blocks: as many pairs per block as fit SCM_SHUFFLE_LDS_KB of LDS sample-index
+  constexpr int kShuffleLdsKb = 16;
+  // Shuffle blocks: as many pairs per block as fit kShuffleLdsKb of LDS sample-index
   // vectors (the swap chains are latency-bound; LDS instead of global memory
   // shortens every step of them).
   // (pairs above 65536 matches: vectors in global memory, stride 0, one pair per block)
   const int sh_stride = max_m <= 65536 ? (max_m + 7) / 8 * 8 : 0;
   const int sh_ppb =
-      sh_stride ? std::max(1, std::min(64, (SCM_SHUFFLE_LDS_KB * 1024) / (2 * sh_stride))) : 1;
+      sh_stride ? std::max(1, std::min(64, (kShuffleLdsKb * 1024) / (2 * sh_stride))) : 1;
   const int sh_blocks = (npairs + sh_ppb - 1) / sh_ppb;
   const int wave_stride = (max_m + 7) / 8 * 8;
   const bool wave_sh = verify_small_batch(npairs, max_m);
@@ -3445,11 +3356,11 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                          snaps, out, rf, rh, lw, sh_ppb, sh_stride, s2);
     }
     if (f)
-      hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(SCM_SOLVE_GRID), dim3(64), 0, stream, pairs, xy1, xy2,
+      hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(kSolveGrid), dim3(64), 0, stream, pairs, xy1, xy2,
                          rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.samp, rf.nmod, rf.fcon, rf.mods,
                          W, P.max_residual);
     if (h)
-      hipLaunchKernelGGL(rs_solve_kernel<KIND_H>, dim3(SCM_SOLVE_GRID), dim3(64), 0, stream, pairs, xy1, xy2,
+      hipLaunchKernelGGL(rs_solve_kernel<KIND_H>, dim3(kSolveGrid), dim3(64), 0, stream, pairs, xy1, xy2,
                          rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.samp, rh.nmod, rh.fcon, rh.mods,
                          W, P.max_residual);
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r], stream);
