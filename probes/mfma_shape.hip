@@ -61,15 +61,117 @@ __global__ __launch_bounds__(512) void shape_kernel(const i32x4* __restrict__ sr
   if ((threadIdx.x & 63) == 0) cyc[tid >> 6] = t1 - t0;
 }
 
+typedef unsigned long long u64;
+__device__ __forceinline__ u64 add_pair_u64(u64 x, u64 k, uint32_t dep) {
+  u64 d;
+  asm volatile("v_lshl_add_u64 %0, %1, 0, %2" : "=v"(d) : "v"(x), "v"(k), "v"(dep));
+  return d;
+}
+__device__ __forceinline__ uint32_t max3u(uint32_t a, uint32_t b, uint32_t c) { return max(max(a, b), c); }
+
+// The matcher's tile with a representative epilogue, operands in registers:
+// MODE 2: 32x32x32 (4 chains of 4 per 64x64 tile): per sub-tile the column
+//   max tree, 8 v_lshl_add_u64 row values, row state max3, a permlane32 fold
+//   of the column maxima per column sub-tile;
+// MODE 3: 16x16x64 (16 chains of 2): per sub-tile 2 v_lshl_add_u64, row state
+//   max3 per column pair, column maxima over the 4 row sub-tiles folded over
+//   the four 16-lane groups (permlane16 + permlane32 swaps).
+template <int MODE>
+__global__ __launch_bounds__(512) void tile_kernel(const i32x4* __restrict__ src, uint32_t* out,
+                                                   long long* cyc) {
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  i32x4 a[8], b[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    a[q] = src[(tid * 16 + q) & 0xFFFFF];
+    b[q] = src[(tid * 16 + 8 + q) & 0xFFFFF];
+  }
+  const u64 kq = ((u64)(uint32_t)src[tid & 0xFFFF][0] << 32) | (uint32_t)src[tid & 0xFFFF][1];
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  uint32_t sink = 0;
+  if (MODE == 2) {
+    uint32_t b1r[2][16] = {};
+    i32x16 ra = {};
+    for (int it = 0; it < kIter / 2; ++it) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        uint32_t cm[2];
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) {
+          i32x16 acc = ra;
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[4 * s2 + q], b[(4 * c + q + it) & 7], acc, 0, 0, 0);
+          uint32_t m = 0;
+#pragma unroll
+          for (int i = 0; i < 16; i += 2) m = max3u(m, (uint32_t)acc[i], (uint32_t)acc[i + 1]);
+          cm[s2] = m;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const u64 k = add_pair_u64(((u64)(uint32_t)acc[2 * i + 1] << 32) | (uint32_t)acc[2 * i], kq, m);
+            b1r[s2][2 * i] = max(b1r[s2][2 * i], (uint32_t)k);
+            b1r[s2][2 * i + 1] = max(b1r[s2][2 * i + 1], (uint32_t)(k >> 32));
+          }
+        }
+        const uint32_t mm = max(cm[0], cm[1]);
+        const auto sw = __builtin_amdgcn_permlane32_swap(mm, mm, false, false);
+        sink += max((uint32_t)sw[0], (uint32_t)sw[1]);
+      }
+    }
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) sink ^= b1r[s2][i];
+  } else {
+    uint32_t b1r[4][4] = {};
+    i32x4 ra = {};
+    for (int it = 0; it < kIter / 2; ++it) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        uint32_t cm = 0;
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          i32x4 acc = ra;
+#pragma unroll
+          for (int q = 0; q < 2; ++q)
+            acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[2 * s4 + q], b[(2 * c + q + it) & 7], acc, 0, 0, 0);
+          cm = max3u(cm, max3u((uint32_t)acc[0], (uint32_t)acc[1], (uint32_t)acc[2]), (uint32_t)acc[3]);
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            const u64 k = add_pair_u64(((u64)(uint32_t)acc[2 * i + 1] << 32) | (uint32_t)acc[2 * i], kq, cm);
+            b1r[s4][2 * i] = max(b1r[s4][2 * i], (uint32_t)k);
+            b1r[s4][2 * i + 1] = max(b1r[s4][2 * i + 1], (uint32_t)(k >> 32));
+          }
+        }
+        const auto s16 = __builtin_amdgcn_permlane16_swap(cm, cm, false, false);
+        const uint32_t m1 = max((uint32_t)s16[0], (uint32_t)s16[1]);
+        const auto s32 = __builtin_amdgcn_permlane32_swap(m1, m1, false, false);
+        sink += max((uint32_t)s32[0], (uint32_t)s32[1]);
+      }
+    }
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) sink ^= b1r[s4][i];
+  }
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  out[tid] = sink;
+  if ((threadIdx.x & 63) == 0) cyc[tid >> 6] = t1 - t0;
+}
+
 template <int MODE>
 static void run(const i32x4* src, int* out, long long* cyc, int blocks) {
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  shape_kernel<MODE><<<blocks, 512>>>(src, out, cyc);  // warm
+  auto launch = [&]() {
+    if (MODE < 2) shape_kernel<MODE><<<blocks, 512>>>(src, out, cyc);
+    else tile_kernel<MODE><<<blocks, 512>>>(src, (uint32_t*)out, cyc);
+  };
+  launch();  // warm
   hipDeviceSynchronize();
   hipEventRecord(e0);
-  shape_kernel<MODE><<<blocks, 512>>>(src, out, cyc);
+  launch();
   hipEventRecord(e1);
   hipEventSynchronize(e1);
   float ms = 0;
@@ -82,10 +184,11 @@ static void run(const i32x4* src, int* out, long long* cyc, int blocks) {
   mean /= waves;
   free(h);
   // ops per wave per iteration: 64 rows x 64 cols x 128 K x 2
-  const double ops = (double)waves * kIter * 64.0 * 64.0 * 128.0 * 2.0;
+  const double ops = (double)waves * (MODE < 2 ? kIter : kIter / 2) * 64.0 * 64.0 * 128.0 * 2.0;
   // s_memtime ticks at a fixed 100 MHz reference on gfx950? report cycles as counted
+  const char* names[4] = {"32x32x32_i8", "16x16x64_i8", "32x32x32_i8 + epilogue", "16x16x64_i8 + epilogue"};
   printf("%s: %.3f ms, %.1f TOP/s (%.3f of 5000), wave ticks %.0f, ticks/ms %.0f\n",
-         MODE == 0 ? "32x32x32_i8" : "16x16x64_i8", ms, ops / (ms * 1e-3) / 1e12,
+         names[MODE], ms, ops / (ms * 1e-3) / 1e12,
          ops / (ms * 1e-3) / 1e12 / 5000.0, mean, mean / ms);
 }
 
@@ -106,6 +209,8 @@ int main() {
   for (int rep = 0; rep < 2; ++rep) {
     run<0>(src, out, cyc, blocks);
     run<1>(src, out, cyc, blocks);
+    run<2>(src, out, cyc, blocks);
+    run<3>(src, out, cyc, blocks);
   }
   return 0;
 }
