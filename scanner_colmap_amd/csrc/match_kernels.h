@@ -58,10 +58,6 @@ hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int nj
 hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
                            int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
                            bool clamp, hipStream_t stream);
-// The same matcher on v_mfma_i32_16x16x64_i8 (same inputs, outputs and formats).
-hipError_t launch_match_g16(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
-                            int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
-                            bool clamp, hipStream_t stream);
 hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* rowres,
                                     uint2* colpart, uint2* rowaux, int32_t* rlist,
                                     const uint8_t* desc8, const int32_t* csum,

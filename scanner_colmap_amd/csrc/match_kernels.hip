@@ -774,295 +774,6 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
 }
 
 // ===========================================================================
-// match_g16_kernel: the same job, ring, column partials and output formats as
-// match_g8_kernel, with v_mfma_i32_16x16x64_i8 instead of 32x32x32.  On
-// random operands the 16x16x64 form runs 0.78 of the i8 peak chip-wide
-// against 0.66-0.67 for 32x32x32 (profiles/r04_a_mfma_shape.log: the same
-// cycles per MAC, a higher clock -- a quarter of the accumulator traffic per
-// MAC).
-//  * Lane l (r = l & 15, g = l >> 4) of a 16 x 16 sub-tile holds column r and
-//    rows 4g .. 4g + 3.  A wave keeps its 64 rows as four row sub-tiles s
-//    (A fragments and the chain offsets ra in registers); a 64-column tile is
-//    four column sub-tiles c; K = 128 is two MFMAs, MFMA q reading the 16-byte
-//    chunk 2g + q of the descriptor (A and B alike, so the dot product is the
-//    same).  The LDS tile image (sw8 swizzle) and its LDS-DMA are unchanged;
-//    a 16-lane group of a B-fragment read covers 16 distinct bank groups.
-//  * Rows by value as in match_g8_kernel: x + cb_j = dot + 2^22 for two rows
-//    of the lane's column is one v_lshl_add_u64; the row state keeps, per row,
-//    the best value over the lane's columns of ONE parity of c, i.e. over the
-//    columns j = 16 c + r with j mod 32 = 16 (c & 1) + r: the same 32 residue
-//    classes as the 32x32 kernel, so row_flush16 emits rowres entries in the
-//    same format (residue = 16 p + r) and match_rowcheck_g8_kernel is unchanged.
-//    A row-state update folds the values of c and c + 2 (one v_max3).
-//  * Columns by best raw value: per column sub-tile a running max3 over the
-//    four row sub-tiles, then folded over the four 16-lane groups
-//    (v_permlane16_swap, v_permlane32_swap): the best of the wave's 64 rows,
-//    written to the same LDS column-partial slots, merged by g8_merge.
-// ===========================================================================
-// Pins a value's computation at this point of the instruction stream (an
-// empty volatile asm that reads and writes it): keeps each chain's epilogue
-// beside the next chain's MFMAs instead of sunk to the end of the tile.
-__device__ __forceinline__ void pin(uint32_t& x) { asm volatile("" : "+v"(x)); }
-
-__device__ __forceinline__ void load_bfrag16(const uint8_t* bt, int col, int g, i32x4 (&b)[2]) {
-#pragma unroll
-  for (int q = 0; q < 2; ++q) b[q] = *reinterpret_cast<const i32x4*>(bt + sw8(col, 2 * g + q));
-}
-
-__device__ __forceinline__ i32x4 chain16(const i32x4 (&a)[2], const i32x4 (&b)[2], const i32x4& ra) {
-  const i32x4 acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[0], b[0], ra, 0, 0, 0);
-  return __builtin_amdgcn_mfma_i32_16x16x64_i8(a[1], b[1], acc, 0, 0, 0);
-}
-
-// Row values of one finished 16 x 16 sub-tile (rows 4g .. 4g + 3, the lane's
-// column), two per v_lshl_add_u64; `dep` = a VALU result computed from acc
-// (the MFMA-result hazard, see add_pair_u64).
-__device__ __forceinline__ void g16_keys(const i32x4& acc, u64 kq, uint32_t dep, u64 (&k)[2]) {
-  k[0] = add_pair_u64(((u64)(uint32_t)acc[1] << 32) | (uint32_t)acc[0], kq, dep);
-  k[1] = add_pair_u64(((u64)(uint32_t)acc[3] << 32) | (uint32_t)acc[2], kq, dep);
-}
-
-// Best raw value of a column over the wave's 64 rows: fold the four 16-lane
-// groups; lanes 0 .. 15 write it for the workgroup merge.
-__device__ __forceinline__ void g16_col_partial(uint32_t m, uint32_t* dst, int g, int r) {
-  const auto s16 = __builtin_amdgcn_permlane16_swap(m, m, false, false);
-  const uint32_t m1 = max((uint32_t)s16[0], (uint32_t)s16[1]);
-  const auto s32 = __builtin_amdgcn_permlane32_swap(m1, m1, false, false);
-  if (g == 0) dst[r] = max((uint32_t)s32[0], (uint32_t)s32[1]);
-}
-
-// Row flush of match_g16_kernel (row_flush_values' format): per row the two
-// parity states of the lane (residues r and 16 + r) and then the 16 lanes of
-// the row's group are reduced to the best (value, lane residue) and the best
-// of the other residues.
-template <bool CLAMP>
-__device__ __forceinline__ void row_flush16(const uint32_t (&b1r)[2][4][4], uint2* rr, int row0,
-                                            int n1, int r, int g) {
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      uint32_t key[2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const uint32_t k1 = b1r[p][s][i];
-        uint32_t v = k1 >= (1u << 22) ? k1 - (1u << 22) : 0u;
-        if (CLAMP) v = min(v, kLutMax);
-        key[p] = (v << kIdxBits) | (kIdxMask - (uint32_t)(16 * p + r));
-      }
-      uint32_t B1 = max(key[0], key[1]);
-      uint32_t B2 = min(key[0], key[1]) & ~kIdxMask;
-#pragma unroll
-      for (int x = 1; x < 16; x <<= 1) {
-        const uint32_t o1 = __shfl_xor(B1, x);
-        const uint32_t o2 = __shfl_xor(B2, x);
-        B2 = merge_second(B1, B2, o1, o2);
-        B1 = max(B1, o1);
-      }
-      const int row = row0 + 16 * s + 4 * g + i;
-      if (r == 4 * s + i && row < n1) rr[row] = make_uint2(B1, B2);
-    }
-  }
-}
-
-template <bool CLAMP>
-__global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g16_kernel(
-    const uint8_t* __restrict__ desc8,  // a ^ 0x80, [rows][128]
-    const int32_t* __restrict__ csum,   // 128 * sum_d a_d per row
-    const MatchJob* __restrict__ jobs, const PairDesc* __restrict__ pairs,
-    uint2* __restrict__ rowres,         // per pair [nseg][n1]
-    uint2* __restrict__ colpart) {      // per pair [nrb][n2pad]
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kG8LdsBytes];
-  uint32_t* csc = reinterpret_cast<uint32_t*>(lds + kG8CscOff);
-  int64_t* meta = reinterpret_cast<int64_t*>(lds + kG8MetaOff);
-
-  const MatchJob job = jobs[blockIdx.x];
-  if (job.npairs == 0 || job.n1 <= 0) return;  // padding job of the XCD order (whole block)
-  const PairDesc* __restrict__ P = pairs + job.pair0;
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int r = lane & 15;
-  const int g = lane >> 4;
-  const int row0 = job.rb * kRowsPerBlock8 + wave * 64;
-
-  i32x4 afrag[4][2];
-  i32x4 ra[4];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const int row = row0 + 16 * s + r;
-    const bool ok = row < job.n1;
-    const i32x4* src = reinterpret_cast<const i32x4*>(desc8 + (job.a_row + (ok ? row : 0)) * 128);
-    const int z = (int)0x80808080u;  // a = 0
-#pragma unroll
-    for (int q = 0; q < 2; ++q) afrag[s][q] = ok ? src[2 * g + q] : i32x4{z, z, z, z};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int rw = row0 + 16 * s + 4 * g + i;
-      const uint32_t cs = (uint32_t)csum[job.a_row + min(rw, job.n1 - 1)];
-      ra[s][i] = (int)((rw < job.n1 ? cs : 0u) + (1u << 21));
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // operands in registers before any LDS-DMA
-
-  int G = 0;
-  for (int p = 0; p < job.npairs; ++p) G += (P[p].n2 + kTile8Cols - 1) / kTile8Cols;
-  int fp = 0, ft = 0;
-  int64_t fb = P[0].b_row;
-  int fn = (P[0].n2 + kTile8Cols - 1) / kTile8Cols;
-  const int gpt = wave == kMatch8Waves - 1 ? 2 : 1;  // LDS-DMA operations per tile
-  auto dma_group = [&](int grp) {
-#pragma unroll 1
-    for (int i = 0; i < kG8T; ++i) {
-      g8_stage(desc8 + fb * 128, csum + fb, ft, (grp * kG8T + i) % kG8Stages, wave, lane, lds);
-      if (++ft == fn) {
-        if (fp + 1 < job.npairs) {
-          ++fp;
-          ft = 0;
-          fb = P[fp].b_row;
-          fn = (P[fp].n2 + kTile8Cols - 1) / kTile8Cols;
-        } else {
-          ft = fn - 1;
-        }
-      }
-    }
-  };
-#pragma unroll
-  for (int j = 0; j < kG8Q - 1; ++j) dma_group(j);
-  g8_wait_vm((kG8Q - 2) * kG8T * gpt);  // group 0 landed
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-
-  int p = 0, t = 0;
-  PairDesc pd = P[0];
-  int nt = (pd.n2 + kTile8Cols - 1) / kTile8Cols;
-  int64_t cpi = pd.colpart_off + (int64_t)job.rb * pd.n2pad;
-  int flushed = -8;
-
-  uint32_t b1r[2][4][4];  // [parity of c][row sub-tile][row]: best value over the lane's columns
-#pragma unroll
-  for (int q = 0; q < 2; ++q)
-#pragma unroll
-    for (int s = 0; s < 4; ++s)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) b1r[q][s][i] = 0u;
-
-  // B fragments and column sums of the tile in use (next tile's c loaded as
-  // soon as this tile's last chain of c has been issued)
-  i32x4 bf[4][2];
-  uint32_t cbv[4];
-  auto load_tile = [&](int gg, int c) {
-    const int stage = gg % kG8Stages;
-    load_bfrag16(lds + stage * kTile8Bytes, 16 * c + r, g, bf[c]);
-    cbv[c] = (uint32_t)reinterpret_cast<const int32_t*>(lds + kG8CbOff + stage * kTile8Cols * 4)[16 * c + r];
-  };
-#pragma unroll
-  for (int c = 0; c < 4; ++c) load_tile(0, c);
-
-  for (int gi = 0; gi < G; ++gi) {
-    const int stage = gi % kG8Stages;
-    if (tid == 0) meta[stage] = cpi + (int64_t)t * kTile8Cols;
-    const int k = t & (kTiles8PerSeg - 1);
-    u64 kq[4];
-#pragma unroll
-    for (int c = 0; c < 4; ++c) kq[c] = ((u64)cbv[c] << 32) | cbv[c];
-    const int m = gi / kG8T;
-    uint32_t* cscw = csc + (((m % kG8CscGroups) * kG8T + (gi & (kG8T - 1))) * kMatch8Waves + wave) * kTile8Cols;
-    const bool group_end = (gi & (kG8T - 1)) == kG8T - 1;
-    uint32_t cm[4];
-    u64 st[2][2];  // row values of c = 0, 1 of the current row sub-tile
-    i32x4 acc = chain16(afrag[0], bf[0], ra[0]);
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      if (s == 3 && group_end) {
-        // Barrier m (before the last row sub-tile of the group's last tile, so
-        // that the next tile's fragments can load under it): as in
-        // match_g8_kernel, this wave's DMA of group m + 1 must be done.
-        const int half = wave >> 2;
-        int stv = 0;
-#pragma unroll
-        for (int j = 1; j <= kG8Q - 2; ++j) stv += (m - j >= 1 && (((m - j - 1) & 1) == half));
-        g8_wait_vm(gi - flushed <= 2 * kG8T ? 0 : (kG8Q - 3) * kG8T * gpt + stv);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        dma_group(m + kG8Q - 1);
-        if (m >= 1 && (((m - 1) & 1) == half)) {  // merge tile (wave & 3) of group m - 1
-          const int tg = (m - 1) * kG8T + (wave & (kG8T - 1));
-          const uint32_t* src =
-              csc + (((m - 1) % kG8CscGroups) * kG8T + (wave & (kG8T - 1))) * kMatch8Waves * kTile8Cols;
-          g8_merge(src + lane, colpart + meta[tg % kG8Stages] + lane);
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        __builtin_amdgcn_sched_barrier(0);
-        // next chain first (its MFMAs run under this chain's epilogue, which
-        // then finds this chain's result complete: no wait states)
-        i32x4 nxt;
-        if (c < 3) nxt = chain16(afrag[s], bf[c + 1], ra[s]);
-        else if (s < 3) nxt = chain16(afrag[s + 1], bf[0], ra[s + 1]);
-        __builtin_amdgcn_sched_barrier(0);
-        const uint32_t m3 = max(max((uint32_t)acc[0], (uint32_t)acc[1]), (uint32_t)acc[2]);
-        cm[c] = s == 0 ? max(m3, (uint32_t)acc[3]) : max(max(cm[c], m3), (uint32_t)acc[3]);
-        u64 kk[2];
-        g16_keys(acc, kq[c], m3, kk);
-        pin(cm[c]);
-        if (c < 2) {
-          st[c][0] = kk[0];
-          st[c][1] = kk[1];
-        } else {
-          const int pq = c - 2;
-#pragma unroll
-          for (int h2 = 0; h2 < 2; ++h2) {
-            b1r[pq][s][2 * h2] = max(max(b1r[pq][s][2 * h2], (uint32_t)kk[h2]), (uint32_t)st[pq][h2]);
-            b1r[pq][s][2 * h2 + 1] =
-                max(max(b1r[pq][s][2 * h2 + 1], (uint32_t)(kk[h2] >> 32)), (uint32_t)(st[pq][h2] >> 32));
-            pin(b1r[pq][s][2 * h2]);
-            pin(b1r[pq][s][2 * h2 + 1]);
-          }
-        }
-        if (s == 3) {
-          // column c of this tile is complete; its fragments are free for the
-          // next tile (inside a group, or after the barrier above)
-          g16_col_partial(cm[c], cscw + 16 * c, g, r);
-          if (gi + 1 < G) load_tile(gi + 1, c);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-        acc = nxt;
-      }
-    }
-    if (k == kTiles8PerSeg - 1 || t + 1 == nt) {
-      row_flush16<CLAMP>(b1r, rowres + pd.rowres_off + (int64_t)(t / kTiles8PerSeg) * pd.n1, row0,
-                         pd.n1, r, g);
-#pragma unroll
-      for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) b1r[q][s][i] = 0u;
-      flushed = gi;
-    }
-    if (++t == nt && p + 1 < job.npairs) {
-      ++p;
-      t = 0;
-      pd = P[p];
-      nt = (pd.n2 + kTile8Cols - 1) / kTile8Cols;
-      cpi = pd.colpart_off + (int64_t)job.rb * pd.n2pad;
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  const int nbar = G / kG8T;
-  const int first = nbar >= 1 ? (nbar - 1) * kG8T : 0;
-  const int tg = first + wave;
-  if (tg < G) {
-    const uint32_t* src = csc + (((tg / kG8T) % kG8CscGroups) * kG8T + (tg & (kG8T - 1))) *
-                                    kMatch8Waves * kTile8Cols;
-    g8_merge(src + lane, colpart + meta[tg % kG8Stages] + lane);
-  }
-}
-
-// ===========================================================================
 // Finalize.
 // ===========================================================================
 // Upper bound, acosf LUT: lut[d] = acosf(min(d * 2^-18, 1.0f)), d in [0, 2^18],
@@ -1600,19 +1311,6 @@ hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const Matc
                        csum, jobs, pairs, rowres, colpart);
   else
     hipLaunchKernelGGL(match_g8_kernel<false>, dim3(njobs), dim3(kMatch8Threads), 0, stream, desc8,
-                       csum, jobs, pairs, rowres, colpart);
-  return hipGetLastError();
-}
-
-hipError_t launch_match_g16(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
-                            int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
-                            bool clamp, hipStream_t stream) {
-  if (njobs <= 0) return hipSuccess;
-  if (clamp)
-    hipLaunchKernelGGL(match_g16_kernel<true>, dim3(njobs), dim3(kMatch8Threads), 0, stream, desc8,
-                       csum, jobs, pairs, rowres, colpart);
-  else
-    hipLaunchKernelGGL(match_g16_kernel<false>, dim3(njobs), dim3(kMatch8Threads), 0, stream, desc8,
                        csum, jobs, pairs, rowres, colpart);
   return hipGetLastError();
 }

@@ -401,7 +401,6 @@ struct scm_context {
   int64_t batch_pairs = kDefaultPairsPerBatch;  // SCM_BATCH_PAIRS overrides
   int64_t batch_bytes = 0;  // HBM budget of one batch set (SCM_BATCH_BYTES; 0 = from free HBM)
   bool match_bf16 = false;  // SCM_MATCH_BF16=1: bf16 MFMA matcher instead of i8
-  bool match16 = false;     // SCM_MATCH16=1: the i8 matcher on 16x16x64 MFMAs (match_g16_kernel)
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
   bool score_split = true;  // SCM_SCORE_SPLIT=0: one-pass scoring with every exact test
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
@@ -1060,9 +1059,9 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
         SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), jb, nj, bs.pairs.as<PairDesc>(),
                                    bs.rowres.as<uint2>(), bs.colpart.as<uint2>(), clamp, sm));
       else
-        SCM_HIP((ctx->match16 ? launch_match_g16 : launch_match_g8)(
-            t.desc8.as<uint8_t>(), t.csum.as<int32_t>(), jb, nj, bs.pairs.as<PairDesc>(),
-            bs.rowres.as<uint2>(), bs.colpart.as<uint2>(), clamp, sm));
+        SCM_HIP(launch_match_g8(t.desc8.as<uint8_t>(), t.csum.as<int32_t>(), jb, nj,
+                                bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
+                                bs.colpart.as<uint2>(), clamp, sm));
     }
   SCM_HIP(hipEventRecord(bs.ev[1], sm));
   // Finalize, the count read-back and (enqueue_verify) the verification run on
@@ -1857,7 +1856,6 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
     ctx->batch_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
   if (const char* e = std::getenv("SCM_BATCH_BYTES")) ctx->batch_bytes = std::max<int64_t>(1, std::atoll(e));
   if (const char* e = std::getenv("SCM_MATCH_BF16")) ctx->match_bf16 = e[0] == '1';
-  if (const char* e = std::getenv("SCM_MATCH16")) ctx->match16 = e[0] == '1';
   // The i8 matcher tracks column top-2 by value only, which decides the
   // cross-check exactly when a tied column best fails the ratio test, i.e.
   // max_ratio <= 1 (match_kernels.hip, i8 section); otherwise the bf16 matcher
