@@ -159,6 +159,88 @@ __global__ __launch_bounds__(512) void tile_kernel(const i32x4* __restrict__ src
   if ((threadIdx.x & 63) == 0) cyc[tid >> 6] = t1 - t0;
 }
 
+// The 32x32x32 tile as match_g8_kernel does it (rows: v_lshl_add_u64 values,
+// one v_max3 per row folding the tile's two column sub-tiles; columns: max
+// tree per sub-tile, permlane32 fold per column sub-tile), and (DIGIT) the
+// digit-block form: a fifth MFMA per chain adds the column sum, so rows fold
+// accumulators directly (no v_lshl_add_u64).  One workgroup per CU (a 160 KB
+// LDS allocation): two waves per SIMD, as in the matcher.
+template <bool DIGIT>
+__global__ __launch_bounds__(512) void g8_model_kernel(const i32x4* __restrict__ src, uint32_t* out,
+                                                       long long* cyc) {
+  __shared__ uint8_t pad[160 * 1024 - 64];
+  const int tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid == 1 << 30) pad[threadIdx.x] = 0;  // keeps the allocation
+  i32x4 a[8], b[8], dg[2];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    a[q] = src[(tid * 16 + q) & 0xFFFFF];
+    b[q] = src[(tid * 16 + 8 + q) & 0xFFFFF];
+  }
+  dg[0] = src[(tid * 3) & 0xFFFFF];
+  dg[1] = src[(tid * 5) & 0xFFFFF];
+  const i32x4 wneg = {(int)0x80808080u, (int)0x80808080u, (int)0x80808080u, (int)0x80808080u};
+  const u64 kq = ((u64)(uint32_t)src[tid & 0xFFFF][0] << 32) | (uint32_t)src[tid & 0xFFFF][1];
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  uint32_t sink = 0;
+  uint32_t b1r[2][16] = {};
+  i32x16 ra2[2];
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) ra2[s2][i] = src[(tid * 7 + 16 * s2 + i) & 0xFFFFF][0] & 0xFFFF;
+  for (int it = 0; it < kIter / 2; ++it) {
+    uint32_t k0[2][16];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint32_t cm[2];
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        i32x16 acc = ra2[s2];
+        if (DIGIT) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(wneg, dg[c], acc, 0, 0, 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[4 * s2 + q], b[4 * c + q], acc, 0, 0, 0);
+        uint32_t m = max3u((uint32_t)acc[0], (uint32_t)acc[1], (uint32_t)acc[2]);
+#pragma unroll
+        for (int i = 3; i < 15; i += 2) m = max3u(m, (uint32_t)acc[i], (uint32_t)acc[i + 1]);
+        m = max(m, (uint32_t)acc[15]);
+        cm[s2] = m;
+        uint32_t kv[16];
+        if (DIGIT) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) kv[i] = (uint32_t)acc[i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            const u64 k = add_pair_u64(((u64)(uint32_t)acc[2 * i + 1] << 32) | (uint32_t)acc[2 * i], kq, m);
+            kv[2 * i] = (uint32_t)k;
+            kv[2 * i + 1] = (uint32_t)(k >> 32);
+          }
+        }
+        if (c == 0) {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) k0[s2][i] = kv[i];
+        } else {
+#pragma unroll
+          for (int i = 0; i < 16; ++i) b1r[s2][i] = max3u(b1r[s2][i], kv[i], k0[s2][i]);
+        }
+      }
+      const uint32_t mm = max(cm[0], cm[1]);
+      const auto sw = __builtin_amdgcn_permlane32_swap(mm, mm, false, false);
+      sink += max((uint32_t)sw[0], (uint32_t)sw[1]);
+    }
+    ra2[it & 1][0] += 1;  // loop-carried: the chains cannot be hoisted
+  }
+#pragma unroll
+  for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sink ^= b1r[s2][i];
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  out[tid] = sink;
+  if ((threadIdx.x & 63) == 0) cyc[tid >> 6] = t1 - t0;
+}
+
 template <int MODE>
 static void run(const i32x4* src, int* out, long long* cyc, int blocks) {
   hipEvent_t e0, e1;
@@ -166,7 +248,8 @@ static void run(const i32x4* src, int* out, long long* cyc, int blocks) {
   hipEventCreate(&e1);
   auto launch = [&]() {
     if (MODE < 2) shape_kernel<MODE><<<blocks, 512>>>(src, out, cyc);
-    else tile_kernel<MODE><<<blocks, 512>>>(src, (uint32_t*)out, cyc);
+    else if (MODE < 4) tile_kernel<MODE><<<blocks, 512>>>(src, (uint32_t*)out, cyc);
+    else g8_model_kernel<MODE == 5><<<blocks, 512>>>(src, (uint32_t*)out, cyc);
   };
   launch();  // warm
   hipDeviceSynchronize();
@@ -186,7 +269,8 @@ static void run(const i32x4* src, int* out, long long* cyc, int blocks) {
   // ops per wave per iteration: 64 rows x 64 cols x 128 K x 2
   const double ops = (double)waves * (MODE < 2 ? kIter : kIter / 2) * 64.0 * 64.0 * 128.0 * 2.0;
   // s_memtime ticks at a fixed 100 MHz reference on gfx950? report cycles as counted
-  const char* names[4] = {"32x32x32_i8", "16x16x64_i8", "32x32x32_i8 + epilogue", "16x16x64_i8 + epilogue"};
+  const char* names[6] = {"32x32x32_i8", "16x16x64_i8", "32x32x32_i8 + epilogue", "16x16x64_i8 + epilogue",
+                          "g8 model (2 waves/SIMD)", "g8 model + digit-block MFMA"};
   printf("%s: %.3f ms, %.1f TOP/s (%.3f of 5000), wave ticks %.0f, ticks/ms %.0f\n",
          names[MODE], ms, ops / (ms * 1e-3) / 1e12,
          ops / (ms * 1e-3) / 1e12 / 5000.0, mean, mean / ms);
@@ -211,6 +295,8 @@ int main() {
     run<1>(src, out, cyc, blocks);
     run<2>(src, out, cyc, blocks);
     run<3>(src, out, cyc, blocks);
+    run<4>(src, out, cyc, blocks / 2);
+    run<5>(src, out, cyc, blocks / 2);
   }
   return 0;
 }

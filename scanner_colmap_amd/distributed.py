@@ -116,6 +116,10 @@ def gather_packed(offsets: np.ndarray, data: np.ndarray, device=None, staging=No
         ops = [dist.P2POp(dist.isend, t, 0) for t in (t_o, t_d) if t.numel()]
         for w in dist.batch_isend_irecv(ops):
             w.wait()
+        if on_gpu:
+            # wait() orders the stream only: the staging buffers are reused by
+            # the next gather, so the copy and the sends must be complete
+            torch.cuda.current_stream(dev).synchronize()
         return None
     starts = np.concatenate([[0], np.cumsum([a + b for a, b in sizes[1:]])]).astype(np.int64)
     total = int(starts[-1])
