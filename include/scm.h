@@ -250,7 +250,9 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset,
  * t[5] = inlier-scoring kernels (F + H), t[6] / t[7] = F / H (model, point)
  * residual evaluations of the sequential LO-RANSAC up to its stop;
  * t[8] / t[9] = host time of the last scm_execute_batch: content keys of its
- * elements, then the image table (reuse + upload staging). */
+ * elements, then the image table (reuse + upload staging); t[10] = its
+ * pipeline run (GPU stages and their host steps up to the serialised rows),
+ * t[11] = building its output blobs. */
 int scm_table_timings(scm_context* ctx, double* t, int32_t n);
 /* Measurement only: serial != 0 runs the following table runs with matching
  * and verification one after the other instead of overlapped (no stage

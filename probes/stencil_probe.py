@@ -33,9 +33,11 @@ def main():
         w = (time.perf_counter() - t0) * 1e3
         t = ctx.table_timings()
         walls.append(w)
+        py = w - t['hash_ms'] - t['stage_ms'] - t['run_ms'] - t['out_ms']
         print(f"call {r0 // B:3d} wall {w:7.2f} ms match {t['match_ms']:6.2f} finalize "
               f"{t['finalize_ms']:5.2f} verify {t['verify_ms']:6.2f} hash {t['hash_ms']:5.2f} "
-              f"stage {t['stage_ms']:5.2f}", flush=True)
+              f"stage {t['stage_ms']:5.2f} run {t['run_ms']:5.2f} out {t['out_ms']:5.2f} "
+              f"rest {py:5.2f}", flush=True)
     walls = sorted(walls[1:])
     print(f"median wall {walls[len(walls) // 2]:.2f} ms per call of {B} stencils", flush=True)
     ctx.close()

@@ -404,6 +404,7 @@ struct scm_context {
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
   bool score_split = true;  // SCM_SCORE_SPLIT=0: one-pass scoring with every exact test
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
+  double t_run = 0, t_out = 0;     // last execute_batch: run_rows (GPU + its host steps), outputs
   double t_hash = 0, t_stage = 0;  // host time of the last execute_batch: content keys, table
   double t_score = 0;                  // scoring kernels (F + H) of the last run
   int64_t evals_f = 0, evals_h = 0;    // their (model, point) evaluations
@@ -2123,7 +2124,10 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
   ctx->evals_f = ctx->evals_h = 0;
   ctx->n_match_launches = 0;
   Packed pk;
+  const auto h2 = std::chrono::steady_clock::now();
   rc = run_rows(ctx, t, plan, -1, &pk);
+  const auto h3 = std::chrono::steady_clock::now();
+  ctx->t_run = std::chrono::duration<double, std::milli>(h3 - h2).count();
   if (rc != SCM_OK) {
     drain(ctx);
     if (!pool_give(pk.data)) std::free(pk.data);
@@ -2174,6 +2178,7 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
     tvgs_out[r] = scm_blob{pb, (size_t)(c - b)};
   }
   if (!pool_give(pk.data)) std::free(pk.data);
+  ctx->t_out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h3).count();
   return SCM_OK;
 }
 
@@ -2436,10 +2441,10 @@ int scm_table_timings(scm_context* ctx, double* t, int32_t n) {
     set_error("invalid arguments");
     return SCM_E_INVALID;
   }
-  const double v[10] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall,
+  const double v[12] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall,
                         (double)ctx->n_match_launches, ctx->t_score, (double)ctx->evals_f,
-                        (double)ctx->evals_h, ctx->t_hash, ctx->t_stage};
-  for (int32_t i = 0; i < n && i < 10; ++i) t[i] = v[i];
+                        (double)ctx->evals_h, ctx->t_hash, ctx->t_stage, ctx->t_run, ctx->t_out};
+  for (int32_t i = 0; i < n && i < 12; ++i) t[i] = v[i];
   return SCM_OK;
 }
 

@@ -3331,6 +3331,11 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   // cost idle CUs only (about 1024 pairs x rounds per window).
   int W = 1;
   while (W < kMaxWindow && (int64_t)npairs * 2 * W <= 1024) W *= 2;
+  static const int w0_env = [] {  // diagnostics: SCM_FIRST_WINDOW=w caps the first window
+    const char* e = getenv("SCM_FIRST_WINDOW");
+    return e ? atoi(e) : 0;
+  }();
+  if (w0_env > 0) W = std::min(W, w0_env);
   int covered = 0, r = 0;
   while (covered < P.max_trials_F || covered < P.max_trials_H) {
     const VerifyRoundBufs& rf = rfp[r & 1];
