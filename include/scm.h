@@ -224,6 +224,22 @@ int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin,
 int scm_table_run_packed(scm_context* ctx, int64_t overlap, int64_t row_begin,
                          int64_t row_end, scm_blob* rows_out,
                          int64_t* row_offsets);
+/* Streamed form of scm_table_run_packed: `passes` runs of the row range
+ * [row_begin, row_end) as ONE batch stream, so the batches of pass k + 1 enter
+ * the pipeline while the last batches of pass k are still being verified and
+ * the GPU does not drain between passes (the serving shape: consecutive
+ * tables, or a table re-run, back to back).  As soon as pass k's rows are
+ * serialised, on_pass(user, k, rows, row_offsets) is called on the calling
+ * thread, passes in order: `rows` (rows_size bytes) is a packed buffer the
+ * callee owns (free it with scm_blob_free on {rows, rows_size}), `row_offsets` the 2 * (row_end - row_begin) + 1 element
+ * offsets of scm_table_run_packed (valid during the call only).  Every pass's
+ * bytes equal scm_table_run_packed's.  With scm_set_keep_matches the raw
+ * matches of the last pass are kept.  scm_table_timings then reports the
+ * whole streamed run. */
+typedef void (*scm_pass_fn)(void* user, int64_t pass, uint8_t* rows, size_t rows_size,
+                            const int64_t* row_offsets);
+int scm_table_run_passes(scm_context* ctx, int64_t overlap, int64_t row_begin,
+                         int64_t row_end, int64_t passes, scm_pass_fn on_pass, void* user);
 /* Keep (keep != 0) the raw cross-checked matches of every pair of the
  * following table runs for scm_table_matches; off by default. */
 int scm_set_keep_matches(scm_context* ctx, int32_t keep);

@@ -35,7 +35,7 @@ EXPORTS = (
     "scm_verify_pair", "scm_execute_stencil", "scm_execute_batch", "scm_stencil_stats",
     "scm_stencil_spec_stats", "scm_stencil_cache_clear",
     "scm_table_load",
-    "scm_table_run", "scm_table_run_packed", "scm_set_keep_matches",
+    "scm_table_run", "scm_table_run_packed", "scm_table_run_passes", "scm_set_keep_matches",
     "scm_set_keep_matches_range", "scm_add_keep_matches_range",
     "scm_table_matches", "scm_table_timings", "scm_set_serial", "scm_extract_frames",
 )
@@ -122,6 +122,8 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                   POINTER(Blob), POINTER(Blob)]
     lib.scm_table_run_packed.argtypes = [c_void_p, c_int64, c_int64, c_int64,
                                          POINTER(Blob), c_void_p]
+    lib.scm_table_run_passes.argtypes = [c_void_p, c_int64, c_int64, c_int64, c_int64, PASS_FN,
+                                         c_void_p]
     lib.scm_set_keep_matches.argtypes = [c_void_p, c_int32]
     lib.scm_set_keep_matches_range.argtypes = [c_void_p, c_int64, c_int64]
     lib.scm_add_keep_matches_range.argtypes = [c_void_p, c_int64, c_int64]
@@ -198,6 +200,10 @@ def _elements(chunks) -> tuple:
         tab[i, 1] = a.nbytes
     keep.append(chunks)
     return tab.ctypes.data_as(POINTER(Element)), keep
+
+
+# scm_pass_fn (include/scm.h): (user, pass, rows, rows_size, row_offsets)
+PASS_FN = ctypes.CFUNCTYPE(None, c_void_p, c_int64, c_void_p, c_size_t, POINTER(c_int64))
 
 
 class PackedRows:
@@ -348,6 +354,30 @@ class Context:
         _check(self._lib.scm_table_run_packed(self._ptr, overlap, row_begin, row_end, byref(b),
                                               offs.ctypes.data))
         return PackedRows(b, offs)
+
+    def table_run_passes(self, overlap: int, row_begin: int, row_end: int, passes: int,
+                         on_pass) -> None:
+        """scm_table_run_passes: `passes` runs of the row range as one batch
+        stream (no drain between passes); on_pass(k, PackedRows) receives pass
+        k's rows as soon as they are serialised, in order."""
+        n = row_end - row_begin
+        err = []
+
+        def cb(user, k, data, size, offs):
+            try:
+                b = Blob()
+                b.data = ctypes.cast(data, POINTER(c_uint8))
+                b.size = size
+                o = np.ctypeslib.as_array(offs, shape=(2 * n + 1,)).copy()
+                on_pass(int(k), PackedRows(b, o))
+            except BaseException as e:  # noqa: BLE001 -- re-raised after the call
+                err.append(e)
+
+        fn = PASS_FN(cb)
+        _check(self._lib.scm_table_run_passes(self._ptr, overlap, row_begin, row_end, passes, fn,
+                                              None))
+        if err:
+            raise err[0]
 
     def extract_frames(self, frames, image_ids=None) -> list:
         """SiftExtractionKernel::execute on each frame (H x W x C uint8 arrays;

@@ -1675,8 +1675,14 @@ struct RowPlan {
 // batch machinery into one packed output.  keep_row0 >= 0 (table path):
 // plan[i] is table row keep_row0 + i and the raw matches of the kept rows are
 // recorded for scm_table_matches.
+// Passes of a streamed run (run_rows with pass_rows > 0): pass k is plan rows
+// [k * pass_rows, (k + 1) * pass_rows); `emit` receives each pass's packed rows
+// (final row offset included) as soon as they are serialised, in order.
+using PassEmit = std::function<int(int64_t, Packed&)>;
+
 int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& plan,
-             int64_t keep_row0, Packed* out);
+             int64_t keep_row0, Packed* out, int64_t pass_rows = 0,
+             const PassEmit* emit = nullptr);
 
 // Runs the sequential stencil over table rows [row_begin, row_end) through
 // the pipelined batch machinery into one packed output.
@@ -1705,16 +1711,20 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
 }
 
 int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& plan,
-             int64_t keep_row0, Packed* out) {
+             int64_t keep_row0, Packed* out, int64_t pass_rows, const PassEmit* emit) {
   struct Batch {
     std::vector<PairSpec> specs;
     std::vector<uint32_t> pair_ids;
     std::vector<int64_t> pairs_begin;
+    int64_t row0 = 0;  // plan index of the batch's first row
   };
   std::vector<Batch> batches;
   const int64_t nr = (int64_t)plan.size();
   const bool keep = keep_row0 >= 0 && ctx->keep_matches;
-  const int64_t row_begin = keep_row0, row_end = keep_row0 + nr;
+  const bool streamed = pass_rows > 0;
+  // kept matches: the last pass's rows (every row of a single run)
+  const int64_t keep_from = streamed ? nr - pass_rows : 0;
+  const int64_t row_begin = keep_row0, row_end = keep_row0 + (nr - keep_from);
   // Batches of whole rows, closed at batch_pairs pairs or when the next row
   // would push the batch's device workspace past the per-set byte budget
   // (three sets are live at once).  A single row larger than the budget still
@@ -1734,6 +1744,7 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
       cur.pairs_begin.push_back(have);
       batches.push_back(std::move(cur));
       cur = Batch();
+      cur.row0 = i;
       cur_bytes = 0;
     }
     cur_bytes += row_bytes;
@@ -1752,24 +1763,51 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
     ctx->last_end = row_end;
     ctx->last_matches.assign(row_end - row_begin, {});
   }
+  // Streamed runs: one output per pass; a batch may span a pass boundary, its
+  // rows are serialised into the pass they belong to.
+  const int64_t npass = streamed ? nr / pass_rows : 0;
+  std::vector<Packed> packs(npass);
+  std::vector<int64_t> rows_done(npass, 0);
+  int64_t next_emit = 0;
   auto finish = [&](const Batch& b, BatchSet& bs) -> int {
     BatchView v;
     SCM_TRY(collect_batch(ctx, bs, &v));
+    const int64_t nrows = (int64_t)b.pairs_begin.size() - 1;
     if (keep)
-      for (int64_t p = 0; p < v.P; ++p) {
-        const int64_t row = b.specs[p].a, o = v.offsets[p];
-        if (!ctx->kept(row)) continue;
-        ctx->last_matches[row - row_begin].push_back(
-            {b.specs[p].b - row, std::vector<Match>(v.matches + o, v.matches + o + v.counts[p])});
+      for (int64_t r = 0; r < nrows; ++r) {
+        if (b.row0 + r < keep_from) continue;
+        for (int64_t p = b.pairs_begin[r]; p < b.pairs_begin[r + 1]; ++p) {
+          const int64_t row = b.specs[p].a, o = v.offsets[p];
+          if (!ctx->kept(row)) continue;
+          ctx->last_matches[row - row_begin].push_back(
+              {b.specs[p].b - row, std::vector<Match>(v.matches + o, v.matches + o + v.counts[p])});
+        }
       }
-    if (ctx->opts.multiple_models) {  // the later Estimates reuse bs: v is consumed first
-      std::vector<Tvg> tv;
+    std::vector<Tvg> tv;
+    if (ctx->opts.multiple_models)  // the later Estimates reuse bs: v is consumed first
       SCM_TRY(estimate_multiple(ctx, bs, v, &tv));
-      return serialize_rows_tvg(tv, b.pair_ids, b.pairs_begin, out);
+    auto ser = [&](const std::vector<int64_t>& pb, Packed* o) {
+      return ctx->opts.multiple_models ? serialize_rows_tvg(tv, b.pair_ids, pb, o)
+                                       : serialize_rows(ctx, v, b.pair_ids, pb, o);
+    };
+    if (!streamed) return ser(b.pairs_begin, out);
+    for (int64_t r0 = 0; r0 < nrows;) {
+      const int64_t pass = (b.row0 + r0) / pass_rows;
+      const int64_t r1 = std::min(nrows, (pass + 1) * pass_rows - b.row0);
+      const std::vector<int64_t> pb(b.pairs_begin.begin() + r0, b.pairs_begin.begin() + r1 + 1);
+      SCM_TRY(ser(pb, &packs[pass]));
+      rows_done[pass] += r1 - r0;
+      r0 = r1;
     }
-    return serialize_rows(ctx, v, b.pair_ids, b.pairs_begin, out);
+    while (next_emit < npass && rows_done[next_emit] == pass_rows) {
+      Packed& pk = packs[next_emit];
+      pk.row_off.push_back((int64_t)pk.size);
+      SCM_TRY((*emit)(next_emit, pk));
+      ++next_emit;
+    }
+    return SCM_OK;
   };
-  out->row_off.reserve(2 * nr + 1);
+  if (!streamed) out->row_off.reserve(2 * nr + 1);
   // Three buffer sets: at step k the GPU holds match(k) on the matching
   // stream and verify(k-1) (+ verify(k-2)) on the verification stream while
   // the host serialises batch k-3.
@@ -1791,8 +1829,7 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
     if (B >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(B - 1) % 3], true));
   }
   for (size_t k = B >= 3 ? B - 3 : 0; k < B; ++k) SCM_TRY(finish(batches[k], ctx->sets[k % 3]));
-  (void)0;
-  out->row_off.push_back((int64_t)out->size);
+  if (!streamed) out->row_off.push_back((int64_t)out->size);
   return SCM_OK;
 }
 
@@ -2321,6 +2358,78 @@ int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t 
   }
   if (!pool_give(pk.data)) std::free(pk.data);
   return SCM_OK;
+}
+
+int scm_table_run_passes(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
+                         int64_t passes, scm_pass_fn on_pass, void* user) {
+  if (!ctx || !on_pass || passes < 0) {
+    set_error("invalid arguments");
+    return SCM_E_INVALID;
+  }
+  if (!ctx->table_loaded) {
+    set_error("scm_table_run_passes before scm_table_load");
+    return SCM_E_STATE;
+  }
+  if (overlap < 1 || row_begin < 0 || row_end > ctx->table.n || row_begin > row_end) {
+    set_error("invalid row range / overlap");
+    return SCM_E_INVALID;
+  }
+  const int64_t n = row_end - row_begin;
+  auto hand_over = [&](int64_t k, Packed& pk) -> int {
+    scm_blob b{pk.data ? pk.data : (uint8_t*)std::malloc(1), pk.size};
+    if (!b.data) {
+      set_error("malloc failed");
+      return SCM_E_NOMEM;
+    }
+    pk.data = nullptr;
+    pk.size = pk.cap = 0;
+    on_pass(user, k, b.data, b.size, pk.row_off.data());
+    std::vector<int64_t>().swap(pk.row_off);
+    return SCM_OK;
+  };
+  if (n == 0 || passes == 0) {
+    for (int64_t k = 0; k < passes; ++k) {
+      Packed pk;
+      pk.row_off.push_back(0);
+      SCM_TRY(hand_over(k, pk));
+    }
+    return SCM_OK;
+  }
+  SCM_HIP(hipSetDevice(ctx->device));
+  ctx->t_match = ctx->t_final = ctx->t_verify = ctx->t_score = 0.0;
+  ctx->evals_f = ctx->evals_h = 0;
+  ctx->n_match_launches = 0;
+  const auto w0 = std::chrono::steady_clock::now();
+  // the stencil plan of the range (run_table), repeated `passes` times
+  const ImageTable& t = ctx->table;
+  std::vector<RowPlan> plan;
+  plan.reserve((size_t)(n * passes));
+  {
+    std::vector<uint32_t> ids(overlap);
+    std::vector<int64_t> rows(overlap), sel;
+    for (int64_t r = row_begin; r < row_end; ++r) {
+      for (int64_t s2 = 0; s2 < overlap; ++s2) {
+        rows[s2] = std::min(r + s2, t.n - 1);
+        ids[s2] = t.ids[rows[s2]];
+      }
+      row_pairs(ids, &sel);
+      RowPlan rp;
+      rp.pivot = (int32_t)r;
+      for (int64_t s2 : sel) {
+        rp.nb.push_back((int32_t)rows[s2]);
+        rp.nb_ids.push_back(ids[s2]);
+      }
+      plan.push_back(std::move(rp));
+    }
+  }
+  for (int64_t k = 1; k < passes; ++k)
+    for (int64_t i = 0; i < n; ++i) plan.push_back(plan[i]);
+  const PassEmit emit = hand_over;
+  const int rc = run_rows(ctx, t, plan, row_begin, nullptr, n, &emit);
+  if (rc != SCM_OK) drain(ctx);
+  ctx->t_wall =
+      std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+  return rc;
 }
 
 int scm_table_run_packed(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,

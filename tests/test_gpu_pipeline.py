@@ -94,3 +94,33 @@ def test_ragged_table_with_empty_images(gpu_ctx):
     gpu_ctx.table_load(ids, kps2, descs2)
     got = gpu_ctx.table_run(4, 0, len(sizes))
     assert got == ref
+
+
+@pytest.mark.parametrize("batch_pairs", [None, "7"])
+def test_streamed_passes_equal_single_runs(batch_pairs):
+    """scm_table_run_passes: three passes of a row range as one batch stream
+    (with 7-pair batches a batch spans every pass boundary): each pass's
+    packed rows are byte-equal to the CPU oracle's table run, passes arrive in
+    order, and the kept matches are the last pass's."""
+    imgs, (ids, kps, descs) = _table(11, 500, 43)
+    ref = oracle.table_run(ids, kps, descs, 4, 1, 10)
+    if batch_pairs:
+        os.environ["SCM_BATCH_PAIRS"] = batch_pairs
+    try:
+        with Context(0) as ctx:
+            ctx.table_load(ids, kps, descs)
+            ctx.set_keep_matches(True)
+            got = []
+            ctx.table_run_passes(4, 1, 10, 3, lambda k, p: got.append((k, p.rows())))
+            assert [k for k, _ in got] == [0, 1, 2]
+            for _, (pa, pb) in got:
+                assert pa == ref[0] and pb == ref[1]
+            m = ctx.table_matches(3, 2)
+            r = oracle.match_pair(imgs[3][2], imgs[5][2])
+            assert m.shape == r.shape and (m == r).all()
+            ctx.set_keep_matches(False)
+            empty = []
+            ctx.table_run_passes(4, 5, 5, 2, lambda k, p: empty.append(len(p)))
+            assert empty == [0, 0]
+    finally:
+        os.environ.pop("SCM_BATCH_PAIRS", None)
