@@ -69,6 +69,9 @@ def parse():
     p.add_argument("--stencil-rows", type=int, default=128,
                    help="rows of the Scanner drop-in path (scm_execute_batch) timed after the "
                         "table run, rank 0 at N = 1 (0 = skip)")
+    p.add_argument("--no-stream", dest="stream", action="store_false",
+                   help="one scm_table_run_packed call per step (the pipeline drains between "
+                        "steps) instead of the K steps as one streamed run")
     p.add_argument("--no-isolated", dest="isolated", action="store_false",
                    help="skip the extra serialised step that measures isolated kernel rates")
     p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
@@ -424,8 +427,18 @@ def main():
         last["packed"] = packed
         return ctx.table_timings()
 
-    for _ in range(args.warmup):
-        step()
+    def streamed(k):
+        # k steps as one batch stream (scm_table_run_passes): no pipeline drain
+        # between steps; every step's rows are produced (and gathered for N > 1)
+        last["packed"] = plan.run_passes(ctx, k, device=device, keep=False)
+        return ctx.table_timings()
+
+    if args.stream:
+        if args.warmup > 0:
+            streamed(args.warmup)
+    else:
+        for _ in range(args.warmup):
+            step()
     plan.drain()
     if world > 1:
         dist.barrier()
@@ -438,8 +451,7 @@ def main():
     score_ms = 0.0
     evals_f = evals_h = 0
     launches = 0
-    for _ in range(args.steps):
-        tm = step()
+    for tm in ([streamed(args.steps)] if args.stream else (step() for _ in range(args.steps))):
         match_ms += tm["match_ms"]
         verify_ms += tm["verify_ms"]
         final_ms += tm["finalize_ms"]
@@ -574,6 +586,9 @@ def main():
             "config": {"workload": args.workload, "description": wl["desc"],
                        "images": total_images, "kpts": kpts, "overlap": overlap,
                        "pairs_per_step": int(total_pairs), "parallelism": f"pairs sharded x{world}",
+                       "steps_as": ("one streamed run (scm_table_run_passes: the batches of step k+1 "
+                                    "enter the GPU pipeline while step k's last batches verify)"
+                                    if args.stream else "one scm_table_run_packed call per step"),
                        "dist_backend": (args.dist_backend if world > 1 else None)},
             "roofline": {
                 "bound": "mfma",

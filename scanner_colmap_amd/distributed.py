@@ -241,6 +241,27 @@ class ShardPlan:
                 gathered = gather_packed(packed.offsets, packed.data, device)
         return packed, gathered
 
+    def run_passes(self, runner, passes: int, device=None, keep: bool = True):
+        """`passes` steps as one streamed run (`runner.table_run_passes`, the
+        scm_table_run_passes binding: the batches of step k + 1 enter the GPU
+        pipeline while step k's last batches are verified).  For world > 1 each
+        step's packed rows go to the plan's Gatherer as soon as the library
+        hands them over, so the gather of step k overlaps the compute of the
+        steps after it; drain() returns the gathered results.  Returns the last
+        step's packed rows."""
+        lb, le = self.local_rows
+        last = {}
+
+        def on_pass(k, packed):
+            last["packed"] = packed
+            if self.world > 1:
+                if self.gatherer is None:
+                    self.gatherer = Gatherer(device)
+                self.gatherer.submit(packed, keep)
+
+        runner.table_run_passes(self.overlap, lb, le, passes, on_pass)
+        return last.get("packed")
+
     def drain(self) -> list:
         """Wait for the background gathers; rank 0: their results in step order."""
         return self.gatherer.drain() if self.gatherer is not None else []

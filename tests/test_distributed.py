@@ -69,8 +69,13 @@ class _OracleRunner:
                     else np.zeros(0, np.uint8))
         return _P()
 
+    def table_run_passes(self, overlap, row_begin, row_end, passes, on_pass):
+        # scm_table_run_passes' contract: each pass's packed rows, in order
+        for k in range(passes):
+            on_pass(k, self.table_run_packed(overlap, row_begin, row_end))
 
-def _rank_main(rank, world, port, n, K, scaling, q, background=False, steps=1):
+
+def _rank_main(rank, world, port, n, K, scaling, q, background=False, steps=1, streamed=False):
     import torch.distributed as dist
 
     from oracle import oracle
@@ -87,10 +92,15 @@ def _rank_main(rank, world, port, n, K, scaling, q, background=False, steps=1):
         c = Corridor(plan.total_images, 400, K, seed=53)
         runner = _OracleRunner(*table_rows(c.images(plan.table_begin, plan.table_end)))
         results = []
-        for _ in range(steps):
-            _, got = plan.step(runner, background=background)
-            results.append(got)
-        if background:
+        if streamed:  # bench.py's default: the steps as one streamed run
+            last = plan.run_passes(runner, steps)
+            assert last is not None
+            results = [None] * steps
+        else:
+            for _ in range(steps):
+                _, got = plan.step(runner, background=background)
+                results.append(got)
+        if background or streamed:
             assert results == [None] * steps
             results = plan.drain()
         if rank == 0:
@@ -215,3 +225,23 @@ def test_shard_plan_scaling():
     assert sum(p.pairs() for p in [sd.ShardPlan(128, 128, 8, r, "strong") for r in range(8)]) == 8128
     with pytest.raises(ValueError):
         sd.ShardPlan(10, 3, 2, 0, "both")
+
+
+def test_gloo_streamed_passes_world2():
+    """ShardPlan.run_passes (bench.py's timed form): three steps as one
+    streamed run, each step's rows handed to the gather thread as the runner
+    produces them; drain() returns every step's rows, equal to a one-rank run."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main,
+                         args=(r, world, port, 7, 4, "strong", q, False, 3, True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert [p.exitcode for p in procs] == [0, 0]
+    ok, _, nrows, total = q.get(timeout=5)
+    assert ok and nrows == total == 7
