@@ -197,3 +197,16 @@ def test_context_without_gpu_fails_loudly():
     with pytest.raises(_abi.ScmError) as e:
         _abi.Context(0)
     assert e.value.code == _abi.SCM_E_DEVICE
+
+
+def test_null_arguments_are_rejected_without_a_gpu():
+    """Entry points validate their arguments before touching the device:
+    a null context or callback is SCM_E_INVALID (no crash, no GPU needed)."""
+    lib = _abi.load_library()
+    cb = _abi.PASS_FN(lambda *a: None)
+    assert lib.scm_table_run_passes(None, 3, 0, 1, 1, cb, None) == _abi.SCM_E_INVALID
+    a, b, c = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+    assert lib.scm_stencil_spec_stats(None, ctypes.byref(a), ctypes.byref(b),
+                                      ctypes.byref(c)) == _abi.SCM_E_INVALID
+    t = (ctypes.c_double * 12)()
+    assert lib.scm_table_timings(None, t, 12) == _abi.SCM_E_INVALID
