@@ -69,9 +69,10 @@ def parse():
     p.add_argument("--stencil-rows", type=int, default=128,
                    help="rows of the Scanner drop-in path (scm_execute_batch) timed after the "
                         "table run, rank 0 at N = 1 (0 = skip)")
-    p.add_argument("--no-stream", dest="stream", action="store_false",
-                   help="one scm_table_run_packed call per step (the pipeline drains between "
-                        "steps) instead of the K steps as one streamed run")
+    p.add_argument("--stream", action="store_true",
+                   help="run the K steps as one streamed run (scm_table_run_passes: no pipeline "
+                        "drain between steps) instead of one scm_table_run_packed call per step; "
+                        "measured equal or slower (DESIGN.md section 4)")
     p.add_argument("--no-isolated", dest="isolated", action="store_false",
                    help="skip the extra serialised step that measures isolated kernel rates")
     p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
