@@ -317,6 +317,7 @@ struct BatchSet {
   hipStream_t rstream = nullptr;  // replay stream of speculative windows (another set's vstream)
   hipStream_t fstream = nullptr;  // early verify_final pass of small batches (the third set's)
   hipEvent_t wev[2 * kMaxVerifyWindows] = {};
+  hipEvent_t dev[2 * kMaxVerifyWindows + 1] = {};  // decoupled draws (VerifySpec::draw_ev)
   hipEvent_t fev = nullptr;
   HostBuf stage, vstage;
   PinnedOut out;
@@ -357,6 +358,10 @@ struct BatchSet {
       e = nullptr;
     }
     for (auto& e : wev) {
+      if (e) (void)hipEventDestroy(e);
+      e = nullptr;
+    }
+    for (auto& e : dev) {
       if (e) (void)hipEventDestroy(e);
       e = nullptr;
     }
@@ -1197,7 +1202,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       SCM_TRY(mods.ensure(V * kWindowTrials * 3 * 9 * sizeof(double)));
       SCM_TRY(cnts.ensure(V * kWindowTrials * 3 * sizeof(uint32_t)));
       if (split) SCM_TRY(ucnt.ensure(V * kWindowTrials * 3 * sizeof(uint32_t)));
-      SCM_TRY(wsnap.ensure(V * kMaxWindow * 640 * sizeof(uint32_t)));
+      SCM_TRY(wsnap.ensure(V * 640 * sizeof(uint32_t)));  // window start states
       SCM_TRY(wb.ensure(V * sizeof(int32_t)));
       SCM_TRY(wstate.ensure(V * kVerifyStateWords * sizeof(uint32_t)));
       rb->samp = samp.as<uint32_t>();
@@ -1257,9 +1262,12 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       const int si = (int)(&bs - ctx->sets);
       bs.rstream = ctx->sets[(si + 1) % 3].vstream;
       bs.fstream = ctx->sets[(si + 2) % 3].vstream;
-      if (!bs.wev[0])
+      if (!bs.wev[0]) {
         for (auto& e : bs.wev)
           SCM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice));
+        for (auto& e : bs.dev)
+          SCM_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventReleaseToDevice));
+      }
 
       if (!bs.fev)
         SCM_HIP(hipEventCreateWithFlags(&bs.fev, hipEventDisableTiming | hipEventReleaseToDevice));
@@ -1270,6 +1278,17 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
         spec.win_ev = bs.wev;
         spec.fstream = bs.fstream;
         spec.fin_ev = bs.fev;
+        // The windows' draws run ahead on the early-final stream (idle until
+        // H's last window is replayed).  SCM_DRAW_STREAM=0 (diagnostics):
+        // draws in order on the scoring stream.
+        static const bool draw_stream = [] {
+          const char* e = getenv("SCM_DRAW_STREAM");
+          return !(e && e[0] == '0');
+        }();
+        if (draw_stream) {
+          spec.dstream = bs.fstream;
+          spec.draw_ev = bs.dev;
+        }
       }
     }
     SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
@@ -1638,7 +1657,7 @@ int64_t pair_workspace_bytes(int64_t n1, int64_t n2) {
   const int64_t verify_pair = verify_scratch_doubles(slots) * 8 + kVerifySnapWords * 4 +
                               (int64_t)sizeof(RansacState) + (int64_t)sizeof(VerifyOut) +
                               2 * ((int64_t)kWindowTrials * (8 * 4 + 4 + 3 * 12 * 4 + 3 * 9 * 8 + 2 * 3 * 4) +
-                                   (int64_t)kMaxWindow * 640 * 4) + 256;  // F and H round buffers
+                                   640 * 4) + 256;  // F and H round buffers
   return match + verify_pts + verify_pair;
 }
 

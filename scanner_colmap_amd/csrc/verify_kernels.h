@@ -83,7 +83,7 @@ constexpr int kWindowTrials = kMaxWindow * kTrialBatch;
 
 // Device buffers of the windowed verifier (V = pairs of a batch, T =
 // kWindowTrials): rst[V], samp[V][T*8], nmod[V][T], fcon[V][3T][12],
-// mods[V][3T][9], cnts[V][3T], wsnap[V][kMaxWindow][640], act[2][V],
+// mods[V][3T][9], cnts[V][3T], wsnap[V][640] (the window's start PRNG state), act[2][V],
 // nact[2].
 // One window parity's buffers of one RANSAC kind.  The per-window buffers
 // (samp .. wstate) exist twice for small batches, so that the draws, shuffles,
@@ -130,6 +130,10 @@ struct VerifySpec {
   hipEvent_t* win_ev = nullptr;
   hipStream_t fstream = nullptr;
   hipEvent_t fin_ev = nullptr;
+  // Decoupled draws (optional): window r's draws run on dstream beside window
+  // r - 1's scoring; draw_ev: 2 * kMaxVerifyWindows + 1 events.
+  hipStream_t dstream = nullptr;
+  hipEvent_t* draw_ev = nullptr;
 };
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,

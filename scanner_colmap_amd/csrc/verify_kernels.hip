@@ -251,6 +251,50 @@ __device__ bool draw_targets_wave(VerifyLds& s, int D, uint32_t n) {
   return ok;
 }
 
+// One round's D draws into s.jbuf, as the sequential generator makes them:
+// wave-parallel, or -- when some draw might need Lemire's rejection step --
+// serially from the round's start state, kept in registers (no round
+// snapshot in memory: its stores would hold every later barrier of the round
+// until they complete).  Any block size from 64 threads up.
+template <int KMIN>
+__device__ void draw_round(VerifyLds& s, int D, uint32_t n) {
+  constexpr int KW = (624 + 63) / 64;
+  uint32_t keep[KW];
+#pragma unroll
+  for (int k = 0; k < KW; ++k) {
+    const int i = threadIdx.x + blockDim.x * k;
+    keep[k] = i < 624 ? s.mt[i] : 0u;
+  }
+  const int kidx = s.mt_idx;
+  if (!draw_targets_wave<KMIN>(s, D, n)) {
+#pragma unroll
+    for (int k = 0; k < KW; ++k) {
+      const int i = threadIdx.x + blockDim.x * k;
+      if (i < 624) s.mt[i] = keep[k];
+    }
+    wsync();
+    if (threadIdx.x == 0) {
+      s.mt_idx = kidx;
+      const uint32_t last = n - 1u;
+      for (int r = 0; r < D; ++r) s.jbuf[r] = uniform_u32(s, (uint32_t)(r % KMIN), last);
+    }
+    wsync();
+  }
+}
+
+// The abort rewind of a window: from the window's start state (the one
+// snapshot its draws keep), the draws of its first `rounds` rounds (full:
+// kTrialBatch trials each) and then `extra` more.
+template <int KMIN>
+__device__ void mt_advance_draws(VerifyLds& s, int rounds, int extra, uint32_t n) {
+  for (int r = 0; r < rounds; ++r) {
+    draw_round<KMIN>(s, kTrialBatch * KMIN, n);
+    wsync();
+  }
+  if (extra > 0) draw_round<KMIN>(s, extra, n);
+  wsync();
+}
+
 // RandomSampler::Sample's Shuffle for B samples with precomputed targets:
 // the kmin hot positions live in registers, cold targets are read from LDS
 // once per sample (several reads in flight) and written back in order.
@@ -2119,22 +2163,13 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
     for (int w = 0; w * kTrialBatch < Btot; ++w) {
       const int B = min(kTrialBatch, Btot - w * kTrialBatch);
-      uint32_t* snap = wsnap + ((int64_t)q * kMaxWindow + w) * 640;
-      for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
-      if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
-      wsync();
-      if (!draw_targets_wave<Tr::kmin>(s, B * Tr::kmin, (uint32_t)n)) {
-        // A draw may need Lemire's rejection step: serial draws from the
-        // round's snapshot (the targets do not depend on the shuffle state).
-        for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
-        wsync();
-        if (lane == 0) {
-          s.mt_idx = (int32_t)snap[624];
-          const uint32_t last = (uint32_t)(n - 1);
-          for (int r = 0; r < B * Tr::kmin; ++r)
-            s.jbuf[r] = uniform_u32(s, (uint32_t)(r % Tr::kmin), last);
-        }
+      if (w == 0) {  // the window's start state, for the abort rewind
+        uint32_t* snap = wsnap + (int64_t)q * 640;
+        for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
+        if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
       }
+      // (the targets do not depend on the shuffle state)
+      draw_round<Tr::kmin>(s, B * Tr::kmin, (uint32_t)n);
       wsync();
       for (int r = lane; r < B * Tr::kmin; r += 64)
         sq[(w * kTrialBatch + r / Tr::kmin) * 8 + r % Tr::kmin] = s.jbuf[r];
@@ -2277,6 +2312,7 @@ struct WsDraw {
   const uint32_t* pcnts;
   const int32_t* pwB;
   int spec, W;
+  int clr;  // clear the list the window's replay fills (0: rs_prune2_kernel does)
 };
 
 template <int K, bool DRAW = false>
@@ -2297,7 +2333,7 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
   uint16_t* V = hsym + 64 * 8;                                           // the vector (+ dummies)
   const int lane = threadIdx.x;
   const uint32_t dummy = (uint32_t)(stride + lane);
-  if (DRAW && bid == 0 && lane == 0) *dr.nact_next = 0;
+  if (DRAW && dr.clr && bid == 0 && lane == 0) *dr.nact_next = 0;
   const int na = *nact;
   for (int a = bid; a < na; a += nblk) {
     const int q = act[a];
@@ -2360,19 +2396,12 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
         for (int w0 = 0; w0 * kTrialBatch < np; ++w0) {
           const int B = min(kTrialBatch, np - w0 * kTrialBatch);
           const int wg = p0 / kTrialBatch + w0;  // round of the window
-          uint32_t* snap = dr.wsnap + ((int64_t)q * kMaxWindow + wg) * 640;
-          for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
-          if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
-          wsync();
-          if (!draw_targets_wave<KM>(s, B * KM, (uint32_t)n)) {
-            for (int i = lane; i < 624; i += 64) s.mt[i] = snap[i];
-            wsync();
-            if (lane == 0) {
-              s.mt_idx = (int32_t)snap[624];
-              const uint32_t last = (uint32_t)(n - 1);
-              for (int r = 0; r < B * KM; ++r) s.jbuf[r] = uniform_u32(s, (uint32_t)(r % KM), last);
-            }
+          if (wg == 0) {  // the window's start state, for the abort rewind
+            uint32_t* snap = dr.wsnap + (int64_t)q * 640;
+            for (int i = lane; i < 624; i += 64) snap[i] = s.mt[i];
+            if (lane == 0) snap[624] = (uint32_t)s.mt_idx;
           }
+          draw_round<KM>(s, B * KM, (uint32_t)n);
           wsync();
           if (lane < B) {
             uint32_t tg[8];
@@ -2551,20 +2580,67 @@ __global__ __launch_bounds__(64) void rs_drawshuffle_wave2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
     VerifyRoundBufs rh, int ain, int aclr, VerifyParams P, int spec, int W,
-    uint64_t* __restrict__ prof, int stride, int split) {
+    uint64_t* __restrict__ prof, int stride, int split, int clr) {
   if ((int)blockIdx.x < split) {
     const WsDraw d{rf.rst, rf.nact + aclr, rf.cnts, rf.ucnt, rf.wsnap, rf.pstate, rf.wstate,
-                   rf.dtrial, rf.pcnts, rf.pwB, spec, W};
+                   rf.dtrial, rf.pcnts, rf.pwB, spec, W, clr};
     rs_shuffle_wave_body<KIND_F, true>(pairs, scratch, snaps, out, rf.wB, rf.act[ain],
                                        rf.nact + ain, rf.samp, prof, stride, blockIdx.x, split, d,
                                        &P);
   } else {
     const WsDraw d{rh.rst, rh.nact + aclr, rh.cnts, rh.ucnt, rh.wsnap, rh.pstate, rh.wstate,
-                   rh.dtrial, rh.pcnts, rh.pwB, spec, W};
+                   rh.dtrial, rh.pcnts, rh.pwB, spec, W, clr};
     rs_shuffle_wave_body<KIND_H, true>(pairs, scratch, snaps, out, rh.wB, rh.act[ain],
                                        rh.nact + ain, rh.samp, prof, stride, blockIdx.x - split,
                                        gridDim.x - split, d, &P);
   }
+}
+
+// Decoupled draws (small batches, run_windows): window r's draws run on their
+// own stream beside window r - 1's scoring, so the two steps of a window's
+// draws that need window r - 1 to be scored run here instead, on the scoring
+// stream, right before window r's solves: the list window r's replay fills
+// (aclr) is cleared, and a pair certain to stop in window r - 1 (the bound of
+// rs_draw_body's speculative skip, over window r - 1's counts) gets no trials
+// in window r (wB = 0: its solves and scores exit; its draws are never used,
+// since window r - 1's replay rewinds the pair's PRNG to its stop).  At this
+// point dtrial holds the draws through window r exactly (window r + 1's draws
+// wait for this kernel), so window r - 1's last trial is dtrial - wB - 1.
+template <int K>
+__device__ __forceinline__ void rs_prune_body(const VerifyPair* __restrict__ pairs,
+                                              const VerifyRoundBufs& rb, int ain,
+                                              const VerifyParams& P, int bid, int nblk) {
+  using Tr = KindTraits<K>;
+  const int lane = threadIdx.x;
+  const int na = rb.nact[ain];
+  for (int a = bid; a < na; a += nblk) {
+    const int q = rb.act[ain][a];
+    const int B = rb.wB[q];
+    const int Bp = rb.pwB[q];
+    if (B <= 0 || Bp <= 0) continue;
+    const uint32_t* pc = rb.pcnts + (int64_t)q * kWindowTrials * 3;
+    uint32_t cm = 0;
+    for (int i = lane; i < Bp * Tr::mm; i += 64) cm = max(cm, pc[i]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cm = max(cm, (uint32_t)__shfl_xor((int)cm, d));
+    const int last = rb.dtrial[q] - B - 1;
+    const uint64_t bound = num_trials((uint64_t)cm, (uint64_t)pairs[q].m, P.confidence,
+                                      P.dyn_num_trials_multiplier, Tr::kmin);
+    if (last >= P.min_num_trials && (uint64_t)last >= bound && lane == 0) rb.wB[q] = 0;
+  }
+}
+
+__global__ __launch_bounds__(64) void rs_prune2_kernel(const VerifyPair* __restrict__ pairs,
+                                                      VerifyRoundBufs rf, VerifyRoundBufs rh,
+                                                      int ain, int aclr, VerifyParams P,
+                                                      int skip, int split) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    rf.nact[aclr] = 0;
+    rh.nact[aclr] = 0;
+  }
+  if (!skip) return;
+  if ((int)blockIdx.x < split) rs_prune_body<KIND_F>(pairs, rf, ain, P, blockIdx.x, split);
+  else rs_prune_body<KIND_H>(pairs, rh, ain, P, blockIdx.x - split, gridDim.x - split);
 }
 
 // Minimal solvers, one thread per hypothesis of the window, plus the fp32
@@ -3095,18 +3171,13 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     wsync();
     if (abort) {
       // Rewind the PRNG to the state right after trial abort_trial's sample:
-      // the state before its round, then that round's draws up to it.
-      const int w = (abort_trial - trial) / kTrialBatch;
-      const uint32_t* snap = wsnap + ((int64_t)q * kMaxWindow + w) * 640;
+      // the window's start state, then its draws up to that trial.
+      const int rel = abort_trial - trial, w = rel / kTrialBatch;
+      const uint32_t* snap = wsnap + (int64_t)q * 640;
       for (int i = threadIdx.x; i < 624; i += 64 * NW) s.mt[i] = snap[i];
+      if (t0th) s.mt_idx = (int32_t)snap[624];
       wsync();
-      if (t0th) {
-        s.mt_idx = (int32_t)snap[624];
-        const uint32_t last = (uint32_t)(n - 1);
-        for (int b = 0; b <= abort_trial - trial - w * kTrialBatch; ++b)
-          for (int i = 0; i < Tr::kmin; ++i) (void)uniform_u32(s, (uint32_t)i, last);
-      }
-      wsync();
+      mt_advance_draws<Tr::kmin>(s, w, (rel - w * kTrialBatch + 1) * Tr::kmin, (uint32_t)n);
       mt_save(s, ps.state);
       st.num_trials = abort_trial + 2;
       st.done = 1;
@@ -3309,7 +3380,8 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                        const VerifyParams& P, const float4* xyf, const VerifyRoundBufs* rfp,
                        const VerifyRoundBufs* rhp, int max_chunks, int max_m, uint64_t* prof,
                        hipStream_t stream, hipEvent_t* score_ev, int* nwin, bool spec,
-                       hipStream_t rstream, hipEvent_t* win_ev, int* last_h) {
+                       hipStream_t rstream, hipEvent_t* win_ev, int* last_h,
+                       hipStream_t dstream, hipEvent_t* draw_ev) {
   const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
   const int gw = npairs < kPairGrid ? npairs : kPairGrid;
   constexpr int kShuffleLdsKb = 16;
@@ -3336,6 +3408,15 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     return e ? atoi(e) : 0;
   }();
   if (w0_env > 0) W = std::min(W, w0_env);
+  // Decoupled draws (speculative schedule with a draw stream): window r's
+  // draws and shuffles run on dstream as soon as window r - 2 is replayed (its
+  // active list) and window r - 1's prune has run (the lists and counts it
+  // reads), i.e. beside window r - 1's solves and scores; rs_prune2_kernel
+  // then does, on `stream`, the parts of the draws that need window r - 1's
+  // scores.  draw_ev: 2r = window r drawn, 2r + 1 = window r pruned, and
+  // 2 * kMaxVerifyWindows = the batch's begin kernel done.
+  const bool dsplit = spec && wave_sh && dstream && draw_ev;
+  if (dsplit) (void)hipEventRecord(draw_ev[2 * kMaxVerifyWindows], stream);
   int covered = 0, r = 0;
   while (covered < P.max_trials_F || covered < P.max_trials_H) {
     const VerifyRoundBufs& rf = rfp[r & 1];
@@ -3349,10 +3430,21 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     if (h && last_h) *last_h = r;
     const int g1 = (f ? gw : 0) + (h ? gw : 0), s1 = f ? gw : 0;
     const int g2 = (f ? sh_blocks : 0) + (h ? sh_blocks : 0), s2 = f ? sh_blocks : 0;
-    if (wave_sh) {
+    if (dsplit && r < kMaxVerifyWindows) {
+      if (r >= 2) (void)hipStreamWaitEvent(dstream, win_ev[2 * (r - 2) + 1], 0);
+      (void)hipStreamWaitEvent(dstream, draw_ev[r == 0 ? 2 * kMaxVerifyWindows : 2 * r - 1], 0);
+      hipLaunchKernelGGL(rs_drawshuffle_wave2_kernel, dim3(g1), dim3(64), kWsDrawHead + wave_lds,
+                         dstream, pairs, scratch, snaps, out, rf, rh, lw, lout, P, 0, W, prof,
+                         wave_stride, s1, 0);
+      (void)hipEventRecord(draw_ev[2 * r], dstream);
+      (void)hipStreamWaitEvent(stream, draw_ev[2 * r], 0);
+      hipLaunchKernelGGL(rs_prune2_kernel, dim3(g1), dim3(64), 0, stream, pairs, rf, rh, lw, lout,
+                         P, r > 0 ? 1 : 0, s1);
+      (void)hipEventRecord(draw_ev[2 * r + 1], stream);
+    } else if (wave_sh) {
       hipLaunchKernelGGL(rs_drawshuffle_wave2_kernel, dim3(g1), dim3(64), kWsDrawHead + wave_lds,
                          stream, pairs, scratch, snaps, out, rf, rh, lw, lout, P,
-                         (spec && r > 0) ? 1 : 0, W, prof, wave_stride, s1);
+                         (spec && r > 0) ? 1 : 0, W, prof, wave_stride, s1, 1);
     } else {
       hipLaunchKernelGGL(rs_draw2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
                          out, rf, rh, lw, lout, P, (spec && r > 0) ? 1 : 0, W, s1);
@@ -3501,7 +3593,8 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   int last_h = -1;
   if ((err = run_windows(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf, rfp,
                          rhp, max_chunks, max_m, prof, stream, score_ev, nwin, sp,
-                         sp ? spec->rstream : stream, sp ? spec->win_ev : nullptr, &last_h)) !=
+                         sp ? spec->rstream : stream, sp ? spec->win_ev : nullptr, &last_h,
+                         sp ? spec->dstream : nullptr, sp ? spec->draw_ev : nullptr)) !=
       hipSuccess)
     return err;
   if (sp && last_h >= 0 && last_h < kMaxVerifyWindows) {
