@@ -1278,15 +1278,16 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
         spec.win_ev = bs.wev;
         spec.fstream = bs.fstream;
         spec.fin_ev = bs.fev;
-        // The windows' draws run ahead on the early-final stream (idle until
-        // H's last window is replayed).  SCM_DRAW_STREAM=0 (diagnostics):
-        // draws in order on the scoring stream.
+        // The windows' draws run ahead on the matching stream (a small
+        // batch's matching is done before its verification starts; on the
+        // early-final stream they held that pass back).  SCM_DRAW_STREAM=0
+        // (diagnostics): draws in order on the scoring stream.
         static const bool draw_stream = [] {
           const char* e = getenv("SCM_DRAW_STREAM");
           return !(e && e[0] == '0');
         }();
         if (draw_stream) {
-          spec.dstream = bs.fstream;
+          spec.dstream = ctx->stream;
           spec.draw_ev = bs.dev;
         }
       }

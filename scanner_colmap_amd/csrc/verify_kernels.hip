@@ -251,6 +251,20 @@ __device__ bool draw_targets_wave(VerifyLds& s, int D, uint32_t n) {
   return ok;
 }
 
+// Trials of the pair's run not drawn yet that its sequential loop can still
+// reach: the loop stops after the first trial tt with tt >= dyn_max and tt >=
+// min_num_trials, and dyn_max only falls as the best grows, so with the last
+// dyn_max a replay stored (rst.dyn_max; a lagging value only bounds higher)
+// no trial past max(dyn_max, min_num_trials) is ever needed -- the window
+// is not drawn (and scored) past it.  Same trials, same order: only the
+// window's length changes.
+__device__ __forceinline__ int trials_left(const RansacState* st, int drawn, int min_trials) {
+  int cap = st->max_trials;
+  const int last = max(st->dyn_max, min_trials);
+  if (last < cap) cap = last + 1;
+  return cap - drawn;
+}
+
 // One round's D draws into s.jbuf, as the sequential generator makes them:
 // wave-parallel, or -- when some draw might need Lemire's rejection step --
 // serially from the round's start state, kept in registers (no round
@@ -2140,7 +2154,7 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     const int n = ps.n;
     // (the trials drawn so far, not the replay's count: this window may be
     // drawn while the previous one is still replayed)
-    int Btot = max(0, min(kTrialBatch * W, rst[q].max_trials - dtrial[q]));
+    int Btot = max(0, min(kTrialBatch * W, trials_left(rst + q, dtrial[q], P.min_num_trials)));
     if (spec && Btot > 0) {
       // Speculative window: skip a pair certain to stop in the previous window.
       // Its best count after that window is at least every count the window
@@ -2343,7 +2357,8 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
     int Bdraw = 0;
     if (DRAW) {  // as rs_draw_body
       const VerifyParams& P = *Pp;
-      Bdraw = max(0, min(kTrialBatch * dr.W, dr.rst[q].max_trials - dr.dtrial[q]));
+      Bdraw = max(0, min(kTrialBatch * dr.W,
+                              trials_left(dr.rst + q, dr.dtrial[q], P.min_num_trials)));
       if (dr.spec && Bdraw > 0) {
         const int Bp = dr.pwB[q];
         const uint32_t* pc2 = dr.pcnts + (int64_t)q * kWindowTrials * 3;
