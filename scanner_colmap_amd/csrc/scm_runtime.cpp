@@ -1192,16 +1192,18 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
     bs.nprof = V;
     SCM_HIP(hipEventRecord(bs.ev[4], sv));
     // Round buffers per kind (H: one model per hypothesis): the window
-    // buffers of one parity, then the per-pair state.
+    // buffers of one parity, then the per-pair state.  Small batches take
+    // windows of up to kMaxWindowSmall rounds (VerifyRoundBufs::wt).
+    const int64_t wt = verify_small_batch((int)V, max_m) ? kWindowTrialsSmall : kWindowTrials;
     auto window_bufs = [&](DevBuf& samp, DevBuf& nmod, DevBuf& fcon, DevBuf& mods, DevBuf& cnts,
                            DevBuf& ucnt, DevBuf& wsnap, DevBuf& wb, DevBuf& wstate, bool split,
                            VerifyRoundBufs* rb) -> int {
-      SCM_TRY(samp.ensure(V * kWindowTrials * 8 * sizeof(uint32_t)));
-      SCM_TRY(nmod.ensure(V * kWindowTrials * sizeof(int32_t)));
-      SCM_TRY(fcon.ensure(V * kWindowTrials * 3 * 12 * sizeof(float)));
-      SCM_TRY(mods.ensure(V * kWindowTrials * 3 * 9 * sizeof(double)));
-      SCM_TRY(cnts.ensure(V * kWindowTrials * 3 * sizeof(uint32_t)));
-      if (split) SCM_TRY(ucnt.ensure(V * kWindowTrials * 3 * sizeof(uint32_t)));
+      SCM_TRY(samp.ensure(V * wt * 8 * sizeof(uint32_t)));
+      SCM_TRY(nmod.ensure(V * wt * sizeof(int32_t)));
+      SCM_TRY(fcon.ensure(V * wt * 3 * 12 * sizeof(float)));
+      SCM_TRY(mods.ensure(V * wt * 3 * 9 * sizeof(double)));
+      SCM_TRY(cnts.ensure(V * wt * 3 * sizeof(uint32_t)));
+      if (split) SCM_TRY(ucnt.ensure(V * wt * 3 * sizeof(uint32_t)));
       SCM_TRY(wsnap.ensure(V * 640 * sizeof(uint32_t)));  // window start states
       SCM_TRY(wb.ensure(V * sizeof(int32_t)));
       SCM_TRY(wstate.ensure(V * kVerifyStateWords * sizeof(uint32_t)));
@@ -1214,6 +1216,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       rb->wsnap = wsnap.as<uint32_t>();
       rb->wB = wb.as<int32_t>();
       rb->wstate = rb->pstate = wstate.as<uint32_t>();
+      rb->wt = (int)wt;
       return SCM_OK;
     };
     auto round_bufs = [&](DevBuf& rst, DevBuf& samp, DevBuf& nmod, DevBuf& fcon, DevBuf& mods,

@@ -78,11 +78,17 @@ struct RansacState {
 };
 
 // Windowed verifier: up to kMaxWindow rounds of kTrialBatch hypotheses.
-constexpr int kMaxWindow = 32;  // rounds per window at most (16: -1.3 %, 64: -1 %, bench s35)
+constexpr int kMaxWindow = 32;  // rounds per window at most (16: -1.3 %, 64: -1 %, bench s35;
+                                // 64 again after trials_left: -0.4 %, profiles/r04_l)
 constexpr int kWindowTrials = kMaxWindow * kTrialBatch;
+// Small batches (verify_small_batch): windows of up to 64 rounds -- every
+// window is one more latency-bound stage of a stencil's chain (19-pair
+// stencil: 3.35 ms per call with 32, 3.13 ms with 64, profiles/r04_k).
+constexpr int kMaxWindowSmall = 64;
+constexpr int kWindowTrialsSmall = kMaxWindowSmall * kTrialBatch;
 
 // Device buffers of the windowed verifier (V = pairs of a batch, T =
-// kWindowTrials): rst[V], samp[V][T*8], nmod[V][T], fcon[V][3T][12],
+// VerifyRoundBufs::wt): rst[V], samp[V][T*8], nmod[V][T], fcon[V][3T][12],
 // mods[V][3T][9], cnts[V][3T], wsnap[V][640] (the window's start PRNG state), act[2][V],
 // nact[2].
 // One window parity's buffers of one RANSAC kind.  The per-window buffers
@@ -107,6 +113,8 @@ struct VerifyRoundBufs {
   int32_t* dtrial;   // trials drawn so far
   int32_t* act[3];   // active-pair lists (rotating: window r's replay reads r % 3)
   int32_t* nact;     // their lengths [3]
+  int wt;            // trials per pair the window buffers hold (T: kWindowTrials or
+                     // kWindowTrialsSmall); the windows' rounds are at most wt / kTrialBatch
 };
 constexpr int kVerifyStateWords = 640;
 

@@ -2141,7 +2141,8 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     uint32_t* __restrict__ ucnt, uint32_t* __restrict__ wsnap, int32_t* __restrict__ wB,
     const uint32_t* __restrict__ pstate, uint32_t* __restrict__ wstate,
     int32_t* __restrict__ dtrial, const uint32_t* __restrict__ pcnts,
-    const int32_t* __restrict__ pwB, const VerifyParams& P, bool spec, int W, int bid, int nblk) {
+    const int32_t* __restrict__ pwB, const VerifyParams& P, bool spec, int W, int bid, int nblk,
+    int WT) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
@@ -2162,7 +2163,7 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
       // its trial bound is at most ComputeNumTrials(cmax); if that bound
       // falls inside the previous window, the pair aborts there.
       const int Bp = pwB[q];
-      const uint32_t* pc = pcnts + (int64_t)q * kWindowTrials * 3;
+      const uint32_t* pc = pcnts + (int64_t)q * WT * 3;
       uint32_t cm = 0;
       for (int i = lane; i < Bp * Tr::mm; i += 64) cm = max(cm, pc[i]);
 #pragma unroll
@@ -2174,7 +2175,7 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
     }
     wsync();
     mt_load(s, pstate + (int64_t)q * kVerifyStateWords);
-    uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
+    uint32_t* sq = samp + (int64_t)q * WT * 8;
     for (int w = 0; w * kTrialBatch < Btot; ++w) {
       const int B = min(kTrialBatch, Btot - w * kTrialBatch);
       if (w == 0) {  // the window's start state, for the abort rewind
@@ -2190,10 +2191,10 @@ __device__ __attribute__((always_inline)) void rs_draw_body(
       wsync();
     }
     mt_save(s, wstate + (int64_t)q * kVerifyStateWords);
-    uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3;
+    uint32_t* cq = cnts + (int64_t)q * WT * 3;
     for (int i = lane; i < Btot * 3; i += 64) cq[i] = 0u;
     if (ucnt) {
-      uint32_t* uq = ucnt + (int64_t)q * kWindowTrials * 3;
+      uint32_t* uq = ucnt + (int64_t)q * WT * 3;
       for (int i = lane; i < Btot * 3; i += 64) uq[i] = 0u;
     }
     if (lane == 0) {
@@ -2243,7 +2244,8 @@ __device__ __attribute__((always_inline)) void rs_shuffle_body(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
     const int32_t* __restrict__ wB, const int32_t* __restrict__ act,
-    const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, int ppb, int stride, int bid, int nblk) {
+    const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, int ppb, int stride, int bid, int nblk,
+    int WT) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   uint16_t* lsidx = reinterpret_cast<uint16_t*>(dyn_lds);
   const int na = *nact;
@@ -2265,7 +2267,7 @@ __device__ __attribute__((always_inline)) void rs_shuffle_body(
   if ((int)threadIdx.x < np) {
     constexpr int KM = KindTraits<K>::kmin;
     const int q = act[a0 + threadIdx.x];
-    uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
+    uint32_t* sq = samp + (int64_t)q * WT * 8;
     const int Btot = wB[q];
     if (staged) shuffle_chain<KM>(lsidx + threadIdx.x * stride, sq, Btot);
     else shuffle_chain<KM>(pair_sidx(pair_at<K>(pairs, q, scratch, snaps, out)), sq, Btot);
@@ -2335,7 +2337,8 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
     int32_t* __restrict__ wB, const int32_t* __restrict__ act,
     const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, uint64_t* __restrict__ prof,
-    int stride, int bid, int nblk, const WsDraw& dr = WsDraw{}, const VerifyParams* Pp = nullptr) {
+    int WT, int stride, int bid, int nblk, const WsDraw& dr = WsDraw{},
+    const VerifyParams* Pp = nullptr) {
   constexpr int KM = KindTraits<K>::kmin;
   using Tr = KindTraits<K>;
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
@@ -2361,7 +2364,7 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
                               trials_left(dr.rst + q, dr.dtrial[q], P.min_num_trials)));
       if (dr.spec && Bdraw > 0) {
         const int Bp = dr.pwB[q];
-        const uint32_t* pc2 = dr.pcnts + (int64_t)q * kWindowTrials * 3;
+        const uint32_t* pc2 = dr.pcnts + (int64_t)q * WT * 3;
         uint32_t cm = 0;
         for (int i = lane; i < Bp * Tr::mm; i += 64) cm = max(cm, pc2[i]);
 #pragma unroll
@@ -2394,7 +2397,7 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
     }
     __syncthreads();
     lap(0);
-    uint32_t* sq = samp + (int64_t)q * kWindowTrials * 8;
+    uint32_t* sq = samp + (int64_t)q * WT * 8;
     const int Btot = DRAW ? Bdraw : wB[q];
     for (int p0 = 0; p0 < Btot; p0 += kWsPass) {
       const int np = min(kWsPass, Btot - p0);
@@ -2561,10 +2564,10 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
     for (int i = lane; i < n; i += 64) g[i] = V[i];
     if (DRAW) {
       mt_save(s, dr.wstate + (int64_t)q * kVerifyStateWords);
-      uint32_t* cq = dr.cnts + (int64_t)q * kWindowTrials * 3;
+      uint32_t* cq = dr.cnts + (int64_t)q * WT * 3;
       for (int i = lane; i < Btot * 3; i += 64) cq[i] = 0u;
       if (dr.ucnt) {
-        uint32_t* uq = dr.ucnt + (int64_t)q * kWindowTrials * 3;
+        uint32_t* uq = dr.ucnt + (int64_t)q * WT * 3;
         for (int i = lane; i < Btot * 3; i += 64) uq[i] = 0u;
       }
       if (lane == 0) {
@@ -2583,10 +2586,10 @@ __global__ __launch_bounds__(64) void rs_shuffle_wave2_kernel(
     VerifyRoundBufs rh, int ain, uint64_t* __restrict__ prof, int stride, int split) {
   if ((int)blockIdx.x < split)
     rs_shuffle_wave_body<KIND_F>(pairs, scratch, snaps, out, rf.wB, rf.act[ain], rf.nact + ain,
-                                 rf.samp, prof, stride, blockIdx.x, split);
+                                 rf.samp, prof, rf.wt, stride, blockIdx.x, split);
   else
     rs_shuffle_wave_body<KIND_H>(pairs, scratch, snaps, out, rh.wB, rh.act[ain], rh.nact + ain,
-                                 rh.samp, prof, stride, blockIdx.x - split, gridDim.x - split);
+                                 rh.samp, prof, rh.wt, stride, blockIdx.x - split, gridDim.x - split);
 }
 
 
@@ -2600,13 +2603,13 @@ __global__ __launch_bounds__(64) void rs_drawshuffle_wave2_kernel(
     const WsDraw d{rf.rst, rf.nact + aclr, rf.cnts, rf.ucnt, rf.wsnap, rf.pstate, rf.wstate,
                    rf.dtrial, rf.pcnts, rf.pwB, spec, W, clr};
     rs_shuffle_wave_body<KIND_F, true>(pairs, scratch, snaps, out, rf.wB, rf.act[ain],
-                                       rf.nact + ain, rf.samp, prof, stride, blockIdx.x, split, d,
+                                       rf.nact + ain, rf.samp, prof, rf.wt, stride, blockIdx.x, split, d,
                                        &P);
   } else {
     const WsDraw d{rh.rst, rh.nact + aclr, rh.cnts, rh.ucnt, rh.wsnap, rh.pstate, rh.wstate,
                    rh.dtrial, rh.pcnts, rh.pwB, spec, W, clr};
     rs_shuffle_wave_body<KIND_H, true>(pairs, scratch, snaps, out, rh.wB, rh.act[ain],
-                                       rh.nact + ain, rh.samp, prof, stride, blockIdx.x - split,
+                                       rh.nact + ain, rh.samp, prof, rh.wt, stride, blockIdx.x - split,
                                        gridDim.x - split, d, &P);
   }
 }
@@ -2627,13 +2630,14 @@ __device__ __forceinline__ void rs_prune_body(const VerifyPair* __restrict__ pai
                                               const VerifyParams& P, int bid, int nblk) {
   using Tr = KindTraits<K>;
   const int lane = threadIdx.x;
+  const int WT = rb.wt;
   const int na = rb.nact[ain];
   for (int a = bid; a < na; a += nblk) {
     const int q = rb.act[ain][a];
     const int B = rb.wB[q];
     const int Bp = rb.pwB[q];
     if (B <= 0 || Bp <= 0) continue;
-    const uint32_t* pc = rb.pcnts + (int64_t)q * kWindowTrials * 3;
+    const uint32_t* pc = rb.pcnts + (int64_t)q * WT * 3;
     uint32_t cm = 0;
     for (int i = lane; i < Bp * Tr::mm; i += 64) cm = max(cm, pc[i]);
 #pragma unroll
@@ -2667,7 +2671,7 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
     const double* __restrict__ xy2_all, const RansacState* __restrict__ rst,
     const int32_t* __restrict__ wB, const int32_t* __restrict__ act, const int32_t* __restrict__ nact,
     const uint32_t* __restrict__ samp, int32_t* __restrict__ nmod, float* __restrict__ fcon,
-    double* __restrict__ mods, int W, double maxr) {
+    double* __restrict__ mods, int W, double maxr, int WT) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   const int na = *nact;
@@ -2680,7 +2684,7 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
     const double S = rst[q].S;
     const double* xy1 = xy1_all + pp.pts_off;
     const double* xy2 = xy2_all + pp.pts_off;
-    const uint32_t* sq = samp + ((int64_t)q * kWindowTrials + h) * 8;
+    const uint32_t* sq = samp + ((int64_t)q * WT + h) * 8;
     double a_[2 * 7], b_[2 * 7];
 #pragma unroll
     for (int i = 0; i < Tr::kmin; ++i) {
@@ -2690,12 +2694,12 @@ __global__ __launch_bounds__(64) void rs_solve_kernel(
       b_[2 * i] = xy2[2 * k];
       b_[2 * i + 1] = xy2[2 * k + 1];
     }
-    double* mo = mods + ((int64_t)q * kWindowTrials * 3 + h * MM) * MS;
+    double* mo = mods + ((int64_t)q * WT * 3 + h * MM) * MS;
     int nm = 1;
     if (K == KIND_F) nm = fundamental_7pt(a_, b_, mo);
     else homography_dlt(a_, b_, 4, mo);
-    nmod[(int64_t)q * kWindowTrials + h] = nm;
-    float* fc = fcon + ((int64_t)q * kWindowTrials * 3 + h * MM) * 12;
+    nmod[(int64_t)q * WT + h] = nm;
+    float* fc = fcon + ((int64_t)q * WT * 3 + h * MM) * 12;
     for (int k = 0; k < nm; ++k) {
       float c[12];
       if (K == KIND_F) f_filter_consts(mo + k * MS, S, maxr, c);
@@ -2730,7 +2734,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
     const float* __restrict__ fcon, const double* __restrict__ mods,
     uint32_t* __restrict__ cnts, uint32_t* __restrict__ ucnt, int max_chunks, int W, double maxr,
-    uint64_t* __restrict__ prof) {
+    uint64_t* __restrict__ prof, int WT) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   __shared__ __attribute__((aligned(16))) float lc[kTrialBatch * MM][12];
@@ -2782,17 +2786,17 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
     for (int r0 = rbeg; r0 < rend; r0 += kTrialBatch) {
       const int B = min(kTrialBatch, rend - r0);
       __syncthreads();
-      if (lane < B) lnm[lane] = nmod[(int64_t)q * kWindowTrials + r0 + lane];
+      if (lane < B) lnm[lane] = nmod[(int64_t)q * WT + r0 + lane];
       {
         const float4* src = reinterpret_cast<const float4*>(
-            fcon + ((int64_t)q * kWindowTrials * 3 + r0 * MM) * 12);
+            fcon + ((int64_t)q * WT * 3 + r0 * MM) * 12);
         float4* dst = reinterpret_cast<float4*>(&lc[0][0]);
         for (int i = lane; i < B * MM * 3; i += kScoreThreads) dst[i] = src[i];
       }
       if (!SPLIT)
         for (int i = lane; i < B * MM; i += kScoreThreads) ldc[i] = 0;
       __syncthreads();
-      const double* mb = mods + ((int64_t)q * kWindowTrials * 3 + r0 * MM) * MS;
+      const double* mb = mods + ((int64_t)q * WT * 3 + r0 * MM) * MS;
       DeferQ dq{ldq, 0, QCAP};
       int nslow = 0;
       uint32_t c0 = 0, c1 = 0, c2 = 0;  // lane t: counts of hypothesis t's models
@@ -2869,14 +2873,14 @@ __global__ __launch_bounds__(kScoreThreads) void rs_score_kernel(
           if (MM > 2) c2 += ldc[lane * MM + 2];
         }
       }
-      uint32_t* cq = cnts + (int64_t)q * kWindowTrials * 3 + r0 * MM;
+      uint32_t* cq = cnts + (int64_t)q * WT * 3 + r0 * MM;
       if (lane < B) {
         if (c0) atomicAdd(&cq[lane * MM], c0);
         if (MM > 1 && c1) atomicAdd(&cq[lane * MM + 1], c1);
         if (MM > 2 && c2) atomicAdd(&cq[lane * MM + 2], c2);
       }
       if (SPLIT && lane < B) {
-        uint32_t* uq = ucnt + (int64_t)q * kWindowTrials * 3 + r0 * MM;
+        uint32_t* uq = ucnt + (int64_t)q * WT * 3 + r0 * MM;
         if (u0) atomicAdd(&uq[lane * MM], u0);
         if (MM > 1 && u1) atomicAdd(&uq[lane * MM + 1], u1);
         if (MM > 2 && u2) atomicAdd(&uq[lane * MM + 2], u2);
@@ -2907,7 +2911,7 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
     const int32_t* __restrict__ act, const int32_t* __restrict__ nact, const int32_t* __restrict__ nmod,
     const float* __restrict__ fcon, const double* __restrict__ mods,
     uint32_t* __restrict__ cnts, const uint32_t* __restrict__ ucnt, int max_chunks, int W,
-    double maxr) {
+    double maxr, int WT) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   const int lane = threadIdx.x;
@@ -2935,11 +2939,11 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
     bool loaded = false;
     for (int r0 = rbeg; r0 < rend; r0 += kTrialBatch) {
       const int B = min(kTrialBatch, rend - r0);
-      const int64_t mo = (int64_t)q * kWindowTrials * 3 + r0 * MM;
+      const int64_t mo = (int64_t)q * WT * 3 + r0 * MM;
       // lane t: the qualifying models of hypothesis t (bit k)
       uint32_t qual = 0;
       if (lane < B) {
-        const int nml = K == KIND_F ? nmod[(int64_t)q * kWindowTrials + r0 + lane] : 1;
+        const int nml = K == KIND_F ? nmod[(int64_t)q * WT + r0 + lane] : 1;
 #pragma unroll
         for (int k = 0; k < MM; ++k) {
           const uint32_t u = k < nml ? ucnt[mo + lane * MM + k] : 0u;
@@ -3010,7 +3014,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     const uint32_t* __restrict__ cnts, const double* __restrict__ mods,
     const uint32_t* __restrict__ wsnap, const int32_t* __restrict__ wB,
     const uint32_t* __restrict__ wstate, VerifyParams P, uint64_t* __restrict__ prof,
-    const float4* __restrict__ xyf_all, int bid, int nblk) {
+    const float4* __restrict__ xyf_all, int bid, int nblk, int WT) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
@@ -3036,7 +3040,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     // buffers, 16-B aligned
     float4* xin = reinterpret_cast<float4*>(
         (reinterpret_cast<uintptr_t>(base + 2 * n) + 15) & ~(uintptr_t)15);
-    const double* mq = mods + (int64_t)q * kWindowTrials * 3 * MS;
+    const double* mq = mods + (int64_t)q * WT * 3 * MS;
     RansacState st = rst[q];
     wsync();
     if (threadIdx.x < 9) s.best_model[threadIdx.x] = st.best_model[threadIdx.x];
@@ -3055,9 +3059,9 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     for (int r0 = 0; r0 < Btot && !abort; r0 += kTrialBatch) {
       const int B = min(kTrialBatch, Btot - r0);
       wsync();
-      for (int i = threadIdx.x; i < B; i += 64 * NW) s.nmodels[i] = nmod[(int64_t)q * kWindowTrials + r0 + i];
+      for (int i = threadIdx.x; i < B; i += 64 * NW) s.nmodels[i] = nmod[(int64_t)q * WT + r0 + i];
       for (int i = threadIdx.x; i < B * MM; i += 64 * NW)
-        s.counts[i] = cnts[(int64_t)q * kWindowTrials * 3 + r0 * MM + i];
+        s.counts[i] = cnts[(int64_t)q * WT * 3 + r0 * MM + i];
       wsync();
       // Trials of the round in order.  Only two kinds need the sequential
       // step: a candidate (a model whose inlier count reaches the best) and
@@ -3258,12 +3262,12 @@ __global__ __launch_bounds__(64) void rs_draw2_kernel(
     rs_draw_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[ain], rf.nact + ain,
                          rf.nact + aclr, rf.samp, rf.cnts, rf.ucnt, rf.wsnap, rf.wB, rf.pstate,
                          rf.wstate, rf.dtrial, rf.pcnts, rf.pwB, P, spec != 0, W, blockIdx.x,
-                         split);
+                         split, rf.wt);
   else
     rs_draw_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[ain], rh.nact + ain,
                          rh.nact + aclr, rh.samp, rh.cnts, rh.ucnt, rh.wsnap, rh.wB, rh.pstate,
                          rh.wstate, rh.dtrial, rh.pcnts, rh.pwB, P, spec != 0, W,
-                         blockIdx.x - split, gridDim.x - split);
+                         blockIdx.x - split, gridDim.x - split, rh.wt);
 }
 
 __global__ __launch_bounds__(64) void rs_shuffle2_kernel(
@@ -3272,10 +3276,10 @@ __global__ __launch_bounds__(64) void rs_shuffle2_kernel(
     VerifyRoundBufs rh, int ain, int ppb, int stride, int split) {
   if ((int)blockIdx.x < split)
     rs_shuffle_body<KIND_F>(pairs, scratch, snaps, out, rf.wB, rf.act[ain], rf.nact + ain,
-                            rf.samp, ppb, stride, blockIdx.x, split);
+                            rf.samp, ppb, stride, blockIdx.x, split, rf.wt);
   else
     rs_shuffle_body<KIND_H>(pairs, scratch, snaps, out, rh.wB, rh.act[ain], rh.nact + ain,
-                            rh.samp, ppb, stride, blockIdx.x - split, gridDim.x - split);
+                            rh.samp, ppb, stride, blockIdx.x - split, gridDim.x - split, rh.wt);
 }
 
 __global__ __launch_bounds__(64) void rs_replay2_kernel(
@@ -3286,11 +3290,11 @@ __global__ __launch_bounds__(64) void rs_replay2_kernel(
   if ((int)blockIdx.x < split)
     rs_replay_body<KIND_F>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[ain], rf.nact + ain,
                            rf.act[aout], rf.nact + aout, rf.nmod, rf.cnts, rf.mods,
-                           rf.wsnap, rf.wB, rf.wstate, P, prof, xyf, blockIdx.x, split);
+                           rf.wsnap, rf.wB, rf.wstate, P, prof, xyf, blockIdx.x, split, rf.wt);
   else
     rs_replay_body<KIND_H>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[ain], rh.nact + ain,
                            rh.act[aout], rh.nact + aout, rh.nmod, rh.cnts, rh.mods,
-                           rh.wsnap, rh.wB, rh.wstate, P, prof, xyf, blockIdx.x - split, gridDim.x - split);
+                           rh.wsnap, rh.wB, rh.wstate, P, prof, xyf, blockIdx.x - split, gridDim.x - split, rh.wt);
 }
 
 // rs_replay2_kernel with four waves per pair (small batches: the window's
@@ -3303,11 +3307,11 @@ __global__ __launch_bounds__(256) void rs_replay2w_kernel(
   if ((int)blockIdx.x < split)
     rs_replay_body<KIND_F, 4>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[ain], rf.nact + ain,
                               rf.act[aout], rf.nact + aout, rf.nmod, rf.cnts, rf.mods,
-                              rf.wsnap, rf.wB, rf.wstate, P, prof, xyf, blockIdx.x, split);
+                              rf.wsnap, rf.wB, rf.wstate, P, prof, xyf, blockIdx.x, split, rf.wt);
   else
     rs_replay_body<KIND_H, 4>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[ain], rh.nact + ain,
                               rh.act[aout], rh.nact + aout, rh.nmod, rh.cnts, rh.mods,
-                              rh.wsnap, rh.wB, rh.wstate, P, prof, xyf, blockIdx.x - split, gridDim.x - split);
+                              rh.wsnap, rh.wB, rh.wstate, P, prof, xyf, blockIdx.x - split, gridDim.x - split, rh.wt);
 }
 
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
@@ -3363,6 +3367,7 @@ void set_lds_attr(F f) {
 }
 
 constexpr int kWaveShufflePairs = 256;
+constexpr int kSmallFirstWindow = 4;  // rounds of a small batch's first window (run_windows)
 // Small batches: a wave per pair (rs_shuffle_wave2_kernel), four waves per
 // pair in the replay, speculative windows -- while the batch leaves most of
 // the GPU idle, latency decides.
@@ -3412,17 +3417,24 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   const bool wave_sh = verify_small_batch(npairs, max_m);
   const size_t wave_lds = wave_shuffle_lds_bytes(wave_stride);
   const int max_chunks_s = (max_m + kScoreThreads * kScorePchSmall - 1) / (kScoreThreads * kScorePchSmall);
-  // First window: one round per pair when the batch fills the GPU; a small
-  // batch (a single Scanner stencil) starts with wider windows -- its chain of
-  // windows is latency-bound, and the speculative rounds past an early stop
-  // cost idle CUs only (about 1024 pairs x rounds per window).
+  // Window sizes.  A batch that fills the GPU: 1, 2, 4, ... kMaxWindow rounds
+  // (a pair's speculative rounds past its stop are GPU work).  A small batch
+  // (a single Scanner stencil): its chain of windows is latency-bound, so
+  // kSmallFirstWindow rounds -- enough for the near pairs' F, which stops
+  // within ~64 trials -- and then the largest windows, each later window being
+  // one more stage of the chain (19-pair stencil, profiles/r04_j: first window
+  // 16 rounds then doubling 3.75 ms per call; first window 16 / 8 / 4 / 2 then
+  // 32: 3.54 / 3.48 / 3.38 / 3.44 ms).
+  const int maxw = rfp[0].wt / kTrialBatch;  // kMaxWindow, or kMaxWindowSmall
   int W = 1;
-  while (W < kMaxWindow && (int64_t)npairs * 2 * W <= 1024) W *= 2;
-  static const int w0_env = [] {  // diagnostics: SCM_FIRST_WINDOW=w caps the first window
+  if (wave_sh) W = std::min(kSmallFirstWindow, maxw);
+  else
+    while (W < maxw && (int64_t)npairs * 2 * W <= 1024) W *= 2;
+  static const int w0_env = [] {  // diagnostics: SCM_FIRST_WINDOW=w sets the first window
     const char* e = getenv("SCM_FIRST_WINDOW");
     return e ? atoi(e) : 0;
   }();
-  if (w0_env > 0) W = std::min(W, w0_env);
+  if (w0_env > 0) W = std::min(w0_env, maxw);
   // Decoupled draws (speculative schedule with a draw stream): window r's
   // draws and shuffles run on dstream as soon as window r - 2 is replayed (its
   // active list) and window r - 1's prune has run (the lists and counts it
@@ -3470,11 +3482,11 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     if (f)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(kSolveGrid), dim3(64), 0, stream, pairs, xy1, xy2,
                          rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.samp, rf.nmod, rf.fcon, rf.mods,
-                         W, P.max_residual);
+                         W, P.max_residual, rf.wt);
     if (h)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_H>, dim3(kSolveGrid), dim3(64), 0, stream, pairs, xy1, xy2,
                          rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.samp, rh.nmod, rh.fcon, rh.mods,
-                         W, P.max_residual);
+                         W, P.max_residual, rh.wt);
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r], stream);
     // Scoring per kind: split (filter counts + undecided counts, then exact
     // tests only for the models that can reach the best; the runtime's
@@ -3485,21 +3497,21 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       if (rf.ucnt) {
         hipLaunchKernelGGL((rs_score_kernel<KIND_F, true>), dim3(8192), dim3(kScoreThreads), 0,
                            stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
-                           rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual, prof);
+                           rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual, prof, rf.wt);
 
         hipLaunchKernelGGL(rs_exact_kernel<KIND_F>, dim3(8192), dim3(kScoreThreads), 0, stream,
                            pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
-                           rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual);
+                           rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual, rf.wt);
       } else {
         if (wave_sh)
           hipLaunchKernelGGL((rs_score_kernel<KIND_F, false, kScorePchSmall>), dim3(8192),
                              dim3(kScoreThreads), 0, stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw],
                              rf.nact + lw, rf.nmod, rf.fcon, rf.mods, rf.cnts, nullptr, max_chunks_s,
-                             W, P.max_residual, prof);
+                             W, P.max_residual, prof, rf.wt);
         else
           hipLaunchKernelGGL((rs_score_kernel<KIND_F, false>), dim3(8192), dim3(kScoreThreads), 0,
                              stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod,
-                             rf.fcon, rf.mods, rf.cnts, nullptr, max_chunks, W, P.max_residual, prof);
+                             rf.fcon, rf.mods, rf.cnts, nullptr, max_chunks, W, P.max_residual, prof, rf.wt);
       }
     }
     if (h) {
@@ -3510,24 +3522,24 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
           hipLaunchKernelGGL((rs_score_kernel<KIND_H, true, kScorePchSmall>), dim3(8192),
                              dim3(kScoreThreads), 0, stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw],
                              rh.nact + lw, rh.nmod, rh.fcon, rh.mods, rh.cnts, rh.ucnt, max_chunks_s,
-                             W, P.max_residual, prof);
+                             W, P.max_residual, prof, rh.wt);
         else
           hipLaunchKernelGGL((rs_score_kernel<KIND_H, true>), dim3(8192), dim3(kScoreThreads), 0,
                              stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod,
-                             rh.fcon, rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, prof);
+                             rh.fcon, rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, prof, rh.wt);
         hipLaunchKernelGGL(rs_exact_kernel<KIND_H>, dim3(8192), dim3(kScoreThreads), 0, stream,
                            pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod, rh.fcon,
-                           rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual);
+                           rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, rh.wt);
       } else {
         if (wave_sh)
           hipLaunchKernelGGL((rs_score_kernel<KIND_H, false, kScorePchSmall>), dim3(8192),
                              dim3(kScoreThreads), 0, stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw],
                              rh.nact + lw, rh.nmod, rh.fcon, rh.mods, rh.cnts, nullptr, max_chunks_s,
-                             W, P.max_residual, prof);
+                             W, P.max_residual, prof, rh.wt);
         else
           hipLaunchKernelGGL((rs_score_kernel<KIND_H, false>), dim3(8192), dim3(kScoreThreads), 0,
                              stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod,
-                             rh.fcon, rh.mods, rh.cnts, nullptr, max_chunks, W, P.max_residual, prof);
+                             rh.fcon, rh.mods, rh.cnts, nullptr, max_chunks, W, P.max_residual, prof, rh.wt);
       }
     }
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r + 1], stream);
@@ -3547,7 +3559,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
     covered += W * kTrialBatch;
-    W = W * 2 > kMaxWindow ? kMaxWindow : W * 2;
+    W = wave_sh || W * 2 > maxw ? maxw : W * 2;
     ++r;
     if (spec && r >= kMaxVerifyWindows) spec = false;  // out of events: the rest in order
   }
