@@ -417,6 +417,7 @@ struct scm_context {
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
   bool profile = false;
   std::vector<uint64_t> prof_sum;
+  std::vector<uint64_t> prof_worst;  // the pair with the most final-kernel cycles (slots 0-8)
   int64_t prof_pairs = 0;
   // raw matches of the last table run (scm_set_keep_matches)
   bool keep_matches = false;
@@ -1360,8 +1361,18 @@ int collect_batch(scm_context* ctx, BatchSet& bs, BatchView* v) {
     SCM_HIP(hipMemcpy(pr.data(), bs.prof.ptr, pr.size() * sizeof(uint64_t),
                       hipMemcpyDeviceToHost));
     ctx->prof_sum.resize(kVerifyProfSlots, 0);
-    for (int64_t k = 0; k < bs.nprof; ++k)
-      for (int j = 0; j < kVerifyProfSlots; ++j) ctx->prof_sum[j] += pr[k * kVerifyProfSlots + j];
+    ctx->prof_worst.resize(kVerifyProfSlots, 0);
+    auto final_cycles = [](const uint64_t* x) {
+      uint64_t t = 0;
+      for (int j = 0; j < 9; ++j) t += x[j];
+      return t;
+    };
+    for (int64_t k = 0; k < bs.nprof; ++k) {
+      const uint64_t* x = pr.data() + k * kVerifyProfSlots;
+      for (int j = 0; j < kVerifyProfSlots; ++j) ctx->prof_sum[j] += x[j];
+      if (final_cycles(x) > final_cycles(ctx->prof_worst.data()))
+        ctx->prof_worst.assign(x, x + kVerifyProfSlots);
+    }
     ctx->prof_pairs += bs.nprof;
   }
   bs.nprof = 0;
@@ -1958,8 +1969,9 @@ void scm_context_destroy(scm_context* ctx) {
     std::fprintf(stderr, "[scm verify profile] pairs=%lld (per pair: cycles / counts)\n",
                  (long long)ctx->prof_pairs);
     for (int j = 0; j < 18; ++j)
-      std::fprintf(stderr, "  %-10s %14.1f\n", names[j],
-                   (double)ctx->prof_sum[j] / (double)ctx->prof_pairs);
+      std::fprintf(stderr, "  %-10s %14.1f   worst pair %12llu\n", names[j],
+                   (double)ctx->prof_sum[j] / (double)ctx->prof_pairs,
+                   (unsigned long long)ctx->prof_worst[j]);
     static const char* rnames[] = {"windows", "n_cand", "n_tie", "n_newbest", "n_lo_iter",
                                    "cyc_cand", "cyc_tie", "cyc_lo", "cyc_total", "trials"};
     for (int kind = 0; kind < 2; ++kind)

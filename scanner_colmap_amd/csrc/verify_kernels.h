@@ -81,10 +81,12 @@ struct RansacState {
 constexpr int kMaxWindow = 32;  // rounds per window at most (16: -1.3 %, 64: -1 %, bench s35;
                                 // 64 again after trials_left: -0.4 %, profiles/r04_l)
 constexpr int kWindowTrials = kMaxWindow * kTrialBatch;
-// Small batches (verify_small_batch): windows of up to 64 rounds -- every
+// Small batches (verify_small_batch): windows of up to 128 rounds -- every
 // window is one more latency-bound stage of a stencil's chain (19-pair
-// stencil: 3.35 ms per call with 32, 3.13 ms with 64, profiles/r04_k).
-constexpr int kMaxWindowSmall = 64;
+// stencil: 3.35 ms per call with 32, 3.13 ms with 64, profiles/r04_k; 3.07-3.16
+// with 64 vs 2.90-2.93 with 128, profiles/r04_n: H's 5,295 trials in two
+// windows).
+constexpr int kMaxWindowSmall = 128;
 constexpr int kWindowTrialsSmall = kMaxWindowSmall * kTrialBatch;
 
 // Device buffers of the windowed verifier (V = pairs of a batch, T =
