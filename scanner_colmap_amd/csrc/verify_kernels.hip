@@ -1532,6 +1532,77 @@ __device__ void ensure_best_sum(VerifyLds& s, const double* res_best, int n, dou
   wsync();
 }
 
+// A tie on the inlier count: InlierSupportMeasurer's Compare keeps the model
+// with the smaller residual sum -- its inlier residuals summed in index order,
+// a strictly ordered chain (~15 cycles per point).  The compare is decided
+// from bounds first, with the chains only when they cannot decide it:
+//  * residual arrays equal bit for bit have equal sums: not better;
+//  * otherwise the inlier residuals (m of them, each >= 0) summed in any order
+//    give T within gamma(m - 1) S of their exact sum S, and so does the index-
+//    order chain; hence |chain - T| <= E = 2 (m + 2) u T (u = 2^-53, with
+//    margin for the rounding of E and of the compares), and when the intervals
+//    [T - E, T + E] of the two models (E = 0 for a best sum already exact) are
+//    disjoint, they order the chains' sums exactly as the chains would.
+// Every thread of the block calls it (block barriers).  Returns whether the
+// new model is better; *sum / *exact: its index-order sum when the chains ran.
+template <int NW>
+__device__ bool tie_better(VerifyLds& s, const double* rt, const double* rb, int n, int m,
+                           double maxr, double* sum, bool* exact) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  double tn = 0.0, tb = 0.0;
+  bool diff = false;
+  for (int i0 = wv * 64 * kSeqU + lane; i0 < n; i0 += 64 * kSeqU * NW) {
+    double a[kSeqU], b[kSeqU];
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u) {
+      const int i = min(i0 + 64 * u, n - 1);
+      a[u] = rt[i];
+      b[u] = rb[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u)
+      if (i0 + 64 * u < n) {
+        diff |= __double_as_longlong(a[u]) != __double_as_longlong(b[u]);
+        if (a[u] <= maxr) tn += a[u];
+        if (b[u] <= maxr) tb += b[u];
+      }
+  }
+  tn = canon_tree_wave(tn);
+  tb = canon_tree_wave(tb);
+  int d = __ballot(diff) != 0 ? 1 : 0;
+  if (NW > 1) {
+    if (lane == 0) {
+      s.redd[2 * wv] = tn;
+      s.redd[2 * wv + 1] = tb;
+      s.redi[wv] = d;
+    }
+    __syncthreads();
+    tn = 0.0;
+    tb = 0.0;
+    d = 0;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      tn += s.redd[2 * w];
+      tb += s.redd[2 * w + 1];
+      d |= s.redi[w];
+    }
+    __syncthreads();
+  }
+  *exact = false;
+  if (!d) return false;
+  const double g = 2.0 * (double)(m + 2) * 1.1102230246251565e-16;
+  const double en = g * tn + 1e-300;
+  const bool bex = s.best_sum_valid != 0;
+  const double Tb = bex ? s.best_sum : tb;
+  const double eb = bex ? 0.0 : g * tb + 1e-300;
+  if (tn + en < Tb - eb) return true;
+  if (tn - en > Tb + eb) return false;
+  *sum = seq_inlier_sum(rt, n, maxr);
+  ensure_best_sum(s, rb, n, maxr);
+  *exact = true;
+  return *sum < s.best_sum;
+}
+
 // LORANSAC<Estimator, LocalEstimator>::Estimate on n points (xy1, xy2).
 // res0 / res1: residual buffers (n doubles each); xin1 / xin2 inlier gather
 // buffers (2n doubles each); snap: 625-word PRNG snapshot (global).  The
@@ -1697,13 +1768,11 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
             double* rt = res[best_sel ^ 1];
             residuals_wave<K, NW>(mk, xy1, xy2, n, maxr, rt, s.redi);
             pf.lap(PR_CAND);
-            bool better = c > bn;
+            bool better = c > bn, exact = false;
             double sum = 0.0;
             if (!better) {  // tie on the inlier count: Compare the residual sums
-              sum = seq_inlier_sum(rt, n, maxr);
-              ensure_best_sum(s, res[best_sel], n, maxr);
-              better = sum < s.best_sum;
-              pf.count(PR_N_SEQSUM);
+              better = tie_better<NW>(s, rt, res[best_sel], n, c, maxr, &sum, &exact);
+              if (exact) pf.count(PR_N_SEQSUM);  // (the chains ran)
               pf.lap(PR_SEQSUM);
             }
             if (better) {
@@ -1713,7 +1782,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                 for (int j = 0; j < MS; ++j) s.best_model[j] = mk[j];
                 s.best_n = c;
                 s.best_sum = sum;
-                s.best_sum_valid = c == bn ? 1 : 0;
+                s.best_sum_valid = exact ? 1 : 0;
               }
               best_sel ^= 1;
               wsync();
@@ -1732,13 +1801,11 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                   double* rl = res[best_sel ^ 1];
                   const int lc = residuals_wave<K, NW>(lm, xy1, xy2, n, maxr, rl, s.redi);
                   pf.lap(PR_LORES);
-                  bool lbetter = lc > prev;
+                  bool lbetter = lc > prev, lexact = false;
                   double lsum = 0.0;
                   if (lc == prev) {
-                    lsum = seq_inlier_sum(rl, n, maxr);
-                    ensure_best_sum(s, res[best_sel], n, maxr);
-                    lbetter = lsum < s.best_sum;
-                    pf.count(PR_N_SEQSUM);
+                    lbetter = tie_better<NW>(s, rl, res[best_sel], n, lc, maxr, &lsum, &lexact);
+                    if (lexact) pf.count(PR_N_SEQSUM);
                     pf.lap(PR_SEQSUM);
                   }
                   if (lbetter) {
@@ -1748,7 +1815,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                       for (int j = 0; j < MS; ++j) s.best_model[j] = lm[j];
                       s.best_n = lc;
                       s.best_sum = lsum;
-                      s.best_sum_valid = lc == prev ? 1 : 0;
+                      s.best_sum_valid = lexact ? 1 : 0;
                     }
                     best_sel ^= 1;
                   }
@@ -3099,7 +3166,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
               for (int j = 0; j < MS; ++j) mk[j] = src[j];
               double* rt = res[best_sel ^ 1];
               residuals_f4<K, NW>(mk, xyf, n, maxr, rt, s.redi);
-              bool better = c > bn;
+              bool better = c > bn, exact = false;
               double sum = 0.0;
               if (pc && t0th) {
                 const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -3108,9 +3175,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                 t0 = t1;
               }
               if (!better) {  // tie on the inlier count: Compare the residual sums
-                sum = seq_inlier_sum(rt, n, maxr);
-                ensure_best_sum(s, res[best_sel], n, maxr);
-                better = sum < s.best_sum;
+                better = tie_better<NW>(s, rt, res[best_sel], n, c, maxr, &sum, &exact);
                 if (pc && t0th) {
                   pc[2] += 1;
                   pc[6] += __builtin_amdgcn_s_memtime() - t0;
@@ -3125,7 +3190,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                   for (int j = 0; j < MS; ++j) s.best_model[j] = mk[j];
                   s.best_n = c;
                   s.best_sum = sum;
-                  s.best_sum_valid = c == bn ? 1 : 0;
+                  s.best_sum_valid = exact ? 1 : 0;
                 }
                 best_sel ^= 1;
                 wsync();
@@ -3144,13 +3209,10 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                     double* rl = res[best_sel ^ 1];
                     const int lcn = residuals_f4<K, NW>(lm, xyf, n, maxr, rl, s.redi);
                     if (pl && t0th) pl[4] += __builtin_amdgcn_s_memtime() - tl0;
-                    bool lbetter = lcn > prev;
+                    bool lbetter = lcn > prev, lexact = false;
                     double lsum = 0.0;
-                    if (lcn == prev) {
-                      lsum = seq_inlier_sum(rl, n, maxr);
-                      ensure_best_sum(s, res[best_sel], n, maxr);
-                      lbetter = lsum < s.best_sum;
-                    }
+                    if (lcn == prev)
+                      lbetter = tie_better<NW>(s, rl, res[best_sel], n, lcn, maxr, &lsum, &lexact);
                     if (lbetter) {
                       wsync();
                       if (t0th) {
@@ -3158,7 +3220,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                         for (int j = 0; j < MS; ++j) s.best_model[j] = lm[j];
                         s.best_n = lcn;
                         s.best_sum = lsum;
-                        s.best_sum_valid = lcn == prev ? 1 : 0;
+                        s.best_sum_valid = lexact ? 1 : 0;
                       }
                       best_sel ^= 1;
                     }
