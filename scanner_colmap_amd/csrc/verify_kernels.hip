@@ -55,9 +55,9 @@ struct __attribute__((aligned(16))) VerifyLds {
   uint32_t counts[kTrialBatch * 3];
   int32_t nmodels[kTrialBatch];
   uint32_t jbuf[kTrialBatch * 7];  // Shuffle targets of one batch of samples
-  double redd[8];  // cross-wave exchange of the multi-wave replay (NW > 1)
+  double redd[16];  // cross-wave exchange of the multi-wave replay (NW > 1)
   double fvec[9];
-  int32_t redi[8];
+  int32_t redi[16];
   int32_t mt_idx;
   int32_t best_n;
   int32_t best_sum_valid;
@@ -503,8 +503,6 @@ __device__ __attribute__((noinline)) bool h_exact_pt(const double* mk, float sx,
   return homography_sq(mk, (double)sx, (double)sy, (double)dx, (double)dy) <= maxr;
 }
 
-
-
 // The hypothesis' constants (LDS, broadcast read), kept in vector registers:
 // no readfirstlane / SGPR copies per model (filter loop 20 % faster,
 // probes/score_bench.hip).
@@ -759,7 +757,6 @@ __device__ __attribute__((noinline)) bool f_exact_pt(const double* mk, float x0,
   return sampson_sq(mk, (double)x0, (double)x1, (double)y0, (double)y1) <= maxr;
 }
 
-
 // Inlier count of one 7-point model (filter f; fp64 model mk in LDS, read
 // only for undecided points) over one chunk of points.
 // UND: no exact tests -- return the sure inliers and write the number of
@@ -836,45 +833,6 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
 // their order).
 constexpr int kSeqU = 8;
 
-// Residuals of one model over all points into res; returns the inlier count.
-// NW > 1: the waves take alternate blocks of 64 kSeqU points; the count is
-// exchanged in redi and every residual is visible to the block on return.
-template <int K, int NW = 1>
-__device__ int residuals_wave(const double* m, const double* xy1, const double* xy2, int n,
-                              double maxr, double* res, int32_t* redi = nullptr) {
-  int c = 0;
-  for (int b = (int)(threadIdx.x >> 6) * 64 * kSeqU + (int)(threadIdx.x & 63); b < n;
-       b += 64 * kSeqU * NW) {
-    double a0[kSeqU], a1[kSeqU], b0[kSeqU], b1[kSeqU];
-#pragma unroll
-    for (int u = 0; u < kSeqU; ++u) {
-      const int i = min(b + 64 * u, n - 1);
-      a0[u] = xy1[2 * i];
-      a1[u] = xy1[2 * i + 1];
-      b0[u] = xy2[2 * i];
-      b1[u] = xy2[2 * i + 1];
-    }
-#pragma unroll
-    for (int u = 0; u < kSeqU; ++u) {
-      const int i = b + 64 * u;
-      if (i < n) {
-        const double r = residual_pt<K>(m, a0[u], a1[u], b0[u], b1[u]);
-        res[i] = r;
-        c += (r <= maxr) ? 1 : 0;
-      }
-    }
-  }
-  c = wave_sum_i(c);
-  if (NW == 1) return c;
-  if ((threadIdx.x & 63) == 0) redi[threadIdx.x >> 6] = c;
-  __syncthreads();
-  int t = 0;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) t += redi[w];
-  __syncthreads();
-  return t;
-}
-
 // InlierSupportMeasurer::Evaluate's residual_sum: inlier residuals summed
 // in index order.  The wave loads 64 x kSeqU residuals at a time; every lane
 // runs the same ordered chain over the 64 lanes' values, broadcast with
@@ -920,13 +878,44 @@ __device__ __noinline__ double seq_inlier_sum(const double* res, int n, double m
   return sum;
 }
 
-// Ordered compaction of the points whose residual is <= maxr.  NW > 1: wave
-// w takes the w-th block of each round, a prefix of the waves' counts (redi)
-// places its inliers; the output is visible to the block on return.
-template <int NW = 1>
-__device__ int gather_inliers(const double* res, int n, double maxr, const double* xy1,
-                              const double* xy2, double* xin1, double* xin2,
-                              int32_t* redi = nullptr) {
+// ---------------------------------------------------------------------------
+// Point loops of the windowed replay (candidate residuals and local
+// optimisation) on the packed fp32 copy of the matches (xyf: x1, y1, x2, y2
+// per point; keypoints are float32, so widening to double reproduces the
+// reference's Eigen::Vector2d values exactly).  Each lane keeps kLoU loads in
+// flight; items are still consumed in index order per lane, so every
+// canonical-order sum performs the same additions as before.
+// ---------------------------------------------------------------------------
+constexpr int kLoU = 4;
+
+__device__ __forceinline__ void load_pts(const float4* p, int b, int n, float4 (&v)[kLoU]) {
+#pragma unroll
+  for (int u = 0; u < kLoU; ++u) {
+    const int i = b + 64 * u;
+    v[u] = i < n ? p[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+}
+
+// apply_normalize (geom_solvers.h) for a transform with last row (0, 0, 1):
+// np2 = 0 p0 + 0 p1 + 1 is exactly 1 and the homogeneous divide by it is the
+// identity, so it is skipped (same values bit for bit).
+__device__ __forceinline__ void apply_norm_affine(const double* T, double p0, double p1,
+                                                  double* o0, double* o1) {
+  *o0 = T[0] * p0 + T[1] * p1 + T[2];
+  *o1 = T[3] * p0 + T[4] * p1 + T[5];
+}
+
+// residuals_wave / residuals_f4 and the ordered gather in one pass: the
+// model's residuals into res and, in index order, its inliers' points into
+// xin (the gather the local optimisation runs next if the model becomes the
+// best: a candidate's pass and every LO step's pass write it, so LO starts
+// from it without another pass over the points).  Same rounds and lane
+// mapping as the gathers; returns the inlier count; residuals and inliers are
+// visible to the block on return.
+template <int K, int NW = 1>
+__device__ int residuals_gather(const double* m, const double* xy1, const double* xy2, int n,
+                                double maxr, double* res, double* xin1, double* xin2,
+                                int32_t* redi = nullptr) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int base_out = 0;
   for (int r0 = 0; r0 < n; r0 += 64 * kSeqU * NW) {
@@ -934,8 +923,7 @@ __device__ int gather_inliers(const double* res, int n, double maxr, const doubl
     double r[kSeqU], a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
 #pragma unroll
     for (int u = 0; u < kSeqU; ++u) {
-      const int i = b0 + 64 * u + lane, ic = min(i, n - 1);
-      r[u] = i < n ? res[i] : 1.7976931348623157e308;
+      const int ic = min(b0 + 64 * u + lane, n - 1);
       a0[u] = xy1[2 * ic];
       a1[u] = xy1[2 * ic + 1];
       c0[u] = xy2[2 * ic];
@@ -945,6 +933,12 @@ __device__ int gather_inliers(const double* res, int n, double maxr, const doubl
     int wc = 0;
 #pragma unroll
     for (int u = 0; u < kSeqU; ++u) {
+      const int i = b0 + 64 * u + lane;
+      r[u] = 1.7976931348623157e308;
+      if (i < n) {
+        r[u] = residual_pt<K>(m, a0[u], a1[u], c0[u], c1[u]);
+        res[i] = r[u];
+      }
       bal[u] = __ballot(r[u] <= maxr);
       wc += __popcll(bal[u]);
     }
@@ -979,74 +973,9 @@ __device__ int gather_inliers(const double* res, int n, double maxr, const doubl
   if (NW > 1) __syncthreads();
   return base_out;
 }
-
-// ---------------------------------------------------------------------------
-// Point loops of the windowed replay (candidate residuals and local
-// optimisation) on the packed fp32 copy of the matches (xyf: x1, y1, x2, y2
-// per point; keypoints are float32, so widening to double reproduces the
-// reference's Eigen::Vector2d values exactly).  Each lane keeps kLoU loads in
-// flight; items are still consumed in index order per lane, so every
-// canonical-order sum performs the same additions as before.
-// ---------------------------------------------------------------------------
-constexpr int kLoU = 4;
-
-__device__ __forceinline__ void load_pts(const float4* p, int b, int n, float4 (&v)[kLoU]) {
-#pragma unroll
-  for (int u = 0; u < kLoU; ++u) {
-    const int i = b + 64 * u;
-    v[u] = i < n ? p[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-  }
-}
-
-// apply_normalize (geom_solvers.h) for a transform with last row (0, 0, 1):
-// np2 = 0 p0 + 0 p1 + 1 is exactly 1 and the homogeneous divide by it is the
-// identity, so it is skipped (same values bit for bit).
-__device__ __forceinline__ void apply_norm_affine(const double* T, double p0, double p1,
-                                                  double* o0, double* o1) {
-  *o0 = T[0] * p0 + T[1] * p1 + T[2];
-  *o1 = T[3] * p0 + T[4] * p1 + T[5];
-}
-
-// NW > 1 (multi-wave replay): the waves take alternate blocks of 64 kLoU
-// points; the count is exchanged in redi and every residual is visible to the
-// whole block on return.
 template <int K, int NW = 1>
-__device__ int residuals_f4(const double* m, const float4* xyf, int n, double maxr, double* res,
-                            int32_t* redi = nullptr) {
-  int c = 0;
-  for (int b = (int)(threadIdx.x >> 6) * 64 * kLoU + (int)(threadIdx.x & 63); b < n;
-       b += 64 * kLoU * NW) {
-    float4 v[kLoU];
-    load_pts(xyf, b, n, v);
-#pragma unroll
-    for (int u = 0; u < kLoU; ++u) {
-      const int i = b + 64 * u;
-      if (i < n) {
-        const double r = residual_pt<K>(m, (double)v[u].x, (double)v[u].y, (double)v[u].z,
-                                        (double)v[u].w);
-        res[i] = r;
-        c += (r <= maxr) ? 1 : 0;
-      }
-    }
-  }
-  c = wave_sum_i(c);
-  if (NW == 1) return c;
-  if ((threadIdx.x & 63) == 0) redi[threadIdx.x >> 6] = c;
-  __syncthreads();
-  int t = 0;
-#pragma unroll
-  for (int w = 0; w < NW; ++w) t += redi[w];
-  __syncthreads();
-  return t;
-}
-
-// Ordered compaction of the points whose residual is <= maxr into xin.  NW >
-// 1: each round of 64 kLoU NW points gives wave w the w-th block; a prefix of
-// the waves' counts (redi) places its inliers, and xin is visible to the
-// whole block on return.
-template <int NW = 1>
-__device__ int gather_inliers_f4(const double* res, int n, double maxr, const float4* xyf,
-                                 float4* xin, int32_t* redi = nullptr) {
+__device__ int residuals_gather_f4(const double* m, const float4* xyf, int n, double maxr,
+                                   double* res, float4* xin, int32_t* redi = nullptr) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int base_out = 0;
   for (int r0 = 0; r0 < n; r0 += 64 * kLoU * NW) {
@@ -1054,15 +983,16 @@ __device__ int gather_inliers_f4(const double* res, int n, double maxr, const fl
     float4 v[kLoU];
     double r[kLoU];
     load_pts(xyf, b0 + lane, n, v);
-#pragma unroll
-    for (int u = 0; u < kLoU; ++u) {
-      const int i = b0 + 64 * u + lane;
-      r[u] = i < n ? res[i] : 1.7976931348623157e308;
-    }
     uint64_t bal[kLoU];
     int wc = 0;
 #pragma unroll
     for (int u = 0; u < kLoU; ++u) {
+      const int i = b0 + 64 * u + lane;
+      r[u] = 1.7976931348623157e308;
+      if (i < n) {
+        r[u] = residual_pt<K>(m, (double)v[u].x, (double)v[u].y, (double)v[u].z, (double)v[u].w);
+        res[i] = r[u];
+      }
       bal[u] = __ballot(r[u] <= maxr);
       wc += __popcll(bal[u]);
     }
@@ -1607,7 +1537,7 @@ __device__ bool tie_better(VerifyLds& s, const double* rt, const double* rb, int
 // res0 / res1: residual buffers (n doubles each); xin1 / xin2 inlier gather
 // buffers (2n doubles each); snap: 625-word PRNG snapshot (global).  The
 // best model ends in s.best_model.
-// NW waves (4: small batches, verify_final_kernel<4>; KIND_T): every wave runs
+// NW waves (8: small batches, verify_final_kernel<8>; KIND_T): every wave runs
 // the same decisions; the point loops split as in the windowed replay.
 template <int K, int NW = 1>
 __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& s, uint32_t* sidx, const double* xy1,
@@ -1766,7 +1696,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
             pf.lap(PR_OTHER);
             pf.count(PR_N_CAND);
             double* rt = res[best_sel ^ 1];
-            residuals_wave<K, NW>(mk, xy1, xy2, n, maxr, rt, s.redi);
+            residuals_gather<K, NW>(mk, xy1, xy2, n, maxr, rt, xin1, xin2, s.redi);
             pf.lap(PR_CAND);
             bool better = c > bn, exact = false;
             double sum = 0.0;
@@ -1791,15 +1721,14 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                 for (int lt = 0; lt < 10; ++lt) {
                   pf.lap(PR_OTHER);
                   pf.count(PR_N_LO);
-                  const int ni =
-                      gather_inliers<NW>(res[best_sel], n, maxr, xy1, xy2, xin1, xin2, s.redi);
+                  const int ni = s.best_n;  // in xin1 / xin2 from the best's residual pass
                   pf.lap(PR_GATHER);
                   double lm[9];
                   local_estimate_wave<K, NW>(s, xin1, xin2, ni, lm);
                   pf.lap(PR_LOEST);
                   const int prev = s.best_n;
                   double* rl = res[best_sel ^ 1];
-                  const int lc = residuals_wave<K, NW>(lm, xy1, xy2, n, maxr, rl, s.redi);
+                  const int lc = residuals_gather<K, NW>(lm, xy1, xy2, n, maxr, rl, xin1, xin2, s.redi);
                   pf.lap(PR_LORES);
                   bool lbetter = lc > prev, lexact = false;
                   double lsum = 0.0;
@@ -1925,11 +1854,11 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
       const int fd = *reinterpret_cast<volatile const int32_t*>(&rstF[q0].done);
       const int hd = *reinterpret_cast<volatile const int32_t*>(&rstH[q0].done);
       const int mk = *reinterpret_cast<volatile const int32_t*>(&rstF[q0].pad_);
-      s.redi[7] = phase == 1 ? (fd && hd) : !mk;
+      s.redi[15] = phase == 1 ? (fd && hd) : !mk;
       __threadfence();
     }
     __syncthreads();
-    const bool go = s.redi[7] != 0;
+    const bool go = s.redi[15] != 0;
     __syncthreads();
     if (!go) return;
     if (phase == 1 && threadIdx.x == 0) rstF[blockIdx.x].pad_ = 1;
@@ -2348,7 +2277,6 @@ __device__ __attribute__((always_inline)) void rs_shuffle_body(
     }
 }
 
-
 // The same window's Shuffle with a whole wave per pair, for small batches
 // (one Scanner stencil: a lane per pair leaves nearly every lane, and the
 // GPU, idle while one pair's chain of kmin dependent LDS round trips per
@@ -2658,7 +2586,6 @@ __global__ __launch_bounds__(64) void rs_shuffle_wave2_kernel(
     rs_shuffle_wave_body<KIND_H>(pairs, scratch, snaps, out, rh.wB, rh.act[ain], rh.nact + ain,
                                  rh.samp, prof, rh.wt, stride, blockIdx.x - split, gridDim.x - split);
 }
-
 
 // Draws and Shuffle of a window in one launch (small batches).
 __global__ __launch_bounds__(64) void rs_drawshuffle_wave2_kernel(
@@ -3165,7 +3092,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
 #pragma unroll
               for (int j = 0; j < MS; ++j) mk[j] = src[j];
               double* rt = res[best_sel ^ 1];
-              residuals_f4<K, NW>(mk, xyf, n, maxr, rt, s.redi);
+              residuals_gather_f4<K, NW>(mk, xyf, n, maxr, rt, xin, s.redi);
               bool better = c > bn, exact = false;
               double sum = 0.0;
               if (pc && t0th) {
@@ -3200,14 +3127,14 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                     if (pc && t0th) pc[4] += 1;
                     uint64_t* pl = pc ? pc + 20 : nullptr;
                     uint64_t tl0 = pl ? __builtin_amdgcn_s_memtime() : 0;
-                    const int ni = gather_inliers_f4<NW>(res[best_sel], n, maxr, xyf, xin, s.redi);
+                    const int ni = s.best_n;  // in xin from the best's residual pass
                     if (pl && t0th) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[0] += t - tl0; tl0 = t; pl[5] += ni; }
                     double lm[9];
                     local_estimate_f4<K, NW>(s, xin, ni, lm, pl);
                     if (pl && t0th) tl0 = __builtin_amdgcn_s_memtime();
                     const int prev = s.best_n;
                     double* rl = res[best_sel ^ 1];
-                    const int lcn = residuals_f4<K, NW>(lm, xyf, n, maxr, rl, s.redi);
+                    const int lcn = residuals_gather_f4<K, NW>(lm, xyf, n, maxr, rl, xin, s.redi);
                     if (pl && t0th) pl[4] += __builtin_amdgcn_s_memtime() - tl0;
                     bool lbetter = lcn > prev, lexact = false;
                     double lsum = 0.0;
@@ -3653,7 +3580,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     set_lds_attr(rs_replay2_kernel);
     set_lds_attr(rs_replay2w_kernel);
     set_lds_attr(verify_final_kernel<1>);
-    set_lds_attr(verify_final_kernel<4>);
+    set_lds_attr(verify_final_kernel<8>);
     attr = true;
   }
   const size_t lds = sizeof(VerifyLds);
@@ -3691,16 +3618,16 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     // replayed (typically all but the far pairs' F), beside the later windows;
     // then the rest after the last window.
     (void)hipStreamWaitEvent(spec->fstream, spec->win_ev[2 * last_h + 1], 0);
-    hipLaunchKernelGGL(verify_final_kernel<4>, dim3(npairs), dim3(256), lds, spec->fstream, pairs,
+    hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, spec->fstream, pairs,
                        xy1, xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst,
                        rb_h.rst, 1);
     (void)hipEventRecord(spec->fin_ev, spec->fstream);
     (void)hipStreamWaitEvent(stream, spec->fin_ev, 0);
-    hipLaunchKernelGGL(verify_final_kernel<4>, dim3(npairs), dim3(256), lds, stream, pairs, xy1,
+    hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, stream, pairs, xy1,
                        xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,
                        2);
   } else if (verify_small_batch(npairs, max_m)) {
-    hipLaunchKernelGGL(verify_final_kernel<4>, dim3(npairs), dim3(256), lds, stream, pairs, xy1,
+    hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, stream, pairs, xy1,
                        xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,
                        0);
   } else {
