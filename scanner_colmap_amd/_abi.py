@@ -206,17 +206,40 @@ def _elements(chunks) -> tuple:
 PASS_FN = ctypes.CFUNCTYPE(None, c_void_p, c_int64, c_void_p, c_size_t, POINTER(c_int64))
 
 
+class _BlobOwner:
+    """Frees a library-owned buffer (scm_blob_free) when the last numpy view
+    of it dies: PackedRows.data and every slice of it keep this alive."""
+
+    def __init__(self, blob: Blob):
+        self.blob = blob
+
+    def __del__(self):
+        try:
+            if self.blob is not None and self.blob.data:
+                load_library().scm_blob_free(byref(self.blob))
+                self.blob = None
+        except Exception:
+            pass
+
+
 class PackedRows:
-    """Output of scm_table_run_packed: one library-owned buffer (freed with
-    scm_blob_free when this object dies) plus the element offsets.  Element
-    2r is row r's pair_image_ids, element 2r+1 its two_view_geometries."""
+    """Output of scm_table_run_packed: one library-owned buffer plus the
+    element offsets.  Element 2r is row r's pair_image_ids, element 2r+1 its
+    two_view_geometries.  The buffer is freed (returned to the library's pool)
+    only when this object and every view of `data` are gone, so views handed
+    to a background gather stay valid however long it keeps them."""
 
     def __init__(self, blob: Blob, offsets: np.ndarray):
-        self._blob = blob
         self.offsets = offsets
         n = int(blob.size)
-        self.data = (np.ctypeslib.as_array(blob.data, shape=(n,)) if n
-                     else np.zeros(0, dtype=np.uint8))
+        if n:
+            owner = _BlobOwner(blob)
+            buf = (ctypes.c_uint8 * n).from_address(ctypes.addressof(blob.data.contents))
+            buf._owner = owner  # the array's base chain ends here
+            self.data = np.frombuffer(buf, dtype=np.uint8)
+        else:
+            _BlobOwner(blob)  # frees a zero-sized allocation at once
+            self.data = np.zeros(0, dtype=np.uint8)
 
     def __len__(self) -> int:
         return (len(self.offsets) - 1) // 2
@@ -228,15 +251,6 @@ class PackedRows:
         n = len(self)
         return ([self.element(2 * r) for r in range(n)],
                 [self.element(2 * r + 1) for r in range(n)])
-
-    def __del__(self):
-        try:
-            if self._blob is not None and self._blob.data:
-                self.data = None
-                load_library().scm_blob_free(byref(self._blob))
-                self._blob = None
-        except Exception:
-            pass
 
 
 class Context:

@@ -1544,7 +1544,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                                       const double* xy2, int n, int max_trials,
                                       const VerifyParams P, double* res0, double* res1,
                                       double* xin1, double* xin2, uint32_t* snap,
-                                      double* mbuf, Prof pf) {
+                                      double* mbuf, Prof pf, uint32_t* scrib = nullptr) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   const int lane = threadIdx.x & 63;
@@ -1577,6 +1577,12 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
     //    index vector, RandomSampler::Sample).
     for (int i = threadIdx.x; i < 624; i += BS) snap[i] = s.mt[i];
     if (t0th) snap[624] = (uint32_t)s.mt_idx;
+    if (scrib) {
+      // Diagnostics (SCM_DIAG_SCRIBBLE_F_SIDX, verify_final_kernel): rewrite the
+      // F area's index vector before every draw, as a speculative F window's
+      // draws may at any point of this RANSAC.  It must change nothing.
+      for (int i = threadIdx.x; i < n; i += BS) scrib[i] = 0u;
+    }
     wsync();
     if (draw_targets_wave<Tr::kmin>(s, B * Tr::kmin, (uint32_t)n)) {
       if (t0th) shuffle_batch_lane0<Tr::kmin>(s, sidx, B);
@@ -1848,6 +1854,9 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
   // phase 1 (early, small batches): only pairs whose F and H RANSACs are both
   // done (read once, by thread 0: the replay of other pairs is still
   // running), marked in rstF[q].pad_; phase 2: the rest; phase 0: every pair.
+  // Bit 8 of the argument: diagnostics (loransac_wave's scrib).
+  const bool scrib = (phase & 8) != 0;
+  phase &= 3;
   if (phase != 0) {
     if (threadIdx.x == 0) {
       const int q0 = blockIdx.x;
@@ -1867,7 +1876,18 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
   pf.start();
   const PairSetup ps = pair_setup(pairs, scratch, snaps, out, counts);
   const int n = ps.n, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  uint32_t* sidx = reinterpret_cast<uint32_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
+  // The watermark RANSAC's sample-index vector lives in the pair's H scratch
+  // area, its points and residuals in the F area (layout below).  H is done
+  // when this kernel runs for a pair and no H draws follow H's last window,
+  // while the F area's index vector may still be rewritten: in a small batch
+  // the early pass (phase 1) runs beside the later windows, whose F draws are
+  // speculative -- window r + 1's draws take the pairs that were running one
+  // window back, so a pair whose F stopped in window r (or whose stop phase 1
+  // observes during window r + 1's replay) is drawn once more.  The draws
+  // write nothing else in the pair's scratch (pair_sidx only).
+  uint32_t* fsidx = reinterpret_cast<uint32_t*>(ps.base + 10 * (int64_t)n + kVerifyModelDoubles);
+  uint32_t* sidx = reinterpret_cast<uint32_t*>(ps.base + verify_kind_scratch_doubles(n) +
+                                               10 * (int64_t)n + kVerifyModelDoubles);
   if (!(n >= P.min_num_inliers && n > 0)) return;
   const double* xy1 = xy1_all + ps.pp.pts_off;
   const double* xy2 = xy2_all + ps.pp.pts_off;
@@ -1977,7 +1997,8 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
         mt_load(s, ps.state);
         const RansacResult rt = loransac_wave<KIND_T, NW>(s, sidx, tin1, tin2, ni, P.max_trials_T, P,
                                                       base + 4 * n, base + 5 * n, base + 6 * n,
-                                                      base + 8 * n, ps.snap, base + 10 * n, pf);
+                                                      base + 8 * n, ps.snap, base + 10 * n, pf,
+                                                      scrib ? fsidx : nullptr);
         const double iratio = (double)rt.num_inliers / (double)ni;
         if (iratio >= P.watermark_min_inlier_ratio) {
           config = SCM_TVG_WATERMARK;
@@ -3613,27 +3634,35 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
                          sp ? spec->dstream : nullptr, sp ? spec->draw_ev : nullptr)) !=
       hipSuccess)
     return err;
+  // Diagnostics: SCM_DIAG_SCRIBBLE_F_SIDX=1 makes the final kernel rewrite the
+  // F area's index vector before every watermark draw (the worst the
+  // speculative F draws beside the early pass can do; outputs must not move,
+  // tests/test_gpu_stencil.py).  Read per call so a test can set it.
+  const char* diag_env = getenv("SCM_DIAG_SCRIBBLE_F_SIDX");
+  const int diag = diag_env && atoi(diag_env) ? 8 : 0;
   if (sp && last_h >= 0 && last_h < kMaxVerifyWindows) {
     // Configuration + watermark of the pairs done when H's last window is
     // replayed (typically all but the far pairs' F), beside the later windows;
-    // then the rest after the last window.
+    // then the rest after the last window.  Nothing orders this pass against
+    // the later windows' F draws on dstream: the watermark's index vector is
+    // in the pair's H area (verify_final_kernel), which they never touch.
     (void)hipStreamWaitEvent(spec->fstream, spec->win_ev[2 * last_h + 1], 0);
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, spec->fstream, pairs,
                        xy1, xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst,
-                       rb_h.rst, 1);
+                       rb_h.rst, 1 | diag);
     (void)hipEventRecord(spec->fin_ev, spec->fstream);
     (void)hipStreamWaitEvent(stream, spec->fin_ev, 0);
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, stream, pairs, xy1,
                        xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,
-                       2);
+                       2 | diag);
   } else if (verify_small_batch(npairs, max_m)) {
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, stream, pairs, xy1,
                        xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,
-                       0);
+                       diag);
   } else {
     hipLaunchKernelGGL(verify_final_kernel<1>, dim3(npairs), dim3(kVerifyThreads), lds, stream,
                        pairs, xy1, xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst,
-                       rb_h.rst, 0);
+                       rb_h.rst, diag);
   }
   return hipGetLastError();
 }

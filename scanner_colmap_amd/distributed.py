@@ -73,7 +73,8 @@ class _Staging:
         return self.ring[self.k]
 
 
-def gather_packed(offsets: np.ndarray, data: np.ndarray, device=None, staging=None):
+def gather_packed(offsets: np.ndarray, data: np.ndarray, device=None, staging=None,
+                  own: bool = False):
     """Gather every rank's scm_table_run_packed output (element offsets and
     packed element bytes) to rank 0: a list of (offsets int64 array, data
     uint8 array) per rank on rank 0, None elsewhere.
@@ -84,8 +85,12 @@ def gather_packed(offsets: np.ndarray, data: np.ndarray, device=None, staging=No
     slices of one flat buffer.  On `nccl` (RCCL over xGMI) a sender stages its
     bytes into a persistent pinned buffer and one H2D copy, each peer's bytes
     travel over its own xGMI link to GPU 0, and rank 0 makes one D2H copy into
-    a pinned ring buffer; the per-rank results are views into it.  On gloo the
-    same group runs on CPU tensors with no staging."""
+    a pinned ring buffer; the per-rank results are views into it, valid until
+    the gather after next.  `own`: results that outlive that (a kept
+    background gather) -- rank 0's D2H lands in a buffer of their own instead
+    of the ring.  Rank 0's own entry is a view of `data` (a PackedRows buffer
+    lives as long as its views).  On gloo the same group runs on CPU tensors
+    with no staging."""
     import torch
     import torch.distributed as dist
 
@@ -135,7 +140,10 @@ def gather_packed(offsets: np.ndarray, data: np.ndarray, device=None, staging=No
         for w in dist.batch_isend_irecv(ops):
             w.wait()
     if on_gpu and total:
-        host_t = (staging or _Staging()).recv_host(total)
+        if own or staging is None:
+            host_t = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+        else:
+            host_t = staging.recv_host(total)
         host_t[:total].copy_(flat)
         host = host_t.numpy()
     else:
@@ -161,13 +169,13 @@ class Gatherer:
         self.staging = _Staging()
         self.ms = []  # duration of each gather (ms)
 
-    def _run(self, packed):
+    def _run(self, packed, keep):
         import time
         if self.device is not None and self.device.type == "cuda":
             import torch
             torch.cuda.set_device(self.device)
         t0 = time.perf_counter()
-        out = gather_packed(packed.offsets, packed.data, self.device, self.staging)
+        out = gather_packed(packed.offsets, packed.data, self.device, self.staging, own=keep)
         self.ms.append((time.perf_counter() - t0) * 1e3)
         return out
 
@@ -177,11 +185,11 @@ class Gatherer:
             r = f.result()
             if k:
                 self.done.append(r)
-        self.pending.append((self.pool.submit(self._run, packed), keep))
+        self.pending.append((self.pool.submit(self._run, packed, keep), keep))
 
     def drain(self) -> list:
         """Wait for every outstanding gather; the kept results in step order
-        (rank 0's (offsets, data) views stay valid until two more gathers ran)."""
+        (each in buffers of its own: valid for as long as the caller keeps it)."""
         for f, k in self.pending:
             r = f.result()
             if k:

@@ -30,6 +30,9 @@ class Corridor:
                  outlier_frac: float = 0.3, noise_px: float = 0.5,
                  desc_noise: float = 0.35, focal: float = 1200.0,
                  confuser_frac: float = 0.1):
+        self._kw = dict(num_images=num_images, num_kpts=num_kpts, overlap=overlap, seed=seed,
+                        outlier_frac=outlier_frac, noise_px=noise_px, desc_noise=desc_noise,
+                        focal=focal, confuser_frac=confuser_frac)
         self.num_images = num_images
         self.num_kpts = num_kpts
         self.seed = seed
@@ -140,8 +143,31 @@ class Corridor:
             pool.join()
         return out
 
+    def table_rows_spawned(self, start: int = 0, stop: int | None = None, workers: int = 16,
+                           chunk: int = 50):
+        """codecs.table_rows of images [start, stop), generated and encoded
+        in `workers` spawned processes (safe once the GPU runtime is up in
+        this process: nothing is forked from it)."""
+        import multiprocessing as mp
+        stop = self.num_images if stop is None else min(stop, self.num_images)
+        jobs = [(self._kw, a, min(stop, a + chunk)) for a in range(start, stop, chunk)]
+        ids, kps, descs = [], [], []
+        with mp.get_context("spawn").Pool(workers) as pool:
+            for a, b, c in pool.imap(_encoded_chunk, jobs):
+                ids += a
+                kps += b
+                descs += c
+        return ids, kps, descs
+
 
 _POOL_CORRIDOR = None
+
+
+def _encoded_chunk(job):
+    from .codecs import table_rows
+    kw, a, b = job
+    c = Corridor(**kw)
+    return table_rows([c.image(i) for i in range(a, b)])
 
 
 def _pool_image(i):
@@ -190,6 +216,13 @@ def geometry_scene(kind: str, num_matches: int, seed: int, outlier_frac: float =
                      moving on its own (the rest before the outliers): two
                      epipolar geometries, so EstimateMultiple (multiple_models)
                      finds both -> MULTIPLE (8); plain Estimate -> UNCALIBRATED.
+    * "two_translations": x2 = x1 + t for 76 % of the matches and
+                     x2 = x1 + 1.6 t for the rest (one epipolar geometry for
+                     both, F = [t]x; H and the watermark's 2-D translation
+                     explain only the first set) -> WATERMARK (7), decided by
+                     the watermark RANSAC's samples: the first match in
+                     index order belongs to the 24 % set, so a RANSAC that
+                     sampled only it would find 24 % (< 0.7).
 
     Returns (kp1 N x 6, kp2 N x 6, matches M x 2 uint32); keypoint order is
     shuffled so the match indices are not the identity."""
@@ -202,6 +235,10 @@ def geometry_scene(kind: str, num_matches: int, seed: int, outlier_frac: float =
         x2 = p[:, :2] / p[:, 2:3]
     elif kind == "translation":
         x2 = x1 + np.array([37.5, -12.25])
+    elif kind == "two_translations":
+        t = np.array([37.5, -12.25])
+        x2 = x1 + t
+        x2[int(round(0.76 * m)):] += 0.6 * t
     elif kind == "random":
         x2 = np.stack([rng.uniform(0, 1920, m), rng.uniform(0, 1080, m)], axis=1)
     elif kind in ("general", "two_motions"):
@@ -229,6 +266,9 @@ def geometry_scene(kind: str, num_matches: int, seed: int, outlier_frac: float =
         x2[:nout] = np.stack([rng.uniform(0, 1920, nout), rng.uniform(0, 1080, nout)], axis=1)
     p1 = rng.permutation(m)
     p2 = rng.permutation(m)
+    if kind == "two_translations":  # keypoint 0 of image 1 (the first match) in the 24 % set
+        j0 = int(np.argmin(p1))
+        p1[[j0, m - 1]] = p1[[m - 1, j0]]
     kp1 = np.zeros((m, 6), np.float32)
     kp2 = np.zeros((m, 6), np.float32)
     kp1[p1, :2] = x1

@@ -63,3 +63,56 @@ def test_gpu_shard_step_world2(n, K, scaling):
     ok_a, ok_b, nrows, total = q.get(timeout=5)
     assert ok_a and ok_b and nrows == total
     assert total == (n if scaling == "strong" else n * world)
+
+
+def _rank_passes_main(rank, world, port, n, K, passes, q):
+    import gc
+
+    import torch.distributed as dist
+
+    from oracle import oracle
+    from scanner_colmap_amd import Context
+    from scanner_colmap_amd.codecs import table_rows
+    from scanner_colmap_amd.synthetic import Corridor
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        plan = sd.ShardPlan(n, K, world, rank, "strong")
+        c = Corridor(plan.total_images, 800, K, seed=58)
+        with Context(0) as ctx:
+            ctx.table_load(*table_rows(c.images(plan.table_begin, plan.table_end)))
+            plan.run_passes(ctx, passes, keep=True)
+            gc.collect()
+            # more library runs: their buffers come from the pool the kept
+            # passes' PackedRows would have returned if the views did not hold them
+            lb, le = plan.local_rows
+            for _ in range(2):
+                ctx.table_run_packed(K, lb, le)
+            gathered = plan.drain()
+        if rank == 0:
+            ids, kps, descs = table_rows(c.images())
+            ref = oracle.table_run(ids, kps, descs, K, 0, plan.total_images)
+            q.put([sd.merge_gathered(g) == ref for g in gathered])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gpu_streamed_passes_kept_world2():
+    """ShardPlan.run_passes with keep=True over the real library
+    (scm_table_run_passes): every pass's gathered rows stay byte-equal to the
+    oracle after later passes and later runs, i.e. rank 0's own entry (a view
+    of a library buffer) and the peers' entries outlive the buffer pool and
+    the staging ring."""
+    world, passes = 2, 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_passes_main, args=(r, world, port, 12, 4, passes, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert [p.exitcode for p in procs] == [0, 0]
+    assert q.get(timeout=5) == [True] * passes

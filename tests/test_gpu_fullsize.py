@@ -162,3 +162,66 @@ def test_k50_shape_many_batches():
     finally:
         del os.environ["SCM_BATCH_PAIRS"]
     assert len(configs) == sum(min(49, 63 - i) for i in range(64))
+
+
+def test_config5_full_table_rank_share():
+    """Config 5 at its size on one GPU: the whole 10,000 x 4096-keypoint table
+    (overlap 50, 488,775 pairs, 5.2 GB of descriptors) resident in HBM, and one
+    strong-scaled rank's share of the 8-GPU job (ShardPlan(10000, 50, 8, 3,
+    "strong"): ~61K pairs) run through scm_table_run_packed.  Every row's pair
+    ids follow the stencil rule (feature_matching.py:43,
+    sequential_matching.cc:139-146); the rank's first row, a middle row and
+    its last 4 rows have raw matches bit-exact and TwoViewGeometry bytes equal
+    to the CPU oracle's; the packed byte volume the RCCL gather would ship is
+    printed."""
+    import time
+    from concurrent.futures import ThreadPoolExecutor
+
+    from scanner_colmap_amd.codecs import decode_pair_ids, split_tvg_list
+    from scanner_colmap_amd.distributed import ShardPlan, pairs_per_row
+    n, k, K = 10000, 4096, 50
+    plan = ShardPlan(n, K, 8, 3, "strong")
+    a, b = plan.row_begin, plan.row_end
+    c = Corridor(n, k, K, seed=20255)
+    t0 = time.perf_counter()
+    ids, kps, descs = c.table_rows_spawned(0, n, workers=THREADS)
+    t_gen = time.perf_counter() - t0
+    sample = [a, (a + b) // 2] + list(range(b - 4, b))
+    with Context(0) as ctx:
+        ctx.table_load(ids, kps, descs)
+        del kps, descs
+        for r in sample:
+            ctx.add_keep_matches_range(r, r + 1)
+        t0 = time.perf_counter()
+        packed = ctx.table_run_packed(K, a, b)
+        t_run = time.perf_counter() - t0
+        got_m = {(r, s): ctx.table_matches(r, s - r) for r in sample
+                 for s in range(r + 1, min(n, r + K))}
+    npairs = int(pairs_per_row(n, K)[a:b].sum())
+    assert npairs == plan.pairs() and npairs > 60000
+    assert len(packed) == b - a
+    for r in range(a, b):
+        got = decode_pair_ids(packed.element(2 * (r - a)))
+        assert got == [s + 1 for s in range(r + 1, min(n, r + K))], r
+    volume = int(packed.data.nbytes + packed.offsets.nbytes)
+    print(f"config 5 rank 3 of 8: rows [{a}, {b}), {npairs} pairs, gen {t_gen:.1f} s, "
+          f"run {t_run:.2f} s ({npairs / t_run:.0f} pairs/s incl. host rows), "
+          f"gather volume {volume / 1e6:.1f} MB ({volume / npairs:.0f} B per pair)")
+    imgs = {i: c.image(i) for i in {i for r in sample for i in range(r, min(n, r + K))}}
+
+    def one(job):
+        r, s = job
+        m = oracle.match_pair_fast(imgs[r][2], imgs[s][2])
+        return m, oracle.verify_pair(imgs[r][1], imgs[s][1], m, imgs[r][0], imgs[s][0])
+
+    jobs = list(got_m)
+    with ThreadPoolExecutor(max_workers=THREADS) as ex:
+        ref = dict(zip(jobs, ex.map(one, jobs)))
+    for r in sample:
+        row = split_tvg_list(packed.element(2 * (r - a) + 1))
+        for s in range(r + 1, min(n, r + K)):
+            m, tvg = ref[(r, s)]
+            g = got_m[(r, s)]
+            assert g.shape == m.shape and (g == m).all(), (r, s)
+            assert row[s - r - 1] == tvg, (r, s)
+    assert len(jobs) == 6 * (K - 1)

@@ -9,8 +9,8 @@ import pytest
 
 from oracle import oracle
 from scanner_colmap_amd import Context, ScmError
-from scanner_colmap_amd.codecs import table_rows
-from scanner_colmap_amd.synthetic import Corridor
+from scanner_colmap_amd.codecs import decode_tvg_list, table_rows
+from scanner_colmap_amd.synthetic import Corridor, descriptors_for_matches, geometry_scene
 
 pytestmark = pytest.mark.gpu
 
@@ -237,3 +237,37 @@ def test_execute_stencil_recycled_buffers():
     assert rerun == 0
     assert refused == n - K  # one recycled buffer per call after the first
     assert uploaded == K + (n - K) and reused == (n - K) * (K - 1)
+
+
+def test_watermark_index_vector_apart_from_speculative_f_draws(monkeypatch):
+    """The early final pass of a small batch (configuration + watermark of the
+    pairs whose F and H are done when H's last window is replayed) runs beside
+    the later windows, whose F draws are speculative: window r + 1 draws for
+    the pairs that were running one window back, so a pair whose F stopped in
+    window r has its F index vector shuffled once more while its watermark
+    RANSAC may be running.  The watermark's own index vector therefore lives in
+    the pair's H area (verify_kernels.hip verify_final_kernel).
+
+    No stream order can force the collision (draws that end before the pass
+    starts are harmless: the watermark RANSAC starts from the identity), so
+    the adversary is deterministic instead: SCM_DIAG_SCRIBBLE_F_SIDX=1 makes
+    the final kernel itself zero the F area's index vector before every
+    watermark draw, the worst those draws could do at any moment.  On this
+    scene the watermark decision depends on the samples (the first inlier is
+    in the 24 % set), so a watermark RANSAC that read the F area's vector
+    would end at 24 % and drop WATERMARK.  Reference: Estimate, then
+    DetectWatermark, sequential per pair (sequential_matching.cc:98-99, 159)."""
+    kp1, kp2, mt = geometry_scene("two_translations", 600, 31, outlier_frac=0.1)
+    d1, d2 = descriptors_for_matches(mt, len(kp1), len(kp2), 31)
+    extra = Corridor(3, 700, 3, seed=32).images()
+    imgs = [(40, kp1, d1), (41, kp2, d2)] + [(42 + i, k, d) for i, (_, k, d) in enumerate(extra)]
+    ids, kps, descs = table_rows(imgs)
+    ref_st = oracle.execute_stencil(ids[:4], kps[:4], descs[:4])
+    ref_tab = oracle.table_run(ids, kps, descs, 3, 0, len(imgs))
+    assert decode_tvg_list(ref_st[1])[0].config == 7  # (40, 41): WATERMARK
+    monkeypatch.setenv("SCM_DIAG_SCRIBBLE_F_SIDX", "1")
+    with Context(0) as ctx:
+        for _ in range(3):  # small batch: early pass beside the speculative windows
+            assert ctx.execute_stencil(ids[:4], kps[:4], descs[:4]) == ref_st
+        ctx.table_load(ids, kps, descs)  # table path (one final pass after all windows)
+        assert ctx.table_run(3, 0, len(imgs)) == ref_tab
