@@ -827,10 +827,9 @@ __device__ __forceinline__ int score_f_chunk(const FFilt& f, const double* mk, c
   return cnt;
 }
 
-// Point loops of the sequential (watermark) LO-RANSAC on the double point
-// arrays: latency-bound on one wave, so each lane keeps kSeqU points' loads in
-// flight; items are consumed in index order per lane (canonical sums keep
-// their order).
+// Point loops of the sequential (watermark) LO-RANSAC and the final kernel:
+// latency-bound, so each lane keeps kSeqU points' loads in flight; items are
+// consumed in index order per lane (canonical sums keep their order).
 constexpr int kSeqU = 8;
 
 // InlierSupportMeasurer::Evaluate's residual_sum: inlier residuals summed
@@ -905,74 +904,14 @@ __device__ __forceinline__ void apply_norm_affine(const double* T, double p0, do
   *o1 = T[3] * p0 + T[4] * p1 + T[5];
 }
 
-// residuals_wave / residuals_f4 and the ordered gather in one pass: the
+// A model's residuals and the ordered gather of its inliers in one pass: the
 // model's residuals into res and, in index order, its inliers' points into
 // xin (the gather the local optimisation runs next if the model becomes the
 // best: a candidate's pass and every LO step's pass write it, so LO starts
-// from it without another pass over the points).  Same rounds and lane
-// mapping as the gathers; returns the inlier count; residuals and inliers are
-// visible to the block on return.
-template <int K, int NW = 1>
-__device__ int residuals_gather(const double* m, const double* xy1, const double* xy2, int n,
-                                double maxr, double* res, double* xin1, double* xin2,
-                                int32_t* redi = nullptr) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  int base_out = 0;
-  for (int r0 = 0; r0 < n; r0 += 64 * kSeqU * NW) {
-    const int b0 = r0 + wv * 64 * kSeqU;
-    double r[kSeqU], a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
-#pragma unroll
-    for (int u = 0; u < kSeqU; ++u) {
-      const int ic = min(b0 + 64 * u + lane, n - 1);
-      a0[u] = xy1[2 * ic];
-      a1[u] = xy1[2 * ic + 1];
-      c0[u] = xy2[2 * ic];
-      c1[u] = xy2[2 * ic + 1];
-    }
-    uint64_t bal[kSeqU];
-    int wc = 0;
-#pragma unroll
-    for (int u = 0; u < kSeqU; ++u) {
-      const int i = b0 + 64 * u + lane;
-      r[u] = 1.7976931348623157e308;
-      if (i < n) {
-        r[u] = residual_pt<K>(m, a0[u], a1[u], c0[u], c1[u]);
-        res[i] = r[u];
-      }
-      bal[u] = __ballot(r[u] <= maxr);
-      wc += __popcll(bal[u]);
-    }
-    int before = 0, total = wc;
-    if (NW > 1) {
-      if (lane == 0) redi[wv] = wc;
-      __syncthreads();
-      total = 0;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        const int x = redi[w];
-        before += w < wv ? x : 0;
-        total += x;
-      }
-      __syncthreads();
-    }
-    int o = base_out + before;
-#pragma unroll
-    for (int u = 0; u < kSeqU; ++u) {
-      if (r[u] <= maxr) {
-        const int oo = o + (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal[u] >> 32),
-                                                          __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
-        xin1[2 * oo] = a0[u];
-        xin1[2 * oo + 1] = a1[u];
-        xin2[2 * oo] = c0[u];
-        xin2[2 * oo + 1] = c1[u];
-      }
-      o += __popcll(bal[u]);
-    }
-    base_out += total;
-  }
-  if (NW > 1) __syncthreads();
-  return base_out;
-}
+// from it without another pass over the points).  Wave w takes block w of
+// each round of 64 kLoU NW points; a prefix of the waves' counts places its
+// inliers.  Returns the inlier count; residuals and inliers are visible to
+// the block on return.
 template <int K, int NW = 1>
 __device__ int residuals_gather_f4(const double* m, const float4* xyf, int n, double maxr,
                                    double* res, float4* xin, int32_t* redi = nullptr) {
@@ -1094,102 +1033,25 @@ __device__ void invsq9_null_wave(const double* ata45, double* A, double* B, doub
   sq9_column_unit(B, jstar, f);
 }
 
-// normalize_transform (geom_solvers.h) of both point sets, canonical sums.
-__device__ void normalize_pair_wave(const double* xy1, const double* xy2, int n, double* T1,
-                                    double* T2) {
-  const int lane = threadIdx.x;
-  double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
-  for (int i = lane; i < n; i += 64) {
-    p0 += xy1[2 * i];
-    p1 += xy1[2 * i + 1];
-    p2 += xy2[2 * i];
-    p3 += xy2[2 * i + 1];
-  }
-  const double c10 = canon_tree_wave(p0) / (double)n, c11 = canon_tree_wave(p1) / (double)n;
-  const double c20 = canon_tree_wave(p2) / (double)n, c21 = canon_tree_wave(p3) / (double)n;
-  p0 = kCanonZero;
-  p1 = kCanonZero;
-  for (int i = lane; i < n; i += 64) {
-    const double d0 = xy1[2 * i] - c10, d1 = xy1[2 * i + 1] - c11;
-    const double e0 = xy2[2 * i] - c20, e1 = xy2[2 * i + 1] - c21;
-    p0 += d0 * d0 + d1 * d1;
-    p1 += e0 * e0 + e1 * e1;
-  }
-  const double rms1 = sqrt(canon_tree_wave(p0) / (double)n);
-  const double rms2 = sqrt(canon_tree_wave(p1) / (double)n);
-  const double s1 = sqrt(2.0) / rms1, s2 = sqrt(2.0) / rms2;
-  T1[0] = s1; T1[1] = 0.0; T1[2] = -s1 * c10;
-  T1[3] = 0.0; T1[4] = s1; T1[5] = -s1 * c11;
-  T1[6] = 0.0; T1[7] = 0.0; T1[8] = 1.0;
-  T2[0] = s2; T2[1] = 0.0; T2[2] = -s2 * c20;
-  T2[3] = 0.0; T2[4] = s2; T2[5] = -s2 * c21;
-  T2[6] = 0.0; T2[7] = 0.0; T2[8] = 1.0;
-}
-
-// Local (least-squares) estimators on n gathered inliers (geom_solvers.h
-// fundamental_8pt / homography_dlt n > 4 / translation_estimate); every lane
-// returns the model.
-// One third (15 packed entries) of the normal equations A^T A of the local
-// estimators, summed in canonical order into s.ata.
-template <int K, int PASS>
-__device__ __forceinline__ void ata_pass_wave(VerifyLds& s, const double* xin1,
-                                                        const double* xin2, int n,
-                                                        const double* T1, const double* T2) {
-  const int lane = threadIdx.x;
-  double part[15];
-#pragma unroll
-  for (int k = 0; k < 15; ++k) part[k] = kCanonZero;
-#pragma unroll 1
-  for (int i = lane; i < n; i += 64) {
-    double x0, y0, x1, y1;
-    apply_normalize(T1, xin1[2 * i], xin1[2 * i + 1], &x0, &y0);
-    apply_normalize(T2, xin2[2 * i], xin2[2 * i + 1], &x1, &y1);
-    double a[9], b[9];
-    if (K == KIND_F) f_row(x0, y0, x1, y1, a);
-    else h_rows(x0, y0, x1, y1, a, b);
-    int k = 0;
-#pragma unroll
-    for (int p = 0; p < 9; ++p)
-#pragma unroll
-      for (int q = p; q < 9; ++q) {
-        if (k >= 15 * PASS && k < 15 * PASS + 15) part[k - 15 * PASS] = part[k - 15 * PASS] + a[p] * a[q];
-        ++k;
-      }
-    if (K == KIND_H) {
-      k = 0;
-#pragma unroll
-      for (int p = 0; p < 9; ++p)
-#pragma unroll
-        for (int q = p; q < 9; ++q) {
-          if (k >= 15 * PASS && k < 15 * PASS + 15)
-            part[k - 15 * PASS] = part[k - 15 * PASS] + b[p] * b[q];
-          ++k;
-        }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 15; ++k) {
-    const double t = canon_tree_wave(part[k]);
-    if (lane == 0) s.ata[15 * PASS + k] = t;
-  }
-}
-
-// NW = 4 (KIND_T only): wave w forms the canonical sum of coordinate w with
-// the one-wave lane mapping (the same sums), exchanged in s.redd.
+// Local estimator of the watermark LO-RANSAC (geom_solvers.h
+// translation_estimate on n gathered inliers, packed fp32 points: keypoints
+// are float32, so widening reproduces the reference's doubles exactly): the
+// mean displacement, its four coordinate sums in canonical order.  NW > 1:
+// wave w < 4 forms the sum of coordinate w with the one-wave lane mapping (the
+// same sums), exchanged in s.redd.  Every lane returns the model.
 template <int K, int NW = 1>
-__device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const double* xin2, int n,
-                                    double* model) {
+__device__ void local_estimate_wave(VerifyLds& s, const float4* xin, int n, double* model) {
+  static_assert(K == KIND_T, "the F / H local estimators run on local_estimate_f4");
   const int lane = threadIdx.x & 63;
-  if (K == KIND_T && NW > 1) {
+  if (NW > 1) {
     const int wv = threadIdx.x >> 6;
-    const double* src = wv < 2 ? xin1 : xin2;
-    const int c = wv & 1;
     double p = kCanonZero;
     if (wv < 4) {
       for (int b = lane; b < n; b += 64 * kSeqU) {
         double a[kSeqU];
+        const float* xc = reinterpret_cast<const float*>(xin) + wv;  // coordinate wv only
 #pragma unroll
-        for (int u = 0; u < kSeqU; ++u) a[u] = src[2 * min(b + 64 * u, n - 1) + c];
+        for (int u = 0; u < kSeqU; ++u) a[u] = (double)xc[4 * min(b + 64 * u, n - 1)];
 #pragma unroll
         for (int u = 0; u < kSeqU; ++u)
           if (b + 64 * u < n) p += a[u];
@@ -1205,46 +1067,24 @@ __device__ void local_estimate_wave(VerifyLds& s, const double* xin1, const doub
     model[1] = d1 - s1;
     return;
   }
-  if (K == KIND_T) {
-    double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
-    for (int b = lane; b < n; b += 64 * kSeqU) {
-      double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
+  double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
+  for (int b = lane; b < n; b += 64 * kSeqU) {
+    float4 v[kSeqU];
 #pragma unroll
-      for (int u = 0; u < kSeqU; ++u) {
-        const int i = min(b + 64 * u, n - 1);
-        a0[u] = xin1[2 * i];
-        a1[u] = xin1[2 * i + 1];
-        c0[u] = xin2[2 * i];
-        c1[u] = xin2[2 * i + 1];
+    for (int u = 0; u < kSeqU; ++u) v[u] = xin[min(b + 64 * u, n - 1)];
+#pragma unroll
+    for (int u = 0; u < kSeqU; ++u)
+      if (b + 64 * u < n) {
+        p0 += (double)v[u].x;
+        p1 += (double)v[u].y;
+        p2 += (double)v[u].z;
+        p3 += (double)v[u].w;
       }
-#pragma unroll
-      for (int u = 0; u < kSeqU; ++u)
-        if (b + 64 * u < n) {
-          p0 += a0[u];
-          p1 += a1[u];
-          p2 += c0[u];
-          p3 += c1[u];
-        }
-    }
-    const double s0 = canon_tree_wave(p0) / (double)n, s1 = canon_tree_wave(p1) / (double)n;
-    const double d0 = canon_tree_wave(p2) / (double)n, d1 = canon_tree_wave(p3) / (double)n;
-    model[0] = d0 - s0;
-    model[1] = d1 - s1;
-    return;
   }
-  double T1[9], T2[9];
-  normalize_pair_wave(xin1, xin2, n, T1, T2);
-  // A^T A in canonical order, 15 packed entries per pass (register budget);
-  // every entry accumulates exactly the terms of ata_accumulate in order.
-  ata_pass_wave<K, 0>(s, xin1, xin2, n, T1, T2);
-  ata_pass_wave<K, 1>(s, xin1, xin2, n, T1, T2);
-  ata_pass_wave<K, 2>(s, xin1, xin2, n, T1, T2);
-  wsync();
-  double f[9];
-  invsq9_null_wave(s.ata, s.jA, s.jV, f);
-  wsync();
-  if (K == KIND_F) fundamental_8pt_finish(f, T1, T2, model);
-  else homography_finish(f, T1, T2, model);
+  const double s0 = canon_tree_wave(p0) / (double)n, s1 = canon_tree_wave(p1) / (double)n;
+  const double d0 = canon_tree_wave(p2) / (double)n, d1 = canon_tree_wave(p3) / (double)n;
+  model[0] = d0 - s0;
+  model[1] = d1 - s1;
 }
 
 __device__ __forceinline__ void norm_transforms(double c10, double c11, double c20, double c21,
@@ -1301,7 +1141,8 @@ __device__ void normalize_pair_f4_w4(const float4* xin, int n, double* T1, doubl
   __syncthreads();
 }
 
-// normalize_pair_wave on packed points (canonical sums, same order).
+// normalize_transform (geom_solvers.h) of both point sets on packed points,
+// canonical sums.
 __device__ void normalize_pair_f4(const float4* xin, int n, double* T1, double* T2) {
   double p0 = kCanonZero, p1 = kCanonZero, p2 = kCanonZero, p3 = kCanonZero;
   for (int b = threadIdx.x; b < n; b += 64 * kLoU) {
@@ -1343,7 +1184,8 @@ __device__ void normalize_pair_f4(const float4* xin, int n, double* T1, double* 
   T2[6] = 0.0; T2[7] = 0.0; T2[8] = 1.0;
 }
 
-// ata_pass_wave on packed points: packed entries [K0, K1) of A^T A.
+// Packed entries [K0, K1) of the normal equations A^T A of the local
+// estimators, summed in canonical order into s.ata.
 template <int K, int K0, int K1>
 __device__ __forceinline__ void ata_range_f4(VerifyLds& s, const float4* xin, int n,
                                              const double* T1, const double* T2) {
@@ -1397,7 +1239,8 @@ __device__ __forceinline__ void ata_pass_f4(VerifyLds& s, const float4* xin, int
   ata_range_f4<K, 15 * PASS, 15 * PASS + 15>(s, xin, n, T1, T2);
 }
 
-// local_estimate_wave (F: 8-point, H: DLT) on packed points.
+// The F / H local estimators (geom_solvers.h fundamental_8pt / homography_dlt
+// n > 4) on packed points, canonical sums.
 // NW = 4: the coordinate sums and the A^T A entries are split between the
 // waves (each sum whole on one wave), the 9 x 9 null vector runs on wave 0.
 template <int K, int NW = 1>
@@ -1533,18 +1376,18 @@ __device__ bool tie_better(VerifyLds& s, const double* rt, const double* rb, int
   return *sum < s.best_sum;
 }
 
-// LORANSAC<Estimator, LocalEstimator>::Estimate on n points (xy1, xy2).
-// res0 / res1: residual buffers (n doubles each); xin1 / xin2 inlier gather
-// buffers (2n doubles each); snap: 625-word PRNG snapshot (global).  The
-// best model ends in s.best_model.
+// LORANSAC<Estimator, LocalEstimator>::Estimate on n points (pts: packed
+// x1, y1, x2, y2; the watermark's translation RANSAC, KIND_T).  res0 / res1:
+// residual buffers (n doubles each); xin: inlier gather buffer (n points);
+// snap: 625-word PRNG snapshot (global).  The best model ends in s.best_model.
 // NW waves (8: small batches, verify_final_kernel<8>; KIND_T): every wave runs
 // the same decisions; the point loops split as in the windowed replay.
 template <int K, int NW = 1>
-__device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& s, uint32_t* sidx, const double* xy1,
-                                      const double* xy2, int n, int max_trials,
+__device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& s, uint32_t* sidx,
+                                      const float4* pts, int n, int max_trials,
                                       const VerifyParams P, double* res0, double* res1,
-                                      double* xin1, double* xin2, uint32_t* snap,
-                                      double* mbuf, Prof pf, uint32_t* scrib = nullptr) {
+                                      float4* xin, uint32_t* snap, double* mbuf, Prof pf,
+                                      uint32_t* scrib = nullptr) {
   using Tr = KindTraits<K>;
   constexpr int MM = Tr::mm, MS = Tr::ms;
   const int lane = threadIdx.x & 63;
@@ -1611,11 +1454,11 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
       double a[2 * 7], b[2 * 7];
 #pragma unroll
       for (int i = 0; i < Tr::kmin; ++i) {
-        const uint32_t k = s.samples[lane][i];
-        a[2 * i] = xy1[2 * k];
-        a[2 * i + 1] = xy1[2 * k + 1];
-        b[2 * i] = xy2[2 * k];
-        b[2 * i + 1] = xy2[2 * k + 1];
+        const float4 v = pts[s.samples[lane][i]];
+        a[2 * i] = (double)v.x;
+        a[2 * i + 1] = (double)v.y;
+        b[2 * i] = (double)v.z;
+        b[2 * i + 1] = (double)v.w;
       }
       double* mo = mbuf + lane * (MM * MS);
       int nm = 1;
@@ -1653,11 +1496,11 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
       for (int p = 0; p < PC; ++p) {
         const int i = base + p * 64 + lane;
         ok[p] = i < n;
-        const int ii = ok[p] ? i : 0;
-        pa0[p] = xy1[2 * ii];
-        pa1[p] = xy1[2 * ii + 1];
-        pb0[p] = xy2[2 * ii];
-        pb1[p] = xy2[2 * ii + 1];
+        const float4 v = pts[ok[p] ? i : 0];
+        pa0[p] = (double)v.x;
+        pa1[p] = (double)v.y;
+        pb0[p] = (double)v.z;
+        pb1[p] = (double)v.w;
       }
       for (int t = 0; t < B; ++t) {
         const int nmt = __builtin_amdgcn_readlane(nm, t);
@@ -1702,7 +1545,7 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
             pf.lap(PR_OTHER);
             pf.count(PR_N_CAND);
             double* rt = res[best_sel ^ 1];
-            residuals_gather<K, NW>(mk, xy1, xy2, n, maxr, rt, xin1, xin2, s.redi);
+            residuals_gather_f4<K, NW>(mk, pts, n, maxr, rt, xin, s.redi);
             pf.lap(PR_CAND);
             bool better = c > bn, exact = false;
             double sum = 0.0;
@@ -1727,14 +1570,14 @@ __device__ __attribute__((always_inline)) RansacResult loransac_wave(VerifyLds& 
                 for (int lt = 0; lt < 10; ++lt) {
                   pf.lap(PR_OTHER);
                   pf.count(PR_N_LO);
-                  const int ni = s.best_n;  // in xin1 / xin2 from the best's residual pass
+                  const int ni = s.best_n;  // in xin from the best's residual pass
                   pf.lap(PR_GATHER);
                   double lm[9];
-                  local_estimate_wave<K, NW>(s, xin1, xin2, ni, lm);
+                  local_estimate_wave<K, NW>(s, xin, ni, lm);
                   pf.lap(PR_LOEST);
                   const int prev = s.best_n;
                   double* rl = res[best_sel ^ 1];
-                  const int lc = residuals_gather<K, NW>(lm, xy1, xy2, n, maxr, rl, xin1, xin2, s.redi);
+                  const int lc = residuals_gather_f4<K, NW>(lm, pts, n, maxr, rl, xin, s.redi);
                   pf.lap(PR_LORES);
                   bool lbetter = lc > prev, lexact = false;
                   double lsum = 0.0;
@@ -1938,12 +1781,16 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
       const int ni = f_in;
       const double bratio = (double)nb / (double)ni;
       if (!(bratio < P.watermark_min_inlier_ratio)) {
-        // Inlier points in index order -> translation LO-RANSAC.  Scratch
-        // layout (10n doubles): tin1 [0,2ni) tin2 [2n,2n+2ni) tres0
-        // [4n,4n+ni) tres1 [5n,5n+ni) tx1 [6n,6n+2ni) tx2 [8n,8n+2ni).
+        // Inlier points in index order -> translation LO-RANSAC, on packed
+        // fp32 points (the doubles are widened float32 keypoints: exact both
+        // ways; half the bytes of every point loop).  Scratch layout (10n
+        // doubles; float4 arrays 16-B aligned): tin [0,2ni+1) tres0
+        // [2n+2,2n+2+ni) tres1 [3n+2,3n+2+ni) tx [4n+2,4n+3+2ni).
         double* base = ps.base;
-        double* tin1 = base;
-        double* tin2 = base + 2 * n;
+        auto align16 = [](double* p) {
+          return reinterpret_cast<float4*>((reinterpret_cast<uintptr_t>(p) + 15) & ~(uintptr_t)15);
+        };
+        float4* tin = align16(base);
         int w = 0;
         for (int r0 = 0; r0 < n; r0 += 64 * kSeqU * NW) {
           const int b0 = r0 + wv * 64 * kSeqU;
@@ -1984,10 +1831,7 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
             if (mk[u]) {
               const int o2 = o + (int)__builtin_amdgcn_mbcnt_hi(
                                      (uint32_t)(bal[u] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
-              tin1[2 * o2] = a0[u];
-              tin1[2 * o2 + 1] = a1[u];
-              tin2[2 * o2] = c0[u];
-              tin2[2 * o2 + 1] = c1[u];
+              tin[o2] = make_float4((float)a0[u], (float)a1[u], (float)c0[u], (float)c1[u]);
             }
             o += __popcll(bal[u]);
           }
@@ -1995,10 +1839,10 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
         }
         if (NW > 1) __syncthreads();
         mt_load(s, ps.state);
-        const RansacResult rt = loransac_wave<KIND_T, NW>(s, sidx, tin1, tin2, ni, P.max_trials_T, P,
-                                                      base + 4 * n, base + 5 * n, base + 6 * n,
-                                                      base + 8 * n, ps.snap, base + 10 * n, pf,
-                                                      scrib ? fsidx : nullptr);
+        const RansacResult rt = loransac_wave<KIND_T, NW>(s, sidx, tin, ni, P.max_trials_T, P,
+                                                      base + 2 * n + 2, base + 3 * n + 2,
+                                                      align16(base + 4 * n + 2), ps.snap,
+                                                      base + 10 * n, pf, scrib ? fsidx : nullptr);
         const double iratio = (double)rt.num_inliers / (double)ni;
         if (iratio >= P.watermark_min_inlier_ratio) {
           config = SCM_TVG_WATERMARK;
@@ -3579,6 +3423,8 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
 }
 
 }  // namespace
+
+int verify_small_batch_pairs() { return wave_pairs_limit(); }
 
 bool verify_small_batch(int npairs, int max_m) {
   return npairs <= wave_pairs_limit() && (max_m + 7) / 8 * 8 <= kWsMaxStride;
