@@ -75,6 +75,10 @@ def parse():
                         "measured equal or slower (DESIGN.md section 4)")
     p.add_argument("--no-isolated", dest="isolated", action="store_false",
                    help="skip the extra serialised step that measures isolated kernel rates")
+    p.add_argument("--gather", choices=("chunked", "step"), default="chunked",
+                   help="N > 1: gather each batch's rows inside the step as soon as they are "
+                        "serialised (scm_table_run_chunks; default), or each step's rows on a "
+                        "background thread while the next step computes")
     p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                    help="nccl = RCCL over xGMI, one GPU per rank (the measured path); gloo = a "
                         "rehearsal of the N > 1 sharding and gather with ranks sharing GPUs")
@@ -421,9 +425,18 @@ def main():
             ctx.add_keep_matches_range(r, r + 1)
     last = {}
 
+    chunked = world > 1 and args.gather == "chunked"
+
     def step():
-        # N > 1: the step's io.cc rows travel to rank 0 on the plan's gather
-        # thread while the next step computes (drained before the clock stops)
+        if chunked:
+            # N > 1: each batch's io.cc rows travel to rank 0 as soon as they are
+            # serialised, while the next batches compute; the step ends when
+            # rank 0 holds every rank's rows
+            plan.step_chunked(ctx, device=device)
+            return ctx.table_timings()
+        # N > 1 (--gather step): the step's io.cc rows travel to rank 0 on the
+        # plan's gather thread while the next step computes (drained before the
+        # clock stops)
         packed, _ = plan.step(ctx, device=device, background=world > 1, keep=False)
         last["packed"] = packed
         return ctx.table_timings()
@@ -463,6 +476,8 @@ def main():
     t_tail = time.perf_counter()
     plan.drain()  # the last steps' gathers: the exposed tail of the overlapped gather
     gather_tail_ms = (time.perf_counter() - t_tail) * 1e3
+    if chunked:  # per step: the rows still travelling once the compute is done
+        gather_tail_ms = float(np.mean(plan.tail_ms[-args.steps:])) if plan.tail_ms else 0.0
     if world > 1:
         dist.barrier()
     if torch.cuda.is_available():
@@ -643,9 +658,14 @@ def main():
             "stage_ms_per_step": {"match": round(match_ms / steps, 3),
                                   "finalize": round(final_ms / steps, 3),
                                   "verify": round(verify_ms / steps, 3)},
-            "gather": ({"how": ("each step's packed io.cc rows (offsets + bytes, two P2P messages per "
-                                "rank) gathered to rank 0 on a background thread while the next step "
-                                "computes; the last ones drained inside the timed region"),
+            "gather": ({"how": (("each batch's packed io.cc rows (a header + offsets + bytes, P2P "
+                                 "messages per chunk) sent to rank 0 from a background thread as soon "
+                                 "as the library serialises them (scm_table_run_chunks), inside the "
+                                 "step; tail_ms_rank0 = mean per step of the gather left after rank "
+                                 "0's compute") if chunked else
+                                ("each step's packed io.cc rows (offsets + bytes, two P2P messages per "
+                                 "rank) gathered to rank 0 on a background thread while the next step "
+                                 "computes; the last ones drained inside the timed region")),
                         "backend": args.dist_backend,
                         "avg_gather_ms": (round(float(np.mean(plan.gatherer.ms)), 2)
                                           if plan.gatherer and plan.gatherer.ms else None),

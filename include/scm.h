@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define SCM_ABI_VERSION 5
+#define SCM_ABI_VERSION 6
 
 enum {
   SCM_OK = 0,
@@ -240,6 +240,19 @@ typedef void (*scm_pass_fn)(void* user, int64_t pass, uint8_t* rows, size_t rows
                             const int64_t* row_offsets);
 int scm_table_run_passes(scm_context* ctx, int64_t overlap, int64_t row_begin,
                          int64_t row_end, int64_t passes, scm_pass_fn on_pass, void* user);
+/* Chunked form of scm_table_run_packed for the multi-GPU gather (SURVEY.md
+ * §8e: the row gather overlaps the tail of the compute): the rows of
+ * [row_begin, row_end) are handed over batch by batch, in row order, as soon
+ * as each batch is serialised -- on_chunk(user, first_row, num_rows, rows,
+ * rows_size, row_offsets) on the calling thread, with `rows` a packed buffer
+ * of num_rows rows the callee owns (scm_blob_free on {rows, rows_size}) and
+ * `row_offsets` its 2 * num_rows + 1 element offsets (valid during the call
+ * only).  The chunks' rows, concatenated, equal scm_table_run_packed's bytes.
+ * No chunk is handed over for an empty range. */
+typedef void (*scm_chunk_fn)(void* user, int64_t first_row, int64_t num_rows, uint8_t* rows,
+                             size_t rows_size, const int64_t* row_offsets);
+int scm_table_run_chunks(scm_context* ctx, int64_t overlap, int64_t row_begin,
+                         int64_t row_end, scm_chunk_fn on_chunk, void* user);
 /* Keep (keep != 0) the raw cross-checked matches of every pair of the
  * following table runs for scm_table_matches; off by default. */
 int scm_set_keep_matches(scm_context* ctx, int32_t keep);

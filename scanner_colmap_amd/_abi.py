@@ -35,7 +35,8 @@ EXPORTS = (
     "scm_verify_pair", "scm_execute_stencil", "scm_execute_batch", "scm_stencil_stats",
     "scm_stencil_spec_stats", "scm_stencil_cache_clear",
     "scm_table_load",
-    "scm_table_run", "scm_table_run_packed", "scm_table_run_passes", "scm_set_keep_matches",
+    "scm_table_run", "scm_table_run_packed", "scm_table_run_passes", "scm_table_run_chunks",
+    "scm_set_keep_matches",
     "scm_set_keep_matches_range", "scm_add_keep_matches_range",
     "scm_table_matches", "scm_table_timings", "scm_set_serial", "scm_extract_frames",
 )
@@ -124,6 +125,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
                                          POINTER(Blob), c_void_p]
     lib.scm_table_run_passes.argtypes = [c_void_p, c_int64, c_int64, c_int64, c_int64, PASS_FN,
                                          c_void_p]
+    lib.scm_table_run_chunks.argtypes = [c_void_p, c_int64, c_int64, c_int64, CHUNK_FN, c_void_p]
     lib.scm_set_keep_matches.argtypes = [c_void_p, c_int32]
     lib.scm_set_keep_matches_range.argtypes = [c_void_p, c_int64, c_int64]
     lib.scm_add_keep_matches_range.argtypes = [c_void_p, c_int64, c_int64]
@@ -204,6 +206,7 @@ def _elements(chunks) -> tuple:
 
 # scm_pass_fn (include/scm.h): (user, pass, rows, rows_size, row_offsets)
 PASS_FN = ctypes.CFUNCTYPE(None, c_void_p, c_int64, c_void_p, c_size_t, POINTER(c_int64))
+CHUNK_FN = ctypes.CFUNCTYPE(None, c_void_p, c_int64, c_int64, c_void_p, c_size_t, POINTER(c_int64))
 
 
 class _BlobOwner:
@@ -390,6 +393,28 @@ class Context:
         fn = PASS_FN(cb)
         _check(self._lib.scm_table_run_passes(self._ptr, overlap, row_begin, row_end, passes, fn,
                                               None))
+        if err:
+            raise err[0]
+
+    def table_run_chunks(self, overlap: int, row_begin: int, row_end: int, on_chunk) -> None:
+        """scm_table_run_chunks: the rows of [row_begin, row_end) handed over
+        batch by batch, in row order -- on_chunk(first_row, PackedRows) as
+        soon as each batch is serialised (the multi-GPU gather starts on them
+        while the next batches compute)."""
+        err = []
+
+        def cb(user, first, nrows, data, size, offs):
+            try:
+                b = Blob()
+                b.data = ctypes.cast(data, POINTER(c_uint8))
+                b.size = size
+                o = np.ctypeslib.as_array(offs, shape=(2 * nrows + 1,)).copy()
+                on_chunk(int(first), PackedRows(b, o))
+            except BaseException as e:  # noqa: BLE001 -- re-raised after the call
+                err.append(e)
+
+        fn = CHUNK_FN(cb)
+        _check(self._lib.scm_table_run_chunks(self._ptr, overlap, row_begin, row_end, fn, None))
         if err:
             raise err[0]
 

@@ -314,6 +314,7 @@ struct BatchSet {
   // odd-parity window buffers of small batches (speculative windows, launch_verify)
   DevBuf o_samp, o_nmod, o_fcon, o_mods, o_cnts, o_ucnt, o_wsnap, o_wb, o_wstate;
   DevBuf oh_samp, oh_nmod, oh_fcon, oh_mods, oh_cnts, oh_ucnt, oh_wsnap, oh_wb, oh_wstate;
+  DevBuf lo_slot[4], lo_data[4];  // small batches' parallel LO: (kind, parity) slots and their data
   hipStream_t rstream = nullptr;  // replay stream of speculative windows (another set's vstream)
   hipStream_t fstream = nullptr;  // early verify_final pass of small batches (the third set's)
   hipEvent_t wev[2 * kMaxVerifyWindows] = {};
@@ -344,7 +345,8 @@ struct BatchSet {
                       &h_mods, &h_wsnap, &ucnt, &h_ucnt, &wb, &wstate, &dtrial, &h_wb, &h_wstate,
                       &h_dtrial, &o_samp, &o_nmod, &o_fcon, &o_mods, &o_cnts, &o_ucnt, &o_wsnap,
                       &o_wb, &o_wstate, &oh_samp, &oh_nmod, &oh_fcon, &oh_mods, &oh_cnts, &oh_ucnt,
-                      &oh_wsnap, &oh_wb, &oh_wstate})
+                      &oh_wsnap, &oh_wb, &oh_wstate, &lo_slot[0], &lo_slot[1], &lo_slot[2],
+                      &lo_slot[3], &lo_data[0], &lo_data[1], &lo_data[2], &lo_data[3]})
       b->release();
     stage.release();
     vstage.release();
@@ -1227,7 +1229,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       SCM_TRY(rst.ensure(V * sizeof(RansacState)));
       SCM_TRY(window_bufs(samp, nmod, fcon, mods, cnts, ucnt, wsnap, wb, wstate, split, rb));
       SCM_TRY(act.ensure(3 * V * sizeof(int32_t)));
-      SCM_TRY(nact.ensure(3 * sizeof(int32_t)));
+      SCM_TRY(nact.ensure((3 + kMaxVerifyWindows) * sizeof(int32_t)));  // + shuffle cursors
       SCM_TRY(dtrial.ensure(V * sizeof(int32_t)));
       rb->rst = rst.as<RansacState>();
       for (int k = 0; k < 3; ++k) rb->act[k] = act.as<int32_t>() + k * V;
@@ -1257,6 +1259,24 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
                           bs.o_wsnap, bs.o_wb, bs.o_wstate, false, &rbf1));
       SCM_TRY(window_bufs(bs.oh_samp, bs.oh_nmod, bs.oh_fcon, bs.oh_mods, bs.oh_cnts, bs.oh_ucnt,
                           bs.oh_wsnap, bs.oh_wb, bs.oh_wstate, ctx->score_split, &rbh1));
+      // Parallel LO slots per kind and parity (rs_lo_chain2_kernel), when they
+      // fit 1 GiB each; otherwise the replay runs every LO chain itself.
+      const int64_t lo_stride = lo_slot_doubles(max_m);
+      const int64_t lo_bytes = V * kLoSlots * lo_stride * (int64_t)sizeof(double);
+      static const bool parallel_lo = [] {  // SCM_PARALLEL_LO=0 (diagnostics): LO inline
+        const char* e = getenv("SCM_PARALLEL_LO");
+        return !(e && e[0] == '0');
+      }();
+      if (parallel_lo && lo_bytes <= (int64_t(1) << 30)) {
+        VerifyRoundBufs* lrb[4] = {&rbf, &rbf1, &rbh, &rbh1};
+        for (int i = 0; i < 4; ++i) {
+          SCM_TRY(bs.lo_slot[i].ensure(V * kLoSlots * sizeof(LoSlot)));
+          SCM_TRY(bs.lo_data[i].ensure(lo_bytes));
+          lrb[i]->lo = bs.lo_slot[i].as<LoSlot>();
+          lrb[i]->lo_data = bs.lo_data[i].as<double>();
+          lrb[i]->lo_stride = lo_stride;
+        }
+      }
       // The replay stream and the early-final stream are the other two batch
       // sets' verification streams: a process has few hardware queues
       // (GPU_MAX_HW_QUEUES, 4 by default) and streams beyond them share one,
@@ -1660,6 +1680,10 @@ void row_pairs(const std::vector<uint32_t>& stencil_ids, std::vector<int64_t>* s
 // matcher's row / column partials and match slots (enqueue_match), and the
 // verifier's points, scratch, window buffers and compaction output with every
 // pivot keypoint matched (enqueue_verify).
+// Round-buffer bytes per trial and kind: samples, model count, filter
+// constants, models, counts (+ split counts).
+constexpr int64_t kRoundTrialBytes = 8 * 4 + 4 + 3 * 12 * 4 + 3 * 9 * 8 + 2 * 3 * 4;
+
 int64_t pair_workspace_bytes(int64_t n1, int64_t n2) {
   const int32_t rpb = kRowsPerBlock8 < kRowsPerBlock ? kRowsPerBlock8 : kRowsPerBlock;
   const int64_t nseg = (n2 + kColsPerSeg - 1) / kColsPerSeg;
@@ -1671,9 +1695,19 @@ int64_t pair_workspace_bytes(int64_t n1, int64_t n2) {
   const int64_t verify_pts = slots * (16 + 16 + 16 + 8 + 1);  // xy1, xy2, xyf, dpack, dpmask
   const int64_t verify_pair = verify_scratch_doubles(slots) * 8 + kVerifySnapWords * 4 +
                               (int64_t)sizeof(RansacState) + (int64_t)sizeof(VerifyOut) +
-                              2 * ((int64_t)kWindowTrials * (8 * 4 + 4 + 3 * 12 * 4 + 3 * 9 * 8 + 2 * 3 * 4) +
-                                   640 * 4) + 256;  // F and H round buffers
+                              2 * ((int64_t)kWindowTrials * kRoundTrialBytes + 640 * 4) +
+                              256;  // F and H round buffers
   return match + verify_pts + verify_pair;
+}
+
+// Bytes per pair beyond pair_workspace_bytes' when a batch takes the
+// small-batch kernels (enqueue_verify): windows of kWindowTrialsSmall trials
+// in two parities, F and H, and the parallel-LO slots of both kinds and
+// parities (at most, for a pivot of n1 keypoints).
+int64_t small_batch_extra_bytes(int64_t n1) {
+  return 2 * (2 * (int64_t)kWindowTrialsSmall - (int64_t)kWindowTrials) * kRoundTrialBytes +
+         2 * 640 * 4 +
+         4 * (int64_t)kLoSlots * (lo_slot_doubles(std::max<int64_t>(n1, 1)) * 8 + (int64_t)sizeof(LoSlot));
 }
 
 // Byte budget of one of the three batch sets: SCM_BATCH_BYTES, or a third of
@@ -1713,6 +1747,9 @@ struct RowPlan {
 // [k * pass_rows, (k + 1) * pass_rows); `emit` receives each pass's packed rows
 // (final row offset included) as soon as they are serialised, in order.
 using PassEmit = std::function<int(int64_t, Packed&)>;
+// Chunked runs (out == nullptr, pass_rows == 0): `emit` receives each batch's
+// rows as its own packed output (first plan row index, then the rows), in row
+// order, as soon as they are serialised.
 
 int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& plan,
              int64_t keep_row0, Packed* out, int64_t pass_rows = 0,
@@ -1721,7 +1758,7 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
 // Runs the sequential stencil over table rows [row_begin, row_end) through
 // the pipelined batch machinery into one packed output.
 int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
-              Packed* out) {
+              Packed* out, const PassEmit* chunk_emit = nullptr) {
   const ImageTable& t = ctx->table;
   std::vector<uint32_t> ids(overlap);
   std::vector<int64_t> rows(overlap), sel;
@@ -1741,7 +1778,7 @@ int run_table(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_
       rp.nb_ids.push_back(ids[s]);
     }
   }
-  return run_rows(ctx, t, plan, row_begin, out);
+  return run_rows(ctx, t, plan, row_begin, out, 0, chunk_emit);
 }
 
 int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& plan,
@@ -1766,22 +1803,38 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
   // Measured on the bench workload: equal-size batches, short first / last
   // batches, and caps of 4,096-9,472 pairs were all slower than 8,192.
   const int64_t budget = set_budget_bytes(ctx);
+  // SCM_BATCH_SMALL_FIRST=1 (measurement): the remainder batch first instead
+  // of last (row order is kept: the first batch is the short one).
+  int64_t first_cap = ctx->batch_pairs;
+  if (const char* e = std::getenv("SCM_BATCH_SMALL_FIRST"); e && e[0] == '1') {
+    int64_t tp = 0;
+    for (const RowPlan& rp : plan) tp += (int64_t)rp.nb.size();
+    if (tp % ctx->batch_pairs) first_cap = tp % ctx->batch_pairs;
+  }
   Batch cur;
-  int64_t cur_bytes = 0;
+  int64_t cur_bytes = 0, cur_small = 0;
   for (int64_t i = 0; i < nr; ++i) {
     const RowPlan& rp = plan[i];
     const int64_t np = (int64_t)rp.nb.size();
     int64_t row_bytes = 0;
     for (int32_t b : rp.nb) row_bytes += pair_workspace_bytes(t.ndesc[rp.pivot], t.ndesc[b]);
     const int64_t have = (int64_t)cur.specs.size();
-    if (have > 0 && (have + np > ctx->batch_pairs || cur_bytes + row_bytes > budget)) {
+    const int64_t cap = batches.empty() ? first_cap : ctx->batch_pairs;
+    // a batch small enough for the small-batch kernels holds their larger
+    // round buffers and parallel-LO slots (enqueue_verify)
+    const int64_t row_small = np * small_batch_extra_bytes(t.ndesc[rp.pivot]);
+    const int64_t small_extra =
+        have + np <= verify_small_batch_pairs() ? cur_small + row_small : 0;
+    if (have > 0 && (have + np > cap || cur_bytes + row_bytes + small_extra > budget)) {
       cur.pairs_begin.push_back(have);
       batches.push_back(std::move(cur));
       cur = Batch();
       cur.row0 = i;
       cur_bytes = 0;
+      cur_small = 0;
     }
     cur_bytes += row_bytes;
+    cur_small += row_small;
     cur.pairs_begin.push_back((int64_t)cur.specs.size());
     for (size_t k = 0; k < rp.nb.size(); ++k) {
       cur.specs.push_back({rp.pivot, rp.nb[k]});
@@ -1801,8 +1854,18 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
   // rows are serialised into the pass they belong to.
   const int64_t npass = streamed ? nr / pass_rows : 0;
   std::vector<Packed> packs(npass);
+  // Passes not handed over when a run fails return their buffers (the
+  // hand-over takes the data of the ones it emits).
+  struct PacksGuard {
+    std::vector<Packed>& v;
+    ~PacksGuard() {
+      for (Packed& p : v)
+        if (p.data && !pool_give(p.data)) std::free(p.data);
+    }
+  } packs_guard{packs};
   std::vector<int64_t> rows_done(npass, 0);
   int64_t next_emit = 0;
+  const bool chunked = !streamed && !out && emit;
   auto finish = [&](const Batch& b, BatchSet& bs) -> int {
     BatchView v;
     SCM_TRY(collect_batch(ctx, bs, &v));
@@ -1824,6 +1887,16 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
       return ctx->opts.multiple_models ? serialize_rows_tvg(tv, b.pair_ids, pb, o)
                                        : serialize_rows(ctx, v, b.pair_ids, pb, o);
     };
+    if (chunked) {
+      Packed pk;
+      int rc = ser(b.pairs_begin, &pk);
+      if (rc == SCM_OK) {
+        pk.row_off.push_back((int64_t)pk.size);
+        rc = (*emit)(b.row0, pk);  // takes pk.data unless it fails
+      }
+      if (pk.data && !pool_give(pk.data)) std::free(pk.data);
+      return rc;
+    }
     if (!streamed) return ser(b.pairs_begin, out);
     for (int64_t r0 = 0; r0 < nrows;) {
       const int64_t pass = (b.row0 + r0) / pass_rows;
@@ -1841,7 +1914,7 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
     }
     return SCM_OK;
   };
-  if (!streamed) out->row_off.reserve(2 * nr + 1);
+  if (!streamed && !chunked) out->row_off.reserve(2 * nr + 1);
   // Three buffer sets: at step k the GPU holds match(k) on the matching
   // stream and verify(k-1) (+ verify(k-2)) on the verification stream while
   // the host serialises batch k-3.
@@ -1863,7 +1936,7 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
     if (B >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(B - 1) % 3], true));
   }
   for (size_t k = B >= 3 ? B - 3 : 0; k < B; ++k) SCM_TRY(finish(batches[k], ctx->sets[k % 3]));
-  if (!streamed) out->row_off.push_back((int64_t)out->size);
+  if (!streamed && !chunked) out->row_off.push_back((int64_t)out->size);
   return SCM_OK;
 }
 
@@ -2337,7 +2410,7 @@ int scm_table_load(scm_context* ctx, int64_t num_rows, const scm_element* image_
 }
 
 static int table_run_common(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
-                            Packed* pk) {
+                            Packed* pk, const PassEmit* chunk_emit = nullptr) {
   if (!ctx->table_loaded) {
     set_error("scm_table_run before scm_table_load");
     return SCM_E_STATE;
@@ -2351,7 +2424,7 @@ static int table_run_common(scm_context* ctx, int64_t overlap, int64_t row_begin
   ctx->evals_f = ctx->evals_h = 0;
   ctx->n_match_launches = 0;
   const auto w0 = std::chrono::steady_clock::now();
-  const int rc = run_table(ctx, overlap, row_begin, row_end, pk);
+  const int rc = run_table(ctx, overlap, row_begin, row_end, pk, chunk_emit);
   if (rc != SCM_OK) drain(ctx);
   ctx->t_wall =
       std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
@@ -2393,6 +2466,27 @@ int scm_table_run(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t 
   }
   if (!pool_give(pk.data)) std::free(pk.data);
   return SCM_OK;
+}
+
+int scm_table_run_chunks(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,
+                         scm_chunk_fn on_chunk, void* user) {
+  if (!ctx || !on_chunk) {
+    set_error("invalid arguments");
+    return SCM_E_INVALID;
+  }
+  const PassEmit emit = [&](int64_t row0, Packed& pk) -> int {
+    const int64_t nrows = ((int64_t)pk.row_off.size() - 1) / 2;
+    scm_blob b{pk.data ? pk.data : (uint8_t*)std::malloc(1), pk.size};
+    if (!b.data) {
+      set_error("malloc failed");
+      return SCM_E_NOMEM;
+    }
+    pk.data = nullptr;
+    pk.size = pk.cap = 0;
+    on_chunk(user, row_begin + row0, nrows, b.data, b.size, pk.row_off.data());
+    return SCM_OK;
+  };
+  return table_run_common(ctx, overlap, row_begin, row_end, nullptr, &emit);
 }
 
 int scm_table_run_passes(scm_context* ctx, int64_t overlap, int64_t row_begin, int64_t row_end,

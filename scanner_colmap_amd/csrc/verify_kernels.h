@@ -98,6 +98,24 @@ constexpr int kWindowTrialsSmall = kMaxWindowSmall * kTrialBatch;
 // solves and scores of window r + 1 can run while window r is replayed
 // (speculative windows, run_windows); rst, dtrial and the active lists are
 // shared by both parities.  Large batches alias both parities.
+// Parallel local optimisation of a small batch's window (rs_lo_chain2_kernel,
+// DESIGN §10): the LO chain of each of a pair's first kLoSlots record models
+// (counts reaching the running maximum of the window's counts before them,
+// from the pair's best at the window start), computed on its own before the
+// replay, which then takes a record's outcome instead of running its LO.
+constexpr int kLoSlots = 8;
+struct LoSlot {
+  int32_t rec;        // record index (trial of the window x models per trial + model), -1: none
+  int32_t count;      // the chain's final inlier count
+  int32_t sum_valid;  // sum is the final model's exact index-order residual sum
+  int32_t buf;        // slot buffer holding the final model's residuals (0: the record's own)
+  double sum;
+  double model[9];
+};
+// A slot's data: three residual buffers of n doubles and the inlier gather
+// buffer (n float4, 16-B aligned) -- lo_stride doubles per slot.
+inline int64_t lo_slot_doubles(int64_t max_m) { return 5 * max_m + 4; }
+
 struct VerifyRoundBufs {
   RansacState* rst;
   uint32_t* samp;
@@ -114,9 +132,13 @@ struct VerifyRoundBufs {
   const int32_t* pwB;     //   by speculative draws to skip pairs certain to stop)
   int32_t* dtrial;   // trials drawn so far
   int32_t* act[3];   // active-pair lists (rotating: window r's replay reads r % 3)
-  int32_t* nact;     // their lengths [3]
+  int32_t* nact;     // their lengths [3], then a work cursor per window of the table
+                     // path's packed Shuffle (rs_shufflepack2_kernel) [kMaxVerifyWindows]
   int wt;            // trials per pair the window buffers hold (T: kWindowTrials or
                      // kWindowTrialsSmall); the windows' rounds are at most wt / kTrialBatch
+  LoSlot* lo = nullptr;       // small batches: [V][kLoSlots] outcomes (nullptr: LO inline)
+  double* lo_data = nullptr;  // [V][kLoSlots][lo_stride]
+  int64_t lo_stride = 0;
 };
 constexpr int kVerifyStateWords = 640;
 
@@ -156,6 +178,8 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
 // four-wave replay, speculative windows) for a batch of npairs pairs with at
 // most max_m matches.
 bool verify_small_batch(int npairs, int max_m);
+// The pair count at or below which a batch may take the small-batch kernels.
+int verify_small_batch_pairs();
 size_t verify_lds_bytes(int max_m);
 constexpr int kVerifyProfSlots = 90;
 

@@ -2142,6 +2142,79 @@ __device__ __attribute__((always_inline)) void rs_shuffle_body(
     }
 }
 
+// The table path's Shuffle with the pairs' index vectors packed into LDS by
+// their own sizes.  rs_shuffle_body gives every pair of a launch the stride
+// of the batch's largest pair, so with pairs of a few thousand matches one
+// pair fills a block's LDS and a CU holds ~10 swap chains; here each block
+// takes the active list's next pairs from a work cursor while their vectors
+// fit its kShPackLdsBytes (a grabbed pair that does not fit opens the block's
+// next round), so a CU holds as many chains as its LDS has vectors of the
+// actual sizes.  Same shuffle_chain per pair: the same samples and vectors.
+constexpr int kShPackLdsBytes = 32 * 1024;
+constexpr int kShPackPairs = 64;  // pairs per round at most (one lane each)
+constexpr int kShPackStaticLds = 1024;  // >= its static LDS (3 x kShPackPairs + 1 int32)
+static_assert((3 * kShPackPairs + 1) * 4 <= kShPackStaticLds, "packed Shuffle static LDS");
+
+template <int K>
+__device__ __attribute__((always_inline)) void rs_shufflepack_body(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
+    const int32_t* __restrict__ wB, const int32_t* __restrict__ act,
+    const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, int32_t* __restrict__ cursor,
+    int cap, int WT) {
+  constexpr int KM = KindTraits<K>::kmin;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  uint16_t* V = reinterpret_cast<uint16_t*>(dyn_lds);  // cap entries
+  __shared__ int32_t s_q[kShPackPairs], s_off[kShPackPairs], s_n[kShPackPairs];
+  __shared__ int32_t s_np;
+  const int na = *nact;
+  int carry = -1;  // thread 0: an active-list index grabbed but not yet placed
+  for (;;) {
+    if (threadIdx.x == 0) {
+      int used = 0, k = 0;
+      for (;;) {
+        const int a = carry >= 0 ? carry : atomicAdd(cursor, 1);
+        carry = -1;
+        if (a >= na) break;
+        const int q = act[a];
+        const int n = pairs[q].m;
+        if (n <= 0 || wB[q] <= 0) continue;  // no trials: nothing to shuffle
+        const int need = (n + 7) & ~7;
+        if (k == kShPackPairs || used + need > cap) {
+          carry = a;
+          break;
+        }
+        s_q[k] = q;
+        s_off[k] = used;
+        s_n[k] = n;
+        used += need;
+        ++k;
+      }
+      s_np = k;
+    }
+    __syncthreads();
+    const int np = s_np;
+    if (np == 0) break;  // the cursor is past the list and nothing is carried
+    for (int l = 0; l < np; ++l) {
+      const uint32_t* g = pair_sidx(pair_at<K>(pairs, s_q[l], scratch, snaps, out));
+      const int n = s_n[l], o = s_off[l];
+      for (int i = threadIdx.x; i < n; i += blockDim.x) V[o + i] = (uint16_t)g[i];
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < np) {
+      const int q = s_q[threadIdx.x];
+      shuffle_chain<KM>(V + s_off[threadIdx.x], samp + (int64_t)q * WT * 8, wB[q]);
+    }
+    __syncthreads();
+    for (int l = 0; l < np; ++l) {
+      uint32_t* g = pair_sidx(pair_at<K>(pairs, s_q[l], scratch, snaps, out));
+      const int n = s_n[l], o = s_off[l];
+      for (int i = threadIdx.x; i < n; i += blockDim.x) g[i] = V[o + i];
+    }
+    __syncthreads();
+  }
+}
+
 // The same window's Shuffle with a whole wave per pair, for small batches
 // (one Scanner stencil: a lane per pair leaves nearly every lane, and the
 // GPU, idle while one pair's chain of kmin dependent LDS round trips per
@@ -2450,6 +2523,19 @@ __global__ __launch_bounds__(64) void rs_shuffle_wave2_kernel(
   else
     rs_shuffle_wave_body<KIND_H>(pairs, scratch, snaps, out, rh.wB, rh.act[ain], rh.nact + ain,
                                  rh.samp, prof, rh.wt, stride, blockIdx.x - split, gridDim.x - split);
+}
+
+// Both kinds: blocks [0, split) the F vectors, the rest H's; cursors cf / ch.
+__global__ __launch_bounds__(64) void rs_shufflepack2_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
+    VerifyRoundBufs rh, int ain, int win, int cap, int split) {
+  if ((int)blockIdx.x < split)
+    rs_shufflepack_body<KIND_F>(pairs, scratch, snaps, out, rf.wB, rf.act[ain], rf.nact + ain,
+                                rf.samp, rf.nact + 3 + win, cap, rf.wt);
+  else
+    rs_shufflepack_body<KIND_H>(pairs, scratch, snaps, out, rh.wB, rh.act[ain], rh.nact + ain,
+                                rh.samp, rh.nact + 3 + win, cap, rh.wt);
 }
 
 // Draws and Shuffle of a window in one launch (small batches).
@@ -2860,6 +2946,153 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
   }
 }
 
+// Parallel local optimisation (small batches; DRAFT, not yet run on a GPU):
+// block (a, slot) takes active pair a's slot-th record model of the window --
+// a model whose count reaches the running maximum of the counts before it,
+// starting from the pair's best at the window start (rst.best_n; a stale,
+// lower value only adds records) -- and runs the LO chain the replay would
+// run if the model became the best: its residual pass (with the inlier
+// gather), then the LO steps with their compares, all against the chain's own
+// models, so the outcome depends on the record alone.  Only records can be
+// candidates (the best after trial s is at least every count up to s), so
+// the replay takes these outcomes instead of running the chains one after
+// another (host model: tests/test_parallel_lo_model.py).  The record's own
+// residuals stay in slot buffer 0 (a tie compare at acceptance needs them);
+// the chain alternates buffers 1 and 2.
+template <int K>
+__device__ __attribute__((always_inline)) void rs_lo_chain_body(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, const VerifyRoundBufs& rb, int ain,
+    const VerifyParams& P, const float4* __restrict__ xyf_all, int bid) {
+  constexpr int NW = 4;
+  using Tr = KindTraits<K>;
+  constexpr int MM = Tr::mm, MS = Tr::ms;
+  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
+  VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
+  const int a = bid / kLoSlots, slot = bid % kLoSlots;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const bool t0th = threadIdx.x == 0;
+  if (a >= rb.nact[ain]) return;
+  const int q = rb.act[ain][a];
+  const int WT = rb.wt;
+  LoSlot* sl = rb.lo + (int64_t)q * kLoSlots + slot;
+  const int B = rb.wB[q];
+  // Records in order, found by wave 0 (prefix maxima over chunks of 64
+  // entries); the slot-th one's index goes to s.redi[8], -1 if none.
+  if (wv == 0) {
+    int run = *reinterpret_cast<volatile const int32_t*>(&rb.rst[q].best_n);
+    int found = 0, rec = -1;
+    const int ne = B * MM;
+    for (int e0 = 0; e0 < ne && rec < 0; e0 += 64) {
+      const int e = e0 + lane;
+      int v = -1;
+      if (e < ne) {
+        const int t = e / MM, k = e - t * MM;
+        const int nm = K == KIND_F ? rb.nmod[(int64_t)q * WT + t] : 1;
+        if (k < nm) v = (int)rb.cnts[(int64_t)q * WT * 3 + e];
+      }
+      // exclusive prefix maximum of v over the chunk, on top of run
+      int incl = v;
+#pragma unroll
+      for (int d = 1; d < 64; d <<= 1) {
+        const int o = __shfl_up(incl, d);
+        if (lane >= d) incl = max(incl, o);
+      }
+      int excl = __shfl_up(incl, 1);
+      if (lane == 0) excl = -1;
+      const bool isrec = v >= 0 && v >= max(run, excl);
+      const uint64_t bal = __ballot(isrec);
+      const int nb = __popcll(bal);
+      if (found + nb > slot) {  // the slot-th record is in this chunk
+        uint64_t b = bal;
+        for (int i = 0; i < slot - found; ++i) b &= b - 1;
+        rec = e0 + (int)__builtin_ctzll(b);
+      }
+      found += nb;
+      run = max(run, __shfl(incl, 63));
+    }
+    if (lane == 0) s.redi[8] = rec;
+  }
+  __syncthreads();
+  const int e = s.redi[8];
+  __syncthreads();
+  if (e < 0) {
+    if (t0th) sl->rec = -1;
+    return;
+  }
+  const PairSetup ps = pair_at<K>(pairs, q, scratch, snaps, out);
+  const int n = ps.n;
+  const double maxr = P.max_residual;
+  const float4* xyf = xyf_all + ps.pp.pts_off / 2;
+  double* data = rb.lo_data + ((int64_t)q * kLoSlots + slot) * rb.lo_stride;
+  double* buf[3] = {data, data + n, data + 2 * n};
+  float4* xin = reinterpret_cast<float4*>((reinterpret_cast<uintptr_t>(data + 3 * n) + 15) &
+                                          ~(uintptr_t)15);
+  double mk[MS];
+  const double* src = rb.mods + ((int64_t)q * WT * 3 + e) * MS;
+#pragma unroll
+  for (int j = 0; j < MS; ++j) mk[j] = src[j];
+  // the record's count as the scoring counted it (the replay starts LO from it)
+  const int c = (int)rb.cnts[(int64_t)q * WT * 3 + e];
+  residuals_gather_f4<K, NW>(mk, xyf, n, maxr, buf[0], xin, s.redi);
+  if (t0th) {
+#pragma unroll
+    for (int j = 0; j < MS; ++j) s.best_model[j] = mk[j];
+    s.best_n = c;
+    s.best_sum = 0.0;
+    s.best_sum_valid = 0;
+  }
+  __syncthreads();
+  int bi = 0;  // buffer of the chain's best
+  if (c > Tr::kmin && c >= Tr::kmin_local) {
+    for (int lt = 0; lt < 10; ++lt) {
+      const int ni = s.best_n;  // in xin from the best's residual pass
+      double lm[9];
+      local_estimate_f4<K, NW>(s, xin, ni, lm);
+      const int prev = s.best_n;
+      const int li = bi == 1 ? 2 : 1;
+      const int lcn = residuals_gather_f4<K, NW>(lm, xyf, n, maxr, buf[li], xin, s.redi);
+      bool lbetter = lcn > prev, lexact = false;
+      double lsum = 0.0;
+      if (lcn == prev)
+        lbetter = tie_better<NW>(s, buf[li], buf[bi], n, lcn, maxr, &lsum, &lexact);
+      if (lbetter) {
+        __syncthreads();
+        if (t0th) {
+#pragma unroll
+          for (int j = 0; j < MS; ++j) s.best_model[j] = lm[j];
+          s.best_n = lcn;
+          s.best_sum = lsum;
+          s.best_sum_valid = lexact ? 1 : 0;
+        }
+        bi = li;
+      }
+      __syncthreads();
+      if (s.best_n <= prev) break;
+    }
+  }
+  if (t0th) {
+    sl->rec = e;
+    sl->count = s.best_n;
+    sl->sum = s.best_sum;
+    sl->sum_valid = s.best_sum_valid;
+    sl->buf = bi;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) sl->model[j] = j < MS ? s.best_model[j] : 0.0;
+  }
+}
+
+// Both kinds in one launch: blocks [0, split) the F records, the rest H's.
+__global__ __launch_bounds__(256) void rs_lo_chain2_kernel(
+    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
+    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
+    VerifyRoundBufs rh, int ain, VerifyParams P, const float4* __restrict__ xyf_all, int split) {
+  if ((int)blockIdx.x < split)
+    rs_lo_chain_body<KIND_F>(pairs, scratch, snaps, out, rf, ain, P, xyf_all, blockIdx.x);
+  else
+    rs_lo_chain_body<KIND_H>(pairs, scratch, snaps, out, rh, ain, P, xyf_all, blockIdx.x - split);
+}
+
 // The sequential part of one window, in trial order, for every active pair.
 // NW waves per pair (4: small batches, see rs_replay2w_kernel): every wave
 // runs the same decisions from the shared LDS state; thread 0 writes it.
@@ -2873,7 +3106,9 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
     const uint32_t* __restrict__ cnts, const double* __restrict__ mods,
     const uint32_t* __restrict__ wsnap, const int32_t* __restrict__ wB,
     const uint32_t* __restrict__ wstate, VerifyParams P, uint64_t* __restrict__ prof,
-    const float4* __restrict__ xyf_all, int bid, int nblk, int WT) {
+    const float4* __restrict__ xyf_all, int bid, int nblk, int WT,
+    const LoSlot* __restrict__ lo = nullptr, double* __restrict__ lo_data = nullptr,
+    int64_t lo_stride = 0) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   using Tr = KindTraits<K>;
@@ -2909,13 +3144,67 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
       s.best_sum_valid = st.best_sum_valid;
     }
     int best_sel = st.res_sel;
+    // The best's residuals: res[0] / res[1], or a slot buffer of the parallel
+    // LO (rs_lo_chain2_kernel) after a record's outcome is taken.
+    double* rbest = res[best_sel];
+    const LoSlot* slots = lo ? lo + (int64_t)q * kLoSlots : nullptr;
+    int si = 0;  // next slot (records in window order)
     int dyn_max = st.dyn_max;
     const int trial = st.trial;
     const int Btot = wB[q];
     bool abort = false;
     int abort_trial = -1;
     int64_t evals = st.evals;
-    for (int r0 = 0; r0 < Btot && !abort; r0 += kTrialBatch) {
+    // Leading rounds with neither a candidate nor the abort trial are skipped
+    // in one scan with several rounds' loads in flight (the round loop below
+    // pays a load latency and two barriers per round: a window of 32 rounds
+    // in which a pair's best is no longer reached was 32 of them).  Until the
+    // first candidate the best and dyn_max keep their entry values, so a
+    // candidate is a count >= the entry best and the abort trial is the first
+    // trial >= max(dyn_max, min_num_trials); the scan finds the earliest of
+    // them, and the loop starts at its round -- the trials before it pass
+    // exactly as the loop would pass them (their models counted in evals).
+    int rstart = 0;
+    {
+      const int bn0 = st.best_n;
+      const int lim = min(Btot, max(0, max(dyn_max, P.min_num_trials) - trial));
+      const int32_t* nm_q = nmod + (int64_t)q * WT;
+      const uint32_t* c_q = cnts + (int64_t)q * WT * 3;
+      int first = lim;
+      constexpr int U = 4;
+      for (int b0 = 0; b0 < lim; b0 += 64 * U) {
+        int nmv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int t = b0 + 64 * u + lane;
+          nmv[u] = t < lim ? nm_q[t] : 0;
+        }
+        uint32_t cv[U][MM];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int k = 0; k < MM; ++k)
+            cv[u][k] = k < nmv[u] ? c_q[(b0 + 64 * u + lane) * MM + k] : 0u;
+        int hit = -1;
+#pragma unroll
+        for (int u = U - 1; u >= 0; --u) {
+          bool cand = false;
+#pragma unroll
+          for (int k = 0; k < MM; ++k) cand |= k < nmv[u] && (int)cv[u][k] >= bn0;
+          const uint64_t bal = __ballot(cand);
+          if (bal) hit = b0 + 64 * u + (int)__builtin_ctzll(bal);
+        }
+        if (hit >= 0) {
+          first = min(first, hit);
+          break;
+        }
+      }
+      rstart = first / kTrialBatch * kTrialBatch;
+      int ns = 0;
+      for (int t = lane; t < rstart; t += 64) ns += nm_q[t];
+      evals += (int64_t)wave_sum_i(ns) * n;
+    }
+    for (int r0 = rstart; r0 < Btot && !abort; r0 += kTrialBatch) {
       const int B = min(kTrialBatch, Btot - r0);
       wsync();
       for (int i = threadIdx.x; i < B; i += 64 * NW) s.nmodels[i] = nmod[(int64_t)q * WT + r0 + i];
@@ -2952,11 +3241,45 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
             const int bn = s.best_n;
             if (c >= bn) {
               uint64_t t0 = pc ? __builtin_amdgcn_s_memtime() : 0;
+              const int e = (r0 + t) * MM + k;
+              const LoSlot* sl = nullptr;
+              if (slots) {
+                while (si < kLoSlots && slots[si].rec >= 0 && slots[si].rec < e) ++si;
+                if (si < kLoSlots && slots[si].rec == e) sl = slots + si;
+              }
+              if (sl) {
+                // A record with its LO chain already run: the acceptance
+                // compare here, the chain's outcome if accepted.
+                double* sd = lo_data + ((int64_t)q * kLoSlots + si) * lo_stride;
+                bool better = c > bn, exact = false;
+                double sum = 0.0;
+                if (!better) better = tie_better<NW>(s, sd, rbest, n, c, maxr, &sum, &exact);
+                if (pc && t0th) {
+                  pc[1] += 1;
+                  if (c == bn) pc[2] += 1;
+                  if (better) pc[3] += 1;
+                }
+                if (better) {
+                  wsync();
+                  if (t0th) {
+#pragma unroll
+                    for (int j = 0; j < MS; ++j) s.best_model[j] = sl->model[j];
+                    s.best_n = sl->count;
+                    s.best_sum = sl->sum;
+                    s.best_sum_valid = sl->sum_valid;
+                  }
+                  rbest = sd + (int64_t)sl->buf * n;
+                  wsync();
+                  dyn_max = (int)min((uint64_t)0x7FFFFFFF,
+                                     num_trials((uint64_t)s.best_n, (uint64_t)n, P.confidence,
+                                                P.dyn_num_trials_multiplier, Tr::kmin));
+                }
+              } else {
               double mk[MS];
-              const double* src = mq + ((r0 + t) * MM + k) * MS;
+              const double* src = mq + e * MS;
 #pragma unroll
               for (int j = 0; j < MS; ++j) mk[j] = src[j];
-              double* rt = res[best_sel ^ 1];
+              double* rt = rbest == res[0] ? res[1] : res[0];
               residuals_gather_f4<K, NW>(mk, xyf, n, maxr, rt, xin, s.redi);
               bool better = c > bn, exact = false;
               double sum = 0.0;
@@ -2967,7 +3290,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                 t0 = t1;
               }
               if (!better) {  // tie on the inlier count: Compare the residual sums
-                better = tie_better<NW>(s, rt, res[best_sel], n, c, maxr, &sum, &exact);
+                better = tie_better<NW>(s, rt, rbest, n, c, maxr, &sum, &exact);
                 if (pc && t0th) {
                   pc[2] += 1;
                   pc[6] += __builtin_amdgcn_s_memtime() - t0;
@@ -2984,7 +3307,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                   s.best_sum = sum;
                   s.best_sum_valid = exact ? 1 : 0;
                 }
-                best_sel ^= 1;
+                rbest = rt;
                 wsync();
                 // Recursive local optimisation.
                 if (c > Tr::kmin && c >= Tr::kmin_local) {
@@ -2993,18 +3316,18 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                     uint64_t* pl = pc ? pc + 20 : nullptr;
                     uint64_t tl0 = pl ? __builtin_amdgcn_s_memtime() : 0;
                     const int ni = s.best_n;  // in xin from the best's residual pass
-                    if (pl && t0th) { const uint64_t t = __builtin_amdgcn_s_memtime(); pl[0] += t - tl0; tl0 = t; pl[5] += ni; }
+                    if (pl && t0th) { const uint64_t tq = __builtin_amdgcn_s_memtime(); pl[0] += tq - tl0; tl0 = tq; pl[5] += ni; }
                     double lm[9];
                     local_estimate_f4<K, NW>(s, xin, ni, lm, pl);
                     if (pl && t0th) tl0 = __builtin_amdgcn_s_memtime();
                     const int prev = s.best_n;
-                    double* rl = res[best_sel ^ 1];
+                    double* rl = rbest == res[0] ? res[1] : res[0];
                     const int lcn = residuals_gather_f4<K, NW>(lm, xyf, n, maxr, rl, xin, s.redi);
                     if (pl && t0th) pl[4] += __builtin_amdgcn_s_memtime() - tl0;
                     bool lbetter = lcn > prev, lexact = false;
                     double lsum = 0.0;
                     if (lcn == prev)
-                      lbetter = tie_better<NW>(s, rl, res[best_sel], n, lcn, maxr, &lsum, &lexact);
+                      lbetter = tie_better<NW>(s, rl, rbest, n, lcn, maxr, &lsum, &lexact);
                     if (lbetter) {
                       wsync();
                       if (t0th) {
@@ -3014,7 +3337,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                         s.best_sum = lsum;
                         s.best_sum_valid = lexact ? 1 : 0;
                       }
-                      best_sel ^= 1;
+                      rbest = rl;
                     }
                     wsync();
                     if (s.best_n <= prev) break;
@@ -3025,6 +3348,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
                                               P.dyn_num_trials_multiplier, Tr::kmin));
               }
               if (pc && t0th) pc[7] += __builtin_amdgcn_s_memtime() - t_lo;
+              }
             }
             if (tt >= dyn_max && tt >= P.min_num_trials) {
               abort = true;
@@ -3065,6 +3389,12 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
         for (int i = threadIdx.x; i < 625; i += blockDim.x) ps.state[i] = ws[i];
       }
     }
+    if (rbest != res[0] && rbest != res[1]) {  // the best's residuals from a slot
+      for (int i = threadIdx.x; i < n; i += 64 * NW) res[0][i] = rbest[i];
+      wsync();
+      rbest = res[0];
+    }
+    best_sel = rbest == res[1] ? 1 : 0;
     st.dyn_max = dyn_max;
     st.evals = evals;
     st.res_sel = best_sel;
@@ -3161,11 +3491,13 @@ __global__ __launch_bounds__(256) void rs_replay2w_kernel(
   if ((int)blockIdx.x < split)
     rs_replay_body<KIND_F, 4>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[ain], rf.nact + ain,
                               rf.act[aout], rf.nact + aout, rf.nmod, rf.cnts, rf.mods,
-                              rf.wsnap, rf.wB, rf.wstate, P, prof, xyf, blockIdx.x, split, rf.wt);
+                              rf.wsnap, rf.wB, rf.wstate, P, prof, xyf, blockIdx.x, split, rf.wt,
+                              rf.lo, rf.lo_data, rf.lo_stride);
   else
     rs_replay_body<KIND_H, 4>(pairs, scratch, snaps, out, masks, rh.rst, rh.act[ain], rh.nact + ain,
                               rh.act[aout], rh.nact + aout, rh.nmod, rh.cnts, rh.mods,
-                              rh.wsnap, rh.wB, rh.wstate, P, prof, xyf, blockIdx.x - split, gridDim.x - split, rh.wt);
+                              rh.wsnap, rh.wB, rh.wstate, P, prof, xyf, blockIdx.x - split, gridDim.x - split, rh.wt,
+                              rh.lo, rh.lo_data, rh.lo_stride);
 }
 
 __global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
@@ -3212,12 +3544,15 @@ namespace {
 
 // Blocks of the wave-per-pair kernels (rs_begin / rs_draw / rs_replay) per
 // kind; pairs beyond it are taken in grid-stride order.
+constexpr int kNumCUsVerify = 256;  // MI355X CUs (the packed Shuffle's resident grid)
 constexpr int kPairGrid = 4096;  // 2048: -1 %, 16384 (a block per pair): +0.4 %, within noise (profiles/r02_o_pairgrid_vbench.log)
 
 template <typename F>
-void set_lds_attr(F f) {
+void set_lds_attr(F f, int static_bytes = 0) {
+  // (a request past the CU's LDS with the kernel's static LDS fails, and the
+  // failure would surface at the next hipGetLastError)
   (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024);
+                            160 * 1024 - static_bytes);
 }
 
 constexpr int kWaveShufflePairs = 256;
@@ -3268,6 +3603,17 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       sh_stride ? std::max(1, std::min(64, (kShuffleLdsKb * 1024) / (2 * sh_stride))) : 1;
   const int sh_blocks = (npairs + sh_ppb - 1) / sh_ppb;
   const int wave_stride = (max_m + 7) / 8 * 8;
+  // Table path: packed Shuffle (rs_shufflepack2_kernel) whenever the vectors
+  // fit uint16 (SCM_SHUFFLE_PACK=0, diagnostics: the per-launch stride form).
+  static const bool sh_pack_env = [] {
+    const char* e = getenv("SCM_SHUFFLE_PACK");
+    return !(e && e[0] == '0');
+  }();
+  const bool sh_pack = sh_pack_env && max_m <= 65536;
+  const int sh_cap = std::max(kShPackLdsBytes / 2, (max_m + 7) / 8 * 8);  // <= 65536 entries
+  // blocks of both kinds resident at once (the LDS of every CU, split by kind)
+  const int sh_pack_grid =
+      std::max(1, std::min(npairs, kNumCUsVerify * std::max(1, 160 * 1024 / (2 * sh_cap)) / 2));
   const bool wave_sh = verify_small_batch(npairs, max_m);
   const size_t wave_lds = wave_shuffle_lds_bytes(wave_stride);
   const int max_chunks_s = (max_m + kScoreThreads * kScorePchSmall - 1) / (kScoreThreads * kScorePchSmall);
@@ -3289,6 +3635,12 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     return e ? atoi(e) : 0;
   }();
   if (w0_env > 0) W = std::min(w0_env, maxw);
+  // Windows whose LO chains run in parallel (small batches with LO slots):
+  // SCM_PARALLEL_LO_WINDOWS (diagnostics), default 1.
+  static const int lo_windows = [] {
+    const char* e = getenv("SCM_PARALLEL_LO_WINDOWS");
+    return e ? atoi(e) : 1;
+  }();
   // Decoupled draws (speculative schedule with a draw stream): window r's
   // draws and shuffles run on dstream as soon as window r - 2 is replayed (its
   // active list) and window r - 1's prune has run (the lists and counts it
@@ -3329,9 +3681,17 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     } else {
       hipLaunchKernelGGL(rs_draw2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
                          out, rf, rh, lw, lout, P, (spec && r > 0) ? 1 : 0, W, s1);
-      hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
-                         (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch,
-                         snaps, out, rf, rh, lw, sh_ppb, sh_stride, s2);
+      if (sh_pack && r < kMaxVerifyWindows) {
+        // packed vectors (rs_shufflepack2_kernel): blocks resident at once per
+        // kind, each looping over the active list by its window's cursor
+        const int gp = (f ? sh_pack_grid : 0) + (h ? sh_pack_grid : 0);
+        hipLaunchKernelGGL(rs_shufflepack2_kernel, dim3(gp), dim3(64), (size_t)sh_cap * 2, stream,
+                           pairs, scratch, snaps, out, rf, rh, lw, r, sh_cap, f ? sh_pack_grid : 0);
+      } else {
+        hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
+                           (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch,
+                           snaps, out, rf, rh, lw, sh_ppb, sh_stride, s2);
+      }
     }
     if (f)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(kSolveGrid), dim3(64), 0, stream, pairs, xy1, xy2,
@@ -3397,6 +3757,19 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       }
     }
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r + 1], stream);
+    // Small batches: the record models' LO chains of the first lo_windows
+    // windows (where nearly all new bests occur), in parallel, before the
+    // replay (rs_lo_chain2_kernel); later windows' replays run their few
+    // chains inline (their slots are not read: lo = nullptr).
+    VerifyRoundBufs rfr = rf, rhr = rh;
+    const bool lo_win = wave_sh && rf.lo && rh.lo && r < lo_windows;
+    if (lo_win) {
+      const int ls = f ? npairs * kLoSlots : 0;
+      hipLaunchKernelGGL(rs_lo_chain2_kernel, dim3(ls + (h ? npairs * kLoSlots : 0)), dim3(256), lds,
+                         stream, pairs, scratch, snaps, out, rf, rh, lw, P, xyf, ls);
+    } else {
+      rfr.lo = rhr.lo = nullptr;
+    }
     hipStream_t rs = stream;
     if (spec && r < kMaxVerifyWindows) {
       (void)hipEventRecord(win_ev[2 * r], stream);
@@ -3405,7 +3778,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     }
     if (wave_sh)
       hipLaunchKernelGGL(rs_replay2w_kernel, dim3(g1), dim3(256), lds, rs, pairs, scratch,
-                         snaps, out, masks, rf, rh, lin, lout, P, prof, xyf, s1);
+                         snaps, out, masks, rfr, rhr, lin, lout, P, prof, xyf, s1);
     else
       hipLaunchKernelGGL(rs_replay2_kernel, dim3(g1), dim3(64), lds, rs, pairs, scratch, snaps,
                          out, masks, rf, rh, lin, lout, P, prof, xyf, s1);
@@ -3442,10 +3815,12 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     set_lds_attr(rs_begin2_kernel);
     set_lds_attr(rs_draw2_kernel);
     set_lds_attr(rs_shuffle2_kernel);
+    set_lds_attr(rs_shufflepack2_kernel, kShPackStaticLds);
     set_lds_attr(rs_shuffle_wave2_kernel);
     set_lds_attr(rs_drawshuffle_wave2_kernel);
     set_lds_attr(rs_replay2_kernel);
     set_lds_attr(rs_replay2w_kernel);
+    set_lds_attr(rs_lo_chain2_kernel);
     set_lds_attr(verify_final_kernel<1>);
     set_lds_attr(verify_final_kernel<8>);
     attr = true;
@@ -3469,8 +3844,9 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   }
   // LORANSAC<7-pt, 8-pt> (F, then its inlier masks) and LORANSAC<H, H>, each
   // on its own PRNG stream, advanced together window by window.
-  if ((err = hipMemsetAsync(rb_f.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
-  if ((err = hipMemsetAsync(rb_h.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  constexpr size_t kNactBytes = (3 + kMaxVerifyWindows) * sizeof(int32_t);
+  if ((err = hipMemsetAsync(rb_f.nact, 0, kNactBytes, stream)) != hipSuccess) return err;
+  if ((err = hipMemsetAsync(rb_h.nact, 0, kNactBytes, stream)) != hipSuccess) return err;
   hipLaunchKernelGGL(rs_begin2_kernel, dim3(2 * gw), dim3(64), kVerifyLdsHead, stream, pairs,
                      npairs, scratch, snaps, out, masks, xyf, rfp[0], rhp[0], params, gw);
   int last_h = -1;

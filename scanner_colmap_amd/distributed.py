@@ -198,6 +198,116 @@ class Gatherer:
         return out
 
 
+class ChunkSender:
+    """rank != 0 of a chunked step: each chunk's packed rows (a batch of the
+    library's pipeline, scm_table_run_chunks) go to rank 0 from a background
+    thread while the next batches compute, in order: a header (offset bytes,
+    data bytes, last flag) and the two messages, one batch_isend_irecv group
+    per chunk (RCCL over xGMI on nccl, staged through the same pinned / device
+    buffers as gather_packed; gloo on CPU tensors)."""
+
+    def __init__(self, device=None):
+        from concurrent.futures import ThreadPoolExecutor
+        self.device = device
+        self.pool = ThreadPoolExecutor(max_workers=1)
+        self.futs = []
+        self.staging = _Staging()
+
+    def _send(self, offsets, data, last):
+        import torch
+        import torch.distributed as dist
+        dev = self.device if self.device is not None else torch.device("cpu")
+        on_gpu = dev.type != "cpu"
+        if on_gpu:
+            torch.cuda.set_device(dev)
+        ob = np.ascontiguousarray(offsets, dtype=np.int64).reshape(-1).view(np.uint8)
+        dat = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
+        no, nd = (0, 0) if last else (ob.size, dat.size)
+        hdr = torch.tensor([no, nd, 1 if last else 0], dtype=torch.int64, device=dev)
+        ops = [dist.P2POp(dist.isend, hdr, 0)]
+        if no + nd:
+            if on_gpu:
+                pin, dbuf = self.staging.send_buffers(no + nd, dev)
+                hp = pin.numpy()
+                hp[:no] = ob
+                hp[no:no + nd] = dat
+                dbuf[:no + nd].copy_(pin[:no + nd], non_blocking=True)
+                t_o, t_d = dbuf[:no], dbuf[no:no + nd]
+            else:
+                t_o = torch.from_numpy(ob.copy())
+                t_d = torch.from_numpy(dat.copy())
+            ops += [dist.P2POp(dist.isend, t, 0) for t in (t_o, t_d) if t.numel()]
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+        if on_gpu:
+            torch.cuda.current_stream(dev).synchronize()  # staging reused by the next chunk
+
+    def submit(self, packed):
+        self.futs.append(self.pool.submit(self._send, packed.offsets, packed.data, False))
+
+    def finish(self):
+        """Sends the end marker and waits until every chunk has left."""
+        self.futs.append(self.pool.submit(self._send, np.zeros(1, np.int64),
+                                          np.zeros(0, np.uint8), True))
+        for f in self.futs:
+            f.result()
+        self.futs = []
+        self.pool.shutdown()
+
+
+class ChunkReceiver:
+    """rank 0 of a chunked step: a background thread receives the peers'
+    chunks as they arrive (round robin over the peers still sending, each
+    chunk into buffers of its own) while rank 0 computes its own rows."""
+
+    def __init__(self, world, device=None):
+        from concurrent.futures import ThreadPoolExecutor
+        self.world = world
+        self.device = device
+        self.pool = ThreadPoolExecutor(max_workers=1)
+        self.fut = self.pool.submit(self._loop)
+
+    def _recv(self, shape, src, dev):
+        import torch
+        import torch.distributed as dist
+        t = torch.empty(shape, dtype=torch.int64 if shape == (3,) else torch.uint8, device=dev)
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, t, src)]):
+            w.wait()
+        return t
+
+    def _loop(self):
+        import torch
+        import torch.distributed as dist
+        dev = self.device if self.device is not None else torch.device("cpu")
+        on_gpu = dev.type != "cpu"
+        if on_gpu:
+            torch.cuda.set_device(dev)
+        per = {r: [] for r in range(1, self.world)}
+        active = list(range(1, self.world))
+        while active:
+            for r in list(active):
+                no, nd, last = (int(x) for x in self._recv((3,), r, dev).cpu())
+                if last:
+                    active.remove(r)
+                    continue
+                flat = torch.empty(no + nd, dtype=torch.uint8, device=dev)
+                ops = []
+                if no:
+                    ops.append(dist.P2POp(dist.irecv, flat[:no], r))
+                if nd:
+                    ops.append(dist.P2POp(dist.irecv, flat[no:], r))
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+                host = (flat.cpu() if on_gpu else flat).numpy()
+                per[r].append((host[:no].view(np.int64), host[no:]))
+        return per
+
+    def result(self):
+        per = self.fut.result()
+        self.pool.shutdown()
+        return per
+
+
 class ShardPlan:
     """One rank's share of a sequential-matching job (bench.py and the job
     script use this; tests/test_distributed.py drives it over gloo).
@@ -218,6 +328,7 @@ class ShardPlan:
         self.table_begin, self.table_end = table_range(self.row_begin, self.row_end,
                                                        self.total_images, overlap)
         self.gatherer = None
+        self.tail_ms = []  # step_chunked: per step, the gather time left after the compute
 
     @property
     def local_rows(self) -> tuple[int, int]:
@@ -248,6 +359,36 @@ class ShardPlan:
             else:
                 gathered = gather_packed(packed.offsets, packed.data, device)
         return packed, gathered
+
+    def step_chunked(self, runner, device=None):
+        """One pass over this rank's rows with the gather inside the step:
+        `runner.table_run_chunks` (scm_table_run_chunks) hands over each
+        batch's rows as soon as they are serialised and they travel to rank 0
+        while the next batches compute, so only the last batch's rows are
+        exposed after the compute.  Returns on rank 0 the gathered (offsets,
+        data) chunks of every rank in row order (merge_gathered's input),
+        elsewhere None.  World 1: the rank's own chunks."""
+        lb, le = self.local_rows
+        own = []
+        if self.world == 1:
+            runner.table_run_chunks(self.overlap, lb, le,
+                                    lambda first, pk: own.append((pk.offsets, pk.data)))
+            return own
+        import time
+        if self.rank == 0:
+            recv = ChunkReceiver(self.world, device)
+            runner.table_run_chunks(self.overlap, lb, le,
+                                    lambda first, pk: own.append((pk.offsets, pk.data)))
+            t0 = time.perf_counter()
+            per = recv.result()
+            self.tail_ms.append((time.perf_counter() - t0) * 1e3)
+            return own + [c for r in range(1, self.world) for c in per[r]]
+        snd = ChunkSender(device)
+        runner.table_run_chunks(self.overlap, lb, le, lambda first, pk: snd.submit(pk))
+        t0 = time.perf_counter()
+        snd.finish()
+        self.tail_ms.append((time.perf_counter() - t0) * 1e3)
+        return None
 
     def run_passes(self, runner, passes: int, device=None, keep: bool = True):
         """`passes` steps as one streamed run (`runner.table_run_passes`, the

@@ -69,13 +69,19 @@ class _OracleRunner:
                     else np.zeros(0, np.uint8))
         return _P()
 
+    def table_run_chunks(self, overlap, row_begin, row_end, on_chunk, rows_per_chunk=2):
+        # scm_table_run_chunks' contract: the rows in order, a batch of rows at a time
+        for a in range(row_begin, row_end, rows_per_chunk):
+            on_chunk(a, self.table_run_packed(overlap, a, min(row_end, a + rows_per_chunk)))
+
     def table_run_passes(self, overlap, row_begin, row_end, passes, on_pass):
         # scm_table_run_passes' contract: each pass's packed rows, in order
         for k in range(passes):
             on_pass(k, self.table_run_packed(overlap, row_begin, row_end))
 
 
-def _rank_main(rank, world, port, n, K, scaling, q, background=False, steps=1, streamed=False):
+def _rank_main(rank, world, port, n, K, scaling, q, background=False, steps=1, streamed=False,
+               chunked=False):
     import torch.distributed as dist
 
     from oracle import oracle
@@ -92,7 +98,12 @@ def _rank_main(rank, world, port, n, K, scaling, q, background=False, steps=1, s
         c = Corridor(plan.total_images, 400, K, seed=53)
         runner = _OracleRunner(*table_rows(c.images(plan.table_begin, plan.table_end)))
         results = []
-        if streamed:  # bench.py's default: the steps as one streamed run
+        if chunked:  # the gather inside the step, batch by batch
+            results = [plan.step_chunked(runner) for _ in range(steps)]
+            if rank != 0:
+                assert results == [None] * steps
+                results = []
+        elif streamed:  # the steps as one streamed run
             last = plan.run_passes(runner, steps)
             assert last is not None
             results = [None] * steps
@@ -100,7 +111,7 @@ def _rank_main(rank, world, port, n, K, scaling, q, background=False, steps=1, s
             for _ in range(steps):
                 _, got = plan.step(runner, background=background)
                 results.append(got)
-        if background or streamed:
+        if (background or streamed) and not chunked:
             assert results == [None] * steps
             results = plan.drain()
         if rank == 0:
@@ -245,3 +256,25 @@ def test_gloo_streamed_passes_world2():
     assert [p.exitcode for p in procs] == [0, 0]
     ok, _, nrows, total = q.get(timeout=5)
     assert ok and nrows == total == 7
+
+
+@pytest.mark.parametrize("world,n,K,scaling", [(2, 9, 4, "strong"), (4, 6, 4, "strong"),
+                                               (4, 3, 5, "weak"), (2, 2, 5, "strong")])
+def test_gloo_chunked_step(world, n, K, scaling):
+    """ShardPlan.step_chunked (the gather inside the step): every rank's rows
+    leave batch by batch while the next batches compute; rank 0 receives the
+    peers' chunks round robin, and the merged rows of two steps equal a
+    one-rank run -- uneven chunk counts per rank, ranks without rows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main,
+                         args=(r, world, port, n, K, scaling, q, False, 2, False, True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert [p.exitcode for p in procs] == [0] * world
+    ok, _, nrows, total = q.get(timeout=5)
+    assert ok and nrows == total

@@ -21,7 +21,7 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, n, K, scaling, q):
+def _rank_main(rank, world, port, n, K, scaling, q, chunked=False):
     import torch.distributed as dist
 
     from oracle import oracle
@@ -34,9 +34,16 @@ def _rank_main(rank, world, port, n, K, scaling, q):
     try:
         plan = sd.ShardPlan(n, K, world, rank, scaling)
         c = Corridor(plan.total_images, 900, K, seed=57)
+        if chunked:
+            os.environ["SCM_BATCH_PAIRS"] = "5"  # several batches = several chunks per rank
         with Context(0) as ctx:
             ctx.table_load(*table_rows(c.images(plan.table_begin, plan.table_end)))
-            _, got = plan.step(ctx)
+            if chunked:
+                got = plan.step_chunked(ctx)
+                if rank == 0:
+                    assert len(got) > world
+            else:
+                _, got = plan.step(ctx)
         if rank == 0:
             rows_a, rows_b = sd.merge_gathered(got)
             ids, kps, descs = table_rows(c.images())
@@ -46,13 +53,16 @@ def _rank_main(rank, world, port, n, K, scaling, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,K,scaling", [(11, 4, "strong"), (6, 3, "weak")])
-def test_gpu_shard_step_world2(n, K, scaling):
+@pytest.mark.parametrize("n,K,scaling,chunked", [(11, 4, "strong", False), (6, 3, "weak", False),
+                                                 (11, 4, "strong", True)])
+def test_gpu_shard_step_world2(n, K, scaling, chunked):
+    """chunked: ShardPlan.step_chunked over scm_table_run_chunks (batches of 5
+    pairs, so each rank hands over several chunks inside the step)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, K, scaling, q))
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, K, scaling, q, chunked))
              for r in range(world)]
     for p in procs:
         p.start()

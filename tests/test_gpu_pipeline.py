@@ -124,3 +124,36 @@ def test_streamed_passes_equal_single_runs(batch_pairs):
             assert empty == [0, 0]
     finally:
         os.environ.pop("SCM_BATCH_PAIRS", None)
+
+
+@pytest.mark.parametrize("batch_pairs", ["7", None])
+def test_chunks_concatenate_to_packed(batch_pairs):
+    """scm_table_run_chunks hands the rows over batch by batch (several
+    batches with 7-pair batches, one without): the chunks cover the row range
+    in order and their rows are scm_table_run_packed's / the oracle's; an
+    empty range hands over nothing."""
+    imgs, (ids, kps, descs) = _table(12, 500, 43)
+    ref = oracle.table_run(ids, kps, descs, 4, 1, 11)
+    if batch_pairs:
+        os.environ["SCM_BATCH_PAIRS"] = batch_pairs
+    try:
+        with Context(0) as ctx:
+            ctx.table_load(ids, kps, descs)
+            chunks = []
+            ctx.table_run_chunks(4, 1, 11, lambda first, pk: chunks.append((first, pk)))
+            empty = []
+            ctx.table_run_chunks(4, 5, 5, lambda first, pk: empty.append(first))
+    finally:
+        os.environ.pop("SCM_BATCH_PAIRS", None)
+    assert empty == []
+    assert (len(chunks) > 1) == (batch_pairs is not None)
+    row = 1
+    rows_a, rows_b = [], []
+    for first, pk in chunks:
+        assert first == row
+        a, b = pk.rows()
+        rows_a += a
+        rows_b += b
+        row += len(pk)
+    assert row == 11
+    assert (rows_a, rows_b) == ref
