@@ -1229,7 +1229,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       SCM_TRY(rst.ensure(V * sizeof(RansacState)));
       SCM_TRY(window_bufs(samp, nmod, fcon, mods, cnts, ucnt, wsnap, wb, wstate, split, rb));
       SCM_TRY(act.ensure(3 * V * sizeof(int32_t)));
-      SCM_TRY(nact.ensure((3 + kMaxVerifyWindows) * sizeof(int32_t)));  // + shuffle cursors
+      SCM_TRY(nact.ensure(3 * sizeof(int32_t)));
       SCM_TRY(dtrial.ensure(V * sizeof(int32_t)));
       rb->rst = rst.as<RansacState>();
       for (int k = 0; k < 3; ++k) rb->act[k] = act.as<int32_t>() + k * V;

@@ -132,8 +132,7 @@ struct VerifyRoundBufs {
   const int32_t* pwB;     //   by speculative draws to skip pairs certain to stop)
   int32_t* dtrial;   // trials drawn so far
   int32_t* act[3];   // active-pair lists (rotating: window r's replay reads r % 3)
-  int32_t* nact;     // their lengths [3], then a work cursor per window of the table
-                     // path's packed Shuffle (rs_shufflepack2_kernel) [kMaxVerifyWindows]
+  int32_t* nact;     // their lengths [3]
   int wt;            // trials per pair the window buffers hold (T: kWindowTrials or
                      // kWindowTrialsSmall); the windows' rounds are at most wt / kTrialBatch
   LoSlot* lo = nullptr;       // small batches: [V][kLoSlots] outcomes (nullptr: LO inline)

@@ -2142,79 +2142,6 @@ __device__ __attribute__((always_inline)) void rs_shuffle_body(
     }
 }
 
-// The table path's Shuffle with the pairs' index vectors packed into LDS by
-// their own sizes.  rs_shuffle_body gives every pair of a launch the stride
-// of the batch's largest pair, so with pairs of a few thousand matches one
-// pair fills a block's LDS and a CU holds ~10 swap chains; here each block
-// takes the active list's next pairs from a work cursor while their vectors
-// fit its kShPackLdsBytes (a grabbed pair that does not fit opens the block's
-// next round), so a CU holds as many chains as its LDS has vectors of the
-// actual sizes.  Same shuffle_chain per pair: the same samples and vectors.
-constexpr int kShPackLdsBytes = 32 * 1024;
-constexpr int kShPackPairs = 64;  // pairs per round at most (one lane each)
-constexpr int kShPackStaticLds = 1024;  // >= its static LDS (3 x kShPackPairs + 1 int32)
-static_assert((3 * kShPackPairs + 1) * 4 <= kShPackStaticLds, "packed Shuffle static LDS");
-
-template <int K>
-__device__ __attribute__((always_inline)) void rs_shufflepack_body(
-    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
-    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out,
-    const int32_t* __restrict__ wB, const int32_t* __restrict__ act,
-    const int32_t* __restrict__ nact, uint32_t* __restrict__ samp, int32_t* __restrict__ cursor,
-    int cap, int WT) {
-  constexpr int KM = KindTraits<K>::kmin;
-  extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
-  uint16_t* V = reinterpret_cast<uint16_t*>(dyn_lds);  // cap entries
-  __shared__ int32_t s_q[kShPackPairs], s_off[kShPackPairs], s_n[kShPackPairs];
-  __shared__ int32_t s_np;
-  const int na = *nact;
-  int carry = -1;  // thread 0: an active-list index grabbed but not yet placed
-  for (;;) {
-    if (threadIdx.x == 0) {
-      int used = 0, k = 0;
-      for (;;) {
-        const int a = carry >= 0 ? carry : atomicAdd(cursor, 1);
-        carry = -1;
-        if (a >= na) break;
-        const int q = act[a];
-        const int n = pairs[q].m;
-        if (n <= 0 || wB[q] <= 0) continue;  // no trials: nothing to shuffle
-        const int need = (n + 7) & ~7;
-        if (k == kShPackPairs || used + need > cap) {
-          carry = a;
-          break;
-        }
-        s_q[k] = q;
-        s_off[k] = used;
-        s_n[k] = n;
-        used += need;
-        ++k;
-      }
-      s_np = k;
-    }
-    __syncthreads();
-    const int np = s_np;
-    if (np == 0) break;  // the cursor is past the list and nothing is carried
-    for (int l = 0; l < np; ++l) {
-      const uint32_t* g = pair_sidx(pair_at<K>(pairs, s_q[l], scratch, snaps, out));
-      const int n = s_n[l], o = s_off[l];
-      for (int i = threadIdx.x; i < n; i += blockDim.x) V[o + i] = (uint16_t)g[i];
-    }
-    __syncthreads();
-    if ((int)threadIdx.x < np) {
-      const int q = s_q[threadIdx.x];
-      shuffle_chain<KM>(V + s_off[threadIdx.x], samp + (int64_t)q * WT * 8, wB[q]);
-    }
-    __syncthreads();
-    for (int l = 0; l < np; ++l) {
-      uint32_t* g = pair_sidx(pair_at<K>(pairs, s_q[l], scratch, snaps, out));
-      const int n = s_n[l], o = s_off[l];
-      for (int i = threadIdx.x; i < n; i += blockDim.x) g[i] = V[o + i];
-    }
-    __syncthreads();
-  }
-}
-
 // The same window's Shuffle with a whole wave per pair, for small batches
 // (one Scanner stencil: a lane per pair leaves nearly every lane, and the
 // GPU, idle while one pair's chain of kmin dependent LDS round trips per
@@ -2231,6 +2158,8 @@ __device__ __attribute__((always_inline)) void rs_shufflepack_body(
 // final vector as the sequential chain, bit for bit.
 constexpr int kWsC = 16;               // trials per lane and pass
 constexpr int kWsTab = 256;            // table slots per lane (>= 2 x kmin x kWsC)
+// (Lane tables 1 KiB apart: a 16-byte skew per lane, against LDS bank
+// conflicts of the phase-A bucket reads, measured no change, round 5.)
 constexpr int kWsPass = 64 * kWsC;     // trials per pass
 constexpr int kWsRow = 65;             // trial slots per row of ssym (64 lanes + 1: no bank conflicts)
 constexpr int kWsMaxStride = 32768;    // vector positions staged as uint16
@@ -2344,6 +2273,10 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
       // memory latency per pass, not one per trial.)
       if (DRAW) {
         // The pass's rounds of 64 draws: snapshot, targets into the slots.
+        // (Measured round 5: drawing a whole pass per state stretch, each
+        // draw's target stored straight into its slot, is slower -- F
+        // targets 549K -> 777K cycles per pair: the per-draw slot addressing
+        // and scattered 16-bit stores cost more than the round's barriers.)
         for (int w0 = 0; w0 * kTrialBatch < np; ++w0) {
           const int B = min(kTrialBatch, np - w0 * kTrialBatch);
           const int wg = p0 / kTrialBatch + w0;  // round of the window
@@ -2525,34 +2458,21 @@ __global__ __launch_bounds__(64) void rs_shuffle_wave2_kernel(
                                  rh.samp, prof, rh.wt, stride, blockIdx.x - split, gridDim.x - split);
 }
 
-// Both kinds: blocks [0, split) the F vectors, the rest H's; cursors cf / ch.
-__global__ __launch_bounds__(64) void rs_shufflepack2_kernel(
-    const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
-    uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
-    VerifyRoundBufs rh, int ain, int win, int cap, int split) {
-  if ((int)blockIdx.x < split)
-    rs_shufflepack_body<KIND_F>(pairs, scratch, snaps, out, rf.wB, rf.act[ain], rf.nact + ain,
-                                rf.samp, rf.nact + 3 + win, cap, rf.wt);
-  else
-    rs_shufflepack_body<KIND_H>(pairs, scratch, snaps, out, rh.wB, rh.act[ain], rh.nact + ain,
-                                rh.samp, rh.nact + 3 + win, cap, rh.wt);
-}
-
 // Draws and Shuffle of a window in one launch (small batches).
 __global__ __launch_bounds__(64) void rs_drawshuffle_wave2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
-    VerifyRoundBufs rh, int ain, int aclr, VerifyParams P, int spec, int W,
+    VerifyRoundBufs rh, int ain, int aclr, VerifyParams P, int spec, int Wf, int Wh,
     uint64_t* __restrict__ prof, int stride, int split, int clr) {
   if ((int)blockIdx.x < split) {
     const WsDraw d{rf.rst, rf.nact + aclr, rf.cnts, rf.ucnt, rf.wsnap, rf.pstate, rf.wstate,
-                   rf.dtrial, rf.pcnts, rf.pwB, spec, W, clr};
+                   rf.dtrial, rf.pcnts, rf.pwB, spec, Wf, clr};
     rs_shuffle_wave_body<KIND_F, true>(pairs, scratch, snaps, out, rf.wB, rf.act[ain],
                                        rf.nact + ain, rf.samp, prof, rf.wt, stride, blockIdx.x, split, d,
                                        &P);
   } else {
     const WsDraw d{rh.rst, rh.nact + aclr, rh.cnts, rh.ucnt, rh.wsnap, rh.pstate, rh.wstate,
-                   rh.dtrial, rh.pcnts, rh.pwB, spec, W, clr};
+                   rh.dtrial, rh.pcnts, rh.pwB, spec, Wh, clr};
     rs_shuffle_wave_body<KIND_H, true>(pairs, scratch, snaps, out, rh.wB, rh.act[ain],
                                        rh.nact + ain, rh.samp, prof, rh.wt, stride, blockIdx.x - split,
                                        gridDim.x - split, d, &P);
@@ -3441,16 +3361,16 @@ __global__ __launch_bounds__(64) void rs_begin2_kernel(
 __global__ __launch_bounds__(64) void rs_draw2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
-    VerifyRoundBufs rh, int ain, int aclr, VerifyParams P, int spec, int W, int split) {
+    VerifyRoundBufs rh, int ain, int aclr, VerifyParams P, int spec, int Wf, int Wh, int split) {
   if ((int)blockIdx.x < split)
     rs_draw_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[ain], rf.nact + ain,
                          rf.nact + aclr, rf.samp, rf.cnts, rf.ucnt, rf.wsnap, rf.wB, rf.pstate,
-                         rf.wstate, rf.dtrial, rf.pcnts, rf.pwB, P, spec != 0, W, blockIdx.x,
+                         rf.wstate, rf.dtrial, rf.pcnts, rf.pwB, P, spec != 0, Wf, blockIdx.x,
                          split, rf.wt);
   else
     rs_draw_body<KIND_H>(pairs, scratch, snaps, out, rh.rst, rh.act[ain], rh.nact + ain,
                          rh.nact + aclr, rh.samp, rh.cnts, rh.ucnt, rh.wsnap, rh.wB, rh.pstate,
-                         rh.wstate, rh.dtrial, rh.pcnts, rh.pwB, P, spec != 0, W,
+                         rh.wstate, rh.dtrial, rh.pcnts, rh.pwB, P, spec != 0, Wh,
                          blockIdx.x - split, gridDim.x - split, rh.wt);
 }
 
@@ -3544,15 +3464,15 @@ namespace {
 
 // Blocks of the wave-per-pair kernels (rs_begin / rs_draw / rs_replay) per
 // kind; pairs beyond it are taken in grid-stride order.
-constexpr int kNumCUsVerify = 256;  // MI355X CUs (the packed Shuffle's resident grid)
 constexpr int kPairGrid = 4096;  // 2048: -1 %, 16384 (a block per pair): +0.4 %, within noise (profiles/r02_o_pairgrid_vbench.log)
 
+// (a request past the CU's LDS together with the kernel's static LDS fails:
+// launch_verify returns that error at once instead of leaving it for the next
+// hipGetLastError)
 template <typename F>
-void set_lds_attr(F f, int static_bytes = 0) {
-  // (a request past the CU's LDS with the kernel's static LDS fails, and the
-  // failure would surface at the next hipGetLastError)
-  (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            160 * 1024 - static_bytes);
+hipError_t set_lds_attr(F f, int static_bytes = 0) {
+  return hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             160 * 1024 - static_bytes);
 }
 
 constexpr int kWaveShufflePairs = 256;
@@ -3603,17 +3523,6 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       sh_stride ? std::max(1, std::min(64, (kShuffleLdsKb * 1024) / (2 * sh_stride))) : 1;
   const int sh_blocks = (npairs + sh_ppb - 1) / sh_ppb;
   const int wave_stride = (max_m + 7) / 8 * 8;
-  // Table path: packed Shuffle (rs_shufflepack2_kernel) whenever the vectors
-  // fit uint16 (SCM_SHUFFLE_PACK=0, diagnostics: the per-launch stride form).
-  static const bool sh_pack_env = [] {
-    const char* e = getenv("SCM_SHUFFLE_PACK");
-    return !(e && e[0] == '0');
-  }();
-  const bool sh_pack = sh_pack_env && max_m <= 65536;
-  const int sh_cap = std::max(kShPackLdsBytes / 2, (max_m + 7) / 8 * 8);  // <= 65536 entries
-  // blocks of both kinds resident at once (the LDS of every CU, split by kind)
-  const int sh_pack_grid =
-      std::max(1, std::min(npairs, kNumCUsVerify * std::max(1, 160 * 1024 / (2 * sh_cap)) / 2));
   const bool wave_sh = verify_small_batch(npairs, max_m);
   const size_t wave_lds = wave_shuffle_lds_bytes(wave_stride);
   const int max_chunks_s = (max_m + kScoreThreads * kScorePchSmall - 1) / (kScoreThreads * kScorePchSmall);
@@ -3635,6 +3544,15 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     return e ? atoi(e) : 0;
   }();
   if (w0_env > 0) W = std::min(w0_env, maxw);
+  // Per-kind window sizes: the same schedule for both kinds, except a small
+  // batch's second F window (SCM_SMALL_F_W1 rounds, diagnostics; default the
+  // largest window): F stops early on most pairs, and that window's draws run
+  // beside the first window's replay on the critical path of a stencil.
+  static const int fw1_env = [] {
+    const char* e = getenv("SCM_SMALL_F_W1");
+    return e ? atoi(e) : 0;
+  }();
+  int Wf = W, Wh = W;
   // Windows whose LO chains run in parallel (small batches with LO slots):
   // SCM_PARALLEL_LO_WINDOWS (diagnostics), default 1.
   static const int lo_windows = [] {
@@ -3650,8 +3568,8 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   // 2 * kMaxVerifyWindows = the batch's begin kernel done.
   const bool dsplit = spec && wave_sh && dstream && draw_ev;
   if (dsplit) (void)hipEventRecord(draw_ev[2 * kMaxVerifyWindows], stream);
-  int covered = 0, r = 0;
-  while (covered < P.max_trials_F || covered < P.max_trials_H) {
+  int covered_f = 0, covered_h = 0, r = 0;
+  while (covered_f < P.max_trials_F || covered_h < P.max_trials_H) {
     const VerifyRoundBufs& rf = rfp[r & 1];
     const VerifyRoundBufs& rh = rhp[r & 1];
     // lists: the replay's input and output, the wide kernels' input
@@ -3659,7 +3577,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     const int lw = spec && r > 0 ? (r - 1) % 3 : lin;
     if (spec && r >= 2 && r - 2 < kMaxVerifyWindows)
       (void)hipStreamWaitEvent(stream, win_ev[2 * (r - 2) + 1], 0);
-    const bool f = covered < P.max_trials_F, h = covered < P.max_trials_H;
+    const bool f = covered_f < P.max_trials_F, h = covered_h < P.max_trials_H;
     if (h && last_h) *last_h = r;
     const int g1 = (f ? gw : 0) + (h ? gw : 0), s1 = f ? gw : 0;
     const int g2 = (f ? sh_blocks : 0) + (h ? sh_blocks : 0), s2 = f ? sh_blocks : 0;
@@ -3667,7 +3585,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       if (r >= 2) (void)hipStreamWaitEvent(dstream, win_ev[2 * (r - 2) + 1], 0);
       (void)hipStreamWaitEvent(dstream, draw_ev[r == 0 ? 2 * kMaxVerifyWindows : 2 * r - 1], 0);
       hipLaunchKernelGGL(rs_drawshuffle_wave2_kernel, dim3(g1), dim3(64), kWsDrawHead + wave_lds,
-                         dstream, pairs, scratch, snaps, out, rf, rh, lw, lout, P, 0, W, prof,
+                         dstream, pairs, scratch, snaps, out, rf, rh, lw, lout, P, 0, Wf, Wh, prof,
                          wave_stride, s1, 0);
       (void)hipEventRecord(draw_ev[2 * r], dstream);
       (void)hipStreamWaitEvent(stream, draw_ev[2 * r], 0);
@@ -3677,30 +3595,22 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     } else if (wave_sh) {
       hipLaunchKernelGGL(rs_drawshuffle_wave2_kernel, dim3(g1), dim3(64), kWsDrawHead + wave_lds,
                          stream, pairs, scratch, snaps, out, rf, rh, lw, lout, P,
-                         (spec && r > 0) ? 1 : 0, W, prof, wave_stride, s1, 1);
+                         (spec && r > 0) ? 1 : 0, Wf, Wh, prof, wave_stride, s1, 1);
     } else {
       hipLaunchKernelGGL(rs_draw2_kernel, dim3(g1), dim3(64), lds, stream, pairs, scratch, snaps,
-                         out, rf, rh, lw, lout, P, (spec && r > 0) ? 1 : 0, W, s1);
-      if (sh_pack && r < kMaxVerifyWindows) {
-        // packed vectors (rs_shufflepack2_kernel): blocks resident at once per
-        // kind, each looping over the active list by its window's cursor
-        const int gp = (f ? sh_pack_grid : 0) + (h ? sh_pack_grid : 0);
-        hipLaunchKernelGGL(rs_shufflepack2_kernel, dim3(gp), dim3(64), (size_t)sh_cap * 2, stream,
-                           pairs, scratch, snaps, out, rf, rh, lw, r, sh_cap, f ? sh_pack_grid : 0);
-      } else {
-        hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
-                           (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch,
-                           snaps, out, rf, rh, lw, sh_ppb, sh_stride, s2);
-      }
+                         out, rf, rh, lw, lout, P, (spec && r > 0) ? 1 : 0, Wf, Wh, s1);
+      hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
+                         (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch,
+                         snaps, out, rf, rh, lw, sh_ppb, sh_stride, s2);
     }
     if (f)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(kSolveGrid), dim3(64), 0, stream, pairs, xy1, xy2,
                          rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.samp, rf.nmod, rf.fcon, rf.mods,
-                         W, P.max_residual, rf.wt);
+                         Wf, P.max_residual, rf.wt);
     if (h)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_H>, dim3(kSolveGrid), dim3(64), 0, stream, pairs, xy1, xy2,
                          rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.samp, rh.nmod, rh.fcon, rh.mods,
-                         W, P.max_residual, rh.wt);
+                         Wh, P.max_residual, rh.wt);
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r], stream);
     // Scoring per kind: split (filter counts + undecided counts, then exact
     // tests only for the models that can reach the best; the runtime's
@@ -3711,21 +3621,21 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       if (rf.ucnt) {
         hipLaunchKernelGGL((rs_score_kernel<KIND_F, true>), dim3(8192), dim3(kScoreThreads), 0,
                            stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
-                           rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual, prof, rf.wt);
+                           rf.mods, rf.cnts, rf.ucnt, max_chunks, Wf, P.max_residual, prof, rf.wt);
 
         hipLaunchKernelGGL(rs_exact_kernel<KIND_F>, dim3(8192), dim3(kScoreThreads), 0, stream,
                            pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod, rf.fcon,
-                           rf.mods, rf.cnts, rf.ucnt, max_chunks, W, P.max_residual, rf.wt);
+                           rf.mods, rf.cnts, rf.ucnt, max_chunks, Wf, P.max_residual, rf.wt);
       } else {
         if (wave_sh)
           hipLaunchKernelGGL((rs_score_kernel<KIND_F, false, kScorePchSmall>), dim3(8192),
                              dim3(kScoreThreads), 0, stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw],
                              rf.nact + lw, rf.nmod, rf.fcon, rf.mods, rf.cnts, nullptr, max_chunks_s,
-                             W, P.max_residual, prof, rf.wt);
+                             Wf, P.max_residual, prof, rf.wt);
         else
           hipLaunchKernelGGL((rs_score_kernel<KIND_F, false>), dim3(8192), dim3(kScoreThreads), 0,
                              stream, pairs, xyf, rf.rst, rf.wB, rf.act[lw], rf.nact + lw, rf.nmod,
-                             rf.fcon, rf.mods, rf.cnts, nullptr, max_chunks, W, P.max_residual, prof, rf.wt);
+                             rf.fcon, rf.mods, rf.cnts, nullptr, max_chunks, Wf, P.max_residual, prof, rf.wt);
       }
     }
     if (h) {
@@ -3736,24 +3646,24 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
           hipLaunchKernelGGL((rs_score_kernel<KIND_H, true, kScorePchSmall>), dim3(8192),
                              dim3(kScoreThreads), 0, stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw],
                              rh.nact + lw, rh.nmod, rh.fcon, rh.mods, rh.cnts, rh.ucnt, max_chunks_s,
-                             W, P.max_residual, prof, rh.wt);
+                             Wh, P.max_residual, prof, rh.wt);
         else
           hipLaunchKernelGGL((rs_score_kernel<KIND_H, true>), dim3(8192), dim3(kScoreThreads), 0,
                              stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod,
-                             rh.fcon, rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, prof, rh.wt);
+                             rh.fcon, rh.mods, rh.cnts, rh.ucnt, max_chunks, Wh, P.max_residual, prof, rh.wt);
         hipLaunchKernelGGL(rs_exact_kernel<KIND_H>, dim3(8192), dim3(kScoreThreads), 0, stream,
                            pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod, rh.fcon,
-                           rh.mods, rh.cnts, rh.ucnt, max_chunks, W, P.max_residual, rh.wt);
+                           rh.mods, rh.cnts, rh.ucnt, max_chunks, Wh, P.max_residual, rh.wt);
       } else {
         if (wave_sh)
           hipLaunchKernelGGL((rs_score_kernel<KIND_H, false, kScorePchSmall>), dim3(8192),
                              dim3(kScoreThreads), 0, stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw],
                              rh.nact + lw, rh.nmod, rh.fcon, rh.mods, rh.cnts, nullptr, max_chunks_s,
-                             W, P.max_residual, prof, rh.wt);
+                             Wh, P.max_residual, prof, rh.wt);
         else
           hipLaunchKernelGGL((rs_score_kernel<KIND_H, false>), dim3(8192), dim3(kScoreThreads), 0,
                              stream, pairs, xyf, rh.rst, rh.wB, rh.act[lw], rh.nact + lw, rh.nmod,
-                             rh.fcon, rh.mods, rh.cnts, nullptr, max_chunks, W, P.max_residual, prof, rh.wt);
+                             rh.fcon, rh.mods, rh.cnts, nullptr, max_chunks, Wh, P.max_residual, prof, rh.wt);
       }
     }
     if (score_ev && r < kMaxVerifyWindows) (void)hipEventRecord(score_ev[2 * r + 1], stream);
@@ -3785,8 +3695,14 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     if (spec && r < kMaxVerifyWindows) (void)hipEventRecord(win_ev[2 * r + 1], rstream);
     const hipError_t err = hipGetLastError();
     if (err != hipSuccess) return err;
-    covered += W * kTrialBatch;
-    W = wave_sh || W * 2 > maxw ? maxw : W * 2;
+    covered_f += Wf * kTrialBatch;
+    covered_h += Wh * kTrialBatch;
+    if (wave_sh) {
+      Wf = r == 0 && fw1_env > 0 ? std::min(fw1_env, maxw) : maxw;
+      Wh = maxw;
+    } else {
+      Wf = Wh = Wf * 2 > maxw ? maxw : Wf * 2;
+    }
     ++r;
     if (spec && r >= kMaxVerifyWindows) spec = false;  // out of events: the rest in order
   }
@@ -3812,17 +3728,19 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   if (npairs <= 0) return hipSuccess;
   static bool attr = false;
   if (!attr) {
-    set_lds_attr(rs_begin2_kernel);
-    set_lds_attr(rs_draw2_kernel);
-    set_lds_attr(rs_shuffle2_kernel);
-    set_lds_attr(rs_shufflepack2_kernel, kShPackStaticLds);
-    set_lds_attr(rs_shuffle_wave2_kernel);
-    set_lds_attr(rs_drawshuffle_wave2_kernel);
-    set_lds_attr(rs_replay2_kernel);
-    set_lds_attr(rs_replay2w_kernel);
-    set_lds_attr(rs_lo_chain2_kernel);
-    set_lds_attr(verify_final_kernel<1>);
-    set_lds_attr(verify_final_kernel<8>);
+    const hipError_t es[] = {
+        set_lds_attr(rs_begin2_kernel),
+        set_lds_attr(rs_draw2_kernel),
+        set_lds_attr(rs_shuffle2_kernel),
+        set_lds_attr(rs_shuffle_wave2_kernel),
+        set_lds_attr(rs_drawshuffle_wave2_kernel),
+        set_lds_attr(rs_replay2_kernel),
+        set_lds_attr(rs_replay2w_kernel),
+        set_lds_attr(rs_lo_chain2_kernel),
+        set_lds_attr(verify_final_kernel<1>),
+        set_lds_attr(verify_final_kernel<8>)};
+    for (hipError_t e : es)
+      if (e != hipSuccess) return e;
     attr = true;
   }
   const size_t lds = sizeof(VerifyLds);
@@ -3844,9 +3762,8 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   }
   // LORANSAC<7-pt, 8-pt> (F, then its inlier masks) and LORANSAC<H, H>, each
   // on its own PRNG stream, advanced together window by window.
-  constexpr size_t kNactBytes = (3 + kMaxVerifyWindows) * sizeof(int32_t);
-  if ((err = hipMemsetAsync(rb_f.nact, 0, kNactBytes, stream)) != hipSuccess) return err;
-  if ((err = hipMemsetAsync(rb_h.nact, 0, kNactBytes, stream)) != hipSuccess) return err;
+  if ((err = hipMemsetAsync(rb_f.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  if ((err = hipMemsetAsync(rb_h.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
   hipLaunchKernelGGL(rs_begin2_kernel, dim3(2 * gw), dim3(64), kVerifyLdsHead, stream, pairs,
                      npairs, scratch, snaps, out, masks, xyf, rfp[0], rhp[0], params, gw);
   int last_h = -1;
