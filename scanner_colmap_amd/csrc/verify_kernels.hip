@@ -3477,6 +3477,7 @@ hipError_t set_lds_attr(F f, int static_bytes = 0) {
 
 constexpr int kWaveShufflePairs = 256;
 constexpr int kSmallFirstWindow = 4;  // rounds of a small batch's first window (run_windows)
+constexpr int kSmallSecondWindowF = 80;  // rounds of its second F window (run_windows)
 // Small batches: a wave per pair (rs_shuffle_wave2_kernel), four waves per
 // pair in the replay, speculative windows -- while the batch leaves most of
 // the GPU idle, latency decides.
@@ -3545,14 +3546,30 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   }();
   if (w0_env > 0) W = std::min(w0_env, maxw);
   // Per-kind window sizes: the same schedule for both kinds, except a small
-  // batch's second F window (SCM_SMALL_F_W1 rounds, diagnostics; default the
-  // largest window): F stops early on most pairs, and that window's draws run
-  // beside the first window's replay on the critical path of a stencil.
+  // batch's second F window, kSmallSecondWindowF rounds (SCM_SMALL_F_W1,
+  // diagnostics): F stops early on most pairs, and that window's draws run
+  // beside the first window's solves, scores and replay -- the two branches
+  // of a stencil's critical path (19-pair stencil, profiles/r05_g, r05_h:
+  // 128 rounds 2.80-2.84 ms per call, 96: 2.60-2.62, 80: 2.58-2.62, 64:
+  // 2.61-2.75, 48: 2.77-2.85, 32: 2.93-2.97; F's 10,000 trials still take
+  // three windows).
   static const int fw1_env = [] {
     const char* e = getenv("SCM_SMALL_F_W1");
     return e ? atoi(e) : 0;
   }();
   int Wf = W, Wh = W;
+  // Table path (diagnostics): SCM_TABLE_W0_H / SCM_TABLE_W0_F set a kind's
+  // first window (rounds); each kind then doubles up to the largest window.
+  static const int tw0h = [] {
+    const char* e = getenv("SCM_TABLE_W0_H");
+    return e ? atoi(e) : 0;
+  }();
+  static const int tw0f = [] {
+    const char* e = getenv("SCM_TABLE_W0_F");
+    return e ? atoi(e) : 0;
+  }();
+  if (!wave_sh && tw0h > 0) Wh = std::min(tw0h, maxw);
+  if (!wave_sh && tw0f > 0) Wf = std::min(tw0f, maxw);
   // Windows whose LO chains run in parallel (small batches with LO slots):
   // SCM_PARALLEL_LO_WINDOWS (diagnostics), default 1.
   static const int lo_windows = [] {
@@ -3698,10 +3715,11 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     covered_f += Wf * kTrialBatch;
     covered_h += Wh * kTrialBatch;
     if (wave_sh) {
-      Wf = r == 0 && fw1_env > 0 ? std::min(fw1_env, maxw) : maxw;
+      Wf = r == 0 ? std::min(fw1_env > 0 ? fw1_env : kSmallSecondWindowF, maxw) : maxw;
       Wh = maxw;
     } else {
-      Wf = Wh = Wf * 2 > maxw ? maxw : Wf * 2;
+      Wf = Wf * 2 > maxw ? maxw : Wf * 2;
+      Wh = Wh * 2 > maxw ? maxw : Wh * 2;
     }
     ++r;
     if (spec && r >= kMaxVerifyWindows) spec = false;  // out of events: the rest in order
