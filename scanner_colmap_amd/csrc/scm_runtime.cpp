@@ -314,6 +314,9 @@ struct BatchSet {
   // odd-parity window buffers of small batches (speculative windows, launch_verify)
   DevBuf o_samp, o_nmod, o_fcon, o_mods, o_cnts, o_ucnt, o_wsnap, o_wb, o_wstate;
   DevBuf oh_samp, oh_nmod, oh_fcon, oh_mods, oh_cnts, oh_ucnt, oh_wsnap, oh_wb, oh_wstate;
+  // their third parity (decoupled draws two windows ahead)
+  DevBuf t_samp, t_nmod, t_fcon, t_mods, t_cnts, t_ucnt, t_wsnap, t_wb, t_wstate;
+  DevBuf th_samp, th_nmod, th_fcon, th_mods, th_cnts, th_ucnt, th_wsnap, th_wb, th_wstate;
   DevBuf lo_slot[4], lo_data[4];  // small batches' parallel LO: (kind, parity) slots and their data
   hipStream_t rstream = nullptr;  // replay stream of speculative windows (another set's vstream)
   hipStream_t fstream = nullptr;  // early verify_final pass of small batches (the third set's)
@@ -345,7 +348,9 @@ struct BatchSet {
                       &h_mods, &h_wsnap, &ucnt, &h_ucnt, &wb, &wstate, &dtrial, &h_wb, &h_wstate,
                       &h_dtrial, &o_samp, &o_nmod, &o_fcon, &o_mods, &o_cnts, &o_ucnt, &o_wsnap,
                       &o_wb, &o_wstate, &oh_samp, &oh_nmod, &oh_fcon, &oh_mods, &oh_cnts, &oh_ucnt,
-                      &oh_wsnap, &oh_wb, &oh_wstate, &lo_slot[0], &lo_slot[1], &lo_slot[2],
+                      &oh_wsnap, &oh_wb, &oh_wstate, &t_samp, &t_nmod, &t_fcon, &t_mods, &t_cnts,
+                      &t_ucnt, &t_wsnap, &t_wb, &t_wstate, &th_samp, &th_nmod, &th_fcon, &th_mods,
+                      &th_cnts, &th_ucnt, &th_wsnap, &th_wb, &th_wstate, &lo_slot[0], &lo_slot[1], &lo_slot[2],
                       &lo_slot[3], &lo_data[0], &lo_data[1], &lo_data[2], &lo_data[3]})
       b->release();
     stage.release();
@@ -1253,7 +1258,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
     // replay stream, so that the next window's draws and scores overlap the
     // replay of this one.
     VerifySpec spec;
-    VerifyRoundBufs rbf1 = rbf, rbh1 = rbh;
+    VerifyRoundBufs rbf1 = rbf, rbh1 = rbh, rbf2 = rbf, rbh2 = rbh;
     if (verify_small_batch((int)V, max_m)) {
       SCM_TRY(window_bufs(bs.o_samp, bs.o_nmod, bs.o_fcon, bs.o_mods, bs.o_cnts, bs.o_ucnt,
                           bs.o_wsnap, bs.o_wb, bs.o_wstate, false, &rbf1));
@@ -1313,6 +1318,16 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
         if (draw_stream) {
           spec.dstream = ctx->stream;
           spec.draw_ev = bs.dev;
+          // the third parity (no parallel-LO slots: only the first windows have them)
+          SCM_TRY(window_bufs(bs.t_samp, bs.t_nmod, bs.t_fcon, bs.t_mods, bs.t_cnts, bs.t_ucnt,
+                              bs.t_wsnap, bs.t_wb, bs.t_wstate, false, &rbf2));
+          SCM_TRY(window_bufs(bs.th_samp, bs.th_nmod, bs.th_fcon, bs.th_mods, bs.th_cnts,
+                              bs.th_ucnt, bs.th_wsnap, bs.th_wb, bs.th_wstate, ctx->score_split,
+                              &rbh2));
+          rbf2.lo = rbh2.lo = nullptr;
+          rbf2.lo_data = rbh2.lo_data = nullptr;
+          spec.rb_f2 = &rbf2;
+          spec.rb_h2 = &rbh2;
         }
       }
     }
@@ -1702,11 +1717,12 @@ int64_t pair_workspace_bytes(int64_t n1, int64_t n2) {
 
 // Bytes per pair beyond pair_workspace_bytes' when a batch takes the
 // small-batch kernels (enqueue_verify): windows of kWindowTrialsSmall trials
-// in two parities, F and H, and the parallel-LO slots of both kinds and
+// in three parities, F and H (window starts, states and trial counts
+// included), and the parallel-LO slots of both kinds and the first two
 // parities (at most, for a pivot of n1 keypoints).
 int64_t small_batch_extra_bytes(int64_t n1) {
-  return 2 * (2 * (int64_t)kWindowTrialsSmall - (int64_t)kWindowTrials) * kRoundTrialBytes +
-         2 * 640 * 4 +
+  return 2 * (3 * (int64_t)kWindowTrialsSmall - (int64_t)kWindowTrials) * kRoundTrialBytes +
+         2 * 2 * (640 * 4 + kVerifyStateWords * 4 + 4) +
          4 * (int64_t)kLoSlots * (lo_slot_doubles(std::max<int64_t>(n1, 1)) * 8 + (int64_t)sizeof(LoSlot));
 }
 

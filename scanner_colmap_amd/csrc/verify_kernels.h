@@ -64,13 +64,19 @@ struct VerifyOut {
   // its stop (speculative trials past the abort excluded): the scoring
   // kernels' algorithmic work (bench.py roofline_verify)
   int64_t f_evals, h_evals;
+  // Small batches: the speculative watermark decision (verify_final_kernel
+  // phase 3) -- spec 0: none, 1: from H's final stream state, 2: from the state
+  // after H's last window's draws (valid unless that window's replay aborted
+  // H); spec_wm the decision.
+  int32_t spec, spec_wm;
 };
 
 // Per-pair state of the round-synchronous LO-RANSAC (verify_kernels.hip).
 struct RansacState {
   int32_t n, done, trial, dyn_max;
   int32_t max_trials, best_n, best_sum_valid, res_sel;
-  int32_t B, num_trials, pad_, pad2_;
+  int32_t B, num_trials, pad_;
+  int32_t aborted;  // the run ended by the abort (dynamic trial bound), not at its cap
   int64_t evals;  // (model, point) evaluations of the trials up to the stop
   double best_sum;
   double S;  // max |coordinate| of the pair's points (fp32 filter bound)
@@ -165,6 +171,10 @@ struct VerifySpec {
   // r - 1's scoring; draw_ev: 2 * kMaxVerifyWindows + 1 events.
   hipStream_t dstream = nullptr;
   hipEvent_t* draw_ev = nullptr;
+  // A third parity's buffers (optional, with decoupled draws): the draws then
+  // run two windows ahead of the replays.
+  const VerifyRoundBufs* rb_f2 = nullptr;
+  const VerifyRoundBufs* rb_h2 = nullptr;
 };
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,

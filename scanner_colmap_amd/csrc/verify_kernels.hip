@@ -1691,29 +1691,40 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
     uint32_t* __restrict__ snaps, const uint8_t* __restrict__ masks,
     VerifyOut* __restrict__ out, VerifyParams P, uint64_t* __restrict__ prof,
     const int32_t* __restrict__ counts, RansacState* __restrict__ rstF,
-    const RansacState* __restrict__ rstH, int phase) {
+    const RansacState* __restrict__ rstH, int phase,
+    const uint32_t* __restrict__ spec_state) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   // phase 1 (early, small batches): only pairs whose F and H RANSACs are both
   // done (read once, by thread 0: the replay of other pairs is still
   // running), marked in rstF[q].pad_; phase 2: the rest; phase 0: every pair.
+  // phase 3 (speculative, small batches; beside H's last window): the
+  // watermark decision only, of the pairs whose F is done, into
+  // VerifyOut::spec / spec_wm -- from H's final stream state when H is done
+  // (spec 1), else from spec_state, the state after H's last window's draws
+  // (spec 2), which that window's replay leaves as H's final state unless it
+  // aborts H (RansacState::aborted).  Phases 1 / 2 take the decision when
+  // spec is 1, or 2 and H did not abort, and run the watermark RANSAC
+  // otherwise: the same decision either way.
   // Bit 8 of the argument: diagnostics (loransac_wave's scrib).
   const bool scrib = (phase & 8) != 0;
   phase &= 3;
+  int src = 0;  // phase 3: the decision's state source (1 / 2)
   if (phase != 0) {
     if (threadIdx.x == 0) {
       const int q0 = blockIdx.x;
       const int fd = *reinterpret_cast<volatile const int32_t*>(&rstF[q0].done);
       const int hd = *reinterpret_cast<volatile const int32_t*>(&rstH[q0].done);
       const int mk = *reinterpret_cast<volatile const int32_t*>(&rstF[q0].pad_);
-      s.redi[15] = phase == 1 ? (fd && hd) : !mk;
+      s.redi[15] = phase == 1 ? (fd && hd) : phase == 2 ? !mk : (fd ? (hd ? 1 : 2) : 0);
       __threadfence();
     }
     __syncthreads();
-    const bool go = s.redi[15] != 0;
+    const int go = s.redi[15];
     __syncthreads();
     if (!go) return;
     if (phase == 1 && threadIdx.x == 0) rstF[blockIdx.x].pad_ = 1;
+    if (phase == 3) src = go;
   }
   Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
   pf.start();
@@ -1739,6 +1750,130 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
   const int f_in = o->f_inliers_raw, h_in = o->h_inliers_raw;
   const bool f_ok = f_in >= KindTraits<KIND_F>::kmin, h_ok = h_in >= KindTraits<KIND_H>::kmin;
   const int mni = P.min_num_inliers;
+  // DetectWatermark's decision (1: the F inliers are mostly one 2-D
+  // translation) from the H stream state st: the watermark RANSAC continues
+  // H's generator.
+  auto detect_wm = [&](const uint32_t* st) -> int {
+    // DetectWatermark with the dummy cameras (width = height = 0): a point
+    // is inside the [0,0]x[0,0] box only if it is exactly (0, 0).
+    int nb = 0;
+    for (int b = wv * 64 * kSeqU + lane; b < n; b += 64 * kSeqU * NW) {
+      uint8_t mk[kSeqU];
+      double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
+#pragma unroll
+      for (int u = 0; u < kSeqU; ++u) {
+        const int i = min(b + 64 * u, n - 1);
+        mk[u] = b + 64 * u < n ? mask[i] : 0;
+        a0[u] = xy1[2 * i];
+        a1[u] = xy1[2 * i + 1];
+        c0[u] = xy2[2 * i];
+        c1[u] = xy2[2 * i + 1];
+      }
+#pragma unroll
+      for (int u = 0; u < kSeqU; ++u) {
+        const bool in1 = a0[u] >= 0.0 && a0[u] <= 0.0 && a1[u] >= 0.0 && a1[u] <= 0.0;
+        const bool in2 = c0[u] >= 0.0 && c0[u] <= 0.0 && c1[u] >= 0.0 && c1[u] <= 0.0;
+        nb += (mk[u] && !in1 && !in2) ? 1 : 0;
+      }
+    }
+    nb = wave_sum_i(nb);
+    if (NW > 1) {
+      if (lane == 0) s.redi[wv] = nb;
+      __syncthreads();
+      nb = 0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) nb += s.redi[w];
+      __syncthreads();
+    }
+    const int ni = f_in;
+    const double bratio = (double)nb / (double)ni;
+    if (bratio < P.watermark_min_inlier_ratio) return 0;
+    {
+      // Inlier points in index order -> translation LO-RANSAC, on packed
+      // fp32 points (the doubles are widened float32 keypoints: exact both
+      // ways; half the bytes of every point loop).  Scratch layout (10n
+      // doubles; float4 arrays 16-B aligned): tin [0,2ni+1) tres0
+      // [2n+2,2n+2+ni) tres1 [3n+2,3n+2+ni) tx [4n+2,4n+3+2ni).
+      double* base = ps.base;
+      auto align16 = [](double* p) {
+        return reinterpret_cast<float4*>((reinterpret_cast<uintptr_t>(p) + 15) & ~(uintptr_t)15);
+      };
+      float4* tin = align16(base);
+      int w = 0;
+      for (int r0 = 0; r0 < n; r0 += 64 * kSeqU * NW) {
+        const int b0 = r0 + wv * 64 * kSeqU;
+        uint8_t mk[kSeqU];
+        double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
+#pragma unroll
+        for (int u = 0; u < kSeqU; ++u) {
+          const int i = b0 + 64 * u + lane, ic = min(i, n - 1);
+          mk[u] = i < n ? mask[ic] : 0;
+          a0[u] = xy1[2 * ic];
+          a1[u] = xy1[2 * ic + 1];
+          c0[u] = xy2[2 * ic];
+          c1[u] = xy2[2 * ic + 1];
+        }
+        uint64_t bal[kSeqU];
+        int wc = 0;
+#pragma unroll
+        for (int u = 0; u < kSeqU; ++u) {
+          bal[u] = __ballot(mk[u] != 0);
+          wc += __popcll(bal[u]);
+        }
+        int before = 0, total = wc;
+        if (NW > 1) {
+          if (lane == 0) s.redi[wv] = wc;
+          __syncthreads();
+          total = 0;
+#pragma unroll
+          for (int q = 0; q < NW; ++q) {
+            const int x = s.redi[q];
+            before += q < wv ? x : 0;
+            total += x;
+          }
+          __syncthreads();
+        }
+        int o = w + before;
+#pragma unroll
+        for (int u = 0; u < kSeqU; ++u) {
+          if (mk[u]) {
+            const int o2 = o + (int)__builtin_amdgcn_mbcnt_hi(
+                                   (uint32_t)(bal[u] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
+            tin[o2] = make_float4((float)a0[u], (float)a1[u], (float)c0[u], (float)c1[u]);
+          }
+          o += __popcll(bal[u]);
+        }
+        w += total;
+      }
+      if (NW > 1) __syncthreads();
+      mt_load(s, st);
+      const RansacResult rt = loransac_wave<KIND_T, NW>(s, sidx, tin, ni, P.max_trials_T, P,
+                                                    base + 2 * n + 2, base + 3 * n + 2,
+                                                    align16(base + 4 * n + 2), ps.snap,
+                                                    base + 10 * n, pf, scrib ? fsidx : nullptr);
+      const double iratio = (double)rt.num_inliers / (double)ni;
+      return iratio >= P.watermark_min_inlier_ratio ? 1 : 0;
+    }
+  };
+  if (phase == 3) {
+    const int wm = P.detect_watermark && f_ok
+                       ? detect_wm(src == 2 ? spec_state + (int64_t)blockIdx.x * kVerifyStateWords
+                                            : ps.state)
+                       : 0;
+    if (threadIdx.x == 0) {
+      o->spec_wm = wm;
+      o->spec = src;
+    }
+    return;
+  }
+  // a decision phase 3 took (thread 0 reads, every thread uses it)
+  if (threadIdx.x == 0) {
+    const int sp = o->spec;
+    s.redi[14] = (sp == 1 || (sp == 2 && !rstH[blockIdx.x].aborted)) ? 1 + o->spec_wm : 0;
+  }
+  __syncthreads();
+  const int known = s.redi[14];
+  __syncthreads();
   int config, num_inliers = 0, watermark = 0;
   if ((!f_ok && !h_ok) || (f_in < mni && h_in < mni)) {
     config = SCM_TVG_DEGENERATE;
@@ -1747,110 +1882,13 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
     config = ratio > P.max_H_inlier_ratio ? SCM_TVG_PLANAR_OR_PANORAMIC : SCM_TVG_UNCALIBRATED;
     num_inliers = f_ok ? f_in : 0;
     if (P.detect_watermark && f_ok) {
-      // DetectWatermark with the dummy cameras (width = height = 0): a point
-      // is inside the [0,0]x[0,0] box only if it is exactly (0, 0).
-      int nb = 0;
-      for (int b = wv * 64 * kSeqU + lane; b < n; b += 64 * kSeqU * NW) {
-        uint8_t mk[kSeqU];
-        double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
-#pragma unroll
-        for (int u = 0; u < kSeqU; ++u) {
-          const int i = min(b + 64 * u, n - 1);
-          mk[u] = b + 64 * u < n ? mask[i] : 0;
-          a0[u] = xy1[2 * i];
-          a1[u] = xy1[2 * i + 1];
-          c0[u] = xy2[2 * i];
-          c1[u] = xy2[2 * i + 1];
-        }
-#pragma unroll
-        for (int u = 0; u < kSeqU; ++u) {
-          const bool in1 = a0[u] >= 0.0 && a0[u] <= 0.0 && a1[u] >= 0.0 && a1[u] <= 0.0;
-          const bool in2 = c0[u] >= 0.0 && c0[u] <= 0.0 && c1[u] >= 0.0 && c1[u] <= 0.0;
-          nb += (mk[u] && !in1 && !in2) ? 1 : 0;
-        }
-      }
-      nb = wave_sum_i(nb);
-      if (NW > 1) {
-        if (lane == 0) s.redi[wv] = nb;
-        __syncthreads();
-        nb = 0;
-#pragma unroll
-        for (int w = 0; w < NW; ++w) nb += s.redi[w];
-        __syncthreads();
-      }
-      const int ni = f_in;
-      const double bratio = (double)nb / (double)ni;
-      if (!(bratio < P.watermark_min_inlier_ratio)) {
-        // Inlier points in index order -> translation LO-RANSAC, on packed
-        // fp32 points (the doubles are widened float32 keypoints: exact both
-        // ways; half the bytes of every point loop).  Scratch layout (10n
-        // doubles; float4 arrays 16-B aligned): tin [0,2ni+1) tres0
-        // [2n+2,2n+2+ni) tres1 [3n+2,3n+2+ni) tx [4n+2,4n+3+2ni).
-        double* base = ps.base;
-        auto align16 = [](double* p) {
-          return reinterpret_cast<float4*>((reinterpret_cast<uintptr_t>(p) + 15) & ~(uintptr_t)15);
-        };
-        float4* tin = align16(base);
-        int w = 0;
-        for (int r0 = 0; r0 < n; r0 += 64 * kSeqU * NW) {
-          const int b0 = r0 + wv * 64 * kSeqU;
-          uint8_t mk[kSeqU];
-          double a0[kSeqU], a1[kSeqU], c0[kSeqU], c1[kSeqU];
-#pragma unroll
-          for (int u = 0; u < kSeqU; ++u) {
-            const int i = b0 + 64 * u + lane, ic = min(i, n - 1);
-            mk[u] = i < n ? mask[ic] : 0;
-            a0[u] = xy1[2 * ic];
-            a1[u] = xy1[2 * ic + 1];
-            c0[u] = xy2[2 * ic];
-            c1[u] = xy2[2 * ic + 1];
-          }
-          uint64_t bal[kSeqU];
-          int wc = 0;
-#pragma unroll
-          for (int u = 0; u < kSeqU; ++u) {
-            bal[u] = __ballot(mk[u] != 0);
-            wc += __popcll(bal[u]);
-          }
-          int before = 0, total = wc;
-          if (NW > 1) {
-            if (lane == 0) s.redi[wv] = wc;
-            __syncthreads();
-            total = 0;
-#pragma unroll
-            for (int q = 0; q < NW; ++q) {
-              const int x = s.redi[q];
-              before += q < wv ? x : 0;
-              total += x;
-            }
-            __syncthreads();
-          }
-          int o = w + before;
-#pragma unroll
-          for (int u = 0; u < kSeqU; ++u) {
-            if (mk[u]) {
-              const int o2 = o + (int)__builtin_amdgcn_mbcnt_hi(
-                                     (uint32_t)(bal[u] >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal[u], 0u));
-              tin[o2] = make_float4((float)a0[u], (float)a1[u], (float)c0[u], (float)c1[u]);
-            }
-            o += __popcll(bal[u]);
-          }
-          w += total;
-        }
-        if (NW > 1) __syncthreads();
-        mt_load(s, ps.state);
-        const RansacResult rt = loransac_wave<KIND_T, NW>(s, sidx, tin, ni, P.max_trials_T, P,
-                                                      base + 2 * n + 2, base + 3 * n + 2,
-                                                      align16(base + 4 * n + 2), ps.snap,
-                                                      base + 10 * n, pf, scrib ? fsidx : nullptr);
-        const double iratio = (double)rt.num_inliers / (double)ni;
-        if (iratio >= P.watermark_min_inlier_ratio) {
-          config = SCM_TVG_WATERMARK;
-          watermark = 1;
-        }
+      if (known ? known - 1 : detect_wm(ps.state)) {
+        config = SCM_TVG_WATERMARK;
+        watermark = 1;
       }
     }
   }
+  if (threadIdx.x == 0) o->spec = 0;
   // Post-filter (sequential_matching.cc:173-178): TwoViewGeometry().
   const bool keep = num_inliers >= mni;
   if (threadIdx.x == 0) {
@@ -1979,6 +2017,8 @@ __device__ __attribute__((always_inline)) void rs_begin_body(
       st.evals = 0;
       st.done = (n < Tr::kmin || st.max_trials <= 0) ? 1 : 0;
       st.pad_ = 0;
+      st.aborted = 0;
+      if (K == KIND_F) ps.o->spec = 0;  // (verify_final_kernel phase 3)
       st.best_sum = 1.7976931348623157e308;  // Support() default: DBL_MAX
       st.S = (double)smax;
 #pragma unroll
@@ -2172,6 +2212,10 @@ size_t wave_shuffle_lds_bytes(int stride) {
   return (size_t)64 * kWsTab * 4 + (size_t)kWsC * kWsRow * 16 + 64 * 8 * 2 +
          (size_t)(stride + 64) * 2;
 }
+
+// The window's first trial, beside its start state in wsnap (decoupled draws:
+// rs_prune_body reads it while later windows' draws advance dtrial).
+constexpr int kWsnapFirst = 632;
 
 // DRAW: the window's draws (rs_draw_body's work: RandomSampler targets from
 // the pair's PRNG stream, round snapshots for the abort rewind, the trial
@@ -2438,6 +2482,7 @@ __device__ __attribute__((always_inline)) void rs_shuffle_wave_body(
       }
       if (lane == 0) {
         wB[q] = Btot;
+        dr.wsnap[(int64_t)q * 640 + kWsnapFirst] = (uint32_t)dr.dtrial[q];
         dr.dtrial[q] += Btot;
       }
     }
@@ -2486,9 +2531,9 @@ __global__ __launch_bounds__(64) void rs_drawshuffle_wave2_kernel(
 // (aclr) is cleared, and a pair certain to stop in window r - 1 (the bound of
 // rs_draw_body's speculative skip, over window r - 1's counts) gets no trials
 // in window r (wB = 0: its solves and scores exit; its draws are never used,
-// since window r - 1's replay rewinds the pair's PRNG to its stop).  At this
-// point dtrial holds the draws through window r exactly (window r + 1's draws
-// wait for this kernel), so window r - 1's last trial is dtrial - wB - 1.
+// since window r - 1's replay rewinds the pair's PRNG to its stop).  Window
+// r - 1's last trial is the one before window r's first (kept by its draws in
+// wsnap: later windows' draws may already have advanced dtrial).
 template <int K>
 __device__ __forceinline__ void rs_prune_body(const VerifyPair* __restrict__ pairs,
                                               const VerifyRoundBufs& rb, int ain,
@@ -2507,7 +2552,7 @@ __device__ __forceinline__ void rs_prune_body(const VerifyPair* __restrict__ pai
     for (int i = lane; i < Bp * Tr::mm; i += 64) cm = max(cm, pc[i]);
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) cm = max(cm, (uint32_t)__shfl_xor((int)cm, d));
-    const int last = rb.dtrial[q] - B - 1;
+    const int last = (int)rb.wsnap[(int64_t)q * 640 + kWsnapFirst] - 1;
     const uint64_t bound = num_trials((uint64_t)cm, (uint64_t)pairs[q].m, P.confidence,
                                       P.dyn_num_trials_multiplier, Tr::kmin);
     if (last >= P.min_num_trials && (uint64_t)last >= bound && lane == 0) rb.wB[q] = 0;
@@ -3298,6 +3343,7 @@ __device__ __attribute__((always_inline)) void rs_replay_body(
       mt_save(s, ps.state);
       st.num_trials = abort_trial + 2;
       st.done = 1;
+      st.aborted = 1;
     } else {
       st.trial = trial + Btot;
       st.num_trials = st.trial;
@@ -3505,13 +3551,22 @@ int wave_pairs_limit() {
 // nothing else changes: the draws count their own trials (dtrial), read and
 // write their parity's PRNG state, and the replay alone decides the pair's
 // state, output and final PRNG state.
+//
+// np parities of window buffers (window r: rb[r % np]): 2, or 3 with decoupled
+// draws, which then run two windows ahead of the replays -- window r's draws
+// wait for the replay of window r - 3 (the last user of their parity's
+// buffers) and take the pairs running after it (list (r - 2) % 3; before any
+// replay, the begin kernel's list 0), a superset of the pairs its solves and
+// scores take (list (r - 1) % 3, after window r - 2's replay, as above).  A
+// pair drawn but no longer running is simply not read: its draws touch only
+// its parity's buffers, its sample-index vectors and dtrial.
 hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, const double* xy2,
                        double* scratch, uint32_t* snaps, uint8_t* masks, VerifyOut* out,
                        const VerifyParams& P, const float4* xyf, const VerifyRoundBufs* rfp,
                        const VerifyRoundBufs* rhp, int max_chunks, int max_m, uint64_t* prof,
                        hipStream_t stream, hipEvent_t* score_ev, int* nwin, bool spec,
                        hipStream_t rstream, hipEvent_t* win_ev, int* last_h,
-                       hipStream_t dstream, hipEvent_t* draw_ev) {
+                       hipStream_t dstream, hipEvent_t* draw_ev, int np) {
   const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
   const int gw = npairs < kPairGrid ? npairs : kPairGrid;
   constexpr int kShuffleLdsKb = 16;
@@ -3587,8 +3642,8 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   if (dsplit) (void)hipEventRecord(draw_ev[2 * kMaxVerifyWindows], stream);
   int covered_f = 0, covered_h = 0, r = 0;
   while (covered_f < P.max_trials_F || covered_h < P.max_trials_H) {
-    const VerifyRoundBufs& rf = rfp[r & 1];
-    const VerifyRoundBufs& rh = rhp[r & 1];
+    const VerifyRoundBufs& rf = rfp[r % np];
+    const VerifyRoundBufs& rh = rhp[r % np];
     // lists: the replay's input and output, the wide kernels' input
     const int lin = r % 3, lout = (r + 1) % 3;
     const int lw = spec && r > 0 ? (r - 1) % 3 : lin;
@@ -3599,10 +3654,22 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     const int g1 = (f ? gw : 0) + (h ? gw : 0), s1 = f ? gw : 0;
     const int g2 = (f ? sh_blocks : 0) + (h ? sh_blocks : 0), s2 = f ? sh_blocks : 0;
     if (dsplit && r < kMaxVerifyWindows) {
-      if (r >= 2) (void)hipStreamWaitEvent(dstream, win_ev[2 * (r - 2) + 1], 0);
-      (void)hipStreamWaitEvent(dstream, draw_ev[r == 0 ? 2 * kMaxVerifyWindows : 2 * r - 1], 0);
+      int ld = lw;  // the list the draws take
+      if (np == 3) {
+        // two windows ahead (above), and after window r - 2's prune, the last
+        // reader of this parity's counts and trial counts (as the previous
+        // window's); not window r - 1's prune (it reads the first trial its
+        // own draws kept, not dtrial)
+        if (r >= 3) (void)hipStreamWaitEvent(dstream, win_ev[2 * (r - 3) + 1], 0);
+        if (r >= 2) (void)hipStreamWaitEvent(dstream, draw_ev[2 * (r - 2) + 1], 0);
+        if (r == 0) (void)hipStreamWaitEvent(dstream, draw_ev[2 * kMaxVerifyWindows], 0);
+        ld = r < 2 ? 0 : (r - 2) % 3;
+      } else {
+        if (r >= 2) (void)hipStreamWaitEvent(dstream, win_ev[2 * (r - 2) + 1], 0);
+        (void)hipStreamWaitEvent(dstream, draw_ev[r == 0 ? 2 * kMaxVerifyWindows : 2 * r - 1], 0);
+      }
       hipLaunchKernelGGL(rs_drawshuffle_wave2_kernel, dim3(g1), dim3(64), kWsDrawHead + wave_lds,
-                         dstream, pairs, scratch, snaps, out, rf, rh, lw, lout, P, 0, Wf, Wh, prof,
+                         dstream, pairs, scratch, snaps, out, rf, rh, ld, lout, P, 0, Wf, Wh, prof,
                          wave_stride, s1, 0);
       (void)hipEventRecord(draw_ev[2 * r], dstream);
       (void)hipStreamWaitEvent(stream, draw_ev[2 * r], 0);
@@ -3688,20 +3755,22 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     // windows (where nearly all new bests occur), in parallel, before the
     // replay (rs_lo_chain2_kernel); later windows' replays run their few
     // chains inline (their slots are not read: lo = nullptr).
-    VerifyRoundBufs rfr = rf, rhr = rh;
-    const bool lo_win = wave_sh && rf.lo && rh.lo && r < lo_windows;
-    if (lo_win) {
-      const int ls = f ? npairs * kLoSlots : 0;
-      hipLaunchKernelGGL(rs_lo_chain2_kernel, dim3(ls + (h ? npairs * kLoSlots : 0)), dim3(256), lds,
-                         stream, pairs, scratch, snaps, out, rf, rh, lw, P, xyf, ls);
-    } else {
-      rfr.lo = rhr.lo = nullptr;
-    }
     hipStream_t rs = stream;
     if (spec && r < kMaxVerifyWindows) {
       (void)hipEventRecord(win_ev[2 * r], stream);
       (void)hipStreamWaitEvent(rstream, win_ev[2 * r], 0);
       rs = rstream;
+    }
+    // (on the replay's stream: the next window's solves and scores do not wait
+    // for the chains; over the replay's input list, complete there)
+    VerifyRoundBufs rfr = rf, rhr = rh;
+    const bool lo_win = wave_sh && rf.lo && rh.lo && r < lo_windows;
+    if (lo_win) {
+      const int ls = f ? npairs * kLoSlots : 0;
+      hipLaunchKernelGGL(rs_lo_chain2_kernel, dim3(ls + (h ? npairs * kLoSlots : 0)), dim3(256), lds,
+                         rs, pairs, scratch, snaps, out, rf, rh, lin, P, xyf, ls);
+    } else {
+      rfr.lo = rhr.lo = nullptr;
     }
     if (wave_sh)
       hipLaunchKernelGGL(rs_replay2w_kernel, dim3(g1), dim3(256), lds, rs, pairs, scratch,
@@ -3732,6 +3801,24 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
 }  // namespace
 
 int verify_small_batch_pairs() { return wave_pairs_limit(); }
+
+// SCM_THREE_PARITIES=0 (diagnostics): decoupled draws one window ahead only.
+static bool three_parities_off() {
+  static const bool v = [] {
+    const char* e = getenv("SCM_THREE_PARITIES");
+    return e && e[0] == '0';
+  }();
+  return v;
+}
+
+// SCM_SPEC_WATERMARK=0 (diagnostics): no speculative watermark pass.
+static bool spec_wm_off() {
+  static const bool v = [] {
+    const char* e = getenv("SCM_SPEC_WATERMARK");
+    return e && e[0] == '0';
+  }();
+  return v;
+}
 
 bool verify_small_batch(int npairs, int max_m) {
   return npairs <= wave_pairs_limit() && (max_m + 7) / 8 * 8 <= kWsMaxStride;
@@ -3769,14 +3856,24 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   // windows then run strictly in order on one stream).
   const bool sp = spec && spec->rb_f1 && spec->rb_h1 && spec->rstream && spec->win_ev &&
                   spec->fstream && spec->fin_ev && verify_small_batch(npairs, max_m);
-  VerifyRoundBufs rfp[2] = {rb_f, sp ? *spec->rb_f1 : rb_f};
-  VerifyRoundBufs rhp[2] = {rb_h, sp ? *spec->rb_h1 : rb_h};
-  for (VerifyRoundBufs* b : {&rfp[0], &rfp[1], &rhp[0], &rhp[1]}) {
-    const VerifyRoundBufs& o = b == &rfp[0] ? rfp[1] : b == &rfp[1] ? rfp[0]
-                             : b == &rhp[0] ? rhp[1] : rhp[0];
-    b->pstate = o.wstate;
-    b->pcnts = o.cnts;
-    b->pwB = o.wB;
+  // A third parity with decoupled draws (run_windows: they run two windows ahead).
+  const int np = sp && spec->dstream && spec->draw_ev && spec->rb_f2 && spec->rb_h2 &&
+                         !three_parities_off()
+                     ? 3
+                     : 2;
+  VerifyRoundBufs rfp[3] = {rb_f, sp ? *spec->rb_f1 : rb_f, np == 3 ? *spec->rb_f2 : rb_f};
+  VerifyRoundBufs rhp[3] = {rb_h, sp ? *spec->rb_h1 : rb_h, np == 3 ? *spec->rb_h2 : rb_h};
+  // each parity's draws start from the previous parity's state; its prune and
+  // speculative skip read the previous window's counts
+  VerifyRoundBufs pf[3] = {rfp[0], rfp[1], rfp[2]}, ph[3] = {rhp[0], rhp[1], rhp[2]};
+  for (int k = 0; k < np; ++k) {
+    const int o = (k + np - 1) % np;
+    rfp[k].pstate = pf[o].wstate;
+    rfp[k].pcnts = pf[o].cnts;
+    rfp[k].pwB = pf[o].wB;
+    rhp[k].pstate = ph[o].wstate;
+    rhp[k].pcnts = ph[o].cnts;
+    rhp[k].pwB = ph[o].wB;
   }
   // LORANSAC<7-pt, 8-pt> (F, then its inlier masks) and LORANSAC<H, H>, each
   // on its own PRNG stream, advanced together window by window.
@@ -3788,7 +3885,7 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   if ((err = run_windows(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf, rfp,
                          rhp, max_chunks, max_m, prof, stream, score_ev, nwin, sp,
                          sp ? spec->rstream : stream, sp ? spec->win_ev : nullptr, &last_h,
-                         sp ? spec->dstream : nullptr, sp ? spec->draw_ev : nullptr)) !=
+                         sp ? spec->dstream : nullptr, sp ? spec->draw_ev : nullptr, np)) !=
       hipSuccess)
     return err;
   // Diagnostics: SCM_DIAG_SCRIBBLE_F_SIDX=1 makes the final kernel rewrite the
@@ -3803,23 +3900,33 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     // then the rest after the last window.  Nothing orders this pass against
     // the later windows' F draws on dstream: the watermark's index vector is
     // in the pair's H area (verify_final_kernel), which they never touch.
+    // Before it, the speculative watermark decisions (phase 3): once H's last
+    // window is drawn and the window before it replayed (F done for the near
+    // pairs), beside H's last window's solves, scores and replay.
+    if (last_h >= 1 && spec->dstream && spec->draw_ev && !spec_wm_off()) {
+      (void)hipStreamWaitEvent(spec->fstream, spec->draw_ev[2 * last_h], 0);
+      (void)hipStreamWaitEvent(spec->fstream, spec->win_ev[2 * (last_h - 1) + 1], 0);
+      hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, spec->fstream,
+                         pairs, xy1, xy2, scratch, snaps, masks, out, params, prof, counts,
+                         rb_f.rst, rb_h.rst, 3 | diag, rhp[last_h % np].wstate);
+    }
     (void)hipStreamWaitEvent(spec->fstream, spec->win_ev[2 * last_h + 1], 0);
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, spec->fstream, pairs,
                        xy1, xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst,
-                       rb_h.rst, 1 | diag);
+                       rb_h.rst, 1 | diag, nullptr);
     (void)hipEventRecord(spec->fin_ev, spec->fstream);
     (void)hipStreamWaitEvent(stream, spec->fin_ev, 0);
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, stream, pairs, xy1,
                        xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,
-                       2 | diag);
+                       2 | diag, nullptr);
   } else if (verify_small_batch(npairs, max_m)) {
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, stream, pairs, xy1,
                        xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,
-                       diag);
+                       diag, nullptr);
   } else {
     hipLaunchKernelGGL(verify_final_kernel<1>, dim3(npairs), dim3(kVerifyThreads), lds, stream,
                        pairs, xy1, xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst,
-                       rb_h.rst, diag);
+                       rb_h.rst, diag, nullptr);
   }
   return hipGetLastError();
 }
