@@ -323,6 +323,7 @@ struct BatchSet {
   hipEvent_t wev[2 * kMaxVerifyWindows] = {};
   hipEvent_t dev[2 * kMaxVerifyWindows + 1] = {};  // decoupled draws (VerifySpec::draw_ev)
   hipEvent_t fev = nullptr;
+  hipEvent_t spev = nullptr;  // the speculative watermark pass done (VerifySpec::spec_ev)
   HostBuf stage, vstage;
   PinnedOut out;
   size_t off_counts = 0, off_offsets = 0, off_vout = 0, off_matches = 0, off_masks = 0;
@@ -374,6 +375,8 @@ struct BatchSet {
     }
     if (fev) (void)hipEventDestroy(fev);
     fev = nullptr;
+    if (spev) (void)hipEventDestroy(spev);
+    spev = nullptr;
   }
 };
 
@@ -1300,6 +1303,8 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
 
       if (!bs.fev)
         SCM_HIP(hipEventCreateWithFlags(&bs.fev, hipEventDisableTiming | hipEventReleaseToDevice));
+      if (!bs.spev)
+        SCM_HIP(hipEventCreateWithFlags(&bs.spev, hipEventDisableTiming | hipEventReleaseToDevice));
       if (!ctx->serial) {
         spec.rb_f1 = &rbf1;
         spec.rb_h1 = &rbh1;
@@ -1307,6 +1312,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
         spec.win_ev = bs.wev;
         spec.fstream = bs.fstream;
         spec.fin_ev = bs.fev;
+        spec.spec_ev = bs.spev;
         // The windows' draws run ahead on the matching stream (a small
         // batch's matching is done before its verification starts; on the
         // early-final stream they held that pass back).  SCM_DRAW_STREAM=0

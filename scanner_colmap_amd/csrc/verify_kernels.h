@@ -167,6 +167,10 @@ struct VerifySpec {
   hipEvent_t* win_ev = nullptr;
   hipStream_t fstream = nullptr;
   hipEvent_t fin_ev = nullptr;
+  // (optional) the speculative watermark pass done: with it the last final
+  // pass waits for that pass only and runs beside the early one, the two
+  // claiming pairs (RansacState::pad_)
+  hipEvent_t spec_ev = nullptr;
   // Decoupled draws (optional): window r's draws run on dstream beside window
   // r - 1's scoring; draw_ev: 2 * kMaxVerifyWindows + 1 events.
   hipStream_t dstream = nullptr;

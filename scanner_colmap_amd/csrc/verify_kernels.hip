@@ -1697,7 +1697,9 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
   // phase 1 (early, small batches): only pairs whose F and H RANSACs are both
   // done (read once, by thread 0: the replay of other pairs is still
-  // running), marked in rstF[q].pad_; phase 2: the rest; phase 0: every pair.
+  // running); phase 2: after every window, every pair; each pair is claimed
+  // once, by whichever of the two runs first (rstF[q].pad_, atomically: the
+  // two may run at once).  phase 0: every pair.
   // phase 3 (speculative, small batches; beside H's last window): the
   // watermark decision only, of the pairs whose F is done, into
   // VerifyOut::spec / spec_wm -- from H's final stream state when H is done
@@ -1716,14 +1718,16 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
       const int fd = *reinterpret_cast<volatile const int32_t*>(&rstF[q0].done);
       const int hd = *reinterpret_cast<volatile const int32_t*>(&rstH[q0].done);
       const int mk = *reinterpret_cast<volatile const int32_t*>(&rstF[q0].pad_);
-      s.redi[15] = phase == 1 ? (fd && hd) : phase == 2 ? !mk : (fd ? (hd ? 1 : 2) : 0);
+      int go;
+      if (phase == 3) go = fd ? (hd ? 1 : 2) : 0;
+      else go = (phase == 2 || (fd && hd)) && !mk && atomicCAS(&rstF[q0].pad_, 0, 1) == 0;
+      s.redi[15] = go;
       __threadfence();
     }
     __syncthreads();
     const int go = s.redi[15];
     __syncthreads();
     if (!go) return;
-    if (phase == 1 && threadIdx.x == 0) rstF[blockIdx.x].pad_ = 1;
     if (phase == 3) src = go;
   }
   Prof pf{prof ? prof + (int64_t)blockIdx.x * kVerifyProfSlots : nullptr, &s.prof_t};
@@ -3811,6 +3815,15 @@ static bool three_parities_off() {
   return v;
 }
 
+// SCM_FINAL_BESIDE=0 (diagnostics): the last final pass after the early one.
+static bool final_beside_off() {
+  static const bool v = [] {
+    const char* e = getenv("SCM_FINAL_BESIDE");
+    return e && e[0] == '0';
+  }();
+  return v;
+}
+
 // SCM_SPEC_WATERMARK=0 (diagnostics): no speculative watermark pass.
 static bool spec_wm_off() {
   static const bool v = [] {
@@ -3910,15 +3923,21 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
                          pairs, xy1, xy2, scratch, snaps, masks, out, params, prof, counts,
                          rb_f.rst, rb_h.rst, 3 | diag, rhp[last_h % np].wstate);
     }
+    // Phase 2 waits for phase 1 (the pairs it left), or, with an event after
+    // phase 3, for phase 3 only (it must not run a pair's watermark RANSAC
+    // while phase 3 may) and claims pairs beside phase 1.
+    const bool beside = spec->spec_ev && !final_beside_off();
+    if (beside) (void)hipEventRecord(spec->spec_ev, spec->fstream);
     (void)hipStreamWaitEvent(spec->fstream, spec->win_ev[2 * last_h + 1], 0);
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, spec->fstream, pairs,
                        xy1, xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst,
                        rb_h.rst, 1 | diag, nullptr);
     (void)hipEventRecord(spec->fin_ev, spec->fstream);
-    (void)hipStreamWaitEvent(stream, spec->fin_ev, 0);
+    (void)hipStreamWaitEvent(stream, beside ? spec->spec_ev : spec->fin_ev, 0);
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, stream, pairs, xy1,
                        xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,
                        2 | diag, nullptr);
+    if (beside) (void)hipStreamWaitEvent(stream, spec->fin_ev, 0);
   } else if (verify_small_batch(npairs, max_m)) {
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, stream, pairs, xy1,
                        xy2, scratch, snaps, masks, out, params, prof, counts, rb_f.rst, rb_h.rst,

@@ -51,7 +51,7 @@ def windows(max_f, max_h, smallf=4, second_f=80, maxw=128, tb=64):
     return out
 
 
-def build(max_f, max_h, np_, lo_windows=1, spec_wm=True):
+def build(max_f, max_h, np_, lo_windows=1, spec_wm=True, beside=True):
     """The launch sequence of launch_verify for a small batch with decoupled
     draws (dsplit), np_ parities."""
     S, R, D, FS = "stream", "rstream", "dstream", "fstream"
@@ -154,11 +154,22 @@ def build(max_f, max_h, np_, lo_windows=1, spec_wm=True):
         # runs -- per pair, outside the model)
         seq.append(s.kernel(FS, "final3", {par("wstate", "H", last_h % np_), "sidxH"},
                             {"sidxH", "spec"}))
+    # phases 1 and 2 claim disjoint pairs (atomically, beside each other):
+    # per-pair resources of the pairs each claims (1 / 2); phase 3 may touch
+    # either
+    both = {"sidxH1", "sidxH2", "spec1", "spec2"}
+    if spec_wm and last_h >= 1:
+        s.ops[seq[-1]] = s.ops[seq[-1]][:3] + (s.ops[seq[-1]][3] | both, s.ops[seq[-1]][4] | both)
+    if beside:
+        s.record(FS, "spec")
     s.wait(FS, ("win", last_h, 1))
-    seq.append(s.kernel(FS, "final1", {"stateH", "sidxH", "spec"}, {"sidxH", "spec", "out"}))
+    seq.append(s.kernel(FS, "final1", {"stateH", "sidxH1", "spec1"}, {"sidxH1", "spec1", "out1"}))
     s.record(FS, "fin")
-    s.wait(S, "fin")
-    seq.append(s.kernel(S, "final2", {"stateH", "sidxH", "spec", "out"}, {"sidxH", "spec", "out"}))
+    s.wait(S, "spec" if beside else "fin")
+    seq.append(s.kernel(S, "final2", {"stateH", "sidxH2", "spec2"}, {"sidxH2", "spec2", "out2"}))
+    if beside:
+        s.wait(S, "fin")
+    seq.append(s.kernel(S, "compact", {"out1", "out2"}, {"rows"}))
     s.seq = seq
     return s, wins
 
@@ -258,3 +269,13 @@ def test_speculative_watermark_needs_the_last_h_draws():
     s2 = drop(s, lambda op: op[0] == "fstream" and op[1] == "wait" and op[2][0] == "draw")
     bad = conflicts(s2)
     assert any(a.startswith("draw") and b == "final3" for a, b, _ in bad)
+
+
+def test_last_final_pass_needs_the_speculative_pass():
+    """The last final pass runs beside the early one but after phase 3 (both
+    may run a pair's watermark RANSAC); and the batch's compaction after both."""
+    s, _ = build(10000, 10000, np_=3)
+    s2 = drop(s, lambda op: op[0] == "stream" and op[1] == "wait" and op[2] == "spec")
+    assert any(a == "final3" and b == "final2" for a, b, _ in conflicts(s2))
+    s3 = drop(s, lambda op: op[0] == "stream" and op[1] == "wait" and op[2] == "fin")
+    assert any(a == "final1" and b == "compact" for a, b, _ in conflicts(s3))
