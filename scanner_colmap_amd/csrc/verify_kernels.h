@@ -37,7 +37,7 @@ struct VerifyParams {
   int32_t min_num_inliers;
   int32_t detect_watermark;
   uint32_t base_seed;
-  int32_t pad_;
+  int32_t prio;  // small batches: the latency-bound kernels' waves issue at raised priority
 };
 
 struct VerifyPair {

@@ -1695,6 +1695,7 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
     const uint32_t* __restrict__ spec_state) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
+  if (NW > 1 && P.prio) __builtin_amdgcn_s_setprio(2);
   // phase 1 (early, small batches): only pairs whose F and H RANSACs are both
   // done (read once, by thread 0: the replay of other pairs is still
   // running); phase 2: after every window, every pair; each pair is claimed
@@ -2513,6 +2514,7 @@ __global__ __launch_bounds__(64) void rs_drawshuffle_wave2_kernel(
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
     VerifyRoundBufs rh, int ain, int aclr, VerifyParams P, int spec, int Wf, int Wh,
     uint64_t* __restrict__ prof, int stride, int split, int clr) {
+  if (P.prio) __builtin_amdgcn_s_setprio(2);
   if ((int)blockIdx.x < split) {
     const WsDraw d{rf.rst, rf.nact + aclr, rf.cnts, rf.ucnt, rf.wsnap, rf.pstate, rf.wstate,
                    rf.dtrial, rf.pcnts, rf.pwB, spec, Wf, clr};
@@ -3056,6 +3058,7 @@ __global__ __launch_bounds__(256) void rs_lo_chain2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
     VerifyRoundBufs rh, int ain, VerifyParams P, const float4* __restrict__ xyf_all, int split) {
+  if (P.prio) __builtin_amdgcn_s_setprio(2);
   if ((int)blockIdx.x < split)
     rs_lo_chain_body<KIND_F>(pairs, scratch, snaps, out, rf, ain, P, xyf_all, blockIdx.x);
   else
@@ -3458,6 +3461,7 @@ __global__ __launch_bounds__(256) void rs_replay2w_kernel(
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
     VerifyRoundBufs rf, VerifyRoundBufs rh, int ain, int aout, VerifyParams P,
     uint64_t* __restrict__ prof, const float4* __restrict__ xyf, int split) {
+  if (P.prio) __builtin_amdgcn_s_setprio(2);
   if ((int)blockIdx.x < split)
     rs_replay_body<KIND_F, 4>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[ain], rf.nact + ain,
                               rf.act[aout], rf.nact + aout, rf.nmod, rf.cnts, rf.mods,
@@ -3839,11 +3843,20 @@ bool verify_small_batch(int npairs, int max_m) {
 
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
                          const double* xy2, double* scratch, uint32_t* snaps, uint8_t* masks,
-                         VerifyOut* out, const VerifyParams& params, uint64_t* prof,
+                         VerifyOut* out, const VerifyParams& params_in, uint64_t* prof,
                          const int32_t* counts, const float4* xyf, const VerifyRoundBufs& rb_f,
                          const VerifyRoundBufs& rb_h, hipStream_t stream, hipEvent_t* score_ev,
                          int* nwin, const VerifySpec* spec) {
   if (npairs <= 0) return hipSuccess;
+  // Small batches: the latency-bound kernels (draws, LO chains, replays, final
+  // passes) raise their waves' issue priority over the wide scoring kernels'
+  // (SCM_PRIO=0, diagnostics: not).
+  static const int prio_env = [] {
+    const char* e = getenv("SCM_PRIO");
+    return e ? atoi(e) : 1;
+  }();
+  VerifyParams params = params_in;
+  params.prio = verify_small_batch(npairs, max_m) ? prio_env : 0;
   static bool attr = false;
   if (!attr) {
     const hipError_t es[] = {
