@@ -1695,7 +1695,7 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
     const uint32_t* __restrict__ spec_state) {
   extern __shared__ __attribute__((aligned(16))) uint8_t dyn_lds[];
   VerifyLds& s = *reinterpret_cast<VerifyLds*>(dyn_lds);
-  if (NW > 1 && P.prio) __builtin_amdgcn_s_setprio(2);
+  if (P.prio) __builtin_amdgcn_s_setprio(2);
   // phase 1 (early, small batches): only pairs whose F and H RANSACs are both
   // done (read once, by thread 0: the replay of other pairs is still
   // running); phase 2: after every window, every pair; each pair is claimed
@@ -3415,6 +3415,7 @@ __global__ __launch_bounds__(64) void rs_draw2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
     VerifyRoundBufs rh, int ain, int aclr, VerifyParams P, int spec, int Wf, int Wh, int split) {
+  if (P.prio) __builtin_amdgcn_s_setprio(2);
   if ((int)blockIdx.x < split)
     rs_draw_body<KIND_F>(pairs, scratch, snaps, out, rf.rst, rf.act[ain], rf.nact + ain,
                          rf.nact + aclr, rf.samp, rf.cnts, rf.ucnt, rf.wsnap, rf.wB, rf.pstate,
@@ -3430,7 +3431,8 @@ __global__ __launch_bounds__(64) void rs_draw2_kernel(
 __global__ __launch_bounds__(64) void rs_shuffle2_kernel(
     const VerifyPair* __restrict__ pairs, double* __restrict__ scratch,
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, VerifyRoundBufs rf,
-    VerifyRoundBufs rh, int ain, int ppb, int stride, int split) {
+    VerifyRoundBufs rh, int ain, int ppb, int stride, int split, int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(2);
   if ((int)blockIdx.x < split)
     rs_shuffle_body<KIND_F>(pairs, scratch, snaps, out, rf.wB, rf.act[ain], rf.nact + ain,
                             rf.samp, ppb, stride, blockIdx.x, split, rf.wt);
@@ -3444,6 +3446,7 @@ __global__ __launch_bounds__(64) void rs_replay2_kernel(
     uint32_t* __restrict__ snaps, VerifyOut* __restrict__ out, uint8_t* __restrict__ masks,
     VerifyRoundBufs rf, VerifyRoundBufs rh, int ain, int aout, VerifyParams P,
     uint64_t* __restrict__ prof, const float4* __restrict__ xyf, int split) {
+  if (P.prio) __builtin_amdgcn_s_setprio(2);
   if ((int)blockIdx.x < split)
     rs_replay_body<KIND_F>(pairs, scratch, snaps, out, masks, rf.rst, rf.act[ain], rf.nact + ain,
                            rf.act[aout], rf.nact + aout, rf.nmod, rf.cnts, rf.mods,
@@ -3693,7 +3696,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                          out, rf, rh, lw, lout, P, (spec && r > 0) ? 1 : 0, Wf, Wh, s1);
       hipLaunchKernelGGL(rs_shuffle2_kernel, dim3(g2), dim3(64),
                          (size_t)sh_ppb * sh_stride * sizeof(uint16_t), stream, pairs, scratch,
-                         snaps, out, rf, rh, lw, sh_ppb, sh_stride, s2);
+                         snaps, out, rf, rh, lw, sh_ppb, sh_stride, s2, P.prio);
     }
     if (f)
       hipLaunchKernelGGL(rs_solve_kernel<KIND_F>, dim3(kSolveGrid), dim3(64), 0, stream, pairs, xy1, xy2,
@@ -3855,8 +3858,13 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     const char* e = getenv("SCM_PRIO");
     return e ? atoi(e) : 1;
   }();
+  // (the table path's replay: SCM_PRIO_TABLE=1, diagnostics)
+  static const int prio_table = [] {
+    const char* e = getenv("SCM_PRIO_TABLE");
+    return e ? atoi(e) : 0;
+  }();
   VerifyParams params = params_in;
-  params.prio = verify_small_batch(npairs, max_m) ? prio_env : 0;
+  params.prio = verify_small_batch(npairs, max_m) ? prio_env : prio_table;
   static bool attr = false;
   if (!attr) {
     const hipError_t es[] = {
