@@ -281,7 +281,11 @@ int scm_table_matches(scm_context* ctx, int64_t row, int64_t offset,
  * t[8] / t[9] = host time of the last scm_execute_batch: content keys of its
  * elements, then the image table (reuse + upload staging); t[10] = its
  * pipeline run (GPU stages and their host steps up to the serialised rows),
- * t[11] = building its output blobs. */
+ * t[11] = building its output blobs; t[12..15] = the run's watermark
+ * decisions of small batches taken from the speculative pass / recomputed
+ * and equal / recomputed and different (both with SCM_DIAG_SPEC_CHECK=1) /
+ * speculation void (H aborted in its last window) and recomputed.  n: the
+ * entries the caller holds (at most 16 are written). */
 int scm_table_timings(scm_context* ctx, double* t, int32_t n);
 /* Measurement only: serial != 0 runs the following table runs with matching
  * and verification one after the other instead of overlapped (no stage

@@ -459,9 +459,10 @@ class Context:
         return out[: n.value].copy()
 
     def table_timings(self) -> dict:
-        t = (c_double * 12)()
-        _check(self._lib.scm_table_timings(self._ptr, t, 12))
+        t = (c_double * 16)()
+        _check(self._lib.scm_table_timings(self._ptr, t, 16))
         return {"match_ms": t[0], "finalize_ms": t[1], "verify_ms": t[2], "wall_ms": t[3],
                 "match_launches": int(t[4]), "score_ms": t[5], "evals_f": int(t[6]),
                 "evals_h": int(t[7]), "hash_ms": t[8], "stage_ms": t[9], "run_ms": t[10],
-                "out_ms": t[11]}
+                "out_ms": t[11], "spec_taken": int(t[12]), "spec_equal": int(t[13]),
+                "spec_differ": int(t[14]), "spec_void": int(t[15])}

@@ -423,6 +423,9 @@ struct scm_context {
   double t_hash = 0, t_stage = 0;  // host time of the last execute_batch: content keys, table
   double t_score = 0;                  // scoring kernels (F + H) of the last run
   int64_t evals_f = 0, evals_h = 0;    // their (model, point) evaluations
+  // small batches' speculative watermark decisions (VerifyOut::spec_check):
+  // taken, recomputed and equal / different (SCM_DIAG_SPEC_CHECK), void
+  int64_t spec_taken = 0, spec_equal = 0, spec_differ = 0, spec_void = 0;
   int64_t n_match_launches = 0;  // matcher kernel launches of the last table run
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
   bool profile = false;
@@ -1396,6 +1399,11 @@ int collect_batch(scm_context* ctx, BatchSet& bs, BatchView* v) {
     for (int64_t p = 0; p < bs.P; ++p) {
       ctx->evals_f += v->vout[p].f_evals;
       ctx->evals_h += v->vout[p].h_evals;
+      const int32_t sc = v->vout[p].spec_check;
+      ctx->spec_taken += sc == 3;
+      ctx->spec_equal += sc == 1;
+      ctx->spec_differ += sc == 2;
+      ctx->spec_void += sc == 4;
     }
   if (ctx->profile && bs.verify && bs.nprof > 0) {
     std::vector<uint64_t> pr(bs.nprof * kVerifyProfSlots);
@@ -2289,6 +2297,7 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
   }
   ctx->t_match = ctx->t_final = ctx->t_verify = ctx->t_score = 0.0;
   ctx->evals_f = ctx->evals_h = 0;
+  ctx->spec_taken = ctx->spec_equal = ctx->spec_differ = ctx->spec_void = 0;
   ctx->n_match_launches = 0;
   Packed pk;
   const auto h2 = std::chrono::steady_clock::now();
@@ -2444,6 +2453,7 @@ static int table_run_common(scm_context* ctx, int64_t overlap, int64_t row_begin
   SCM_HIP(hipSetDevice(ctx->device));
   ctx->t_match = ctx->t_final = ctx->t_verify = ctx->t_score = 0.0;
   ctx->evals_f = ctx->evals_h = 0;
+  ctx->spec_taken = ctx->spec_equal = ctx->spec_differ = ctx->spec_void = 0;
   ctx->n_match_launches = 0;
   const auto w0 = std::chrono::steady_clock::now();
   const int rc = run_table(ctx, overlap, row_begin, row_end, pk, chunk_emit);
@@ -2549,6 +2559,7 @@ int scm_table_run_passes(scm_context* ctx, int64_t overlap, int64_t row_begin, i
   SCM_HIP(hipSetDevice(ctx->device));
   ctx->t_match = ctx->t_final = ctx->t_verify = ctx->t_score = 0.0;
   ctx->evals_f = ctx->evals_h = 0;
+  ctx->spec_taken = ctx->spec_equal = ctx->spec_differ = ctx->spec_void = 0;
   ctx->n_match_launches = 0;
   const auto w0 = std::chrono::steady_clock::now();
   // the stencil plan of the range (run_table), repeated `passes` times
@@ -2701,10 +2712,12 @@ int scm_table_timings(scm_context* ctx, double* t, int32_t n) {
     set_error("invalid arguments");
     return SCM_E_INVALID;
   }
-  const double v[12] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall,
+  const double v[16] = {ctx->t_match, ctx->t_final, ctx->t_verify, ctx->t_wall,
                         (double)ctx->n_match_launches, ctx->t_score, (double)ctx->evals_f,
-                        (double)ctx->evals_h, ctx->t_hash, ctx->t_stage, ctx->t_run, ctx->t_out};
-  for (int32_t i = 0; i < n && i < 12; ++i) t[i] = v[i];
+                        (double)ctx->evals_h, ctx->t_hash, ctx->t_stage, ctx->t_run, ctx->t_out,
+                        (double)ctx->spec_taken, (double)ctx->spec_equal, (double)ctx->spec_differ,
+                        (double)ctx->spec_void};
+  for (int32_t i = 0; i < n && i < 16; ++i) t[i] = v[i];
   return SCM_OK;
 }
 

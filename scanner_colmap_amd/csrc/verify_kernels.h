@@ -69,6 +69,12 @@ struct VerifyOut {
   // after H's last window's draws (valid unless that window's replay aborted
   // H); spec_wm the decision.
   int32_t spec, spec_wm;
+  // How phases 1 / 2 took the watermark decision (counted by the runtime):
+  // 0 no speculation, 3 the speculative decision, 1 the speculative decision
+  // recomputed and equal (SCM_DIAG_SPEC_CHECK=1), 2 recomputed and different
+  // (never: a test asserts it), 4 the speculation void (H aborted in its
+  // last window) and recomputed.
+  int32_t spec_check, pad3_;
 };
 
 // Per-pair state of the round-synchronous LO-RANSAC (verify_kernels.hip).

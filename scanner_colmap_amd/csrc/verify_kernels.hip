@@ -1709,8 +1709,11 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
   // aborts H (RansacState::aborted).  Phases 1 / 2 take the decision when
   // spec is 1, or 2 and H did not abort, and run the watermark RANSAC
   // otherwise: the same decision either way.
-  // Bit 8 of the argument: diagnostics (loransac_wave's scrib).
+  // Bit 8 of the argument: diagnostics (loransac_wave's scrib); bit 16:
+  // diagnostics, phases 1 / 2 recompute a speculative decision they would
+  // take and record whether it was equal (VerifyOut::spec_check).
   const bool scrib = (phase & 8) != 0;
+  const bool chk = (phase & 16) != 0;
   phase &= 3;
   int src = 0;  // phase 3: the decision's state source (1 / 2)
   if (phase != 0) {
@@ -1874,10 +1877,13 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
   // a decision phase 3 took (thread 0 reads, every thread uses it)
   if (threadIdx.x == 0) {
     const int sp = o->spec;
-    s.redi[14] = (sp == 1 || (sp == 2 && !rstH[blockIdx.x].aborted)) ? 1 + o->spec_wm : 0;
+    const bool valid = sp == 1 || (sp == 2 && !rstH[blockIdx.x].aborted);
+    s.redi[14] = valid ? 1 + o->spec_wm : 0;
+    s.redi[13] = sp == 2 && !valid ? 4 : 0;
   }
   __syncthreads();
   const int known = s.redi[14];
+  int check = s.redi[13];
   __syncthreads();
   int config, num_inliers = 0, watermark = 0;
   if ((!f_ok && !h_ok) || (f_in < mni && h_in < mni)) {
@@ -1887,13 +1893,26 @@ __global__ __launch_bounds__(64 * NW) void verify_final_kernel(
     config = ratio > P.max_H_inlier_ratio ? SCM_TVG_PLANAR_OR_PANORAMIC : SCM_TVG_UNCALIBRATED;
     num_inliers = f_ok ? f_in : 0;
     if (P.detect_watermark && f_ok) {
-      if (known ? known - 1 : detect_wm(ps.state)) {
+      int wm;
+      if (known && chk) {
+        wm = detect_wm(ps.state);
+        check = wm == known - 1 ? 1 : 2;
+      } else if (known) {
+        wm = known - 1;
+        check = 3;
+      } else {
+        wm = detect_wm(ps.state);
+      }
+      if (wm) {
         config = SCM_TVG_WATERMARK;
         watermark = 1;
       }
     }
   }
-  if (threadIdx.x == 0) o->spec = 0;
+  if (threadIdx.x == 0) {
+    o->spec = 0;
+    o->spec_check = check;
+  }
   // Post-filter (sequential_matching.cc:173-178): TwoViewGeometry().
   const bool keep = num_inliers >= mni;
   if (threadIdx.x == 0) {
@@ -3927,7 +3946,8 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   // speculative F draws beside the early pass can do; outputs must not move,
   // tests/test_gpu_stencil.py).  Read per call so a test can set it.
   const char* diag_env = getenv("SCM_DIAG_SCRIBBLE_F_SIDX");
-  const int diag = diag_env && atoi(diag_env) ? 8 : 0;
+  const char* chk_env = getenv("SCM_DIAG_SPEC_CHECK");  // (verify_final_kernel bit 16)
+  const int diag = (diag_env && atoi(diag_env) ? 8 : 0) | (chk_env && atoi(chk_env) ? 16 : 0);
   if (sp && last_h >= 0 && last_h < kMaxVerifyWindows) {
     // Configuration + watermark of the pairs done when H's last window is
     // replayed (typically all but the far pairs' F), beside the later windows;

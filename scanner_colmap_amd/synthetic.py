@@ -223,6 +223,11 @@ def geometry_scene(kind: str, num_matches: int, seed: int, outlier_frac: float =
                      the watermark RANSAC's samples: the first match in
                      index order belongs to the 24 % set, so a RANSAC that
                      sampled only it would find 24 % (< 0.7).
+    * "plane_and_depth": a rigid 3-D scene whose first 45 % of points lie on
+                     one plane: F explains every inlier and stops within a few
+                     dozen trials, H only the plane, so its dynamic trial bound
+                     (~500) ends H in the middle of a small batch's second
+                     window -> UNCALIBRATED (3).
 
     Returns (kp1 N x 6, kp2 N x 6, matches M x 2 uint32); keypoint order is
     shuffled so the match indices are not the identity."""
@@ -241,8 +246,10 @@ def geometry_scene(kind: str, num_matches: int, seed: int, outlier_frac: float =
         x2[int(round(0.76 * m)):] += 0.6 * t
     elif kind == "random":
         x2 = np.stack([rng.uniform(0, 1920, m), rng.uniform(0, 1080, m)], axis=1)
-    elif kind in ("general", "two_motions"):
+    elif kind in ("general", "two_motions", "plane_and_depth"):
         X = np.stack([rng.uniform(-4, 4, m), rng.uniform(-2.5, 2.5, m), rng.uniform(6, 20, m)], 1)
+        if kind == "plane_and_depth":
+            X[:int(round(0.45 * m)), 2] = 10.0
         f = 1200.0
 
         def proj(R, c, P=None):

@@ -271,3 +271,53 @@ def test_watermark_index_vector_apart_from_speculative_f_draws(monkeypatch):
             assert ctx.execute_stencil(ids[:4], kps[:4], descs[:4]) == ref_st
         ctx.table_load(ids, kps, descs)  # table path (one final pass after all windows)
         assert ctx.table_run(3, 0, len(imgs)) == ref_tab
+
+
+def test_speculative_watermark_decisions_equal_recomputed(monkeypatch):
+    """A small batch takes a pair's watermark decision early (verify_final_kernel
+    phase 3), beside H's last window: from H's final PRNG state when H is done,
+    else from the state after H's last window's draws, which that window's
+    replay leaves as H's final state unless it aborts H.  The decision is used
+    only when it was taken from H's final state, or H did not abort; otherwise
+    it is void and recomputed.  With SCM_DIAG_SPEC_CHECK=1 every decision the
+    pass would use is recomputed from H's final state and compared
+    (scm_table_timings entries 12-15).
+
+    Scenes: two_translations (WATERMARK decided by the watermark RANSAC's
+    samples, H running its whole trial cap: a draw-state decision that holds),
+    plane_and_depth (F stops at once, H's dynamic bound ends it inside its
+    last window: a void decision), translation (H done early: a final-state
+    decision).  Every row equals the oracle's, no decision differs, and each
+    kind of decision occurs.  Reference: Estimate, then DetectWatermark, per
+    pair (sequential_matching.cc:98-99, 159)."""
+    scenes = [("two_translations", 600, 31, 0.1), ("plane_and_depth", 600, 33, 0.1),
+              ("translation", 500, 35, 0.4)]
+    extra = Corridor(3, 700, 3, seed=36).images()
+    monkeypatch.setenv("SCM_DIAG_SPEC_CHECK", "1")
+    seen = {"spec_equal": 0, "spec_void": 0, "spec_differ": 0}
+    with Context(0) as ctx:
+        for i, (kind, m, seed, out) in enumerate(scenes):
+            kp1, kp2, mt = geometry_scene(kind, m, seed, outlier_frac=out)
+            d1, d2 = descriptors_for_matches(mt, len(kp1), len(kp2), seed)
+            base = 100 * (i + 1)
+            imgs = [(base, kp1, d1), (base + 1, kp2, d2)] + [
+                (base + 2 + j, k, d) for j, (_, k, d) in enumerate(extra)]
+            ids, kps, descs = table_rows(imgs)
+            ref = oracle.execute_stencil(ids[:4], kps[:4], descs[:4])
+            for _ in range(2):
+                assert ctx.execute_stencil(ids[:4], kps[:4], descs[:4]) == ref, kind
+                t = ctx.table_timings()
+                for k in seen:
+                    seen[k] += t[k]
+    assert seen["spec_differ"] == 0, seen
+    assert seen["spec_equal"] > 0 and seen["spec_void"] > 0, seen
+    monkeypatch.delenv("SCM_DIAG_SPEC_CHECK")
+    with Context(0) as ctx:  # without the check the decisions are taken as they are
+        kp1, kp2, mt = geometry_scene("two_translations", 600, 31, outlier_frac=0.1)
+        d1, d2 = descriptors_for_matches(mt, len(kp1), len(kp2), 31)
+        imgs = [(100, kp1, d1), (101, kp2, d2)] + [(102 + j, k, d) for j, (_, k, d) in enumerate(extra)]
+        ids, kps, descs = table_rows(imgs)
+        assert ctx.execute_stencil(ids[:4], kps[:4], descs[:4]) == oracle.execute_stencil(
+            ids[:4], kps[:4], descs[:4])
+        t = ctx.table_timings()
+        assert t["spec_taken"] > 0 and t["spec_equal"] == 0, t
