@@ -923,6 +923,10 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     const uint8_t* __restrict__ desc8, const int32_t* __restrict__ csum,
     const float* __restrict__ lut, float max_ratio, float max_distance, int cross_check,
     uint2* __restrict__ matches, int32_t* __restrict__ counts, int phase) {
+  // bit 4 of phase: raised wave priority (the batch's verification waits for
+  // this chain; launch_match_finalize_g8)
+  if (phase & 4) __builtin_amdgcn_s_setprio(2);
+  phase &= 3;
   __shared__ int32_t wave_tot[kFinThreads / 64];
   __shared__ int32_t bcnt[32], bcur[32];
   const PairDesc pd = pairs[blockIdx.x];
@@ -1069,7 +1073,9 @@ __global__ __launch_bounds__(kRcThreads) void match_rowcheck_g8_kernel(
     const uint2* __restrict__ colpart,
     const uint2* __restrict__ rowaux, const int32_t* __restrict__ rlist,
     const uint8_t* __restrict__ desc8, const int32_t* __restrict__ csum,
-    const float* __restrict__ lut, float max_ratio, float max_distance, int cross_check) {
+    const float* __restrict__ lut, float max_ratio, float max_distance, int cross_check,
+    int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(2);
   __shared__ __attribute__((aligned(16))) uint8_t lcol[kRcChunk * 128];
   __shared__ int32_t lcs[kRcChunk + 32];
   const PairDesc pd = pairs[blockIdx.y];
@@ -1168,7 +1174,8 @@ __global__ __launch_bounds__(kRcThreads) void match_rowcheck_g8_kernel(
 __global__ __launch_bounds__(256) void match_recheck_g8_kernel(
     const PairDesc* __restrict__ pairs, uint2* __restrict__ rowres, uint2* __restrict__ colpart,
     const uint8_t* __restrict__ desc8, const int32_t* __restrict__ csum,
-    const float* __restrict__ lut, float max_ratio, float max_distance) {
+    const float* __restrict__ lut, float max_ratio, float max_distance, int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(2);
   __shared__ int32_t cand_lane[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = lane & 31, h = lane >> 5;
@@ -1322,19 +1329,27 @@ hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* ro
                                     int cross_check, uint2* matches, int32_t* counts,
                                     int max_groups, hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
+  // The finalize chain's waves at raised issue priority over the verification
+  // kernels of earlier batches beside it: the batch's own verification waits
+  // for this chain (SCM_PRIO_MATCH=0, diagnostics: not).
+  static const int prio = [] {
+    const char* e = getenv("SCM_PRIO_MATCH");
+    return e ? atoi(e) : 1;
+  }();
+  const int pbit = prio ? 4 : 0;
   hipLaunchKernelGGL(match_finalize_g8_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
                      rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
-                     cross_check, matches, counts, 0);
+                     cross_check, matches, counts, 0 | pbit);
   hipLaunchKernelGGL(match_rowcheck_g8_kernel, dim3(32, npairs), dim3(kRcThreads), 0, stream,
                      pairs, rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
-                     cross_check);
+                     cross_check, prio);
   if (cross_check && max_groups > 0)
     hipLaunchKernelGGL(match_recheck_g8_kernel, dim3((unsigned)((max_groups + 3) / 4), npairs),
                        dim3(256), 0, stream, pairs, rowres, colpart, desc8, csum, lut, max_ratio,
-                       max_distance);
+                       max_distance, prio);
   hipLaunchKernelGGL(match_finalize_g8_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
                      rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
-                     cross_check, matches, counts, 1);
+                     cross_check, matches, counts, 1 | pbit);
   return hipGetLastError();
 }
 
