@@ -593,7 +593,9 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
     const int32_t* __restrict__ csum,   // 128 * sum_d a_d per row
     const MatchJob* __restrict__ jobs, const PairDesc* __restrict__ pairs,
     uint2* __restrict__ rowres,         // per pair [nseg][n1]
-    uint2* __restrict__ colpart) {      // per pair [nrb][n2pad]
+    uint2* __restrict__ colpart,        // per pair [nrb][n2pad]
+    int prio) {                         // raised wave priority (launch_match_g8)
+  if (prio) __builtin_amdgcn_s_setprio(1);
   // One array for every LDS use (a second __shared__ object can make the
   // compiler drain the LDS-DMA queue before each ds_read).
   __shared__ __attribute__((aligned(16))) uint8_t lds[kG8LdsBytes];
@@ -1311,14 +1313,14 @@ hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int nj
 
 hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
                            int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
-                           bool clamp, hipStream_t stream) {
+                           bool clamp, hipStream_t stream, int prio) {
   if (njobs <= 0) return hipSuccess;
   if (clamp)
     hipLaunchKernelGGL(match_g8_kernel<true>, dim3(njobs), dim3(kMatch8Threads), 0, stream, desc8,
-                       csum, jobs, pairs, rowres, colpart);
+                       csum, jobs, pairs, rowres, colpart, prio);
   else
     hipLaunchKernelGGL(match_g8_kernel<false>, dim3(njobs), dim3(kMatch8Threads), 0, stream, desc8,
-                       csum, jobs, pairs, rowres, colpart);
+                       csum, jobs, pairs, rowres, colpart, prio);
   return hipGetLastError();
 }
 

@@ -426,6 +426,9 @@ struct scm_context {
   // small batches' speculative watermark decisions (VerifyOut::spec_check):
   // taken, recomputed and equal / different (SCM_DIAG_SPEC_CHECK), void
   int64_t spec_taken = 0, spec_equal = 0, spec_differ = 0, spec_void = 0;
+  // matcher wave priority (diagnostics, SCM_PRIO_MATCHER: 1 every launch, 2
+  // the last batch of a run's) and whether the launch being enqueued takes it
+  int match_prio = 0, match_prio_now = 0;
   int64_t n_match_launches = 0;  // matcher kernel launches of the last table run
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
   bool profile = false;
@@ -1081,7 +1084,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
       else
         SCM_HIP(launch_match_g8(t.desc8.as<uint8_t>(), t.csum.as<int32_t>(), jb, nj,
                                 bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
-                                bs.colpart.as<uint2>(), clamp, sm));
+                                bs.colpart.as<uint2>(), clamp, sm, ctx->match_prio_now));
     }
   SCM_HIP(hipEventRecord(bs.ev[1], sm));
   // Finalize, the count read-back and (enqueue_verify) the verification run on
@@ -1960,7 +1963,9 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
   } else {
     for (size_t k = 0; k < B; ++k) {
       if (k >= 3) SCM_TRY(finish(batches[k - 3], ctx->sets[(k - 3) % 3]));
+      ctx->match_prio_now = ctx->match_prio == 1 || (ctx->match_prio == 2 && k + 1 == B && B > 1);
       SCM_TRY(enqueue_match(ctx, ctx->sets[k % 3], t, batches[k].specs, nullptr, nullptr));
+      ctx->match_prio_now = 0;
       if (k >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(k - 1) % 3], true));
     }
     if (B >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(B - 1) % 3], true));
@@ -2020,6 +2025,7 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   ctx->device = device_index;
   ctx->opts = o;
   if (const char* e = std::getenv("SCM_PROFILE")) ctx->profile = e[0] == '1';
+  if (const char* e = std::getenv("SCM_PRIO_MATCHER")) ctx->match_prio = std::atoi(e);
   int hw = (int)std::thread::hardware_concurrency();
   if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::max(1, std::atoi(e));
   ctx->threads = std::max(1, std::min(16, hw));
