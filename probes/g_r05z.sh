@@ -1,0 +1,15 @@
+# Round 5: the verification's zeroing enqueued before the count read-back:
+# full GPU suite, batch-1 latency (stencil probe), bench.
+# usage (on the box): bash probes/g_r05z.sh SET
+set -e
+S=${1:-r05z}
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$S
+mkdir -p $O
+cd $R
+sha256sum scanner_colmap_amd/lib/libscm.so | cut -c1-16 > $O/lib_sha16
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1
+for i in 1 2 3; do
+  ROWS=40 timeout -k 10 200 python -u probes/stencil_probe.py > $O/stencil_$i.log 2>&1
+done
+timeout -k 10 400 python -u bench.py --no-cpu-baseline --extract-frames 0 > $O/bench.log 2>&1

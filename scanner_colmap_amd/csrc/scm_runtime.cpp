@@ -1113,6 +1113,14 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   SCM_HIP(hipMemcpyAsync(outh + bs.off_counts, bs.counts.ptr, P * sizeof(int32_t),
                          hipMemcpyDeviceToHost, sf));
   SCM_HIP(hipEventRecord(bs.ev[3], sf));
+  // The verification's zeroed state (TwoViewGeometry() outputs, empty active
+  // lists), enqueued now: off the host's round trip on the counts.
+  SCM_TRY(bs.dvout.ensure(P * sizeof(VerifyOut)));
+  SCM_HIP(hipMemsetAsync(bs.dvout.ptr, 0, P * sizeof(VerifyOut), sf));
+  SCM_TRY(bs.nact.ensure(3 * sizeof(int32_t)));
+  SCM_TRY(bs.h_nact.ensure(3 * sizeof(int32_t)));
+  SCM_HIP(hipMemsetAsync(bs.nact.ptr, 0, 3 * sizeof(int32_t), sf));
+  SCM_HIP(hipMemsetAsync(bs.h_nact.ptr, 0, 3 * sizeof(int32_t), sf));
   bs.pending = true;
   return SCM_OK;
 }
@@ -1150,10 +1158,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
   offs[P] = total;
   const int64_t V = (int64_t)order.size();
   SCM_HIP(hipEventRecord(bs.ev[4], sv));
-  if (verify) {
-    SCM_TRY(bs.dvout.ensure(P * sizeof(VerifyOut)));
-    SCM_HIP(hipMemsetAsync(bs.dvout.ptr, 0, P * sizeof(VerifyOut), sv));  // TwoViewGeometry()
-  }
+  if (verify) SCM_TRY(bs.dvout.ensure(P * sizeof(VerifyOut)));  // zeroed by enqueue_match
   if (V > 0) {
     std::vector<GatherPair> gps(V);
     std::vector<VerifyPair> vps(V);
@@ -1267,6 +1272,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
     // replay stream, so that the next window's draws and scores overlap the
     // replay of this one.
     VerifySpec spec;
+    spec.lists_zeroed = true;  // enqueue_match
     VerifyRoundBufs rbf1 = rbf, rbh1 = rbh, rbf2 = rbf, rbh2 = rbh;
     if (verify_small_batch((int)V, max_m)) {
       SCM_TRY(window_bufs(bs.o_samp, bs.o_nmod, bs.o_fcon, bs.o_mods, bs.o_cnts, bs.o_ucnt,

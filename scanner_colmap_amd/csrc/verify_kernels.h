@@ -177,6 +177,9 @@ struct VerifySpec {
   // pass waits for that pass only and runs beside the early one, the two
   // claiming pairs (RansacState::pad_)
   hipEvent_t spec_ev = nullptr;
+  // The caller zeroed both kinds' list lengths (rb_f.nact / rb_h.nact) on
+  // `stream` already (the runtime does it before the count read-back).
+  bool lists_zeroed = false;
   // Decoupled draws (optional): window r's draws run on dstream beside window
   // r - 1's scoring; draw_ev: 2 * kMaxVerifyWindows + 1 events.
   hipStream_t dstream = nullptr;

@@ -3930,8 +3930,10 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   }
   // LORANSAC<7-pt, 8-pt> (F, then its inlier masks) and LORANSAC<H, H>, each
   // on its own PRNG stream, advanced together window by window.
-  if ((err = hipMemsetAsync(rb_f.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
-  if ((err = hipMemsetAsync(rb_h.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  if (!(spec && spec->lists_zeroed)) {
+    if ((err = hipMemsetAsync(rb_f.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
+    if ((err = hipMemsetAsync(rb_h.nact, 0, 3 * sizeof(int32_t), stream)) != hipSuccess) return err;
+  }
   hipLaunchKernelGGL(rs_begin2_kernel, dim3(2 * gw), dim3(64), kVerifyLdsHead, stream, pairs,
                      npairs, scratch, snaps, out, masks, xyf, rfp[0], rhp[0], params, gw);
   int last_h = -1;
