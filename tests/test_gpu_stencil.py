@@ -321,3 +321,42 @@ def test_speculative_watermark_decisions_equal_recomputed(monkeypatch):
             ids[:4], kps[:4], descs[:4])
         t = ctx.table_timings()
         assert t["spec_taken"] > 0 and t["spec_equal"] == 0, t
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_mixed_scene_small_batches_equal_oracle(monkeypatch, seed):
+    """Small batches mixing pairs whose F and H end in different windows:
+    F early with H running its whole cap (general, two_translations), H
+    ended by its dynamic bound inside a later window (plane_and_depth,
+    planar with outliers), both early (translation), degenerate (random) --
+    so the speculative schedule's paths (draws two windows ahead of the
+    replays, the early and speculative final passes, the last pass beside the
+    early one) meet in one batch.  Each Scanner batch holds several two-image
+    stencils of different scenes; every row equals the oracle's, and with
+    SCM_DIAG_SPEC_CHECK=1 no speculative watermark decision differs from its
+    recomputation.  Reference: sequential_matching.cc:103-185."""
+    kinds = [("general", 0.2), ("two_translations", 0.1), ("plane_and_depth", 0.1),
+             ("planar", 0.55), ("translation", 0.4), ("random", 0.0), ("general", 0.6),
+             ("plane_and_depth", 0.3)]
+    rng = np.random.default_rng(700 + seed)
+    stencils, refs = [], []
+    for i, (kind, out) in enumerate(kinds):
+        m = int(rng.integers(300, 900))
+        s = 7000 + 100 * seed + i
+        kp1, kp2, mt = geometry_scene(kind, m, s, outlier_frac=out)
+        d1, d2 = descriptors_for_matches(mt, len(kp1), len(kp2), s)
+        ids, kps, descs = table_rows([(2 * s, kp1, d1), (2 * s + 1, kp2, d2)])
+        stencils.append((ids, kps, descs))
+        refs.append(oracle.execute_stencil(ids, kps, descs))
+    monkeypatch.setenv("SCM_DIAG_SPEC_CHECK", "1")
+    differ = 0
+    with Context(0) as ctx:
+        for B in (3, 5, len(stencils)):
+            order = list(rng.permutation(len(stencils)))
+            for b0 in range(0, len(order), B):
+                sel = order[b0:b0 + B]
+                got_ids, got_tvgs = ctx.execute_batch([stencils[j] for j in sel])
+                for j, a, t in zip(sel, got_ids, got_tvgs):
+                    assert (a, t) == refs[j], kinds[j]
+                differ += ctx.table_timings()["spec_differ"]
+    assert differ == 0
