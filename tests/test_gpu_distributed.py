@@ -21,7 +21,8 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _rank_main(rank, world, port, n, K, scaling, q, chunked=False):
+def _rank_main(rank, world, port, n, K, scaling, q, chunked=False, on_device=False):
+    import torch
     import torch.distributed as dist
 
     from oracle import oracle
@@ -36,14 +37,17 @@ def _rank_main(rank, world, port, n, K, scaling, q, chunked=False):
         c = Corridor(plan.total_images, 900, K, seed=57)
         if chunked:
             os.environ["SCM_BATCH_PAIRS"] = "5"  # several batches = several chunks per rank
+        # on_device: the gather's device-staging branch (pinned staging, one
+        # H2D hop, device messages, rank 0's D2H) -- the nccl path's, over gloo
+        dev = torch.device("cuda:0") if on_device else None
         with Context(0) as ctx:
             ctx.table_load(*table_rows(c.images(plan.table_begin, plan.table_end)))
             if chunked:
-                got = plan.step_chunked(ctx)
+                got = plan.step_chunked(ctx, dev)
                 if rank == 0:
                     assert len(got) > world
             else:
-                _, got = plan.step(ctx)
+                _, got = plan.step(ctx, dev)
         if rank == 0:
             rows_a, rows_b = sd.merge_gathered(got)
             ids, kps, descs = table_rows(c.images())
@@ -53,16 +57,19 @@ def _rank_main(rank, world, port, n, K, scaling, q, chunked=False):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,K,scaling,chunked", [(11, 4, "strong", False), (6, 3, "weak", False),
-                                                 (11, 4, "strong", True)])
-def test_gpu_shard_step_world2(n, K, scaling, chunked):
+@pytest.mark.parametrize("n,K,scaling,chunked,on_device", [
+    (11, 4, "strong", False, False), (6, 3, "weak", False, False), (11, 4, "strong", True, False),
+    (11, 4, "strong", False, True), (11, 4, "strong", True, True)])
+def test_gpu_shard_step_world2(n, K, scaling, chunked, on_device):
     """chunked: ShardPlan.step_chunked over scm_table_run_chunks (batches of 5
-    pairs, so each rank hands over several chunks inside the step)."""
+    pairs, so each rank hands over several chunks inside the step).
+    on_device: the messages are device tensors staged as on nccl (RCCL itself
+    refuses two ranks on one GPU, profiles/r05_rc_rccl_same_gpu.log)."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, K, scaling, q, chunked))
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, n, K, scaling, q, chunked, on_device))
              for r in range(world)]
     for p in procs:
         p.start()
