@@ -66,19 +66,23 @@ def parse():
     p.add_argument("--gen-workers", type=int, default=16)
     p.add_argument("--cpu-baseline-pairs", type=int, default=64)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--stencil-rows", type=int, default=128,
+    p.add_argument("--stencil-rows", type=int, default=1024,
                    help="rows of the Scanner drop-in path (scm_execute_batch) timed after the "
-                        "table run, rank 0 at N = 1 (0 = skip)")
+                        "table run, rank 0 at N = 1 (0 = skip): the most any --stencil-batches "
+                        "leg takes; its images come from a corridor of their own (rows + overlap "
+                        "images)")
     p.add_argument("--stream", action="store_true",
                    help="run the K steps as one streamed run (scm_table_run_passes: no pipeline "
                         "drain between steps) instead of one scm_table_run_packed call per step; "
                         "measured equal or slower (DESIGN.md section 4)")
     p.add_argument("--no-isolated", dest="isolated", action="store_false",
                    help="skip the extra serialised step that measures isolated kernel rates")
-    p.add_argument("--gather", choices=("chunked", "step"), default="chunked",
+    p.add_argument("--gather", choices=("chunked", "step"), default=None,
                    help="N > 1: gather each batch's rows inside the step as soon as they are "
-                        "serialised (scm_table_run_chunks; default), or each step's rows on a "
-                        "background thread while the next step computes")
+                        "serialised (scm_table_run_chunks), or each step's rows on a background "
+                        "thread while the next step computes.  Default: step on nccl (the form "
+                        "whose collectives have the simplest RCCL pattern; the chunked form's "
+                        "per-peer receive threads have run on gloo only), chunked on gloo")
     p.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
                    help="nccl = RCCL over xGMI, one GPU per rank (the measured path); gloo = a "
                         "rehearsal of the N > 1 sharding and gather with ranks sharing GPUs")
@@ -86,8 +90,9 @@ def parse():
                    help="frames of the SIFT extraction leg (§8f rank 4; 0 = skip), rank 0 at N = 1")
     p.add_argument("--extract-height", type=int, default=1080)
     p.add_argument("--extract-width", type=int, default=1920)
-    p.add_argument("--stencil-batches", default="1,64",
-                   help="Scanner batch sizes (stencils per execute() call) to time")
+    p.add_argument("--stencil-batches", default="1:128,64:128,256:1024,512:1024",
+                   help="Scanner batch sizes (stencils per execute() call) to time, each as "
+                        "batch[:rows] (rows default --stencil-rows)")
     return p.parse_args()
 
 
@@ -218,15 +223,15 @@ def parity_check(ctx, packed, row_lo: int, oracle_out: dict, pairs: list) -> dic
             "source": "GPU outputs of the last timed step (raw matches kept for these rows)"}
 
 
-def stencil_bench(ctx, src, overlap: int, rows: int, batches: list) -> dict:
+def stencil_bench(ctx, src, overlap: int, legs: list) -> dict:
     """The Scanner drop-in path (scm_execute_batch, what the op's execute()
-    calls; sequential_matching.cc:103-185): output rows 0..rows-1 of the same
-    table in consecutive calls of `b` stencils each, inputs as host io.cc
-    elements (so every new image crosses PCIe inside the timed region), the
-    HBM image cache carried across calls.  One untimed call warms it up."""
+    calls; sequential_matching.cc:103-185): per leg (b, rows), output rows
+    0..rows-1 of a sequence in consecutive calls of `b` stencils each (the
+    job's `batch`; feature_matching.py:50-54), inputs as host io.cc elements
+    (so every new image crosses PCIe inside the timed region), the HBM image
+    cache carried across calls.  One untimed call warms each leg up."""
     ids, kps, descs = src
     n = len(ids)
-    rows = min(rows, n)
 
     def stencils(r0, r1):
         out = []
@@ -235,8 +240,10 @@ def stencil_bench(ctx, src, overlap: int, rows: int, batches: list) -> dict:
             out.append(([ids[i] for i in sel], [kps[i] for i in sel], [descs[i] for i in sel]))
         return out
 
-    res = {"rows": rows, "stencil": overlap, "inputs": "host io.cc elements (PCIe inside the timed region)"}
-    for b in batches:
+    res = {"stencil": overlap, "inputs": "host io.cc elements (PCIe inside the timed region)",
+           "source": f"a corridor of {n} images (8192 kpts) of its own"}
+    for b, rows in legs:
+        rows = min(rows, n)
         calls = [stencils(r0, min(rows, r0 + b)) for r0 in range(0, rows, b)]
         ctx.execute_batch(calls[0])  # warm-up (buffers, cache)
         r0_, u0_ = ctx.stencil_stats()
@@ -250,7 +257,7 @@ def stencil_bench(ctx, src, overlap: int, rows: int, batches: list) -> dict:
         r1_, u1_ = ctx.stencil_stats()
         s1_ = ctx.stencil_spec_stats()
         res[f"batch{b}"] = {"pairs_per_s": round(npairs / dt, 1), "ms_per_call": round(dt / len(calls) * 1e3, 2),
-                            "calls": len(calls), "pairs": npairs,
+                            "rows": rows, "calls": len(calls), "pairs": npairs,
                             "images_uploaded": u1_ - u0_, "images_reused": r1_ - r0_,
                             "keys_speculated": s1_[0] - s0_[0], "speculation_refused": s1_[1] - s0_[1],
                             "calls_rerun": s1_[2] - s0_[2]}
@@ -376,6 +383,16 @@ def main():
     gen_s = time.perf_counter() - t0
     ids, kps, descs = table_rows(imgs)
     n_per_img = [im[2].shape[0] for im in imgs]
+    # The drop-in legs' stencils: images of a corridor of their own, so a leg
+    # may take more rows than the table holds (generated here, before the GPU
+    # runtime starts: forked workers).
+    srows = args.stencil_rows if world == 1 else 0
+    stencil_src = None
+    if srows:
+        s_imgs = Corridor(srows + overlap, kpts, overlap, seed=wl["seed"] + 7).images(
+            0, srows + overlap, workers=args.gen_workers)
+        stencil_src = table_rows(s_imgs)
+        del s_imgs
     # Pairs the CPU baseline times and the parity check compares (rank 0, N = 1).
     check_pairs = (sample_pairs(n_per_img, overlap, args.cpu_baseline_pairs)
                    if world == 1 and args.cpu_baseline_pairs > 0 else [])
@@ -405,8 +422,6 @@ def main():
     if torch.cuda.is_available():
         torch.cuda.synchronize()
     table_load_ms = (time.perf_counter() - t_load) * 1e3
-    srows = args.stencil_rows if world == 1 else 0
-    stencil_src = (ids[:srows + overlap], kps[:srows + overlap], descs[:srows + overlap]) if srows else None
     del ids, kps, descs
     lr_b, lr_e = plan.local_rows
 
@@ -425,6 +440,8 @@ def main():
             ctx.add_keep_matches_range(r, r + 1)
     last = {}
 
+    if args.gather is None:
+        args.gather = "step" if args.dist_backend == "nccl" else "chunked"
     chunked = world > 1 and args.gather == "chunked"
 
     def step():
@@ -579,8 +596,12 @@ def main():
                                        args.extract_width, check=bool(check_pairs),
                                        cpu=not args.no_cpu_baseline)
                       if world == 1 and args.extract_frames > 0 else None)
-        drop_in = stencil_bench(ctx, stencil_src, overlap, srows,
-                                [int(x) for x in args.stencil_batches.split(",") if x]) if srows else None
+        legs = []
+        for x in args.stencil_batches.split(","):
+            if x:
+                b, _, r = x.partition(":")
+                legs.append((int(b), min(srows, int(r) if r else srows)))
+        drop_in = stencil_bench(ctx, stencil_src, overlap, legs) if srows else None
         score_flops = (SAMPSON_FLOPS + 1) * evals_f + (TRANSFER_FLOPS + 1) * evals_h
         # SURVEY.md §8d headline fraction: kernel-1 work over the whole step's wall time.
         wall_tops = flops_rank / elapsed / 1e12

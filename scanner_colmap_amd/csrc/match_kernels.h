@@ -57,7 +57,7 @@ hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int nj
 // finalize (exact recompute of the deciding column seconds).
 hipError_t launch_match_g8(const uint8_t* desc8, const int32_t* csum, const MatchJob* jobs,
                            int njobs, const PairDesc* pairs, uint2* rowres, uint2* colpart,
-                           bool clamp, hipStream_t stream, int prio = 0);
+                           bool clamp, hipStream_t stream);
 hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* rowres,
                                     uint2* colpart, uint2* rowaux, int32_t* rlist,
                                     const uint8_t* desc8, const int32_t* csum,

@@ -417,7 +417,7 @@ struct scm_context {
   int64_t batch_bytes = 0;  // HBM budget of one batch set (SCM_BATCH_BYTES; 0 = from free HBM)
   bool match_bf16 = false;  // SCM_MATCH_BF16=1: bf16 MFMA matcher instead of i8
   bool serial = false;  // SCM_SERIAL=1: no overlap of the stages (diagnostics)
-  bool score_split = true;  // SCM_SCORE_SPLIT=0: one-pass scoring with every exact test
+  bool score_split = true;  // H split scoring (rs_score_kernel<1> + exact recount), always
   double t_match = 0, t_final = 0, t_verify = 0, t_wall = 0;
   double t_run = 0, t_out = 0;     // last execute_batch: run_rows (GPU + its host steps), outputs
   double t_hash = 0, t_stage = 0;  // host time of the last execute_batch: content keys, table
@@ -426,9 +426,6 @@ struct scm_context {
   // small batches' speculative watermark decisions (VerifyOut::spec_check):
   // taken, recomputed and equal / different (SCM_DIAG_SPEC_CHECK), void
   int64_t spec_taken = 0, spec_equal = 0, spec_differ = 0, spec_void = 0;
-  // matcher wave priority (diagnostics, SCM_PRIO_MATCHER: 1 every launch, 2
-  // the last batch of a run's) and whether the launch being enqueued takes it
-  int match_prio = 0, match_prio_now = 0;
   int64_t n_match_launches = 0;  // matcher kernel launches of the last table run
   // diagnostic phase profile of the verify kernel (SCM_PROFILE=1)
   bool profile = false;
@@ -852,15 +849,12 @@ size_t align256(size_t x) { return (x + 255) / 256 * 256; }
 // Stream priorities: the verification streams (the longer stage, whose
 // windows are short dependent kernels) run at high priority so that their
 // launches are not queued behind the matcher's large grids (+1 % measured);
-// SCM_MATCH_PRIO / SCM_VERIFY_PRIO = high | low | default override.
-int stream_priority(const char* var, bool high_by_default) {
-  const char* v = std::getenv(var);
+// the matching stream at the default (matcher-high measured equal on the
+// table path and slower on the drop-in path, profiles/r02_o_*).
+int stream_priority(bool high) {
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-  if (v && std::strcmp(v, "high") == 0) return hi;
-  if (v && std::strcmp(v, "low") == 0) return lo;
-  if (v && std::strcmp(v, "default") == 0) return 0;
-  return high_by_default ? hi : 0;
+  return high ? hi : 0;
 }
 
 // XCD-aware job order.  Workgroups are dispatched round-robin over the 8
@@ -1084,7 +1078,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
       else
         SCM_HIP(launch_match_g8(t.desc8.as<uint8_t>(), t.csum.as<int32_t>(), jb, nj,
                                 bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
-                                bs.colpart.as<uint2>(), clamp, sm, ctx->match_prio_now));
+                                bs.colpart.as<uint2>(), clamp, sm));
     }
   SCM_HIP(hipEventRecord(bs.ev[1], sm));
   // Finalize, the count read-back and (enqueue_verify) the verification run on
@@ -1283,10 +1277,10 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       // fit 1 GiB each; otherwise the replay runs every LO chain itself.
       const int64_t lo_stride = lo_slot_doubles(max_m);
       const int64_t lo_bytes = V * kLoSlots * lo_stride * (int64_t)sizeof(double);
-      static const bool parallel_lo = [] {  // SCM_PARALLEL_LO=0 (diagnostics): LO inline
-        const char* e = getenv("SCM_PARALLEL_LO");
-        return !(e && e[0] == '0');
-      }();
+      // SCM_PARALLEL_LO=0 (checks, read per call): every LO chain inline
+      // (tests/test_gpu_stencil.py compares both forms with the oracle)
+      const char* plo = getenv("SCM_PARALLEL_LO");
+      const bool parallel_lo = !(plo && plo[0] == '0');
       if (parallel_lo && lo_bytes <= (int64_t(1) << 30)) {
         VerifyRoundBufs* lrb[4] = {&rbf, &rbf1, &rbh, &rbh1};
         for (int i = 0; i < 4; ++i) {
@@ -1327,13 +1321,9 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
         spec.spec_ev = bs.spev;
         // The windows' draws run ahead on the matching stream (a small
         // batch's matching is done before its verification starts; on the
-        // early-final stream they held that pass back).  SCM_DRAW_STREAM=0
-        // (diagnostics): draws in order on the scoring stream.
-        static const bool draw_stream = [] {
-          const char* e = getenv("SCM_DRAW_STREAM");
-          return !(e && e[0] == '0');
-        }();
-        if (draw_stream) {
+        // early-final stream they held that pass back; in order on the scoring
+        // stream: 3.74-3.77 vs 3.63-3.67 ms per call, profiles/r04_h, r04_j).
+        {
           spec.dstream = ctx->stream;
           spec.draw_ev = bs.dev;
           // the third parity (no parallel-LO slots: only the first windows have them)
@@ -1349,10 +1339,11 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
         }
       }
     }
+    const VerifyParams vparams = make_params(ctx->opts, iteration);
     SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
                           bs.xy2.as<double>(), bs.scratch.as<double>(), bs.snaps.as<uint32_t>(),
                           bs.masks.as<uint8_t>(), bs.dvout.as<VerifyOut>(),
-                          make_params(ctx->opts, iteration), prof, nullptr, bs.xyf.as<float4>(), rbf, rbh,
+                          vparams, prof, nullptr, bs.xyf.as<float4>(), rbf, rbh,
                           sv, bs.sev, &bs.nwin, &spec));
   }
   SCM_HIP(hipEventRecord(bs.ev[5], sv));
@@ -1842,14 +1833,9 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
   // Measured on the bench workload: equal-size batches, short first / last
   // batches, and caps of 4,096-9,472 pairs were all slower than 8,192.
   const int64_t budget = set_budget_bytes(ctx);
-  // SCM_BATCH_SMALL_FIRST=1 (measurement): the remainder batch first instead
-  // of last (row order is kept: the first batch is the short one).
-  int64_t first_cap = ctx->batch_pairs;
-  if (const char* e = std::getenv("SCM_BATCH_SMALL_FIRST"); e && e[0] == '1') {
-    int64_t tp = 0;
-    for (const RowPlan& rp : plan) tp += (int64_t)rp.nb.size();
-    if (tp % ctx->batch_pairs) first_cap = tp % ctx->batch_pairs;
-  }
+  // (The remainder batch first instead of last measured slower, 44.4/44.5K vs
+  // 47.4/47.6K pairs/s, profiles/r05_b_ab_*.)
+  const int64_t first_cap = ctx->batch_pairs;
   Batch cur;
   int64_t cur_bytes = 0, cur_small = 0;
   for (int64_t i = 0; i < nr; ++i) {
@@ -1969,9 +1955,7 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
   } else {
     for (size_t k = 0; k < B; ++k) {
       if (k >= 3) SCM_TRY(finish(batches[k - 3], ctx->sets[(k - 3) % 3]));
-      ctx->match_prio_now = ctx->match_prio == 1 || (ctx->match_prio == 2 && k + 1 == B && B > 1);
       SCM_TRY(enqueue_match(ctx, ctx->sets[k % 3], t, batches[k].specs, nullptr, nullptr));
-      ctx->match_prio_now = 0;
       if (k >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(k - 1) % 3], true));
     }
     if (B >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(B - 1) % 3], true));
@@ -2031,13 +2015,11 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   ctx->device = device_index;
   ctx->opts = o;
   if (const char* e = std::getenv("SCM_PROFILE")) ctx->profile = e[0] == '1';
-  if (const char* e = std::getenv("SCM_PRIO_MATCHER")) ctx->match_prio = std::atoi(e);
   int hw = (int)std::thread::hardware_concurrency();
   if (const char* e = std::getenv("OMP_NUM_THREADS")) hw = std::max(1, std::atoi(e));
   ctx->threads = std::max(1, std::min(16, hw));
   ctx->pool.start(ctx->threads - 1);
   ctx->vpool.start(std::max(1, ctx->threads - 1));
-  if (const char* e = std::getenv("SCM_SCORE_SPLIT")) ctx->score_split = e[0] != '0';
   if (const char* e = std::getenv("SCM_SERIAL")) ctx->serial = e[0] == '1';
   if (const char* e = std::getenv("SCM_BATCH_PAIRS"))
     ctx->batch_pairs = std::max<int64_t>(1, std::min<int64_t>(kMaxPairsPerBatch, std::atoll(e)));
@@ -2049,10 +2031,10 @@ int scm_context_create(int32_t device_index, const scm_matching_options* opts,
   // keeps the lowest-row tie rule with column keys.
   if ((float)o.max_ratio > 1.0f) ctx->match_bf16 = true;
   if (hipSetDevice(device_index) != hipSuccess ||
-      hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, stream_priority("SCM_MATCH_PRIO", false)) != hipSuccess ||
-      hipStreamCreateWithPriority(&ctx->sets[0].vstream, hipStreamNonBlocking, stream_priority("SCM_VERIFY_PRIO", true)) != hipSuccess ||
-      hipStreamCreateWithPriority(&ctx->sets[1].vstream, hipStreamNonBlocking, stream_priority("SCM_VERIFY_PRIO", true)) != hipSuccess ||
-      hipStreamCreateWithPriority(&ctx->sets[2].vstream, hipStreamNonBlocking, stream_priority("SCM_VERIFY_PRIO", true)) != hipSuccess) {
+      hipStreamCreateWithPriority(&ctx->stream, hipStreamNonBlocking, stream_priority(false)) != hipSuccess ||
+      hipStreamCreateWithPriority(&ctx->sets[0].vstream, hipStreamNonBlocking, stream_priority(true)) != hipSuccess ||
+      hipStreamCreateWithPriority(&ctx->sets[1].vstream, hipStreamNonBlocking, stream_priority(true)) != hipSuccess ||
+      hipStreamCreateWithPriority(&ctx->sets[2].vstream, hipStreamNonBlocking, stream_priority(true)) != hipSuccess) {
     scm_context_destroy(ctx);
     set_error("failed to create HIP streams");
     return SCM_E_DEVICE;
@@ -2631,12 +2613,12 @@ int scm_extract_frames(scm_context* ctx, int64_t n, const uint64_t* image_ids,
     set_error("null context");
     return SCM_E_INVALID;
   }
-  // the slots run on the context's four streams (one hardware queue each);
-  // SCM_SIFT_OWN_STREAMS=1 gives them streams of their own
-  const char* own = std::getenv("SCM_SIFT_OWN_STREAMS");
+  // the slots run on the context's four streams (one hardware queue each:
+  // streams beyond GPU_MAX_HW_QUEUES share one and serialise, 418 vs 570
+  // frames/s)
   const hipStream_t lent[kSiftSlotStreams] = {ctx->stream, ctx->sets[0].vstream,
                                               ctx->sets[1].vstream, ctx->sets[2].vstream};
-  return sift_extract_frames(&ctx->sift, ctx->device, own && own[0] == '1' ? nullptr : lent, n,
+  return sift_extract_frames(&ctx->sift, ctx->device, lent, n,
                              image_ids, frames, keypoints_out, descriptors_out, cameras_out);
 }
 

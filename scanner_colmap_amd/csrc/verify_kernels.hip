@@ -23,6 +23,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <functional>
+#include <mutex>
+
 #include "../../include/scm.h"
 #include "geom_solvers.h"
 #include "verify_kernels.h"
@@ -2936,7 +2939,10 @@ __global__ __launch_bounds__(kScoreThreads) void rs_exact_kernel(
   }
 }
 
-// Parallel local optimisation (small batches; DRAFT, not yet run on a GPU):
+// Parallel local optimisation (small batches, the first window; shipped by
+// default since round 5, byte-identical to the inline chains: every
+// small-batch GPU test, and tests/test_gpu_stencil.py::
+// test_parallel_lo_more_records_than_slots with SCM_PARALLEL_LO=1 and =0):
 // block (a, slot) takes active pair a's slot-th record model of the window --
 // a model whose count reaches the running maximum of the counts before it,
 // starting from the pair's best at the window start (rst.best_n; a stale,
@@ -3552,18 +3558,12 @@ hipError_t set_lds_attr(F f, int static_bytes = 0) {
 }
 
 constexpr int kWaveShufflePairs = 256;
+constexpr int kMaxDevices = 64;  // launch_verify's per-device attribute set-up
 constexpr int kSmallFirstWindow = 4;  // rounds of a small batch's first window (run_windows)
 constexpr int kSmallSecondWindowF = 80;  // rounds of its second F window (run_windows)
-// Small batches: a wave per pair (rs_shuffle_wave2_kernel), four waves per
-// pair in the replay, speculative windows -- while the batch leaves most of
-// the GPU idle, latency decides.
-int wave_pairs_limit() {
-  static const int v = [] {
-    const char* e = getenv("SCM_WAVE_SHUFFLE_PAIRS");
-    return e ? atoi(e) : kWaveShufflePairs;
-  }();
-  return v;
-}
+// Small batches (up to kWaveShufflePairs pairs): a wave per pair
+// (rs_shuffle_wave2_kernel), four waves per pair in the replay, speculative
+// windows -- while the batch leaves most of the GPU idle, latency decides.
 
 // Windows of both RANSAC kinds (W = 1, 2, 4, ..., kMaxWindow rounds) until
 // each kind's trial cap: draw / shuffle / replay as dual-kind launches, the
@@ -3596,7 +3596,8 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
                        const VerifyRoundBufs* rhp, int max_chunks, int max_m, uint64_t* prof,
                        hipStream_t stream, hipEvent_t* score_ev, int* nwin, bool spec,
                        hipStream_t rstream, hipEvent_t* win_ev, int* last_h,
-                       hipStream_t dstream, hipEvent_t* draw_ev, int np) {
+                       hipStream_t dstream, hipEvent_t* draw_ev, int np,
+                       const std::function<void(int)>* before_last_h_replay) {
   const size_t lds = kVerifyLdsHead;  // rs_draw / rs_replay touch only the head
   const int gw = npairs < kPairGrid ? npairs : kPairGrid;
   constexpr int kShuffleLdsKb = 16;
@@ -3609,6 +3610,9 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       sh_stride ? std::max(1, std::min(64, (kShuffleLdsKb * 1024) / (2 * sh_stride))) : 1;
   const int sh_blocks = (npairs + sh_ppb - 1) / sh_ppb;
   const int wave_stride = (max_m + 7) / 8 * 8;
+  // (A run's last batch on the small-batch kernels -- a wave per pair in the
+  // draws and Shuffle, four in the replay -- with the table schedule measured
+  // 47.98/47.97K vs 48.35/48.33K pairs/s, profiles/r06_e: not kept.)
   const bool wave_sh = verify_small_batch(npairs, max_m);
   const size_t wave_lds = wave_shuffle_lds_bytes(wave_stride);
   const int max_chunks_s = (max_m + kScoreThreads * kScorePchSmall - 1) / (kScoreThreads * kScorePchSmall);
@@ -3625,42 +3629,20 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   if (wave_sh) W = std::min(kSmallFirstWindow, maxw);
   else
     while (W < maxw && (int64_t)npairs * 2 * W <= 1024) W *= 2;
-  static const int w0_env = [] {  // diagnostics: SCM_FIRST_WINDOW=w sets the first window
-    const char* e = getenv("SCM_FIRST_WINDOW");
-    return e ? atoi(e) : 0;
-  }();
-  if (w0_env > 0) W = std::min(w0_env, maxw);
   // Per-kind window sizes: the same schedule for both kinds, except a small
-  // batch's second F window, kSmallSecondWindowF rounds (SCM_SMALL_F_W1,
-  // diagnostics): F stops early on most pairs, and that window's draws run
-  // beside the first window's solves, scores and replay -- the two branches
-  // of a stencil's critical path (19-pair stencil, profiles/r05_g, r05_h:
-  // 128 rounds 2.80-2.84 ms per call, 96: 2.60-2.62, 80: 2.58-2.62, 64:
-  // 2.61-2.75, 48: 2.77-2.85, 32: 2.93-2.97; F's 10,000 trials still take
-  // three windows).
-  static const int fw1_env = [] {
-    const char* e = getenv("SCM_SMALL_F_W1");
-    return e ? atoi(e) : 0;
-  }();
+  // batch's second F window, kSmallSecondWindowF rounds: F stops early on
+  // most pairs, and that window's draws run beside the first window's solves,
+  // scores and replay -- the two branches of a stencil's critical path
+  // (19-pair stencil, profiles/r05_g, r05_h: 128 rounds 2.80-2.84 ms per
+  // call, 96: 2.60-2.62, 80: 2.58-2.62, 64: 2.61-2.75, 48: 2.77-2.85, 32:
+  // 2.93-2.97; F's 10,000 trials still take three windows).  The table
+  // path's first windows per kind were measured at H 4 / 8 / 16 and F 2
+  // rounds against the doubling schedule from W: no gain (round 5).
   int Wf = W, Wh = W;
-  // Table path (diagnostics): SCM_TABLE_W0_H / SCM_TABLE_W0_F set a kind's
-  // first window (rounds); each kind then doubles up to the largest window.
-  static const int tw0h = [] {
-    const char* e = getenv("SCM_TABLE_W0_H");
-    return e ? atoi(e) : 0;
-  }();
-  static const int tw0f = [] {
-    const char* e = getenv("SCM_TABLE_W0_F");
-    return e ? atoi(e) : 0;
-  }();
-  if (!wave_sh && tw0h > 0) Wh = std::min(tw0h, maxw);
-  if (!wave_sh && tw0f > 0) Wf = std::min(tw0f, maxw);
   // Windows whose LO chains run in parallel (small batches with LO slots):
-  // SCM_PARALLEL_LO_WINDOWS (diagnostics), default 1.
-  static const int lo_windows = [] {
-    const char* e = getenv("SCM_PARALLEL_LO_WINDOWS");
-    return e ? atoi(e) : 1;
-  }();
+  // the first (later windows' records are many and mostly superseded; two
+  // windows measured slower, profiles/r05_m).
+  constexpr int lo_windows = 1;
   // Decoupled draws (speculative schedule with a draw stream): window r's
   // draws and shuffles run on dstream as soon as window r - 2 is replayed (its
   // active list) and window r - 1's prune has run (the lists and counts it
@@ -3790,6 +3772,10 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       (void)hipEventRecord(win_ev[2 * r], stream);
       (void)hipStreamWaitEvent(rstream, win_ev[2 * r], 0);
       rs = rstream;
+      // (checks: work that must run before H's last window's replay is
+      // enqueued -- launch_verify's SCM_DIAG_HOLD_LAST_REPLAY)
+      if (h && before_last_h_replay && covered_h + Wh * kTrialBatch >= P.max_trials_H)
+        (*before_last_h_replay)(r);
     }
     // (on the replay's stream: the next window's solves and scores do not wait
     // for the chains; over the replay's input list, complete there)
@@ -3814,7 +3800,7 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     covered_f += Wf * kTrialBatch;
     covered_h += Wh * kTrialBatch;
     if (wave_sh) {
-      Wf = r == 0 ? std::min(fw1_env > 0 ? fw1_env : kSmallSecondWindowF, maxw) : maxw;
+      Wf = r == 0 ? std::min(kSmallSecondWindowF, maxw) : maxw;
       Wh = maxw;
     } else {
       Wf = Wf * 2 > maxw ? maxw : Wf * 2;
@@ -3830,37 +3816,10 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
 
 }  // namespace
 
-int verify_small_batch_pairs() { return wave_pairs_limit(); }
-
-// SCM_THREE_PARITIES=0 (diagnostics): decoupled draws one window ahead only.
-static bool three_parities_off() {
-  static const bool v = [] {
-    const char* e = getenv("SCM_THREE_PARITIES");
-    return e && e[0] == '0';
-  }();
-  return v;
-}
-
-// SCM_FINAL_BESIDE=0 (diagnostics): the last final pass after the early one.
-static bool final_beside_off() {
-  static const bool v = [] {
-    const char* e = getenv("SCM_FINAL_BESIDE");
-    return e && e[0] == '0';
-  }();
-  return v;
-}
-
-// SCM_SPEC_WATERMARK=0 (diagnostics): no speculative watermark pass.
-static bool spec_wm_off() {
-  static const bool v = [] {
-    const char* e = getenv("SCM_SPEC_WATERMARK");
-    return e && e[0] == '0';
-  }();
-  return v;
-}
+int verify_small_batch_pairs() { return kWaveShufflePairs; }
 
 bool verify_small_batch(int npairs, int max_m) {
-  return npairs <= wave_pairs_limit() && (max_m + 7) / 8 * 8 <= kWsMaxStride;
+  return npairs <= kWaveShufflePairs && (max_m + 7) / 8 * 8 <= kWsMaxStride;
 }
 
 hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const double* xy1,
@@ -3870,22 +3829,22 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
                          const VerifyRoundBufs& rb_h, hipStream_t stream, hipEvent_t* score_ev,
                          int* nwin, const VerifySpec* spec) {
   if (npairs <= 0) return hipSuccess;
+  hipError_t err;
   // Small batches: the latency-bound kernels (draws, LO chains, replays, final
   // passes) raise their waves' issue priority over the wide scoring kernels'
-  // (SCM_PRIO=0, diagnostics: not).
-  static const int prio_env = [] {
-    const char* e = getenv("SCM_PRIO");
-    return e ? atoi(e) : 1;
-  }();
-  // (the table path's replay: SCM_PRIO_TABLE=1, diagnostics)
-  static const int prio_table = [] {
-    const char* e = getenv("SCM_PRIO_TABLE");
-    return e ? atoi(e) : 0;
-  }();
+  // (2.34-2.35 vs 2.35-2.36 ms per batch-1 call, profiles/r05_o); the table
+  // path keeps the default (the same priority there: within the noise,
+  // profiles/r05_r, r05_s).
   VerifyParams params = params_in;
-  params.prio = verify_small_batch(npairs, max_m) ? prio_env : prio_table;
-  static bool attr = false;
-  if (!attr) {
+  params.prio = verify_small_batch(npairs, max_m) ? 1 : 0;
+  // The kernels' dynamic LDS limit, once per device and process (contexts on
+  // several threads may launch at once: std::call_once, not a plain flag).
+  int dev = 0;
+  if ((err = hipGetDevice(&dev)) != hipSuccess) return err;
+  static std::once_flag attr_once[kMaxDevices];
+  static hipError_t attr_err[kMaxDevices];
+  if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+  std::call_once(attr_once[dev], [&] {
     const hipError_t es[] = {
         set_lds_attr(rs_begin2_kernel),
         set_lds_attr(rs_draw2_kernel),
@@ -3897,23 +3856,20 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
         set_lds_attr(rs_lo_chain2_kernel),
         set_lds_attr(verify_final_kernel<1>),
         set_lds_attr(verify_final_kernel<8>)};
+    attr_err[dev] = hipSuccess;
     for (hipError_t e : es)
-      if (e != hipSuccess) return e;
-    attr = true;
-  }
+      if (e != hipSuccess && attr_err[dev] == hipSuccess) attr_err[dev] = e;
+  });
+  if (attr_err[dev] != hipSuccess) return attr_err[dev];
   const size_t lds = sizeof(VerifyLds);
   const int gw = npairs < kPairGrid ? npairs : kPairGrid;
   const int max_chunks = (max_m + kScoreChunk - 1) / kScoreChunk;
-  hipError_t err;
   // Parity buffers: the odd ones from spec, else both parities alias (the
   // windows then run strictly in order on one stream).
   const bool sp = spec && spec->rb_f1 && spec->rb_h1 && spec->rstream && spec->win_ev &&
                   spec->fstream && spec->fin_ev && verify_small_batch(npairs, max_m);
   // A third parity with decoupled draws (run_windows: they run two windows ahead).
-  const int np = sp && spec->dstream && spec->draw_ev && spec->rb_f2 && spec->rb_h2 &&
-                         !three_parities_off()
-                     ? 3
-                     : 2;
+  const int np = sp && spec->dstream && spec->draw_ev && spec->rb_f2 && spec->rb_h2 ? 3 : 2;
   VerifyRoundBufs rfp[3] = {rb_f, sp ? *spec->rb_f1 : rb_f, np == 3 ? *spec->rb_f2 : rb_f};
   VerifyRoundBufs rhp[3] = {rb_h, sp ? *spec->rb_h1 : rb_h, np == 3 ? *spec->rb_h2 : rb_h};
   // each parity's draws start from the previous parity's state; its prune and
@@ -3936,13 +3892,6 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   }
   hipLaunchKernelGGL(rs_begin2_kernel, dim3(2 * gw), dim3(64), kVerifyLdsHead, stream, pairs,
                      npairs, scratch, snaps, out, masks, xyf, rfp[0], rhp[0], params, gw);
-  int last_h = -1;
-  if ((err = run_windows(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf, rfp,
-                         rhp, max_chunks, max_m, prof, stream, score_ev, nwin, sp,
-                         sp ? spec->rstream : stream, sp ? spec->win_ev : nullptr, &last_h,
-                         sp ? spec->dstream : nullptr, sp ? spec->draw_ev : nullptr, np)) !=
-      hipSuccess)
-    return err;
   // Diagnostics: SCM_DIAG_SCRIBBLE_F_SIDX=1 makes the final kernel rewrite the
   // F area's index vector before every watermark draw (the worst the
   // speculative F draws beside the early pass can do; outputs must not move,
@@ -3950,6 +3899,37 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   const char* diag_env = getenv("SCM_DIAG_SCRIBBLE_F_SIDX");
   const char* chk_env = getenv("SCM_DIAG_SPEC_CHECK");  // (verify_final_kernel bit 16)
   const int diag = (diag_env && atoi(diag_env) ? 8 : 0) | (chk_env && atoi(chk_env) ? 16 : 0);
+  // The speculative watermark pass (phase 3, below) reads the pairs' F / H
+  // states while H's last window's replay may be writing them.
+  // SCM_DIAG_HOLD_LAST_REPLAY=1 (checks, read per call) forces one extreme
+  // order: phase 3 is enqueued before that replay and the replay waits for it,
+  // so phase 3 sees every pair whose F or H ends in that window still running
+  // (tests/test_gpu_stencil.py).
+  const char* hold_env = getenv("SCM_DIAG_HOLD_LAST_REPLAY");
+  const bool spec_pass = sp && spec->dstream && spec->draw_ev;
+  const bool hold = spec_pass && spec->spec_ev && hold_env && atoi(hold_env);
+  bool phase3_done = false;
+  auto phase3 = [&](int lh) {
+    (void)hipStreamWaitEvent(spec->fstream, spec->draw_ev[2 * lh], 0);
+    (void)hipStreamWaitEvent(spec->fstream, spec->win_ev[2 * (lh - 1) + 1], 0);
+    hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, spec->fstream,
+                       pairs, xy1, xy2, scratch, snaps, masks, out, params, prof, counts,
+                       rb_f.rst, rb_h.rst, 3 | diag, rhp[lh % np].wstate);
+  };
+  const std::function<void(int)> hold_fn = [&](int lh) {
+    if (lh < 1) return;  // (no phase 3 when H ends in the first window)
+    phase3(lh);
+    phase3_done = true;
+    (void)hipEventRecord(spec->spec_ev, spec->fstream);
+    (void)hipStreamWaitEvent(spec->rstream, spec->spec_ev, 0);
+  };
+  int last_h = -1;
+  if ((err = run_windows(pairs, npairs, xy1, xy2, scratch, snaps, masks, out, params, xyf, rfp,
+                         rhp, max_chunks, max_m, prof, stream, score_ev, nwin, sp,
+                         sp ? spec->rstream : stream, sp ? spec->win_ev : nullptr, &last_h,
+                         sp ? spec->dstream : nullptr, sp ? spec->draw_ev : nullptr, np,
+                         hold ? &hold_fn : nullptr)) != hipSuccess)
+    return err;
   if (sp && last_h >= 0 && last_h < kMaxVerifyWindows) {
     // Configuration + watermark of the pairs done when H's last window is
     // replayed (typically all but the far pairs' F), beside the later windows;
@@ -3959,17 +3939,11 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
     // Before it, the speculative watermark decisions (phase 3): once H's last
     // window is drawn and the window before it replayed (F done for the near
     // pairs), beside H's last window's solves, scores and replay.
-    if (last_h >= 1 && spec->dstream && spec->draw_ev && !spec_wm_off()) {
-      (void)hipStreamWaitEvent(spec->fstream, spec->draw_ev[2 * last_h], 0);
-      (void)hipStreamWaitEvent(spec->fstream, spec->win_ev[2 * (last_h - 1) + 1], 0);
-      hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, spec->fstream,
-                         pairs, xy1, xy2, scratch, snaps, masks, out, params, prof, counts,
-                         rb_f.rst, rb_h.rst, 3 | diag, rhp[last_h % np].wstate);
-    }
+    if (last_h >= 1 && spec_pass && !phase3_done) phase3(last_h);
     // Phase 2 waits for phase 1 (the pairs it left), or, with an event after
     // phase 3, for phase 3 only (it must not run a pair's watermark RANSAC
     // while phase 3 may) and claims pairs beside phase 1.
-    const bool beside = spec->spec_ev && !final_beside_off();
+    const bool beside = spec->spec_ev != nullptr;
     if (beside) (void)hipEventRecord(spec->spec_ev, spec->fstream);
     (void)hipStreamWaitEvent(spec->fstream, spec->win_ev[2 * last_h + 1], 0);
     hipLaunchKernelGGL(verify_final_kernel<8>, dim3(npairs), dim3(512), lds, spec->fstream, pairs,

@@ -198,13 +198,19 @@ class Gatherer:
         return out
 
 
+# Chunk header flags (the third int64 of a chunk header).
+CHUNK_DATA, CHUNK_END, CHUNK_ERROR = 0, 1, 2
+
+
 class ChunkSender:
     """rank != 0 of a chunked step: each chunk's packed rows (a batch of the
     library's pipeline, scm_table_run_chunks) go to rank 0 from a background
     thread while the next batches compute, in order: a header (offset bytes,
-    data bytes, last flag) and the two messages, one batch_isend_irecv group
-    per chunk (RCCL over xGMI on nccl, staged through the same pinned / device
-    buffers as gather_packed; gloo on CPU tensors)."""
+    data bytes, flag) and the two messages, one batch_isend_irecv group per
+    chunk (RCCL over xGMI on nccl, staged through the same pinned / device
+    buffers as gather_packed; gloo on CPU tensors).  The last header carries
+    CHUNK_END, or CHUNK_ERROR when this rank's run failed (finish(error=True)):
+    rank 0 then raises instead of waiting for rows that will not come."""
 
     def __init__(self, device=None):
         from concurrent.futures import ThreadPoolExecutor
@@ -213,7 +219,7 @@ class ChunkSender:
         self.futs = []
         self.staging = _Staging()
 
-    def _send(self, offsets, data, last):
+    def _send(self, offsets, data, flag):
         import torch
         import torch.distributed as dist
         dev = self.device if self.device is not None else torch.device("cpu")
@@ -222,8 +228,8 @@ class ChunkSender:
             torch.cuda.set_device(dev)
         ob = np.ascontiguousarray(offsets, dtype=np.int64).reshape(-1).view(np.uint8)
         dat = np.ascontiguousarray(data, dtype=np.uint8).reshape(-1)
-        no, nd = (0, 0) if last else (ob.size, dat.size)
-        hdr = torch.tensor([no, nd, 1 if last else 0], dtype=torch.int64, device=dev)
+        no, nd = (0, 0) if flag != CHUNK_DATA else (ob.size, dat.size)
+        hdr = torch.tensor([no, nd, flag], dtype=torch.int64, device=dev)
         ops = [dist.P2POp(dist.isend, hdr, 0)]
         if no + nd:
             if on_gpu:
@@ -243,53 +249,72 @@ class ChunkSender:
             torch.cuda.current_stream(dev).synchronize()  # staging reused by the next chunk
 
     def submit(self, packed):
-        self.futs.append(self.pool.submit(self._send, packed.offsets, packed.data, False))
+        self.futs.append(self.pool.submit(self._send, packed.offsets, packed.data, CHUNK_DATA))
 
-    def finish(self):
-        """Sends the end marker and waits until every chunk has left."""
-        self.futs.append(self.pool.submit(self._send, np.zeros(1, np.int64),
-                                          np.zeros(0, np.uint8), True))
+    def finish(self, error: bool = False):
+        """Sends the end marker (CHUNK_ERROR after a failed run) and waits
+        until every chunk has left.  After a failed run the chunks already
+        queued still go first (rank 0 receives in order), and a failure of
+        one of them does not keep the end marker back."""
+        flag = CHUNK_ERROR if error else CHUNK_END
+        first_exc = None
         for f in self.futs:
-            f.result()
+            try:
+                f.result()
+            except BaseException as e:  # noqa: BLE001 -- re-raised below
+                if first_exc is None:
+                    first_exc = e
+                flag = CHUNK_ERROR
         self.futs = []
-        self.pool.shutdown()
+        try:
+            self.pool.submit(self._send, np.zeros(1, np.int64), np.zeros(0, np.uint8), flag).result()
+        finally:
+            self.pool.shutdown()
+        if first_exc is not None and not error:
+            raise first_exc
 
 
 class ChunkReceiver:
-    """rank 0 of a chunked step: a background thread receives the peers'
-    chunks as they arrive (round robin over the peers still sending, each
-    chunk into buffers of its own) while rank 0 computes its own rows."""
+    """rank 0 of a chunked step: one receive thread per peer takes that
+    peer's chunks as they arrive (each into buffers of its own) while rank 0
+    computes its own rows, so a slow peer holds back only its own chunks
+    (on nccl each peer's point-to-point traffic runs on its own pair
+    communicator and stream).  The threads are daemons: a rank-0 failure
+    never leaves the interpreter waiting on them at exit."""
 
     def __init__(self, world, device=None):
-        from concurrent.futures import ThreadPoolExecutor
+        import threading
+        import time
         self.world = world
         self.device = device
-        self.pool = ThreadPoolExecutor(max_workers=1)
-        self.fut = self.pool.submit(self._loop)
+        self.per = {r: [] for r in range(1, world)}
+        self.arrival = {r: [] for r in range(1, world)}  # perf_counter of each chunk's arrival
+        self.status = {r: None for r in range(1, world)}  # "end", "error", or an exception
+        self._t0 = time.perf_counter
+        self.threads = [threading.Thread(target=self._peer, args=(r,), daemon=True,
+                                         name=f"chunk-recv-{r}") for r in range(1, world)]
+        for t in self.threads:
+            t.start()
 
-    def _recv(self, shape, src, dev):
+    def _peer(self, r):
         import torch
         import torch.distributed as dist
-        t = torch.empty(shape, dtype=torch.int64 if shape == (3,) else torch.uint8, device=dev)
-        for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, t, src)]):
-            w.wait()
-        return t
-
-    def _loop(self):
-        import torch
-        import torch.distributed as dist
-        dev = self.device if self.device is not None else torch.device("cpu")
-        on_gpu = dev.type != "cpu"
-        if on_gpu:
-            torch.cuda.set_device(dev)
-        per = {r: [] for r in range(1, self.world)}
-        active = list(range(1, self.world))
-        while active:
-            for r in list(active):
-                no, nd, last = (int(x) for x in self._recv((3,), r, dev).cpu())
-                if last:
-                    active.remove(r)
-                    continue
+        try:
+            dev = self.device if self.device is not None else torch.device("cpu")
+            on_gpu = dev.type != "cpu"
+            if on_gpu:
+                torch.cuda.set_device(dev)
+            while True:
+                hdr = torch.empty(3, dtype=torch.int64, device=dev)
+                for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, hdr, r)]):
+                    w.wait()
+                no, nd, flag = (int(x) for x in hdr.cpu())
+                if flag == CHUNK_END:
+                    self.status[r] = "end"
+                    return
+                if flag == CHUNK_ERROR:
+                    self.status[r] = "error"
+                    return
                 flat = torch.empty(no + nd, dtype=torch.uint8, device=dev)
                 ops = []
                 if no:
@@ -299,13 +324,29 @@ class ChunkReceiver:
                 for w in dist.batch_isend_irecv(ops):
                     w.wait()
                 host = (flat.cpu() if on_gpu else flat).numpy()
-                per[r].append((host[:no].view(np.int64), host[no:]))
-        return per
+                self.per[r].append((host[:no].view(np.int64), host[no:]))
+                self.arrival[r].append(self._t0())
+        except BaseException as e:  # noqa: BLE001 -- reported by result()
+            self.status[r] = e
 
-    def result(self):
-        per = self.fut.result()
-        self.pool.shutdown()
-        return per
+    def result(self, timeout=None):
+        """Every peer's chunks in order ({rank: [(offsets, data), ...]});
+        raises if a peer reported a failed run or a receive failed, and
+        TimeoutError if a peer has not finished within `timeout` seconds."""
+        import time
+        deadline = None if timeout is None else time.monotonic() + timeout
+        for t in self.threads:
+            t.join(None if deadline is None else max(0.0, deadline - time.monotonic()))
+            if t.is_alive():
+                raise TimeoutError(f"{t.name}: peer still sending after {timeout} s")
+        failed = {r: s for r, s in self.status.items() if s != "end"}
+        if failed:
+            r, s = sorted(failed.items())[0]
+            if s == "error":
+                raise RuntimeError(f"rank {r} reported a failed run (chunked gather)")
+            raise RuntimeError(f"chunked gather: receiving from rank {r} failed: {s!r}") from (
+                s if isinstance(s, BaseException) else None)
+        return self.per
 
 
 class ShardPlan:
@@ -329,6 +370,8 @@ class ShardPlan:
                                                        self.total_images, overlap)
         self.gatherer = None
         self.tail_ms = []  # step_chunked: per step, the gather time left after the compute
+        self.last_arrival = None  # step_chunked, rank 0: per peer, the arrival time of each chunk
+        self.drain_timeout_s = 120.0  # step_chunked, rank 0 after its own failure
 
     @property
     def local_rows(self) -> tuple[int, int]:
@@ -377,14 +420,28 @@ class ShardPlan:
         import time
         if self.rank == 0:
             recv = ChunkReceiver(self.world, device)
-            runner.table_run_chunks(self.overlap, lb, le,
-                                    lambda first, pk: own.append((pk.offsets, pk.data)))
+            try:
+                runner.table_run_chunks(self.overlap, lb, le,
+                                        lambda first, pk: own.append((pk.offsets, pk.data)))
+            except BaseException:
+                # The peers still send their rows and end markers; take them
+                # (bounded) so that the job ends cleanly, then fail.
+                try:
+                    recv.result(timeout=self.drain_timeout_s)
+                except Exception:  # noqa: BLE001 -- rank 0's own failure is the one raised
+                    pass
+                raise
             t0 = time.perf_counter()
             per = recv.result()
             self.tail_ms.append((time.perf_counter() - t0) * 1e3)
+            self.last_arrival = recv.arrival
             return own + [c for r in range(1, self.world) for c in per[r]]
         snd = ChunkSender(device)
-        runner.table_run_chunks(self.overlap, lb, le, lambda first, pk: snd.submit(pk))
+        try:
+            runner.table_run_chunks(self.overlap, lb, le, lambda first, pk: snd.submit(pk))
+        except BaseException:
+            snd.finish(error=True)  # rank 0 raises instead of waiting for this rank's rows
+            raise
         t0 = time.perf_counter()
         snd.finish()
         self.tail_ms.append((time.perf_counter() - t0) * 1e3)

@@ -262,8 +262,8 @@ def test_gloo_streamed_passes_world2():
                                                (4, 3, 5, "weak"), (2, 2, 5, "strong")])
 def test_gloo_chunked_step(world, n, K, scaling):
     """ShardPlan.step_chunked (the gather inside the step): every rank's rows
-    leave batch by batch while the next batches compute; rank 0 receives the
-    peers' chunks round robin, and the merged rows of two steps equal a
+    leave batch by batch while the next batches compute; rank 0 receives each
+    peer's chunks on a thread of its own, and the merged rows of two steps equal a
     one-rank run -- uneven chunk counts per rank, ranks without rows."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -278,3 +278,113 @@ def test_gloo_chunked_step(world, n, K, scaling):
     assert [p.exitcode for p in procs] == [0] * world
     ok, _, nrows, total = q.get(timeout=5)
     assert ok and nrows == total
+
+
+class _SyntheticChunks:
+    """Stand-in runner for the chunked-gather tests: `nchunks` chunks of
+    deterministic packed rows per rank; `sleep_after` = (chunk, seconds)
+    pauses mid-step after that chunk, `fail_after` raises after that chunk."""
+
+    def __init__(self, rank, nchunks, sleep_after=None, fail_after=None):
+        self.rank, self.nchunks = rank, nchunks
+        self.sleep_after, self.fail_after = sleep_after, fail_after
+
+    @staticmethod
+    def chunk(rank, k):
+        offs, data = _payload(100 * rank + k, 1000 + 37 * k)
+        return offs, data
+
+    def table_run_chunks(self, overlap, row_begin, row_end, on_chunk):
+        import time
+
+        for k in range(self.nchunks):
+            offs, data = self.chunk(self.rank, k)
+
+            class _P:
+                pass
+            pk = _P()
+            pk.offsets, pk.data = offs, data
+            on_chunk(k, pk)
+            if self.fail_after == k:
+                raise RuntimeError(f"rank {self.rank}: runner failed after chunk {k}")
+            if self.sleep_after and self.sleep_after[0] == k:
+                time.sleep(self.sleep_after[1])
+
+
+def _chunk_main(rank, world, port, q, sleepy=None, failing=None):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        plan = sd.ShardPlan(8 * world, 3, world, rank, "strong")
+        runner = _SyntheticChunks(rank, 3, sleep_after=(0, 3.0) if rank == sleepy else None,
+                                  fail_after=0 if rank == failing else None)
+        try:
+            got = plan.step_chunked(runner)
+        except Exception as e:  # noqa: BLE001 -- reported to the test
+            q.put((rank, "raised", str(e)))
+            return
+        if rank == 0:
+            want = [_SyntheticChunks.chunk(r, k) for r in range(world) for k in range(3)]
+            same = len(got) == len(want) and all(
+                (a[0] == b[0]).all() and a[1].tobytes() == b[1].tobytes() for a, b in zip(got, want))
+            arr = plan.last_arrival
+            q.put((rank, "ok", (bool(same), {r: list(v) for r, v in arr.items()})))
+        else:
+            q.put((rank, "ok", None))
+    finally:
+        dist.destroy_process_group()
+
+
+def _run_chunk_world(world, **kw):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_chunk_main, args=(r, world, port, q), kwargs=kw)
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    alive = [p for p in procs if p.is_alive()]
+    for p in alive:
+        p.kill()
+    assert not alive, "a rank hung"
+    out = {}
+    while len(out) < world:
+        r, what, info = q.get(timeout=5)
+        out[r] = (what, info)
+    return [p.exitcode for p in procs], out
+
+
+def test_gloo_chunked_slow_rank_does_not_block_others():
+    """Rank 0 receives each peer's chunks on that peer's own thread: while
+    rank 1 sleeps 3 s after its first chunk, ranks 2 and 3 deliver all their
+    chunks (a round-robin receiver would have waited on rank 1's second
+    chunk first); the rows arrive in order and byte-equal."""
+    codes, out = _run_chunk_world(4, sleepy=1)
+    assert codes == [0] * 4
+    same, arr = out[0][1]
+    assert same
+    late = arr[1][1]  # rank 1's second chunk comes after its sleep
+    assert late - arr[1][0] > 2.5
+    for r in (2, 3):
+        assert len(arr[r]) == 3 and max(arr[r]) < late - 1.0, (r, arr)
+
+
+@pytest.mark.parametrize("failing", [2, 0])
+def test_gloo_chunked_failure_is_reported(failing):
+    """A runner that raises mid-step: on a peer, its end marker carries the
+    error flag and rank 0 raises naming it instead of waiting for rows that
+    never come; on rank 0, the peers' chunks are still taken (the peers end
+    cleanly) and rank 0 raises its own error.  No rank hangs."""
+    world = 3
+    codes, out = _run_chunk_world(world, failing=failing)
+    assert codes == [0] * world  # every rank returned (the failures were reported, not hung)
+    assert out[failing][0] == "raised" and "runner failed" in out[failing][1]
+    if failing != 0:
+        assert out[0][0] == "raised" and f"rank {failing} reported a failed run" in out[0][1]
+    for r in range(world):
+        if r not in (0, failing):
+            assert out[r][0] == "ok"

@@ -360,3 +360,130 @@ def test_mixed_scene_small_batches_equal_oracle(monkeypatch, seed):
                     assert (a, t) == refs[j], kinds[j]
                 differ += ctx.table_timings()["spec_differ"]
     assert differ == 0
+
+
+@pytest.mark.parametrize("batch", [1, 4])
+def test_speculative_watermark_pass_before_last_replay(monkeypatch, batch):
+    """The speculative watermark pass (verify_final_kernel phase 3) reads the
+    pairs' F and H states while H's last window's replay may be setting them
+    on another stream; nothing orders the two.  SCM_DIAG_HOLD_LAST_REPLAY=1
+    forces one extreme: the pass is enqueued before that replay and the replay
+    waits for it, so every pair whose F or H ends in that window is still
+    running when the pass reads its state (the corridor stencil's middle
+    pairs, whose F stops within its 256-5,376th trials, i.e. in H's last
+    window; the watermark scenes, whose H runs to its cap there).  Rows equal
+    the oracle's, with SCM_DIAG_SPEC_CHECK=1 no speculative decision differs
+    from its recomputation (held, draw-state decisions occur, and void ones),
+    and without the check decisions are taken and rows still equal.  The other extreme (the
+    pass after the replay) is the normal form's fallback order, covered by the
+    tests above.  Reference: Estimate, then DetectWatermark, per pair
+    (sequential_matching.cc:98-99, 159)."""
+    scenes = [("two_translations", 600, 31, 0.1), ("plane_and_depth", 600, 33, 0.1),
+              ("translation", 500, 35, 0.4), ("general", 700, 37, 0.3)]
+    stencils = []
+    for i, (kind, m, seed, out) in enumerate(scenes):
+        kp1, kp2, mt = geometry_scene(kind, m, seed, outlier_frac=out)
+        d1, d2 = descriptors_for_matches(mt, len(kp1), len(kp2), seed)
+        stencils.append(table_rows([(500 + 2 * i, kp1, d1), (501 + 2 * i, kp2, d2)]))
+    ids, kps, descs = table_rows(Corridor(40, 900, 20, seed=38).images(0, 20))
+    stencils.append((ids, kps, descs))
+    refs = [oracle.execute_stencil(*s) for s in stencils]
+    monkeypatch.setenv("SCM_DIAG_HOLD_LAST_REPLAY", "1")
+    monkeypatch.setenv("SCM_DIAG_SPEC_CHECK", "1")
+    seen = {"spec_taken": 0, "spec_equal": 0, "spec_void": 0, "spec_differ": 0}
+    with Context(0) as ctx:
+        for rep in range(2):
+            for b0 in range(0, len(stencils), batch):
+                sel = list(range(b0, min(len(stencils), b0 + batch)))
+                got_ids, got_tvgs = ctx.execute_batch([stencils[j] for j in sel])
+                for j, a, t in zip(sel, got_ids, got_tvgs):
+                    assert (a, t) == refs[j], (j, rep)
+                tt = ctx.table_timings()
+                for k in seen:
+                    seen[k] += tt[k]
+    # (with the check every decision the pass would use is recomputed and
+    # counted as equal / different; void ones are recomputed anyway)
+    assert seen["spec_differ"] == 0, seen
+    assert seen["spec_equal"] > 0 and seen["spec_void"] > 0, seen
+    monkeypatch.delenv("SCM_DIAG_SPEC_CHECK")
+    taken = 0
+    with Context(0) as ctx:  # the held order without the check: decisions taken as they are
+        for j, st in enumerate(stencils):
+            assert ctx.execute_stencil(*st) == refs[j], j
+            taken += ctx.table_timings()["spec_taken"]
+    assert taken > 0
+
+
+@pytest.mark.parametrize("parallel_lo", ["1", "0"])
+def test_parallel_lo_more_records_than_slots(monkeypatch, parallel_lo):
+    """A small batch runs the LO chains of the first window's record models
+    (counts reaching the running maximum) in parallel, one slot per record up
+    to kLoSlots = 8 (rs_lo_chain2_kernel); records past the slots run inline in
+    the replay, in the same window.  A noise-free planar scene with 40 %
+    outliers gives every all-inlier 4-point sample the same H inlier count
+    (ties reach the maximum: ~33 records in 256 trials), and min_num_trials =
+    256 keeps the whole first window in play, so slot outcomes and inline
+    chains mix in one window, with residual-sum ties between them.  Rows
+    equal the oracle's with the parallel chains (SCM_PARALLEL_LO=1, the
+    default) and with every chain inline (=0).  Reference: LORANSAC's loop
+    (sequential_matching.cc:98-99 -> TwoViewGeometry::Estimate)."""
+    from scanner_colmap_amd import default_options
+    monkeypatch.setenv("SCM_PARALLEL_LO", parallel_lo)
+    o_gpu, o_ref = default_options(), oracle.default_options()
+    for o in (o_gpu, o_ref):
+        o.min_num_trials = 256
+    stencils = []
+    for i, (kind, m, seed, out) in enumerate([("planar", 800, 41, 0.4), ("planar", 600, 42, 0.3),
+                                             ("general", 700, 43, 0.3)]):
+        kp1, kp2, mt = geometry_scene(kind, m, seed, outlier_frac=out, noise_px=0.0)
+        d1, d2 = descriptors_for_matches(mt, len(kp1), len(kp2), seed)
+        stencils.append(table_rows([(600 + 2 * i, kp1, d1), (601 + 2 * i, kp2, d2)]))
+    refs = [oracle.execute_stencil(*s, opts=o_ref) for s in stencils]
+    assert decode_tvg_list(refs[0][1])[0].config == 6  # PLANAR_OR_PANORAMIC
+    with Context(0, o_gpu) as ctx:
+        for s, ref in zip(stencils, refs):
+            assert ctx.execute_stencil(*s) == ref
+        got_ids, got_tvgs = ctx.execute_batch(stencils)
+        assert list(zip(got_ids, got_tvgs)) == refs
+
+
+def test_concurrent_contexts_on_threads():
+    """Scanner runs one kernel object per pipeline instance, and instances
+    share a worker process (the per-instance constructor,
+    sequential_matching.cc:30-33; registration :202-205; SURVEY.md §8b
+    Threading).  Two threads, each with its own Context on device 0, run
+    interleaved batch-1 stencil streams of two different scenes at the same
+    time (ctypes releases the GIL in every library call); every row equals
+    the oracle's, and the second pass over the same streams (HBM image
+    caches warm, speculated content keys) too."""
+    import threading
+
+    K = 6
+    srcs = [table_rows(Corridor(14, 700, K, seed=900 + s).images()) for s in range(2)]
+    streams = []
+    for ids, kps, descs in srcs:
+        calls = [(ids[r:r + K], kps[r:r + K], descs[r:r + K]) for r in range(len(ids) - K + 1)]
+        streams.append((calls, [oracle.execute_stencil(*c) for c in calls]))
+    errors = []
+    start = threading.Barrier(2)
+
+    def run(i):
+        calls, refs = streams[i]
+        try:
+            with Context(0) as ctx:
+                start.wait()
+                for rep in range(2):
+                    for j, (c, ref) in enumerate(zip(calls, refs)):
+                        got = ctx.execute_stencil(*c)
+                        if got != ref:
+                            errors.append((i, rep, j))
+        except Exception as e:  # noqa: BLE001 -- reported below
+            errors.append((i, repr(e)))
+
+    threads = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in threads)
+    assert errors == []

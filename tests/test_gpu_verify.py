@@ -54,3 +54,22 @@ def test_table_run_bytes(gpu_ctx):
     for i in range(len(imgs)):
         assert got[0][i] == ref[0][i], i
         assert got[1][i] == ref[1][i], i
+
+
+@pytest.mark.parametrize("batch_pairs", ["0", "7"])
+def test_profile_diagnostic_keeps_outputs(monkeypatch, capfd, batch_pairs):
+    """SCM_PROFILE=1 (read at context creation) records per-pair phase cycles
+    in the verification kernels and prints their summary at context
+    destruction; the rows stay the oracle's.  With SCM_BATCH_PAIRS=7 the
+    table runs as several batches (the pipelined form, the last batch among
+    them)."""
+    from scanner_colmap_amd import Context
+    ids, kps, descs = table_rows(Corridor(10, 600, 4, seed=77).images())
+    ref = oracle.table_run(ids, kps, descs, 4, 0, len(ids))
+    monkeypatch.setenv("SCM_PROFILE", "1")
+    if batch_pairs != "0":
+        monkeypatch.setenv("SCM_BATCH_PAIRS", batch_pairs)
+    with Context(0) as ctx:
+        ctx.table_load(ids, kps, descs)
+        assert ctx.table_run(4, 0, len(ids)) == ref
+    assert "[scm verify profile]" in capfd.readouterr().err
