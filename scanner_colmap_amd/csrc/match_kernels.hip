@@ -691,7 +691,10 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
   // wave's row-heavy half tile (sections 3-4) runs beside the other's
   // MFMA-dense half (sections 1-2): -1 % matcher time (profiles/r06_d).  A
   // stagger of two whole tiles (the same phase within a tile) measured +2.5 %,
-  // static priority for waves 4-7 no change (profiles/r06_a).
+  // static priority for waves 4-7 no change (profiles/r06_a); with the half-tile
+  // stagger, priority for either half +1 to +2 %, and the loop unrolled by a
+  // group (4 tiles, compile-time barrier position: 32 B of spills) +7 %
+  // (profiles/r06_g).
   const bool late = wave >= kMatch8Waves / 2;
   const int nbar_loop = G / kG8T;  // barriers in the loop (full groups)
 

@@ -3610,9 +3610,6 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
       sh_stride ? std::max(1, std::min(64, (kShuffleLdsKb * 1024) / (2 * sh_stride))) : 1;
   const int sh_blocks = (npairs + sh_ppb - 1) / sh_ppb;
   const int wave_stride = (max_m + 7) / 8 * 8;
-  // (A run's last batch on the small-batch kernels -- a wave per pair in the
-  // draws and Shuffle, four in the replay -- with the table schedule measured
-  // 47.98/47.97K vs 48.35/48.33K pairs/s, profiles/r06_e: not kept.)
   const bool wave_sh = verify_small_batch(npairs, max_m);
   const size_t wave_lds = wave_shuffle_lds_bytes(wave_stride);
   const int max_chunks_s = (max_m + kScoreThreads * kScorePchSmall - 1) / (kScoreThreads * kScorePchSmall);
@@ -3629,6 +3626,11 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   if (wave_sh) W = std::min(kSmallFirstWindow, maxw);
   else
     while (W < maxw && (int64_t)npairs * 2 * W <= 1024) W *= 2;
+  // (A run's last batch -- its window chain runs with nothing beside it --
+  // starting at 4 / 8 / 16 rounds instead of the doubling rule's 1: 48.32 /
+  // 48.40 / 46.86K vs 48.38K pairs/s, and the small-batch kernels on the table
+  // schedule 47.98 vs 48.35K, profiles/r06_e, r06_h: fewer windows do not
+  // shorten the tail, not kept.)
   // Per-kind window sizes: the same schedule for both kinds, except a small
   // batch's second F window, kSmallSecondWindowF rounds: F stops early on
   // most pairs, and that window's draws run beside the first window's solves,
