@@ -27,14 +27,23 @@ constexpr int kFinThreads = 1024;
 constexpr int kXcds = 8;                         // MI355X: 8 XCDs, round-robin dispatch
 constexpr int kNumCUs = 256;                     // MI355X: 32 CUs per XCD
 
+// Column split of the i8 matcher (small batches): a pair's columns in up to
+// kMaxColSplit parts of 2^seg8_log2 64-column tiles, one job and one row
+// segment each.
+constexpr int kMaxColSplit = 8;
+constexpr int kSeg8Log2 = 7;  // unsplit: 128 tiles (8192 columns) per row segment
+
 // One workgroup of match_tiles_kernel: 512 rows of a pivot image against
 // every column of `npairs` neighbour images (pairs[pair0 .. pair0+npairs)).
+// i8 kernel: the first pair from 64-column tile t0, the last up to tile t1
+// (exclusive; 0 = its last tile): a column part of a split pair (npairs 1).
 struct MatchJob {
   int64_t a_row;   // table row of the pivot image's descriptor 0
   int32_t rb;      // row block
   int32_t n1;      // pivot keypoints
   int32_t pair0;   // first PairDesc of this pivot
   int32_t npairs;
+  int32_t t0, t1;
 };
 
 struct PairDesc {
@@ -48,6 +57,8 @@ struct PairDesc {
   int64_t rlist_off;    // int32 offset: [33 + n1] row-recheck buckets (v2 finalize)
   int32_t n1, n2, n2pad, nseg, nrb;
   int32_t clamp;        // 1: the pivot run took the CLAMP matcher variant
+  int32_t seg8_log2;    // i8 kernel: 64-column tiles per row segment, log2 (7: 8192 columns)
+  int32_t pad_;
 };
 
 hipError_t launch_match_tiles(const uint16_t* desc, const MatchJob* jobs, int njobs,
@@ -63,7 +74,7 @@ hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* ro
                                     const uint8_t* desc8, const int32_t* csum,
                                     const float* lut, float max_ratio, float max_distance,
                                     int cross_check, uint2* matches, int32_t* counts,
-                                    int max_groups, hipStream_t stream);
+                                    int max_groups, int max_cols, hipStream_t stream);
 hipError_t launch_match_finalize(const PairDesc* pairs, int npairs, const uint2* rowres,
                                  const uint2* colpart, int32_t* m21, const float* lut,
                                  float max_ratio, float max_distance, int cross_check,

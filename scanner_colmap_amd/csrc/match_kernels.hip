@@ -365,7 +365,7 @@ __global__ __launch_bounds__(kMatchThreads, 1) void match_tiles_kernel(
 // t-bits), which is (dot << 13) | t-bits mod 2^32 (the 2^22 offset shifts out).
 // Per element: 1 (key) + 2 (row state) + ~1.3 (column tree) VALU ops.
 // ===========================================================================
-constexpr int kTiles8PerSeg = kTilesPerSeg / 2;  // 64-column tiles per 8192-column segment
+static_assert((kTile8Cols << kSeg8Log2) == kColsPerSeg, "i8 row segments of the bf16 kernel's width");
 
 // Byte offset of 16-B chunk c (of 8) of column col in an i8 LDS tile.  The
 // XOR with (col >> 1) & 7 makes each 16-lane group of a ds_read_b128 (one
@@ -565,8 +565,10 @@ __device__ __forceinline__ void g8_merge(const uint32_t* src, uint2* dst) {
 }
 
 // One workgroup = one MatchJob (512 pivot rows, 8 waves x 64) swept against
-// every column of its neighbour images.  The tiles of the job's pairs form one
-// stream (tile g -> pair p, tile t of p).  Groups of kG8T = 4 tiles share one
+// every column of its neighbour images, or one column part of one (the
+// small-batch column split: tiles [t0, t1), row segments of 2^seg8_log2
+// tiles).  The tiles of the job's pairs form one stream (tile g -> pair p,
+// tile t of p).  Groups of kG8T = 4 tiles share one
 // barrier: at the barrier ending group m every wave has (a) waited for its
 // LDS-DMA of group m + 1, (b) finished reading group m - 1's stages, which
 // then receive group m + 3, and (c) written its column partials of group
@@ -623,14 +625,20 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // operands in registers before any LDS-DMA
 
-  int G = 0;
-  for (int p = 0; p < job.npairs; ++p) G += (P[p].n2 + kTile8Cols - 1) / kTile8Cols;
+  // Tiles of pair p in this job: [p == 0 ? t0 : 0, tile_end(p)) (a column
+  // part of a split pair: its first and last pair are the same).
+  auto tile_end = [&](int pp) {
+    const int ntp = (P[pp].n2 + kTile8Cols - 1) / kTile8Cols;
+    return pp == job.npairs - 1 && job.t1 > 0 ? min(job.t1, ntp) : ntp;
+  };
+  int G = -job.t0;
+  for (int p = 0; p < job.npairs; ++p) G += tile_end(p);
   // LDS-DMA cursor (groups ahead of the compute cursor; past the last tile it
   // re-stages the last one, so every wave issues the same number of
   // operations per group and the vmcnt counts stay fixed).
-  int fp = 0, ft = 0;
-  int64_t fb = P[0].b_row;
-  int fn = (P[0].n2 + kTile8Cols - 1) / kTile8Cols;
+  int fp = 0, ft = job.t0;
+  int64_t fb = P[0].b_row + (int64_t)job.t0 * kTile8Cols;
+  int fn = tile_end(0);
   const int gpt = wave == kMatch8Waves - 1 ? 2 : 1;  // LDS-DMA operations per tile
   // LDS-DMA of a tile into ring stage `stage`: wave w moves columns 8w ..
   // 8w + 7; lane L writes LDS byte 16 L of the wave's block, i.e. (column 8w +
@@ -658,7 +666,7 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
           ++fp;
           ft = 0;
           fb = P[fp].b_row;
-          fn = (P[fp].n2 + kTile8Cols - 1) / kTile8Cols;
+          fn = tile_end(fp);
           fptr = desc8 + fb * 128;
           fsum = csum + fb;
         } else {
@@ -680,9 +688,10 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
   __builtin_amdgcn_s_barrier();
 
   // Compute cursor.
-  int p = 0, t = 0;
+  int p = 0, t = job.t0;
   PairDesc pd = P[0];
-  int nt = (pd.n2 + kTile8Cols - 1) / kTile8Cols;
+  int nt = tile_end(0);
+  int segm = (1 << pd.seg8_log2) - 1;  // a row segment ends at tile t with (t & segm) == segm
   int64_t cpi = pd.colpart_off + (int64_t)job.rb * pd.n2pad;  // colpart index of tile 0 of pair p
   int flushed = -8;  // iteration of the last row flush (its stores)
   // Waves 4-7 (the second wave of each SIMD) meet group barrier m half a tile
@@ -719,7 +728,6 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
     const int stage = g % kG8Stages;
     const uint32_t cb0 = cbn0, cb1 = cbn1;  // read with the tile's c0 fragments
     if (tid == 0) meta[stage] = cpi + (int64_t)t * kTile8Cols;
-    const int k = t & (kTiles8PerSeg - 1);  // 64-column tile within the segment
     const u64 kq0 = ((u64)cb0 << 32) | cb0, kq1 = ((u64)cb1 << 32) | cb1;  // row value addends
     u64 k00[8], k10[8], k01[8], k11[8];
     const int m = g / kG8T;
@@ -779,8 +787,8 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
     g8_rows(k10, k11, b1r[1]);
     g8_col_partial(e01, e11, cscw + 32, h, r);
     // Row flush at the end of a segment (or of the pair).
-    if (k == kTiles8PerSeg - 1 || t + 1 == nt) {
-      row_flush_values<CLAMP>(b1r, rowres + pd.rowres_off + (int64_t)(t / kTiles8PerSeg) * pd.n1, row0,
+    if ((t & segm) == segm || t + 1 == nt) {
+      row_flush_values<CLAMP>(b1r, rowres + pd.rowres_off + (int64_t)(t >> pd.seg8_log2) * pd.n1, row0,
                 pd.n1, r, h);
 #pragma unroll
       for (int s = 0; s < 2; ++s)
@@ -792,7 +800,8 @@ __global__ __launch_bounds__(kMatch8Threads, 512 / kMatch8Threads) void match_g8
       ++p;
       t = 0;
       pd = P[p];
-      nt = (pd.n2 + kTile8Cols - 1) / kTile8Cols;
+      nt = tile_end(p);
+      segm = (1 << pd.seg8_log2) - 1;
       cpi = pd.colpart_off + (int64_t)job.rb * pd.n2pad;
     }
   }
@@ -935,31 +944,71 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
 }
 
 // Finalize of the version-2 i8 matcher (best-only column partials, value
-// mode: max_ratio <= 1 with the cross-check, or no cross-check).  One
-// workgroup per pair:
-//  1. columns: merge the row blocks' (B1, B2', wave) (raw accumulator units,
-//     converted here with the column's sum) into colpart row 0 as
-//     x = B1 | rb << 19, y = B2' << 3 | wave (B1, B2' < 2^19: fast variant
-//     dots are < 2^19, clamp-variant values <= 2^18);
-//  2. rows: merge the segments' row keys, ratio / distance tests; with the
-//     cross-check a row i with best column j stays a CANDIDATE only if
-//     B1(j) equals its best value, the 64-row group holding B1 is the one
-//     of row i (otherwise another row ties B1: the column's second equals its
-//     best and fails), and column j passes with second >= B2';
-//  3. candidates, per 64-row group (one wave, one lane per row, the group's
-//     descriptors register-resident): the 64 exact dots of column j
-//     (v_dot4 on the offset operands, the same integers as the MFMA path),
-//     their top-2 (multiset), and the final column test with second =
-//     max(B2', second within the group);
-//  4. ordered compaction of the accepted rows (idx1 ascending).
-// The per-row decisions live in rowres segment 0 between the phases.
+// mode: max_ratio <= 1 with the cross-check, or no cross-check):
+//  1. columns (match_colmerge_g8_kernel, one thread per column): merge the
+//     row blocks' (B1, B2', wave) (raw accumulator units, converted here with
+//     the column's sum) into colpart row 0 as x = B1 | rb << 19, y = B2' << 3
+//     | wave (B1, B2' < 2^19: fast variant dots are < 2^19, clamp-variant
+//     values <= 2^18);
+//  2. rows (match_finalize_g8_kernel phase 0, a workgroup per pair): merge
+//     the segments' row values, ratio / distance tests with the second's
+//     lower bound, the passing rows queued by residue for
+//     match_rowcheck_g8_kernel, which decides them; with the cross-check a
+//     row i with best column j stays a CANDIDATE only if B1(j) equals its
+//     best value, the 64-row group holding B1 is the one of row i (otherwise
+//     another row ties B1: the column's second equals its best and fails),
+//     and column j passes with second >= B2';
+//  3. candidates (match_recheck_g8_kernel), per 64-row group: the exact
+//     top-2 of the group's dots of column j on MFMA, and the final column
+//     test with second = max(B2', second within the group);
+//  4. ordered compaction of the accepted rows (idx1 ascending; phase 1).
+// The per-row decisions live in rowres segment 0 between the phases.  The
+// loops keep several rows' (row blocks') loads in flight: the chain runs on
+// the small-batch critical path, where a pair's workgroup is latency-bound.
+constexpr int kFinU = 8;         // rows per thread and pass (loads in flight)
+constexpr int kCmThreads = 256;  // match_colmerge_g8_kernel: columns per workgroup
+
+__global__ __launch_bounds__(kCmThreads) void match_colmerge_g8_kernel(
+    const PairDesc* __restrict__ pairs, uint2* __restrict__ colpart,
+    const int32_t* __restrict__ csum, int prio) {
+  if (prio) __builtin_amdgcn_s_setprio(2);
+  const PairDesc pd = pairs[blockIdx.y];
+  const int j = blockIdx.x * kCmThreads + threadIdx.x;
+  if (pd.n1 == 0 || j >= pd.n2) return;
+  uint2* cp = colpart + pd.colpart_off;
+  const uint2 m = cp[j];
+  uint32_t b1 = m.x, b2 = m.y >> 3, w = m.y & 7u, rbest = 0u;
+  // ascending row blocks, eight loads in flight; a block past nrb reads as
+  // (0, 0), which changes nothing (0 > b1 never holds, max(b2, 0) = b2)
+  for (int b = 1; b < pd.nrb; b += 8) {
+    uint2 o[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      o[u] = b + u < pd.nrb ? cp[(int64_t)(b + u) * pd.n2pad + j] : make_uint2(0u, 0u);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const bool gt = o[u].x > b1;
+      b2 = gt ? max(o[u].y >> 3, b1) : max(b2, o[u].x);
+      w = gt ? (o[u].y & 7u) : w;
+      rbest = gt ? (uint32_t)(b + u) : rbest;
+      b1 = gt ? o[u].x : b1;
+    }
+  }
+  // raw accumulator units (dot - cb_j + 2^22) -> dot values of the column
+  const uint32_t cbm = (uint32_t)csum[pd.b_row + j] - (1u << 22);
+  b1 += cbm;
+  b2 += cbm;
+  if (pd.clamp) {
+    b1 = min(b1, kLutMax);
+    b2 = min(b2, kLutMax);
+  }
+  cp[j] = make_uint2(b1 | (rbest << 19), (b2 << 3) | w);
+}
 
 __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
-    const PairDesc* __restrict__ pairs, uint2* __restrict__ rowres, uint2* __restrict__ colpart,
-    uint2* __restrict__ rowaux, int32_t* __restrict__ rlist,
-    const uint8_t* __restrict__ desc8, const int32_t* __restrict__ csum,
-    const float* __restrict__ lut, float max_ratio, float max_distance, int cross_check,
-    uint2* __restrict__ matches, int32_t* __restrict__ counts, int phase) {
+    const PairDesc* __restrict__ pairs, uint2* __restrict__ rowres, uint2* __restrict__ rowaux,
+    int32_t* __restrict__ rlist, const float* __restrict__ lut, float max_ratio,
+    float max_distance, uint2* __restrict__ matches, int32_t* __restrict__ counts, int phase) {
   // bit 4 of phase: raised wave priority (the batch's verification waits for
   // this chain; launch_match_finalize_g8)
   if (phase & 4) __builtin_amdgcn_s_setprio(2);
@@ -973,72 +1022,52 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     if (tid == 0) counts[blockIdx.x] = 0;
     return;
   }
-  uint2* cp = colpart + pd.colpart_off;
   uint2* rr = rowres + pd.rowres_off;
   if (phase == 0) {
-  if (cross_check) {
-    for (int j = tid; j < pd.n2; j += kFinThreads) {
-      const uint2 m = cp[j];
-      uint32_t b1 = m.x, b2 = m.y >> 3, w = m.y & 7u, rbest = 0u;
-      int b = 1;
-      for (; b + 8 <= pd.nrb; b += 8) {  // eight row blocks' loads in flight
-        uint2 o[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) o[u] = cp[(int64_t)(b + u) * pd.n2pad + j];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-          const bool gt = o[u].x > b1;
-          b2 = gt ? max(o[u].y >> 3, b1) : max(b2, o[u].x);
-          w = gt ? (o[u].y & 7u) : w;
-          rbest = gt ? (uint32_t)(b + u) : rbest;
-          b1 = gt ? o[u].x : b1;
-        }
-      }
-      for (; b < pd.nrb; ++b) {
-        const uint2 o = cp[(int64_t)b * pd.n2pad + j];
-        const bool gt = o.x > b1;
-        b2 = gt ? max(o.y >> 3, b1) : max(b2, o.x);
-        w = gt ? (o.y & 7u) : w;
-        rbest = gt ? (uint32_t)b : rbest;
-        b1 = gt ? o.x : b1;
-      }
-      // raw accumulator units (dot - cb_j + 2^22) -> dot values of the column
-      const uint32_t cbm = (uint32_t)csum[pd.b_row + j] - (1u << 22);
-      b1 += cbm;
-      b2 += cbm;
-      if (pd.clamp) {
-        b1 = min(b1, kLutMax);
-        b2 = min(b2, kLutMax);
-      }
-      cp[j] = make_uint2(b1 | (rbest << 19), (b2 << 3) | w);
-    }
-    __syncthreads();
-  }
-  // Phase 2: per-row decisions (rows strided over the threads, coalesced).
-  // The matcher's rows carry their best VALUE, the residue (mod 32) of the
-  // best column, and as second a lower bound (best of the other lanes, see
-  // row_flush_values): a row that fails with it fails; a row that passes is
-  // queued in the bucket of its residue (state 3) for
-  // match_rowcheck_g8_kernel, which finds the best column, the exact second
-  // and (with the cross-check) whether the row can still be its column's match.
+  // Phase 2: per-row decisions (rows strided over the threads, coalesced;
+  // kFinU rows per thread and pass).  The matcher's rows carry their best
+  // VALUE, the residue (mod 32) of the best column, and as second a lower
+  // bound (best of the other lanes, see row_flush_values): a row that fails
+  // with it fails; a row that passes is queued in the bucket of its residue
+  // (state 3) for match_rowcheck_g8_kernel, which finds the best column, the
+  // exact second and (with the cross-check) whether the row can still be its
+  // column's match.
   int32_t* rl = rlist + pd.rlist_off;
   uint2* ax = rowaux + pd.aux_off;
   if (tid < 32) bcnt[tid] = 0;
   __syncthreads();
-  for (int i = tid; i < pd.n1; i += kFinThreads) {
-    uint2 m = rr[i];
-    for (int sg = 1; sg < pd.nseg; ++sg) {
-      const uint2 o = rr[(int64_t)sg * pd.n1 + i];
-      m.y = merge_second(m.x, m.y, o.x, o.y);
-      m.x = max(m.x, o.x);
+  for (int i0 = tid; i0 < pd.n1; i0 += kFinU * kFinThreads) {
+    uint2 m[kFinU];
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u) {
+      const int i = i0 + u * kFinThreads;
+      m[u] = i < pd.n1 ? rr[i] : make_uint2(0u, 0u);
     }
-    const uint32_t best = m.x >> kIdxBits, second = m.y >> kIdxBits;
-    const int32_t col = (int32_t)((kIdxMask - (m.x & kIdxMask)) & 31u);  // residue of the best
-    const uint32_t state = passes(lut, best, second, max_ratio, max_distance) ? 3u : 0u;
-    rr[i] = make_uint2((uint32_t)col, state);
-    if (state == 3u) {
-      ax[i] = make_uint2(best, second);
-      atomicAdd(&bcnt[col & 31], 1);
+    for (int sg = 1; sg < pd.nseg; ++sg) {
+      uint2 o[kFinU];
+#pragma unroll
+      for (int u = 0; u < kFinU; ++u) {
+        const int i = i0 + u * kFinThreads;
+        o[u] = i < pd.n1 ? rr[(int64_t)sg * pd.n1 + i] : make_uint2(0u, 0u);
+      }
+#pragma unroll
+      for (int u = 0; u < kFinU; ++u) {
+        m[u].y = merge_second(m[u].x, m[u].y, o[u].x, o[u].y);
+        m[u].x = max(m[u].x, o[u].x);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u) {
+      const int i = i0 + u * kFinThreads;
+      if (i >= pd.n1) break;
+      const uint32_t best = m[u].x >> kIdxBits, second = m[u].y >> kIdxBits;
+      const int32_t col = (int32_t)((kIdxMask - (m[u].x & kIdxMask)) & 31u);  // residue of the best
+      const uint32_t state = passes(lut, best, second, max_ratio, max_distance) ? 3u : 0u;
+      rr[i] = make_uint2((uint32_t)col, state);
+      if (state == 3u) {
+        ax[i] = make_uint2(best, second);
+        atomicAdd(&bcnt[col & 31], 1);
+      }
     }
   }
   __syncthreads();
@@ -1052,37 +1081,57 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
     rl[32] = acc;
   }
   __syncthreads();
-  // (the order within a bucket is immaterial: every queued row is decided alone)
-  for (int i = tid; i < pd.n1; i += kFinThreads) {
-    const uint2 st = rr[i];
-    if (st.y == 3u) rl[33 + atomicAdd(&bcur[st.x & 31u], 1)] = i;
+  // (the order within a bucket is immaterial: every queued row is decided
+  // alone; each thread re-reads the states it wrote above)
+  for (int i0 = tid; i0 < pd.n1; i0 += kFinU * kFinThreads) {
+    uint2 st[kFinU];
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u) {
+      const int i = i0 + u * kFinThreads;
+      st[u] = i < pd.n1 ? rr[i] : make_uint2(0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u)
+      if (st[u].y == 3u) rl[33 + atomicAdd(&bcur[st[u].x & 31u], 1)] = i0 + u * kFinThreads;
   }
   return;
   }
   // Phase 4: ordered compaction (idx1 ascending), one tile of kFinThreads
-  // consecutive rows at a time: ballot prefixes within the waves, wave
-  // offsets through LDS, a running offset over the tiles.
+  // consecutive rows at a time (the states of kFinU tiles loaded together):
+  // ballot prefixes within the waves, wave offsets through LDS, a running
+  // offset over the tiles.
   int run = 0;
-  for (int t0 = 0; t0 < pd.n1; t0 += kFinThreads) {
-    const int i = t0 + tid;
-    const uint2 st = i < pd.n1 ? rr[i] : make_uint2(0u, 0u);
-    const bool f = st.y == 1u;
-    const uint64_t bm = __ballot(f);
-    if (lane == 0) wave_tot[wave] = __popcll(bm);
-    __syncthreads();
-    int off = run, tot = 0;
-    for (int w = 0; w < kFinThreads / 64; ++w) {
-      const int c = wave_tot[w];
-      off += w < wave ? c : 0;
-      tot += c;
+  for (int r0 = 0; r0 < pd.n1; r0 += kFinU * kFinThreads) {
+    uint2 sts[kFinU];
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u) {
+      const int i = r0 + u * kFinThreads + tid;
+      sts[u] = i < pd.n1 ? rr[i] : make_uint2(0u, 0u);
     }
-    if (f) {
-      const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
-                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-      matches[pd.match_off + off + pre] = make_uint2((uint32_t)i, st.x);
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u) {
+      const int t0 = r0 + u * kFinThreads;
+      if (t0 >= pd.n1) break;
+      const int i = t0 + tid;
+      const uint2 st = sts[u];
+      const bool f = st.y == 1u;
+      const uint64_t bm = __ballot(f);
+      if (lane == 0) wave_tot[wave] = __popcll(bm);
+      __syncthreads();
+      int off = run, tot = 0;
+      for (int w = 0; w < kFinThreads / 64; ++w) {
+        const int c = wave_tot[w];
+        off += w < wave ? c : 0;
+        tot += c;
+      }
+      if (f) {
+        const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32),
+                                                       __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+        matches[pd.match_off + off + pre] = make_uint2((uint32_t)i, st.x);
+      }
+      run += tot;
+      __syncthreads();  // wave_tot is rewritten by the next tile
     }
-    run += tot;
-    __syncthreads();  // wave_tot is rewritten by the next tile
   }
   if (tid == 0) counts[blockIdx.x] = run;
 }
@@ -1364,16 +1413,19 @@ hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* ro
                                     const uint8_t* desc8, const int32_t* csum,
                                     const float* lut, float max_ratio, float max_distance,
                                     int cross_check, uint2* matches, int32_t* counts,
-                                    int max_groups, hipStream_t stream) {
+                                    int max_groups, int max_cols, hipStream_t stream) {
   if (npairs <= 0) return hipSuccess;
   // The finalize chain's waves at raised issue priority over the verification
   // kernels of earlier batches beside it: the batch's own verification waits
   // for this chain (46.90/47.00K vs 46.78/46.75K pairs/s, profiles/r05_v).
   constexpr int prio = 1;
   const int pbit = prio ? 4 : 0;
+  if (cross_check && max_cols > 0)
+    hipLaunchKernelGGL(match_colmerge_g8_kernel,
+                       dim3((unsigned)((max_cols + kCmThreads - 1) / kCmThreads), npairs),
+                       dim3(kCmThreads), 0, stream, pairs, colpart, csum, prio);
   hipLaunchKernelGGL(match_finalize_g8_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
-                     rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
-                     cross_check, matches, counts, 0 | pbit);
+                     rowres, rowaux, rlist, lut, max_ratio, max_distance, matches, counts, 0 | pbit);
   hipLaunchKernelGGL(match_rowcheck_g8_kernel, dim3(32, npairs), dim3(kRcThreads), 0, stream,
                      pairs, rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
                      cross_check, prio);
@@ -1382,8 +1434,7 @@ hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* ro
                        dim3(256), 0, stream, pairs, rowres, colpart, desc8, csum, lut, max_ratio,
                        max_distance, prio);
   hipLaunchKernelGGL(match_finalize_g8_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
-                     rowres, colpart, rowaux, rlist, desc8, csum, lut, max_ratio, max_distance,
-                     cross_check, matches, counts, 1 | pbit);
+                     rowres, rowaux, rlist, lut, max_ratio, max_distance, matches, counts, 1 | pbit);
   return hipGetLastError();
 }
 

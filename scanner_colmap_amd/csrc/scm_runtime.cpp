@@ -860,7 +860,7 @@ int stream_priority(bool high) {
 // XCD-aware job order.  Workgroups are dispatched round-robin over the 8
 // XCDs (workgroup b -> XCD b mod 8), each XCD with its own L2.  The jobs of
 // one pivot run (its row blocks, which all sweep the same neighbour
-// descriptors) are kept on one XCD so that the neighbour tiles are fetched
+// descriptors; with the column split, of one column part) are kept on one XCD so that the neighbour tiles are fetched
 // into that XCD's L2 once instead of once per XCD; the runs are spread over
 // the XCDs by work (least-loaded first) and the queues interleaved, padding
 // with empty jobs.
@@ -870,9 +870,13 @@ void xcd_order(std::vector<MatchJob>& jobs, const std::vector<PairDesc>& pds) {
   std::vector<double> load(kXcds, 0.0);
   for (size_t i = 0; i < jobs.size();) {
     size_t j = i;
-    while (j < jobs.size() && jobs[j].a_row == jobs[i].a_row && jobs[j].pair0 == jobs[i].pair0) ++j;
+    while (j < jobs.size() && jobs[j].a_row == jobs[i].a_row && jobs[j].pair0 == jobs[i].pair0 &&
+           jobs[j].t0 == jobs[i].t0)
+      ++j;
     double cols = 0.0;
     for (int32_t k = 0; k < jobs[i].npairs; ++k) cols += pds[jobs[i].pair0 + k].n2;
+    if (jobs[i].t1 > 0)  // a column part
+      cols = std::min<double>(cols, (double)(jobs[i].t1 - jobs[i].t0) * kTile8Cols);
     const int x = (int)(std::min_element(load.begin(), load.end()) - load.begin());
     load[x] += cols * (double)(j - i);
     q[x].insert(q[x].end(), jobs.begin() + i, jobs.begin() + j);
@@ -921,6 +925,20 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   bs.moff.resize(P);
   int64_t rr = 0, cp = 0, m21 = 0, mo = 0, ax = 0, rlo = 0;
   const int32_t rpb = ctx->match_bf16 ? kRowsPerBlock : kRowsPerBlock8;  // pivot rows per job
+  const int64_t want_jobs = 4 * kNumCUs;  // jobs of a batch that fills the GPU (below)
+  // Column split (i8 matcher, small batches): with one pair per job a single
+  // stencil (K - 1 pairs x 16 row blocks: 304 jobs) still leaves the last of
+  // two rounds of jobs on 48 of the 256 CUs; cutting each pair's columns into
+  // csplit parts (row segments of their own, merged by the finalize like the
+  // 8192-column segments) gives ~4 rounds of shorter jobs.
+  int32_t csplit = 1;
+  if (!given && !ctx->match_bf16 && P <= verify_small_batch_pairs()) {
+    int64_t pair_jobs = 0;
+    for (int64_t k = 0; k < P; ++k)
+      if (t.ndesc[specs[k].a] > 0 && t.ndesc[specs[k].b] > 0)
+        pair_jobs += (t.ndesc[specs[k].a] + rpb - 1) / rpb;
+    while (pair_jobs > 0 && csplit < kMaxColSplit && pair_jobs * csplit < want_jobs) csplit *= 2;
+  }
   for (int64_t i = 0; i < P;) {
     const int32_t a = specs[i].a;
     int64_t j = i;
@@ -936,6 +954,15 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
       pd.n2 = given ? 0 : t.ndesc[b];
       pd.n2pad = (pd.n2 + kTile8Cols - 1) / kTile8Cols * kTile8Cols;  // whole 64-column tiles
       pd.nseg = (pd.n2 + kColsPerSeg - 1) / kColsPerSeg;
+      pd.seg8_log2 = kSeg8Log2;
+      if (csplit > 1) {
+        // segments of 2^seg8_log2 tiles, at least ceil(tiles / csplit) each
+        const int32_t nt = pd.n2pad / kTile8Cols, per = (nt + csplit - 1) / csplit;
+        int32_t lg = 0;
+        while (lg < kSeg8Log2 && (1 << lg) < per) ++lg;
+        pd.seg8_log2 = lg;
+        pd.nseg = (nt + (1 << lg) - 1) >> lg;
+      }
       pd.nrb = (pd.n1 + rpb - 1) / rpb;
       pd.b_row = given ? 0 : t.desc_row[b];
       pd.a_row = given ? 0 : t.desc_row[a];
@@ -979,26 +1006,38 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   {
     int64_t base_jobs = 0;
     for (const Run& r : runs) base_jobs += (t.ndesc[r.a] + rpb - 1) / rpb;
-    const int64_t want = 4 * kNumCUs;
     for (const Run& r : runs) {
       const int32_t n1 = t.ndesc[r.a];
       const int32_t nrb = (n1 + rpb - 1) / rpb;
-      int32_t parts = 1;
-      if (base_jobs > 0 && base_jobs < want)
-        parts = (int32_t)std::min<int64_t>(r.npairs, (want + base_jobs - 1) / base_jobs);
-      for (int32_t q = 0; q < parts; ++q) {
-        const int32_t p0 = r.pair0 + (int32_t)((int64_t)r.npairs * q / parts);
-        const int32_t p1 = r.pair0 + (int32_t)((int64_t)r.npairs * (q + 1) / parts);
-        if (p1 <= p0) continue;
+      auto add = [&](int32_t p0, int32_t np, int32_t t0, int32_t t1) {
         for (int32_t rb = 0; rb < nrb; ++rb) {
           MatchJob jb;
           jb.a_row = t.desc_row[r.a];
           jb.rb = rb;
           jb.n1 = n1;
           jb.pair0 = p0;
-          jb.npairs = p1 - p0;
+          jb.npairs = np;
+          jb.t0 = t0;
+          jb.t1 = t1;
           (r.clamp ? jobs_clamp : jobs).push_back(jb);
         }
+      };
+      if (csplit > 1) {  // one job per pair, row block and row segment
+        for (int32_t k = r.pair0; k < r.pair0 + r.npairs; ++k) {
+          const PairDesc& pd = pds[k];
+          const int32_t nt = pd.n2pad / kTile8Cols;
+          for (int32_t sg = 0; sg < pd.nseg; ++sg)
+            add(k, 1, sg << pd.seg8_log2, std::min(nt, (sg + 1) << pd.seg8_log2));
+        }
+        continue;
+      }
+      int32_t parts = 1;
+      if (base_jobs > 0 && base_jobs < want_jobs)
+        parts = (int32_t)std::min<int64_t>(r.npairs, (want_jobs + base_jobs - 1) / base_jobs);
+      for (int32_t q = 0; q < parts; ++q) {
+        const int32_t p0 = r.pair0 + (int32_t)((int64_t)r.npairs * q / parts);
+        const int32_t p1 = r.pair0 + (int32_t)((int64_t)r.npairs * (q + 1) / parts);
+        if (p1 > p0) add(p0, p1 - p0, 0, 0);
       }
     }
   }
@@ -1042,8 +1081,12 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   std::memcpy(st + s_pairs, pds.data(), P * sizeof(PairDesc));
   std::memcpy(st + s_mo, bs.moff.data(), P * sizeof(int64_t));
   // 64-row groups of the largest pivot (grid of match_recheck_g8_kernel)
-  int max_groups = 0;
-  for (int64_t k = 0; k < P; ++k) max_groups = std::max(max_groups, (pds[k].n1 + 63) / 64);
+  // and the widest neighbour (grid of match_colmerge_g8_kernel)
+  int max_groups = 0, max_cols = 0;
+  for (int64_t k = 0; k < P; ++k) {
+    max_groups = std::max(max_groups, (pds[k].n1 + 63) / 64);
+    max_cols = std::max(max_cols, pds[k].n2);
+  }
   hipStream_t sm = ctx->stream;
   if (NJ)
     SCM_HIP(hipMemcpyAsync(bs.jobs.ptr, st, NJ * sizeof(MatchJob), hipMemcpyHostToDevice, sm));
@@ -1094,7 +1137,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
                                      t.csum.as<int32_t>(), ctx->lut.as<float>(),
                                      (float)ctx->opts.max_ratio, (float)ctx->opts.max_distance,
                                      ctx->opts.cross_check, bs.matches.as<uint2>(),
-                                     bs.counts.as<int32_t>(), max_groups, sf));
+                                     bs.counts.as<int32_t>(), max_groups, max_cols, sf));
   else if (!given)
     SCM_HIP(launch_match_finalize(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
                                   bs.colpart.as<uint2>(), bs.m21.as<int32_t>(),
@@ -1733,9 +1776,11 @@ int64_t pair_workspace_bytes(int64_t n1, int64_t n2) {
 // small-batch kernels (enqueue_verify): windows of kWindowTrialsSmall trials
 // in three parities, F and H (window starts, states and trial counts
 // included), and the parallel-LO slots of both kinds and the first two
-// parities (at most, for a pivot of n1 keypoints).
+// parities (at most, for a pivot of n1 keypoints), and the row segments of
+// the matcher's column split (enqueue_match).
 int64_t small_batch_extra_bytes(int64_t n1) {
-  return 2 * (3 * (int64_t)kWindowTrialsSmall - (int64_t)kWindowTrials) * kRoundTrialBytes +
+  return (int64_t)kMaxColSplit * n1 * 8 +
+         2 * (3 * (int64_t)kWindowTrialsSmall - (int64_t)kWindowTrials) * kRoundTrialBytes +
          2 * 2 * (640 * 4 + kVerifyStateWords * 4 + 4) +
          4 * (int64_t)kLoSlots * (lo_slot_doubles(std::max<int64_t>(n1, 1)) * 8 + (int64_t)sizeof(LoSlot));
 }

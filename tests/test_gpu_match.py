@@ -76,6 +76,35 @@ def test_segmented_columns(gpu_ctx):
     _same(gpu_ctx, a, b)
 
 
+def test_segmented_columns_unsplit_batch():
+    """A batch of more pairs than the small-batch column split takes
+    (verify_small_batch_pairs, 256): the matcher sweeps whole pairs and n2 >
+    8192 crosses its own 8192-column row segments (a single pair, as in
+    test_segmented_columns, takes the column split).  Table path, kept
+    matches of every row against the oracle's pair matcher."""
+    from scanner_colmap_amd import Context
+    from scanner_colmap_amd.codecs import table_rows
+    n = 260
+    rng = np.random.default_rng(31)
+    descs = [random_descriptors(64 if i % 2 == 0 else 8192 + 700, 300 + i) for i in range(n)]
+    for i in range(0, n - 1, 2):
+        descs[i + 1][8500:8564] = descs[i]  # pivot i's matches in the second segment
+        descs[i + 1][100:132] = descs[i][:32]  # and duplicates in the first (ties)
+    imgs = [(i + 1, np.concatenate([rng.uniform(0, 1000, (len(d), 2)),
+                                    np.zeros((len(d), 4))], 1).astype(np.float32), d)
+            for i, d in enumerate(descs)]
+    ids, kps, enc = table_rows(imgs)
+    with Context(0) as ctx:
+        ctx.table_load(ids, kps, enc)
+        ctx.set_keep_matches(True)
+        ctx.table_run(2, 0, n)
+        got = [ctx.table_matches(r, 1) for r in range(n - 1)]
+    for r in range(n - 1):
+        ref = oracle.match_pair(descs[r], descs[r + 1])
+        np.testing.assert_array_equal(got[r], ref, err_msg=f"row {r}")
+    assert sum(len(g) for g in got[0::2]) >= 32 * ((n - 1) // 2 + 1)
+
+
 def test_high_bytes_fast_variant(gpu_ctx):
     # Bytes >= 128 (outside the i8 range before the offset) with norms small
     # enough for the fast keys: exercises the a - 128 correction terms.
