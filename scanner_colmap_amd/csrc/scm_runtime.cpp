@@ -301,12 +301,29 @@ struct PinnedOut {
   }
 };
 
+// Diagnostics builds only (-DSCM_DIAG_HOST_TIMES, probes/build_*): host
+// timestamps of one execute() call's steps, printed to stderr per call.
+#ifdef SCM_DIAG_HOST_TIMES
+std::chrono::steady_clock::time_point g_ht[16];
+#define SCM_HT(k) (g_ht[k] = std::chrono::steady_clock::now())
+#else
+#define SCM_HT(k) ((void)0)
+#endif
+
 // One in-flight batch: device workspace, descriptor staging, results.
 struct BatchSet {
   DevBuf rowaux, rlist;  // v2 finalize: row (best, second bound), row-recheck buckets
-  DevBuf jobs, pairs, rowres, colpart, m21, matches, counts, gpairs, vpairs, xy1, xy2, scratch,
-      snaps, masks, offsets, match_off, prof, xyf, dvout, dpack, dpmask, rst, samp, nmod, fcon,
+  // mdesc: the matcher's jobs, pair descriptors and match offsets, vdesc: the
+  // gather and verification pair tables -- each one upload (one copy) of the
+  // staging layout; d_* point into them
+  DevBuf mdesc, rowres, colpart, m21, matches, counts, vdesc, xy1, xy2, scratch,
+      snaps, masks, offsets, prof, xyf, dvout, dpack, dpmask, rst, samp, nmod, fcon,
       cnts, act, nact, mods, wsnap;
+  MatchJob* d_jobs = nullptr;
+  PairDesc* d_pairs = nullptr;
+  int64_t* d_moff = nullptr;
+  GatherPair* d_gpairs = nullptr;
+  VerifyPair* d_vpairs = nullptr;
   // round buffers of the H LO-RANSAC (advanced beside F's, own PRNG stream)
   DevBuf h_rst, h_samp, h_nmod, h_fcon, h_cnts, h_act, h_nact, h_mods, h_wsnap;
   DevBuf ucnt, h_ucnt;  // split scoring: undecided points per model
@@ -342,8 +359,8 @@ struct BatchSet {
   bool posted = false;   // stage 2 enqueued
   bool matched = false;
   void release() {
-    for (DevBuf* b : {&rowaux, &rlist, &jobs, &pairs, &rowres, &colpart, &m21, &matches, &counts, &gpairs, &vpairs,
-                      &xy1, &xy2, &scratch, &snaps, &masks, &offsets, &match_off, &prof, &xyf, &dvout,
+    for (DevBuf* b : {&rowaux, &rlist, &mdesc, &rowres, &colpart, &m21, &matches, &counts, &vdesc,
+                      &xy1, &xy2, &scratch, &snaps, &masks, &offsets, &prof, &xyf, &dvout,
                       &dpack, &dpmask, &rst, &samp, &nmod, &fcon, &cnts, &act, &nact,
                       &mods, &wsnap, &h_rst, &h_samp, &h_nmod, &h_fcon, &h_cnts, &h_act, &h_nact,
                       &h_mods, &h_wsnap, &ucnt, &h_ucnt, &wb, &wstate, &dtrial, &h_wb, &h_wstate,
@@ -1048,8 +1065,6 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   jobs.insert(jobs.end(), jobs_clamp.begin(), jobs_clamp.end());
   const int64_t NJ = (int64_t)jobs.size();
   // ---- buffers.
-  SCM_TRY(bs.jobs.ensure(std::max<int64_t>(NJ, 1) * sizeof(MatchJob)));
-  SCM_TRY(bs.pairs.ensure(P * sizeof(PairDesc)));
   SCM_TRY(bs.rowres.ensure(std::max<int64_t>(rr, 1) * sizeof(uint2)));
   SCM_TRY(bs.colpart.ensure(std::max<int64_t>(cp, 1) * sizeof(uint2)));
   SCM_TRY(bs.m21.ensure(std::max<int64_t>(m21, 1) * sizeof(int32_t)));
@@ -1059,7 +1074,6 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   SCM_TRY(bs.masks.ensure(std::max<int64_t>(mo, 1)));
   SCM_TRY(bs.counts.ensure(P * sizeof(int32_t)));
   SCM_TRY(bs.offsets.ensure((P + 1) * sizeof(int64_t)));
-  SCM_TRY(bs.match_off.ensure(P * sizeof(int64_t)));
   bs.off_counts = 0;
   bs.off_offsets = align256(bs.off_counts + P * sizeof(int32_t));
   bs.off_vout = align256(bs.off_offsets + (P + 1) * sizeof(int64_t));
@@ -1088,12 +1102,13 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
     max_cols = std::max(max_cols, pds[k].n2);
   }
   hipStream_t sm = ctx->stream;
-  if (NJ)
-    SCM_HIP(hipMemcpyAsync(bs.jobs.ptr, st, NJ * sizeof(MatchJob), hipMemcpyHostToDevice, sm));
-  SCM_HIP(hipMemcpyAsync(bs.pairs.ptr, st + s_pairs, P * sizeof(PairDesc), hipMemcpyHostToDevice,
-                         sm));
-  SCM_HIP(hipMemcpyAsync(bs.match_off.ptr, st + s_mo, P * sizeof(int64_t), hipMemcpyHostToDevice,
-                         sm));
+  // jobs, pair descriptors and match offsets in one copy (one blit on the
+  // small-batch critical path instead of three)
+  SCM_TRY(bs.mdesc.ensure(s_cnt));
+  bs.d_jobs = reinterpret_cast<MatchJob*>(bs.mdesc.as<uint8_t>());
+  bs.d_pairs = reinterpret_cast<PairDesc*>(bs.mdesc.as<uint8_t>() + s_pairs);
+  bs.d_moff = reinterpret_cast<int64_t*>(bs.mdesc.as<uint8_t>() + s_mo);
+  SCM_HIP(hipMemcpyAsync(bs.mdesc.ptr, st, s_mo + P * sizeof(int64_t), hipMemcpyHostToDevice, sm));
   if (given) {
     std::memcpy(st + s_cnt, given_counts, P * sizeof(int32_t));
     SCM_HIP(hipMemcpyAsync(bs.counts.ptr, st + s_cnt, P * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -1112,15 +1127,15 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   SCM_HIP(hipEventRecord(bs.ev[0], sm));
   if (!given)
     for (int clamp = 0; clamp < 2; ++clamp) {
-      const MatchJob* jb = bs.jobs.as<MatchJob>() + (clamp ? nfast : 0);
+      const MatchJob* jb = bs.d_jobs + (clamp ? nfast : 0);
       const int nj = (int)(clamp ? NJ - nfast : nfast);
       if (nj > 0) ctx->n_match_launches += 1;
       if (ctx->match_bf16)
-        SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), jb, nj, bs.pairs.as<PairDesc>(),
+        SCM_HIP(launch_match_tiles(t.desc.as<uint16_t>(), jb, nj, bs.d_pairs,
                                    bs.rowres.as<uint2>(), bs.colpart.as<uint2>(), clamp, sm));
       else
         SCM_HIP(launch_match_g8(t.desc8.as<uint8_t>(), t.csum.as<int32_t>(), jb, nj,
-                                bs.pairs.as<PairDesc>(), bs.rowres.as<uint2>(),
+                                bs.d_pairs, bs.rowres.as<uint2>(),
                                 bs.colpart.as<uint2>(), clamp, sm));
     }
   SCM_HIP(hipEventRecord(bs.ev[1], sm));
@@ -1131,7 +1146,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   hipStream_t sf = bs.vstream;
   SCM_HIP(hipStreamWaitEvent(sf, bs.ev[1], 0));
   if (!given && !ctx->match_bf16)
-    SCM_HIP(launch_match_finalize_g8(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
+    SCM_HIP(launch_match_finalize_g8(bs.d_pairs, (int)P, bs.rowres.as<uint2>(),
                                      bs.colpart.as<uint2>(), bs.rowaux.as<uint2>(),
                                      bs.rlist.as<int32_t>(), t.desc8.as<uint8_t>(),
                                      t.csum.as<int32_t>(), ctx->lut.as<float>(),
@@ -1139,7 +1154,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
                                      ctx->opts.cross_check, bs.matches.as<uint2>(),
                                      bs.counts.as<int32_t>(), max_groups, max_cols, sf));
   else if (!given)
-    SCM_HIP(launch_match_finalize(bs.pairs.as<PairDesc>(), (int)P, bs.rowres.as<uint2>(),
+    SCM_HIP(launch_match_finalize(bs.d_pairs, (int)P, bs.rowres.as<uint2>(),
                                   bs.colpart.as<uint2>(), bs.m21.as<int32_t>(),
                                   ctx->lut.as<float>(), (float)ctx->opts.max_ratio,
                                   (float)ctx->opts.max_distance, ctx->opts.cross_check,
@@ -1173,7 +1188,9 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
   if (!bs.pending || bs.P == 0) return SCM_OK;
   const int64_t P = bs.P;
   const ImageTable& t = *bs.table;
+  SCM_HT(5);
   SCM_HIP(hipEventSynchronize(bs.ev[3]));
+  SCM_HT(6);
   uint8_t* outh = reinterpret_cast<uint8_t*>(bs.out.host);
   const int32_t* counts = reinterpret_cast<const int32_t*>(outh + bs.off_counts);
   hipStream_t sv = bs.vstream;
@@ -1224,8 +1241,6 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       scr += verify_scratch_doubles(m);
     }
     const int max_m = counts[order[0]];
-    SCM_TRY(bs.gpairs.ensure(V * sizeof(GatherPair)));
-    SCM_TRY(bs.vpairs.ensure(V * sizeof(VerifyPair)));
     SCM_TRY(bs.xy1.ensure(2 * std::max<int64_t>(bs.slots, 1) * sizeof(double)));
     SCM_TRY(bs.xy2.ensure(2 * std::max<int64_t>(bs.slots, 1) * sizeof(double)));
     SCM_TRY(bs.xyf.ensure(std::max<int64_t>(bs.slots, 1) * sizeof(float4)));
@@ -1236,10 +1251,12 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
     uint8_t* st = bs.vstage.as<uint8_t>();
     std::memcpy(st, gps.data(), V * sizeof(GatherPair));
     std::memcpy(st + s_v, vps.data(), V * sizeof(VerifyPair));
-    SCM_HIP(hipMemcpyAsync(bs.gpairs.ptr, st, V * sizeof(GatherPair), hipMemcpyHostToDevice, sv));
-    SCM_HIP(hipMemcpyAsync(bs.vpairs.ptr, st + s_v, V * sizeof(VerifyPair),
-                           hipMemcpyHostToDevice, sv));
-    SCM_HIP(launch_gather(bs.gpairs.as<GatherPair>(), (int)V, bs.matches.as<uint2>(),
+    // both tables in one copy
+    SCM_TRY(bs.vdesc.ensure(s_v + V * sizeof(VerifyPair)));
+    bs.d_gpairs = reinterpret_cast<GatherPair*>(bs.vdesc.as<uint8_t>());
+    bs.d_vpairs = reinterpret_cast<VerifyPair*>(bs.vdesc.as<uint8_t>() + s_v);
+    SCM_HIP(hipMemcpyAsync(bs.vdesc.ptr, st, s_v + V * sizeof(VerifyPair), hipMemcpyHostToDevice, sv));
+    SCM_HIP(launch_gather(bs.d_gpairs, (int)V, max_m, bs.matches.as<uint2>(),
                           t.kpxy.as<float2>(), bs.xy1.as<double>(), bs.xy2.as<double>(), nullptr,
                           bs.xyf.as<float4>(), sv));
     uint64_t* prof = nullptr;
@@ -1383,12 +1400,14 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       }
     }
     const VerifyParams vparams = make_params(ctx->opts, iteration);
-    SCM_HIP(launch_verify(bs.vpairs.as<VerifyPair>(), (int)V, max_m, bs.xy1.as<double>(),
+    SCM_HT(7);
+    SCM_HIP(launch_verify(bs.d_vpairs, (int)V, max_m, bs.xy1.as<double>(),
                           bs.xy2.as<double>(), bs.scratch.as<double>(), bs.snaps.as<uint32_t>(),
                           bs.masks.as<uint8_t>(), bs.dvout.as<VerifyOut>(),
                           vparams, prof, nullptr, bs.xyf.as<float4>(), rbf, rbh,
                           sv, bs.sev, &bs.nwin, &spec));
   }
+  SCM_HT(8);
   SCM_HIP(hipEventRecord(bs.ev[5], sv));
   // Compact matches + F-inlier masks in HBM, then DMA the results into the
   // pinned host buffer (counts are already there).
@@ -1397,7 +1416,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
   SCM_HIP(hipMemcpyAsync(bs.offsets.ptr, offs, (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
                          sv));
   SCM_HIP(launch_compact(bs.counts.as<int32_t>(), (int)P, bs.offsets.as<int64_t>(),
-                         bs.match_off.as<int64_t>(), bs.matches.as<uint2>(),
+                         bs.d_moff, bs.matches.as<uint2>(),
                          bs.masks.as<uint8_t>(), bs.dpack.as<uint2>(), bs.dpmask.as<uint8_t>(),
                          sv));
   if (total > 0) {
@@ -1421,7 +1440,9 @@ int collect_batch(scm_context* ctx, BatchSet& bs, BatchView* v) {
     set_error("internal: batch collected before its verification stage was enqueued");
     return SCM_E_STATE;
   }
+  SCM_HT(10);
   SCM_HIP(hipEventSynchronize(bs.ev[6]));
+  SCM_HT(11);
   bs.pending = bs.posted = false;
   if (bs.matched) {
     ctx->t_match += event_ms(bs.ev[0], bs.ev[1]);
@@ -1432,6 +1453,7 @@ int collect_batch(scm_context* ctx, BatchSet& bs, BatchView* v) {
     for (int w = 0; w < bs.nwin; ++w) ctx->t_score += event_ms(bs.sev[2 * w], bs.sev[2 * w + 1]);
     bs.nwin = 0;
   }
+  SCM_HT(14);
   const uint8_t* o = reinterpret_cast<const uint8_t*>(bs.out.host);
   v->counts = reinterpret_cast<const int32_t*>(o + bs.off_counts);
   v->offsets = reinterpret_cast<const int64_t*>(o + bs.off_offsets);
@@ -1486,7 +1508,7 @@ int64_t inlier_count(const BatchView& v, int64_t p) {
   if (!v.vout || v.vout[p].config == 0) return 0;
   const uint8_t* m = v.masks + v.offsets[p];
   int64_t c = 0;
-  for (int32_t i = 0; i < v.counts[p]; ++i) c += m[i];
+  for (int32_t i = 0; i < v.counts[p]; ++i) c += m[i] != 0;
   return c;
 }
 
@@ -1513,13 +1535,20 @@ uint8_t* write_tvg(uint8_t* d, const BatchView& v, int64_t p, int64_t ninl) {
   std::memcpy(d, &n, 8);
   d += 8;
   if (ninl > 0) {
+    // Branch-free compaction (the masks are data-dependent: a branch per match
+    // mispredicts about every other time, ~8x slower): every match is stored
+    // at the next output slot, which advances only past an inlier.  Up to the
+    // last inlier L, the slot is always < ninl.
     const int64_t o = v.offsets[p];
+    const uint8_t* mk = v.masks + o;
+    const Match* mt = v.matches + o;
+    int32_t last = v.counts[p] - 1;
+    while (!mk[last]) --last;  // ninl > 0: an inlier exists
     int64_t w = 0;
-    for (int32_t i = 0; i < v.counts[p]; ++i)
-      if (v.masks[o + i]) {
-        std::memcpy(d + 8 * w, &v.matches[o + i], 8);
-        ++w;
-      }
+    for (int32_t i = 0; i <= last; ++i) {
+      std::memcpy(d + 8 * w, &mt[i], 8);
+      w += mk[i] ? 1 : 0;
+    }
     d += 8 * ninl;
   }
   return d;
@@ -1793,9 +1822,9 @@ int64_t set_budget_bytes(scm_context* ctx) {
   if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return INT64_MAX;
   int64_t held = 0;
   for (const BatchSet& bs : ctx->sets)
-    for (const DevBuf* b : {&bs.rowaux, &bs.rlist, &bs.jobs, &bs.pairs, &bs.rowres, &bs.colpart, &bs.m21, &bs.matches,
-                            &bs.counts, &bs.gpairs, &bs.vpairs, &bs.xy1, &bs.xy2, &bs.scratch,
-                            &bs.snaps, &bs.masks, &bs.offsets, &bs.match_off, &bs.prof, &bs.xyf,
+    for (const DevBuf* b : {&bs.rowaux, &bs.rlist, &bs.mdesc, &bs.rowres, &bs.colpart, &bs.m21, &bs.matches,
+                            &bs.counts, &bs.vdesc, &bs.xy1, &bs.xy2, &bs.scratch,
+                            &bs.snaps, &bs.masks, &bs.offsets, &bs.prof, &bs.xyf,
                             &bs.dvout, &bs.dpack, &bs.dpmask, &bs.rst, &bs.samp, &bs.nmod,
                             &bs.fcon, &bs.cnts, &bs.act, &bs.nact, &bs.mods, &bs.wsnap,
                             &bs.h_rst, &bs.h_samp, &bs.h_nmod, &bs.h_fcon, &bs.h_cnts, &bs.h_act,
@@ -1950,6 +1979,7 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
               {b.specs[p].b - row, std::vector<Match>(v.matches + o, v.matches + o + v.counts[p])});
         }
       }
+    SCM_HT(15);
     std::vector<Tvg> tv;
     if (ctx->opts.multiple_models)  // the later Estimates reuse bs: v is consumed first
       SCM_TRY(estimate_multiple(ctx, bs, v, &tv));
@@ -2000,10 +2030,12 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
   } else {
     for (size_t k = 0; k < B; ++k) {
       if (k >= 3) SCM_TRY(finish(batches[k - 3], ctx->sets[(k - 3) % 3]));
+      SCM_HT(4);
       SCM_TRY(enqueue_match(ctx, ctx->sets[k % 3], t, batches[k].specs, nullptr, nullptr));
       if (k >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(k - 1) % 3], true));
     }
     if (B >= 1) SCM_TRY(enqueue_verify(ctx, ctx->sets[(B - 1) % 3], true));
+    SCM_HT(9);
   }
   for (size_t k = B >= 3 ? B - 3 : 0; k < B; ++k) SCM_TRY(finish(batches[k], ctx->sets[k % 3]));
   if (!streamed && !chunked) out->row_off.push_back((int64_t)out->size);
@@ -2256,6 +2288,7 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
                  scm_blob* tvgs_out) {
   const int64_t ne = batch * stencil_size;
   const auto h0 = std::chrono::steady_clock::now();
+  SCM_HT(0);
   std::unordered_map<Src, int64_t, SrcHash> first;  // buffers -> first element
   std::vector<int64_t> of(ne), now_e, spec_e;
   for (int64_t e = 0; e < ne; ++e) {
@@ -2340,8 +2373,10 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
   ctx->n_match_launches = 0;
   Packed pk;
   const auto h2 = std::chrono::steady_clock::now();
+  SCM_HT(3);
   rc = run_rows(ctx, t, plan, -1, &pk);
   const auto h3 = std::chrono::steady_clock::now();
+  SCM_HT(12);
   ctx->t_run = std::chrono::duration<double, std::milli>(h3 - h2).count();
   if (rc != SCM_OK) {
     drain(ctx);
@@ -2394,6 +2429,17 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
   }
   if (!pool_give(pk.data)) std::free(pk.data);
   ctx->t_out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h3).count();
+#ifdef SCM_DIAG_HOST_TIMES
+  SCM_HT(13);
+  {
+    static const int ks[] = {0, 3, 4, 5, 6, 7, 8, 9, 10, 11, 14, 15, 12, 13};
+    std::string line = "[scm host us]";
+    for (size_t i = 1; i < sizeof(ks) / sizeof(ks[0]); ++i)
+      line += " " + std::to_string(ks[i]) + ":" +
+              std::to_string((int)std::chrono::duration<double, std::micro>(g_ht[ks[i]] - g_ht[ks[0]]).count());
+    fprintf(stderr, "%s\n", line.c_str());
+  }
+#endif
   return SCM_OK;
 }
 

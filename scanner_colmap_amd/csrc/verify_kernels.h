@@ -215,7 +215,8 @@ struct GatherPair {
   int32_t m;          // number of matches when cidx < 0
   int32_t cidx;       // index into the device match counts (>= 0: read m there)
 };
-hipError_t launch_gather(const GatherPair* pairs, int npairs, const uint2* matches,
+// (max_m: at least every pair's match count)
+hipError_t launch_gather(const GatherPair* pairs, int npairs, int max_m, const uint2* matches,
                          const float2* kpxy, double* xy1, double* xy2, const int32_t* counts,
                          float4* xyf, hipStream_t stream);
 // Packs each pair's matches / F-inlier mask contiguously at offsets[p].

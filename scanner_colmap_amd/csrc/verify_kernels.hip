@@ -2014,9 +2014,13 @@ __device__ __attribute__((always_inline)) void rs_begin_body(
     const int n = ps.n;
     const float4* xyf = xyf_all + ps.pp.pts_off / 2;
     float smax = 0.0f;
-    for (int i = lane; i < n; i += 64) {
-      const float4 v = xyf[i];
-      smax = fmaxf(smax, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+    for (int i0 = lane; i0 < n; i0 += 64 * 8) {  // eight loads in flight (clamped: same max)
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = xyf[min(i0 + 64 * u, n - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        smax = fmaxf(smax, fmaxf(fmaxf(fabsf(v[u].x), fabsf(v[u].y)), fmaxf(fabsf(v[u].z), fabsf(v[u].w))));
     }
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) smax = fmaxf(smax, __shfl_xor(smax, d));
@@ -3502,21 +3506,39 @@ __global__ __launch_bounds__(256) void rs_replay2w_kernel(
                               rh.lo, rh.lo_data, rh.lo_stride);
 }
 
-__global__ void gather_kernel(const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
-                              const float2* __restrict__ kpxy, double* __restrict__ xy1,
-                              double* __restrict__ xy2, const int32_t* __restrict__ counts,
-                              float4* __restrict__ xyf) {
-  const GatherPair g = pairs[blockIdx.x];
+// Points of the verified pairs: block (x, q) takes matches [x * kGatherChunk,
+// ...) of pair q, kGatherU per thread with their loads in flight (the
+// gather is on a small batch's critical path).
+constexpr int kGatherThreads = 256, kGatherU = 4, kGatherChunk = kGatherThreads * kGatherU;
+__global__ __launch_bounds__(kGatherThreads) void gather_kernel(
+    const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
+    const float2* __restrict__ kpxy, double* __restrict__ xy1, double* __restrict__ xy2,
+    const int32_t* __restrict__ counts, float4* __restrict__ xyf) {
+  const GatherPair g = pairs[blockIdx.y];
   const int m = g.cidx >= 0 ? counts[g.cidx] : g.m;
-  for (int i = threadIdx.x; i < m; i += blockDim.x) {
-    const uint2 mt = matches[g.match_off + i];
-    const float2 a = kpxy[g.kp1_off + mt.x];
-    const float2 b = kpxy[g.kp2_off + mt.y];
-    xy1[2 * (g.pts_off + i)] = (double)a.x;
-    xy1[2 * (g.pts_off + i) + 1] = (double)a.y;
-    xy2[2 * (g.pts_off + i)] = (double)b.x;
-    xy2[2 * (g.pts_off + i) + 1] = (double)b.y;
-    xyf[g.pts_off + i] = make_float4(a.x, a.y, b.x, b.y);
+  const int i0 = blockIdx.x * kGatherChunk + threadIdx.x;
+  if (i0 >= m) return;
+  uint2 mt[kGatherU];
+#pragma unroll
+  for (int u = 0; u < kGatherU; ++u) {
+    const int i = i0 + u * kGatherThreads;
+    mt[u] = matches[g.match_off + (i < m ? i : i0)];
+  }
+  float2 a[kGatherU], b[kGatherU];
+#pragma unroll
+  for (int u = 0; u < kGatherU; ++u) {
+    a[u] = kpxy[g.kp1_off + mt[u].x];
+    b[u] = kpxy[g.kp2_off + mt[u].y];
+  }
+#pragma unroll
+  for (int u = 0; u < kGatherU; ++u) {
+    const int i = i0 + u * kGatherThreads;
+    if (i >= m) break;
+    xy1[2 * (g.pts_off + i)] = (double)a[u].x;
+    xy1[2 * (g.pts_off + i) + 1] = (double)a[u].y;
+    xy2[2 * (g.pts_off + i)] = (double)b[u].x;
+    xy2[2 * (g.pts_off + i) + 1] = (double)b[u].y;
+    xyf[g.pts_off + i] = make_float4(a[u].x, a[u].y, b[u].x, b[u].y);
   }
 }
 
@@ -3802,6 +3824,10 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
     covered_f += Wf * kTrialBatch;
     covered_h += Wh * kTrialBatch;
     if (wave_sh) {
+      // (H's second window at 96 / 64 / 48 / 32 rounds: 2.34-2.36 / 2.41-2.44 /
+      // 2.48 / 2.53-2.58 vs 2.30-2.35 ms per batch-1 call, and F 64 with H
+      // 64: 2.42-2.47, profiles/r06_q; window cap 160 / 192 rounds: within the
+      // noise, profiles/r06_r -- not kept)
       Wf = r == 0 ? std::min(kSmallSecondWindowF, maxw) : maxw;
       Wh = maxw;
     } else {
@@ -3969,12 +3995,12 @@ hipError_t launch_verify(const VerifyPair* pairs, int npairs, int max_m, const d
   return hipGetLastError();
 }
 
-hipError_t launch_gather(const GatherPair* pairs, int npairs, const uint2* matches,
+hipError_t launch_gather(const GatherPair* pairs, int npairs, int max_m, const uint2* matches,
                          const float2* kpxy, double* xy1, double* xy2, const int32_t* counts,
                          float4* xyf, hipStream_t stream) {
-  if (npairs <= 0) return hipSuccess;
-  hipLaunchKernelGGL(gather_kernel, dim3(npairs), dim3(256), 0, stream, pairs, matches, kpxy,
-                     xy1, xy2, counts, xyf);
+  if (npairs <= 0 || max_m <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)((max_m + kGatherChunk - 1) / kGatherChunk), npairs),
+                     dim3(kGatherThreads), 0, stream, pairs, matches, kpxy, xy1, xy2, counts, xyf);
   return hipGetLastError();
 }
 
