@@ -3666,7 +3666,10 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   // Windows whose LO chains run in parallel (small batches with LO slots):
   // the first (later windows' records are many and mostly superseded; two
   // windows measured slower, profiles/r05_m).
-  constexpr int lo_windows = 1;
+#ifndef SCM_VAR_LOW
+#define SCM_VAR_LOW 1
+#endif
+  constexpr int lo_windows = SCM_VAR_LOW;
   // Decoupled draws (speculative schedule with a draw stream): window r's
   // draws and shuffles run on dstream as soon as window r - 2 is replayed (its
   // active list) and window r - 1's prune has run (the lists and counts it
