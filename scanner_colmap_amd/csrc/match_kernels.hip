@@ -965,44 +965,51 @@ __global__ __launch_bounds__(kFinThreads) void match_finalize_kernel(
 // The per-row decisions live in rowres segment 0 between the phases.  The
 // loops keep several rows' (row blocks') loads in flight: the chain runs on
 // the small-batch critical path, where a pair's workgroup is latency-bound.
-constexpr int kFinU = 8;         // rows per thread and pass (loads in flight)
-constexpr int kCmThreads = 256;  // match_colmerge_g8_kernel: columns per workgroup
+constexpr int kFinU = 8;  // rows per thread and pass (loads in flight)
+// match_colmerge_g8_kernel: small batches spread a pair's columns over
+// workgroups of kCmThreads (one column per thread); large batches take one
+// workgroup of kFinThreads per pair (the table path: a grid of many small
+// workgroups took CUs from the next batch's matcher beside it, matcher 4.5 %
+// slower in the overlapped step, profiles/r06_s).
+constexpr int kCmThreads = 256;
+constexpr int kCmWidePairs = 256;  // up to this many pairs: the wide grid
 
-__global__ __launch_bounds__(kCmThreads) void match_colmerge_g8_kernel(
+__global__ __launch_bounds__(kFinThreads) void match_colmerge_g8_kernel(
     const PairDesc* __restrict__ pairs, uint2* __restrict__ colpart,
     const int32_t* __restrict__ csum, int prio) {
   if (prio) __builtin_amdgcn_s_setprio(2);
   const PairDesc pd = pairs[blockIdx.y];
-  const int j = blockIdx.x * kCmThreads + threadIdx.x;
-  if (pd.n1 == 0 || j >= pd.n2) return;
+  if (pd.n1 == 0) return;
   uint2* cp = colpart + pd.colpart_off;
-  const uint2 m = cp[j];
-  uint32_t b1 = m.x, b2 = m.y >> 3, w = m.y & 7u, rbest = 0u;
-  // ascending row blocks, eight loads in flight; a block past nrb reads as
-  // (0, 0), which changes nothing (0 > b1 never holds, max(b2, 0) = b2)
-  for (int b = 1; b < pd.nrb; b += 8) {
-    uint2 o[8];
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < pd.n2; j += gridDim.x * blockDim.x) {
+    const uint2 m = cp[j];
+    uint32_t b1 = m.x, b2 = m.y >> 3, w = m.y & 7u, rbest = 0u;
+    // ascending row blocks, eight loads in flight; a block past nrb reads as
+    // (0, 0), which changes nothing (0 > b1 never holds, max(b2, 0) = b2)
+    for (int b = 1; b < pd.nrb; b += 8) {
+      uint2 o[8];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      o[u] = b + u < pd.nrb ? cp[(int64_t)(b + u) * pd.n2pad + j] : make_uint2(0u, 0u);
+      for (int u = 0; u < 8; ++u)
+        o[u] = b + u < pd.nrb ? cp[(int64_t)(b + u) * pd.n2pad + j] : make_uint2(0u, 0u);
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const bool gt = o[u].x > b1;
-      b2 = gt ? max(o[u].y >> 3, b1) : max(b2, o[u].x);
-      w = gt ? (o[u].y & 7u) : w;
-      rbest = gt ? (uint32_t)(b + u) : rbest;
-      b1 = gt ? o[u].x : b1;
+      for (int u = 0; u < 8; ++u) {
+        const bool gt = o[u].x > b1;
+        b2 = gt ? max(o[u].y >> 3, b1) : max(b2, o[u].x);
+        w = gt ? (o[u].y & 7u) : w;
+        rbest = gt ? (uint32_t)(b + u) : rbest;
+        b1 = gt ? o[u].x : b1;
+      }
     }
+    // raw accumulator units (dot - cb_j + 2^22) -> dot values of the column
+    const uint32_t cbm = (uint32_t)csum[pd.b_row + j] - (1u << 22);
+    b1 += cbm;
+    b2 += cbm;
+    if (pd.clamp) {
+      b1 = min(b1, kLutMax);
+      b2 = min(b2, kLutMax);
+    }
+    cp[j] = make_uint2(b1 | (rbest << 19), (b2 << 3) | w);
   }
-  // raw accumulator units (dot - cb_j + 2^22) -> dot values of the column
-  const uint32_t cbm = (uint32_t)csum[pd.b_row + j] - (1u << 22);
-  b1 += cbm;
-  b2 += cbm;
-  if (pd.clamp) {
-    b1 = min(b1, kLutMax);
-    b2 = min(b2, kLutMax);
-  }
-  cp[j] = make_uint2(b1 | (rbest << 19), (b2 << 3) | w);
 }
 
 __global__ __launch_bounds__(kFinThreads) void match_finalize_g8_kernel(
@@ -1420,10 +1427,12 @@ hipError_t launch_match_finalize_g8(const PairDesc* pairs, int npairs, uint2* ro
   // for this chain (46.90/47.00K vs 46.78/46.75K pairs/s, profiles/r05_v).
   constexpr int prio = 1;
   const int pbit = prio ? 4 : 0;
-  if (cross_check && max_cols > 0)
+  if (cross_check && max_cols > 0) {
+    const bool wide = npairs <= kCmWidePairs;
     hipLaunchKernelGGL(match_colmerge_g8_kernel,
-                       dim3((unsigned)((max_cols + kCmThreads - 1) / kCmThreads), npairs),
-                       dim3(kCmThreads), 0, stream, pairs, colpart, csum, prio);
+                       dim3(wide ? (unsigned)((max_cols + kCmThreads - 1) / kCmThreads) : 1u, npairs),
+                       dim3(wide ? kCmThreads : kFinThreads), 0, stream, pairs, colpart, csum, prio);
+  }
   hipLaunchKernelGGL(match_finalize_g8_kernel, dim3(npairs), dim3(kFinThreads), 0, stream, pairs,
                      rowres, rowaux, rlist, lut, max_ratio, max_distance, matches, counts, 0 | pbit);
   hipLaunchKernelGGL(match_rowcheck_g8_kernel, dim3(32, npairs), dim3(kRcThreads), 0, stream,

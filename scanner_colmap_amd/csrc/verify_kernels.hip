@@ -3506,39 +3506,42 @@ __global__ __launch_bounds__(256) void rs_replay2w_kernel(
                               rh.lo, rh.lo_data, rh.lo_stride);
 }
 
-// Points of the verified pairs: block (x, q) takes matches [x * kGatherChunk,
-// ...) of pair q, kGatherU per thread with their loads in flight (the
-// gather is on a small batch's critical path).
+// Points of the verified pairs: block (x, q) takes chunks x, x + gridDim.x,
+// ... of kGatherChunk matches of pair q, kGatherU per thread with their loads
+// in flight.  Small batches (the gather is on their critical path) spread a
+// pair over max_m / kGatherChunk blocks; large ones take a block per pair (a
+// grid of many more blocks beside the next batch's matcher takes its CUs).
 constexpr int kGatherThreads = 256, kGatherU = 4, kGatherChunk = kGatherThreads * kGatherU;
+constexpr int kGatherWidePairs = 256;
 __global__ __launch_bounds__(kGatherThreads) void gather_kernel(
     const GatherPair* __restrict__ pairs, const uint2* __restrict__ matches,
     const float2* __restrict__ kpxy, double* __restrict__ xy1, double* __restrict__ xy2,
     const int32_t* __restrict__ counts, float4* __restrict__ xyf) {
   const GatherPair g = pairs[blockIdx.y];
   const int m = g.cidx >= 0 ? counts[g.cidx] : g.m;
-  const int i0 = blockIdx.x * kGatherChunk + threadIdx.x;
-  if (i0 >= m) return;
-  uint2 mt[kGatherU];
+  for (int i0 = blockIdx.x * kGatherChunk + threadIdx.x; i0 < m; i0 += gridDim.x * kGatherChunk) {
+    uint2 mt[kGatherU];
 #pragma unroll
-  for (int u = 0; u < kGatherU; ++u) {
-    const int i = i0 + u * kGatherThreads;
-    mt[u] = matches[g.match_off + (i < m ? i : i0)];
-  }
-  float2 a[kGatherU], b[kGatherU];
+    for (int u = 0; u < kGatherU; ++u) {
+      const int i = i0 + u * kGatherThreads;
+      mt[u] = matches[g.match_off + (i < m ? i : i0)];
+    }
+    float2 a[kGatherU], b[kGatherU];
 #pragma unroll
-  for (int u = 0; u < kGatherU; ++u) {
-    a[u] = kpxy[g.kp1_off + mt[u].x];
-    b[u] = kpxy[g.kp2_off + mt[u].y];
-  }
+    for (int u = 0; u < kGatherU; ++u) {
+      a[u] = kpxy[g.kp1_off + mt[u].x];
+      b[u] = kpxy[g.kp2_off + mt[u].y];
+    }
 #pragma unroll
-  for (int u = 0; u < kGatherU; ++u) {
-    const int i = i0 + u * kGatherThreads;
-    if (i >= m) break;
-    xy1[2 * (g.pts_off + i)] = (double)a[u].x;
-    xy1[2 * (g.pts_off + i) + 1] = (double)a[u].y;
-    xy2[2 * (g.pts_off + i)] = (double)b[u].x;
-    xy2[2 * (g.pts_off + i) + 1] = (double)b[u].y;
-    xyf[g.pts_off + i] = make_float4(a[u].x, a[u].y, b[u].x, b[u].y);
+    for (int u = 0; u < kGatherU; ++u) {
+      const int i = i0 + u * kGatherThreads;
+      if (i >= m) break;
+      xy1[2 * (g.pts_off + i)] = (double)a[u].x;
+      xy1[2 * (g.pts_off + i) + 1] = (double)a[u].y;
+      xy2[2 * (g.pts_off + i)] = (double)b[u].x;
+      xy2[2 * (g.pts_off + i) + 1] = (double)b[u].y;
+      xyf[g.pts_off + i] = make_float4(a[u].x, a[u].y, b[u].x, b[u].y);
+    }
   }
 }
 
@@ -3666,10 +3669,10 @@ hipError_t run_windows(const VerifyPair* pairs, int npairs, const double* xy1, c
   // Windows whose LO chains run in parallel (small batches with LO slots):
   // the first (later windows' records are many and mostly superseded; two
   // windows measured slower, profiles/r05_m).
-#ifndef SCM_VAR_LOW
-#define SCM_VAR_LOW 1
-#endif
-  constexpr int lo_windows = SCM_VAR_LOW;
+  // (Two windows measured again in round 6, with three parities and the draw
+  // stream: 2.18-2.30 vs 2.19-2.25 ms per batch-1 call, profiles/r06_s -- no
+  // gain.)
+  constexpr int lo_windows = 1;
   // Decoupled draws (speculative schedule with a draw stream): window r's
   // draws and shuffles run on dstream as soon as window r - 2 is replayed (its
   // active list) and window r - 1's prune has run (the lists and counts it
@@ -4002,8 +4005,10 @@ hipError_t launch_gather(const GatherPair* pairs, int npairs, int max_m, const u
                          const float2* kpxy, double* xy1, double* xy2, const int32_t* counts,
                          float4* xyf, hipStream_t stream) {
   if (npairs <= 0 || max_m <= 0) return hipSuccess;
-  hipLaunchKernelGGL(gather_kernel, dim3((unsigned)((max_m + kGatherChunk - 1) / kGatherChunk), npairs),
-                     dim3(kGatherThreads), 0, stream, pairs, matches, kpxy, xy1, xy2, counts, xyf);
+  const unsigned gx =
+      npairs <= kGatherWidePairs ? (unsigned)((max_m + kGatherChunk - 1) / kGatherChunk) : 1u;
+  hipLaunchKernelGGL(gather_kernel, dim3(gx, npairs), dim3(kGatherThreads), 0, stream, pairs, matches,
+                     kpxy, xy1, xy2, counts, xyf);
   return hipGetLastError();
 }
 
