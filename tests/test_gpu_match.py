@@ -76,15 +76,18 @@ def test_segmented_columns(gpu_ctx):
     _same(gpu_ctx, a, b)
 
 
-def test_segmented_columns_unsplit_batch():
-    """A batch of more pairs than the small-batch column split takes
-    (verify_small_batch_pairs, 256): the matcher sweeps whole pairs and n2 >
-    8192 crosses its own 8192-column row segments (a single pair, as in
-    test_segmented_columns, takes the column split).  Table path, kept
-    matches of every row against the oracle's pair matcher."""
+@pytest.mark.parametrize("n", [33, 81, 260])
+def test_segmented_columns_batches(n):
+    """Batches of pairs with n2 > 8192 through the table path, kept matches of
+    every row against the oracle's pair matcher: 259 pairs are more than the
+    small-batch column split takes (verify_small_batch_pairs, 256), so the
+    matcher sweeps whole pairs and crosses its own 8192-column row segments;
+    80 and 32 pairs take the split into 2 and 4 column parts (one-pair jobs
+    below 1,024), whose 8892-column pairs need more tiles than a part's
+    power-of-two width allows -- 2 segments of 128 tiles, 3 of 64.  (A single
+    pair, as in test_segmented_columns, takes 8 parts.)"""
     from scanner_colmap_amd import Context
     from scanner_colmap_amd.codecs import table_rows
-    n = 260
     rng = np.random.default_rng(31)
     descs = [random_descriptors(64 if i % 2 == 0 else 8192 + 700, 300 + i) for i in range(n)]
     for i in range(0, n - 1, 2):
@@ -102,7 +105,7 @@ def test_segmented_columns_unsplit_batch():
     for r in range(n - 1):
         ref = oracle.match_pair(descs[r], descs[r + 1])
         np.testing.assert_array_equal(got[r], ref, err_msg=f"row {r}")
-    assert sum(len(g) for g in got[0::2]) >= 32 * ((n - 1) // 2 + 1)
+    assert sum(len(g) for g in got[0::2]) >= 32 * (n // 2)  # the even rows: 32 unique copies each
 
 
 def test_high_bytes_fast_variant(gpu_ctx):
