@@ -45,6 +45,11 @@ void set_error(const std::string& msg) { g_last_error = msg; }
 namespace {
 
 constexpr int64_t kMaxPairsPerBatch = 16384;
+// (a batch's pairs index grid dimension y of the finalize, rowcheck, recheck and
+// gather launches, at most 65,535; a batch exceeds the cap only with a single
+// row of more pairs -- a stencil of over 16,385 images -- and a launch past
+// 65,535 then fails with its error)
+static_assert(kMaxPairsPerBatch <= 65535, "pairs of a batch on grid y");
 constexpr int64_t kDefaultPairsPerBatch = 8192;
 
 struct ImageTable {
