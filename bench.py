@@ -90,7 +90,7 @@ def parse():
                    help="frames of the SIFT extraction leg (§8f rank 4; 0 = skip), rank 0 at N = 1")
     p.add_argument("--extract-height", type=int, default=1080)
     p.add_argument("--extract-width", type=int, default=1920)
-    p.add_argument("--stencil-batches", default="1:128,64:128,256:1024,512:1024",
+    p.add_argument("--stencil-batches", default="1:128,16:256,64:128,256:1024,512:1024",
                    help="Scanner batch sizes (stencils per execute() call) to time, each as "
                         "batch[:rows] (rows default --stencil-rows)")
     return p.parse_args()
@@ -324,20 +324,36 @@ def lib_sha16() -> str:
     return hashlib.sha256(open(LIB_PATH, "rb").read()).hexdigest()[:16]
 
 
+def pmc_summary_file(pattern: str):
+    """The committed PMC summary to use: the one recorded for the library this
+    process loads (lib_sha16), else the last by name (then reported stale)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)))
+    if not files:
+        return None
+    sha = lib_sha16()
+    for f in reversed(files):
+        try:
+            if json.load(open(f)).get("lib_sha16") == sha:
+                return f
+        except (OSError, ValueError):
+            continue
+    return files[-1]
+
+
 def pmc_traffic(workload: str, kpts: int, images: int, kernel: str):
     """HBM bytes per matcher launch from the committed rocprofv3 PMC summary
     of this workload (profiles/rNN_pmc_match.json, profiles/pmc_summary.py),
     or None when no summary matches the configuration being run."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_match.json")))
-    if not files:
+    f = pmc_summary_file("r*_pmc_match.json")
+    if f is None:
         return None
-    d = json.load(open(files[-1]))
+    d = json.load(open(f))
     wl = WORKLOADS.get(workload, {})
     if (d.get("workload") != workload or kpts != wl.get("kpts") or images != wl.get("images")
             or d.get("kernel") != kernel):
         return None
-    return d, os.path.relpath(files[-1], ROOT)
+    return d, os.path.relpath(f, ROOT)
 
 
 def pmc_sq(kernels: tuple):
@@ -345,15 +361,14 @@ def pmc_sq(kernels: tuple):
     rocprofv3 SQ summary (profiles/rNN_pmc_sq.json, profiles/pmc_sq_summary.py:
     SQ_INSTS_VALU / SQ_INSTS_MFMA, SQ_VALU_MFMA_BUSY_CYCLES and
     SQ_ACTIVE_INST_VALU over the chip's SIMD cycles), or None."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_sq.json")))
-    if not files:
+    f = pmc_summary_file("r*_pmc_sq.json")
+    if f is None:
         return None
-    d = json.load(open(files[-1]))
+    d = json.load(open(f))
     out = {k: d[k] for k in kernels if k in d}
     if out:
         out["lib_sha16"] = d.get("lib_sha16")
-    return (out, os.path.relpath(files[-1], ROOT)) if out else None
+    return (out, os.path.relpath(f, ROOT)) if out else None
 
 
 def main():

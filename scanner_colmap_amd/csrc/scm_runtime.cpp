@@ -1279,7 +1279,11 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
       // (GPU_MAX_HW_QUEUES, 4 by default) and streams beyond them share one,
       // serialising their work; these three are created on distinct queues.
       // (A small batch's neighbours have nothing pending on the drop-in path;
-      // sharing a stream with a pending batch only adds ordering.)
+      // on the table path -- batch caps of <= 1,024 pairs, or a run's last
+      // batch -- they may: sharing a stream with a pending batch only adds
+      // ordering, never a cycle, since a batch waits only on its own events
+      // and on work enqueued before it; tests/test_gpu_fullsize.py
+      // test_k50_shape_many_batches runs several in flight.)
       const int si = (int)(&bs - ctx->sets);
       bs.rstream = ctx->sets[(si + 1) % 3].vstream;
       bs.fstream = ctx->sets[(si + 2) % 3].vstream;

@@ -3582,7 +3582,14 @@ hipError_t set_lds_attr(F f, int static_bytes = 0) {
                              160 * 1024 - static_bytes);
 }
 
-constexpr int kWaveShufflePairs = 256;
+// Small-batch threshold: 1,024 pairs (Scanner op batches up to 53 stencils of
+// 20): the table path's schedule -- one-wave replays, windows doubling from 1
+// round -- left batches of 266-1,007 pairs latency-bound (op batch 16 = 304
+// pairs: 22 ms per call vs 13.8 ms on the small-batch kernels, batch 32: 32
+// vs 26 ms); at 1,216 pairs (batch 64) the small-batch schedule's wider
+// speculative windows cost more than they save (49-50 vs 51-52 ms),
+// profiles/r06_ad.
+constexpr int kWaveShufflePairs = 1024;
 constexpr int kMaxDevices = 64;  // launch_verify's per-device attribute set-up
 constexpr int kSmallFirstWindow = 4;  // rounds of a small batch's first window (run_windows)
 constexpr int kSmallSecondWindowF = 80;  // rounds of its second F window (run_windows)

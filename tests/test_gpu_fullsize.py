@@ -96,11 +96,12 @@ def test_roofline_workload_prefix():
 
 def test_exhaustive_shape():
     """Config 4 shape (South-Building exhaustive: overlap = number of images):
-    40 images x 2048 (780 pairs)."""
-    imgs = Corridor(40, 2048, 40, seed=20253).images()
+    48 images x 2048 (1,128 pairs: one batch above the small-batch threshold,
+    verify_small_batch_pairs, so the table path's window kernels)."""
+    imgs = Corridor(48, 2048, 48, seed=20253).images()
     with Context(0) as ctx:
-        configs = _check_table(ctx, imgs, 40)
-    assert len(configs) == 780
+        configs = _check_table(ctx, imgs, 48)
+    assert len(configs) == 1128
 
 
 def test_exhaustive_full_size_config4():
@@ -153,7 +154,9 @@ def test_exhaustive_full_size_config4():
 
 def test_k50_shape_many_batches():
     """Config 5 shape (4096 kpts, overlap 50): 64 images (1,911 pairs) in
-    batches of 400 pairs, so several batches are in flight at once."""
+    batches of 400 pairs, so several batches are in flight at once (each on
+    the small-batch kernels, whose replay and early-final streams are the
+    other sets' verification streams, here busy with their own batches)."""
     imgs = Corridor(10000, 4096, 50, seed=20254).images(0, 64)
     os.environ["SCM_BATCH_PAIRS"] = "400"
     try:

@@ -79,13 +79,13 @@ def test_segmented_columns(gpu_ctx):
 @pytest.mark.parametrize("n", [33, 81, 260])
 def test_segmented_columns_batches(n):
     """Batches of pairs with n2 > 8192 through the table path, kept matches of
-    every row against the oracle's pair matcher: 259 pairs are more than the
-    small-batch column split takes (verify_small_batch_pairs, 256), so the
-    matcher sweeps whole pairs and crosses its own 8192-column row segments;
-    80 and 32 pairs take the split into 2 and 4 column parts (one-pair jobs
-    below 1,024), whose 8892-column pairs need more tiles than a part's
-    power-of-two width allows -- 2 segments of 128 tiles, 3 of 64.  (A single
-    pair, as in test_segmented_columns, takes 8 parts.)"""
+    every row against the oracle's pair matcher: 259 pairs make 2,452 one-pair
+    matcher jobs, enough to fill the CUs, so the matcher sweeps whole pairs and
+    crosses its own 8192-column row segments; 80 and 32 pairs take the column
+    split into 2 and 4 parts (one-pair jobs below 1,024), whose 8892-column
+    pairs need more tiles than a part's power-of-two width allows -- 2
+    segments of 128 tiles, 3 of 64.  (A single pair, as in
+    test_segmented_columns, takes 8 parts.)"""
     from scanner_colmap_amd import Context
     from scanner_colmap_amd.codecs import table_rows
     rng = np.random.default_rng(31)
