@@ -1,0 +1,9 @@
+# Round 6: kernel trace of Scanner op batches of 64 stencils (stencil probe).
+# usage (on the box): bash probes/g_r06ag.sh SET
+set -e
+S=$1
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/$S
+mkdir -p $O
+cd /tmp && export TMPDIR=/tmp
+ROWS=256 B=64 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $O/trace -o run -- python3 $R/probes/stencil_probe.py > $O/stencil_trace.log 2>&1
