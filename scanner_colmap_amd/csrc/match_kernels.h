@@ -83,5 +83,11 @@ hipError_t launch_match_finalize(const PairDesc* pairs, int npairs, const uint2*
 hipError_t launch_u8_to_bf16(const uint8_t* in, uint16_t* out, int64_t n, hipStream_t stream);
 hipError_t launch_u8_to_i8(const uint8_t* in, uint8_t* out, int32_t* csum, int64_t nrows,
                            hipStream_t stream);
+// Copies `bytes` (a multiple of 16) from pinned host memory (its device
+// address, hipHostGetDevicePointer) into device memory with a kernel on
+// `stream`: a batch's descriptor tables, uploaded on the stream's own queue
+// instead of the copy engine, where a copy waits behind every earlier copy of
+// another stream that shares the engine (profiles/r06_ah).
+hipError_t launch_stage_upload(const void* host_dev_src, void* dst, size_t bytes, hipStream_t stream);
 
 }  // namespace scm

@@ -40,6 +40,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <climits>
 
 #include "match_kernels.h"
@@ -1473,6 +1474,28 @@ hipError_t launch_u8_to_i8(const uint8_t* in, uint8_t* out, int32_t* csum, int64
   const int64_t threads = nrows * 8;
   hipLaunchKernelGGL(u8_to_i8_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0,
                      stream, in, out, csum, nrows);
+  return hipGetLastError();
+}
+
+namespace {
+constexpr int kUploadThreads = 256;
+constexpr int kUploadMaxBlocks = 512;
+__global__ void __launch_bounds__(kUploadThreads)
+    stage_upload_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, int64_t n) {
+  const int64_t step = (int64_t)gridDim.x * kUploadThreads;
+  for (int64_t i = (int64_t)blockIdx.x * kUploadThreads + threadIdx.x; i < n; i += step)
+    dst[i] = src[i];
+}
+}  // namespace
+
+hipError_t launch_stage_upload(const void* host_dev_src, void* dst, size_t bytes,
+                               hipStream_t stream) {
+  if (bytes == 0) return hipSuccess;
+  if (bytes % sizeof(uint4) != 0) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)(bytes / sizeof(uint4));
+  const int64_t blocks = std::min<int64_t>((n + kUploadThreads - 1) / kUploadThreads, kUploadMaxBlocks);
+  hipLaunchKernelGGL(stage_upload_kernel, dim3((unsigned)blocks), dim3(kUploadThreads), 0, stream,
+                     reinterpret_cast<const uint4*>(host_dev_src), reinterpret_cast<uint4*>(dst), n);
   return hipGetLastError();
 }
 

@@ -57,6 +57,7 @@ struct DevBuf {
 // Pinned host staging buffer.
 struct HostBuf {
   void* ptr = nullptr;
+  void* dptr = nullptr;  // its device address (kernels read it: launch_stage_upload)
   size_t bytes = 0;
   int ensure(size_t need) {
     if (need <= bytes) return SCM_OK;
@@ -68,13 +69,19 @@ struct HostBuf {
       set_error("hipHostMalloc failed");
       return SCM_E_NOMEM;
     }
+    if (hipHostGetDevicePointer(&dptr, ptr, 0) != hipSuccess) {
+      (void)hipHostFree(ptr);
+      ptr = dptr = nullptr;
+      set_error("hipHostGetDevicePointer failed");
+      return SCM_E_DEVICE;
+    }
     bytes = want;
     return SCM_OK;
   }
   template <typename T> T* as() const { return reinterpret_cast<T*>(ptr); }
   void release() {
     if (ptr) (void)hipHostFree(ptr);
-    ptr = nullptr;
+    ptr = dptr = nullptr;
     bytes = 0;
   }
 };

@@ -204,6 +204,7 @@ struct SpecKey {
 // Pinned host result buffer: the DMA target of each batch's results.
 struct PinnedOut {
   void* host = nullptr;
+  void* dev = nullptr;  // its device address (launch_stage_upload reads the offsets there)
   size_t bytes = 0;
   int ensure(size_t need) {
     if (need <= bytes) return SCM_OK;
@@ -214,12 +215,18 @@ struct PinnedOut {
       set_error("hipHostMalloc of " + std::to_string(want) + " bytes failed");
       return SCM_E_NOMEM;
     }
+    if (hipHostGetDevicePointer(&dev, host, 0) != hipSuccess) {
+      (void)hipHostFree(host);
+      host = dev = nullptr;
+      set_error("hipHostGetDevicePointer failed");
+      return SCM_E_DEVICE;
+    }
     bytes = want;
     return SCM_OK;
   }
   void release() {
     if (host) (void)hipHostFree(host);
-    host = nullptr;
+    host = dev = nullptr;
     bytes = 0;
   }
 };
@@ -785,6 +792,7 @@ VerifyParams make_params(const scm_matching_options& o, int iteration = 0) {
 }
 
 size_t align256(size_t x) { return (x + 255) / 256 * 256; }
+size_t align16(size_t x) { return (x + 15) / 16 * 16; }
 
 // Stream priorities: the verification streams (the longer stage, whose
 // windows are short dependent kernels) run at high priority so that their
@@ -996,7 +1004,7 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
   SCM_TRY(bs.matches.ensure(std::max<int64_t>(mo, 1) * sizeof(uint2)));
   SCM_TRY(bs.masks.ensure(std::max<int64_t>(mo, 1)));
   SCM_TRY(bs.counts.ensure(P * sizeof(int32_t)));
-  SCM_TRY(bs.offsets.ensure((P + 1) * sizeof(int64_t)));
+  SCM_TRY(bs.offsets.ensure(align16((P + 1) * sizeof(int64_t))));
   bs.off_counts = 0;
   bs.off_offsets = align256(bs.off_counts + P * sizeof(int32_t));
   bs.off_vout = align256(bs.off_offsets + (P + 1) * sizeof(int64_t));
@@ -1025,13 +1033,17 @@ int enqueue_match(scm_context* ctx, BatchSet& bs, const ImageTable& t,
     max_cols = std::max(max_cols, pds[k].n2);
   }
   hipStream_t sm = ctx->stream;
-  // jobs, pair descriptors and match offsets in one copy (one blit on the
-  // small-batch critical path instead of three)
+  // jobs, pair descriptors and match offsets in one upload (one launch on the
+  // small-batch critical path instead of three), by kernel on the matching
+  // stream: as a copy-engine transfer it queued behind the previous batch's
+  // result copies (another stream's, waiting for that batch's verification
+  // chain), and the bench's last matcher started ~110 ms after its launch
+  // (profiles/r06_ah)
   SCM_TRY(bs.mdesc.ensure(s_cnt));
   bs.d_jobs = reinterpret_cast<MatchJob*>(bs.mdesc.as<uint8_t>());
   bs.d_pairs = reinterpret_cast<PairDesc*>(bs.mdesc.as<uint8_t>() + s_pairs);
   bs.d_moff = reinterpret_cast<int64_t*>(bs.mdesc.as<uint8_t>() + s_mo);
-  SCM_HIP(hipMemcpyAsync(bs.mdesc.ptr, st, s_mo + P * sizeof(int64_t), hipMemcpyHostToDevice, sm));
+  SCM_HIP(launch_stage_upload(bs.stage.dptr, bs.mdesc.ptr, align16(s_mo + P * sizeof(int64_t)), sm));
   if (given) {
     std::memcpy(st + s_cnt, given_counts, P * sizeof(int32_t));
     SCM_HIP(hipMemcpyAsync(bs.counts.ptr, st + s_cnt, P * sizeof(int32_t), hipMemcpyHostToDevice,
@@ -1133,6 +1145,10 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
     total += counts[k];
   }
   offs[P] = total;
+  // The offsets go to the device now (by kernel, as every table upload of the
+  // pipeline: launch_stage_upload), ahead of the verification chain.
+  SCM_HIP(launch_stage_upload(reinterpret_cast<uint8_t*>(bs.out.dev) + bs.off_offsets,
+                              bs.offsets.ptr, align16((P + 1) * sizeof(int64_t)), sv));
   const int64_t V = (int64_t)order.size();
   SCM_HIP(hipEventRecord(bs.ev[4], sv));
   if (verify) SCM_TRY(bs.dvout.ensure(P * sizeof(VerifyOut)));  // zeroed by enqueue_match
@@ -1170,15 +1186,15 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
     SCM_TRY(bs.scratch.ensure(std::max<int64_t>(scr, 1) * sizeof(double)));
     SCM_TRY(bs.snaps.ensure(V * kVerifySnapWords * sizeof(uint32_t)));
     const size_t s_v = align256(V * sizeof(GatherPair));
-    SCM_TRY(bs.vstage.ensure(s_v + V * sizeof(VerifyPair)));
+    SCM_TRY(bs.vstage.ensure(align16(s_v + V * sizeof(VerifyPair))));
     uint8_t* st = bs.vstage.as<uint8_t>();
     std::memcpy(st, gps.data(), V * sizeof(GatherPair));
     std::memcpy(st + s_v, vps.data(), V * sizeof(VerifyPair));
     // both tables in one copy
-    SCM_TRY(bs.vdesc.ensure(s_v + V * sizeof(VerifyPair)));
+    SCM_TRY(bs.vdesc.ensure(align16(s_v + V * sizeof(VerifyPair))));
     bs.d_gpairs = reinterpret_cast<GatherPair*>(bs.vdesc.as<uint8_t>());
     bs.d_vpairs = reinterpret_cast<VerifyPair*>(bs.vdesc.as<uint8_t>() + s_v);
-    SCM_HIP(hipMemcpyAsync(bs.vdesc.ptr, st, s_v + V * sizeof(VerifyPair), hipMemcpyHostToDevice, sv));
+    SCM_HIP(launch_stage_upload(bs.vstage.dptr, bs.vdesc.ptr, align16(s_v + V * sizeof(VerifyPair)), sv));
     SCM_HIP(launch_gather(bs.d_gpairs, (int)V, max_m, bs.matches.as<uint2>(),
                           t.kpxy.as<float2>(), bs.xy1.as<double>(), bs.xy2.as<double>(), nullptr,
                           bs.xyf.as<float4>(), sv));
@@ -1340,8 +1356,6 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
   // pinned host buffer (counts are already there).
   SCM_TRY(bs.dpack.ensure(std::max<int64_t>(total, 1) * sizeof(uint2)));
   SCM_TRY(bs.dpmask.ensure(std::max<int64_t>(total, 1)));
-  SCM_HIP(hipMemcpyAsync(bs.offsets.ptr, offs, (P + 1) * sizeof(int64_t), hipMemcpyHostToDevice,
-                         sv));
   SCM_HIP(launch_compact(bs.counts.as<int32_t>(), (int)P, bs.offsets.as<int64_t>(),
                          bs.d_moff, bs.matches.as<uint2>(),
                          bs.masks.as<uint8_t>(), bs.dpack.as<uint2>(), bs.dpmask.as<uint8_t>(),
