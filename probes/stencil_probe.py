@@ -15,6 +15,15 @@ def main():
     B = int(os.environ.get("B", "1"))
     kpts = int(os.environ.get("KPTS", "8192"))
     K = int(os.environ.get("K", "20"))
+    pre = os.environ.get("PRE", "")
+    if pre == "torch":  # torch's HIP initialisation first (as in bench.py)
+        import torch
+        torch.zeros(1, device="cuda")
+    elif pre in ("spin", "yield", "block"):  # the device's host-wait mode
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        flag = {"spin": 1, "yield": 2, "block": 4}[pre]
+        print("hipSetDeviceFlags", pre, hip.hipSetDeviceFlags(flag), flush=True)
     from scanner_colmap_amd import Context
     from scanner_colmap_amd.codecs import table_rows
     from scanner_colmap_amd.synthetic import Corridor

@@ -51,6 +51,9 @@ constexpr int64_t kMaxPairsPerBatch = 16384;
 // 65,535 then fails with its error)
 static_assert(kMaxPairsPerBatch <= 65535, "pairs of a batch on grid y");
 constexpr int64_t kDefaultPairsPerBatch = 8192;
+// Scanner op calls that fit one batch: cut into up to kOpCallBatches batches
+// of at least verify_small_batch_pairs() pairs each (run_rows).
+constexpr int64_t kOpCallBatches = 3;
 
 struct ImageTable {
   int64_t n = 0;
@@ -233,11 +236,30 @@ struct PinnedOut {
 
 // Diagnostics builds only (-DSCM_DIAG_HOST_TIMES, probes/build_*): host
 // timestamps of one execute() call's steps, printed to stderr per call.
+// With them, GPU times of the first batch's stage events from an event
+// recorded on the matching stream at the call's start (g_hte, microseconds).
 #ifdef SCM_DIAG_HOST_TIMES
 std::chrono::steady_clock::time_point g_ht[16];
 #define SCM_HT(k) (g_ht[k] = std::chrono::steady_clock::now())
+hipEvent_t g_hte = nullptr;
+float g_hte_us[4] = {0, 0, 0, 0};
+#define SCM_HTE_RECORD(s) \
+  do { \
+    if (!g_hte) (void)hipEventCreate(&g_hte); \
+    (void)hipEventRecord(g_hte, s); \
+  } while (0)
+#define SCM_HTE_READ(evs) \
+  do { \
+    for (int i_ = 0; i_ < 4; ++i_) { \
+      float ms_ = -1.f; \
+      (void)hipEventElapsedTime(&ms_, g_hte, (evs)[i_]); \
+      g_hte_us[i_] = ms_ * 1000.f; \
+    } \
+  } while (0)
 #else
 #define SCM_HT(k) ((void)0)
+#define SCM_HTE_RECORD(s) ((void)0)
+#define SCM_HTE_READ(evs) ((void)0)
 #endif
 
 // One in-flight batch: device workspace, descriptor staging, results.
@@ -1126,6 +1148,7 @@ int enqueue_verify(scm_context* ctx, BatchSet& bs, bool verify, int iteration = 
   SCM_HT(5);
   SCM_HIP(hipEventSynchronize(bs.ev[3]));
   SCM_HT(6);
+  SCM_HTE_READ(bs.ev);
   uint8_t* outh = reinterpret_cast<uint8_t*>(bs.out.host);
   const int32_t* counts = reinterpret_cast<const int32_t*>(outh + bs.off_counts);
   hipStream_t sv = bs.vstream;
@@ -1851,6 +1874,31 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
   // (The remainder batch first instead of last measured slower, 44.4/44.5K vs
   // 47.4/47.6K pairs/s, profiles/r05_b_ab_*.)
   const int64_t first_cap = ctx->batch_pairs;
+  // Scanner op calls (execute(): one packed output, no kept rows) that fit
+  // one batch: cut into nb <= kOpCallBatches batches of about equal pairs
+  // (whole rows), each of at least a small batch's pairs, so that each
+  // batch's matching overlaps the previous batch's verification instead of
+  // the call running its matcher and then its verification alone.  Op calls
+  // of 256 stencils (4,864 pairs): 164.4 ms per call in one batch, 147.2 in
+  // two, 136.9 in three; 64 stencils (1,216 pairs) stay one batch (49.2 vs
+  // 50.8 in two); calls beyond one batch keep the table path's cut (two
+  // equal batches at 512 stencils: no gain), profiles/r06_ao.
+  std::vector<char> opens(nr, 0);  // rows that open a batch of their own
+  if (keep_row0 < 0 && !streamed && !emit) {
+    int64_t total = 0;
+    for (const RowPlan& rp : plan) total += (int64_t)rp.nb.size();
+    const int64_t nb = std::min<int64_t>(kOpCallBatches, total / verify_small_batch_pairs());
+    if (nb >= 2 && total <= ctx->batch_pairs) {
+      int64_t acc = 0, k = 1;
+      for (int64_t i = 0; i < nr && k < nb; ++i) {
+        if (acc > 0 && acc * nb >= k * total) {
+          opens[i] = 1;
+          ++k;
+        }
+        acc += (int64_t)plan[i].nb.size();
+      }
+    }
+  }
   Batch cur;
   int64_t cur_bytes = 0, cur_small = 0;
   for (int64_t i = 0; i < nr; ++i) {
@@ -1859,7 +1907,7 @@ int run_rows(scm_context* ctx, const ImageTable& t, const std::vector<RowPlan>& 
     int64_t row_bytes = 0;
     for (int32_t b : rp.nb) row_bytes += pair_workspace_bytes(t.ndesc[rp.pivot], t.ndesc[b]);
     const int64_t have = (int64_t)cur.specs.size();
-    const int64_t cap = batches.empty() ? first_cap : ctx->batch_pairs;
+    const int64_t cap = opens[i] ? have : batches.empty() ? first_cap : ctx->batch_pairs;
     // a batch small enough for the small-batch kernels holds their larger
     // round buffers and parallel-LO slots (enqueue_verify)
     const int64_t row_small = np * small_batch_extra_bytes(t.ndesc[rp.pivot]);
@@ -2230,6 +2278,7 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
   const int64_t ne = batch * stencil_size;
   const auto h0 = std::chrono::steady_clock::now();
   SCM_HT(0);
+  SCM_HTE_RECORD(ctx->stream);
   std::unordered_map<Src, int64_t, SrcHash> first;  // buffers -> first element
   std::vector<int64_t> of(ne), now_e, spec_e;
   for (int64_t e = 0; e < ne; ++e) {
@@ -2378,6 +2427,8 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
     for (size_t i = 1; i < sizeof(ks) / sizeof(ks[0]); ++i)
       line += " " + std::to_string(ks[i]) + ":" +
               std::to_string((int)std::chrono::duration<double, std::micro>(g_ht[ks[i]] - g_ht[ks[0]]).count());
+    line += " | gpu ev0-3 us";
+    for (float u : g_hte_us) line += " " + std::to_string((int)u);
     fprintf(stderr, "%s\n", line.c_str());
   }
 #endif

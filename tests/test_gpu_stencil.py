@@ -46,6 +46,28 @@ def test_execute_batches_equal_table_oracle(batch):
     assert calls >= 1
 
 
+def test_execute_batch_split_into_batches_equal_table_oracle():
+    """Op calls of more than two small batches' pairs run as 2 or 3 pipelined
+    batches (run_rows kOpCallBatches): 110 stencils of 19 pairs (2,090: two
+    batches), then 70 (1,330: one), and a call of 170 (3,230: three) in a
+    second context.  Every row equals the oracle's table run."""
+    n, K = 180, 20
+    ids, kps, descs = table_rows(Corridor(n, 160, K, seed=64).images())
+    ref_ids, ref_tvgs = oracle.table_run(ids, kps, descs, K, 0, n)
+    with Context(0) as ctx:
+        got_ids, got_tvgs = [], []
+        for r0, r1 in ((0, 110), (110, n)):
+            a, b = ctx.execute_batch(_stencils(ids, kps, descs, K, r0, r1))
+            got_ids += a
+            got_tvgs += b
+    assert got_ids == ref_ids
+    assert got_tvgs == ref_tvgs
+    with Context(0) as ctx:
+        a, b = ctx.execute_batch(_stencils(ids, kps, descs, K, 0, 170))
+    assert a == ref_ids[:170]
+    assert b == ref_tvgs[:170]
+
+
 def test_execute_stencil_repeated_ids_and_table_interleave():
     """Repeated ids inside a stencil (the :141-144 dedup), a table run between
     two execute calls (separate HBM tables), and an id whose features change
