@@ -2397,27 +2397,34 @@ int execute_rows(scm_context* ctx, int64_t batch, int64_t stencil_size,
   }
   ctx->spec_keys.clear();
   for (const auto& f : first) ctx->spec_keys[f.first] = SpecKey{ekey[f.second], fingerprint(rows[f.second])};
-  for (int64_t r = 0; r < batch; ++r) {
+  // The output elements, one task per row on the worker pool (their fresh
+  // pages' first touch and the copies in parallel).
+  for (int64_t r = 0; r < batch; ++r) pair_image_ids_out[r] = tvgs_out[r] = scm_blob{nullptr, 0};
+  std::atomic<bool> oom{false};
+  ctx->pool.run(batch, [&](int64_t r) {
     const int64_t a = pk.row_off[2 * r], b = pk.row_off[2 * r + 1], c = pk.row_off[2 * r + 2];
     uint8_t* pa = (uint8_t*)std::malloc((size_t)std::max<int64_t>(b - a, 1));
     uint8_t* pb = (uint8_t*)std::malloc((size_t)std::max<int64_t>(c - b, 1));
     if (!pa || !pb) {
       std::free(pa);
       std::free(pb);
-      for (int64_t q = 0; q < r; ++q) {
-        scm_blob_free(&pair_image_ids_out[q]);
-        scm_blob_free(&tvgs_out[q]);
-      }
-      if (!pool_give(pk.data)) std::free(pk.data);
-      set_error("malloc failed");
-      return SCM_E_NOMEM;
+      oom.store(true);
+      return;
     }
     std::memcpy(pa, pk.data + a, (size_t)(b - a));
     std::memcpy(pb, pk.data + b, (size_t)(c - b));
     pair_image_ids_out[r] = scm_blob{pa, (size_t)(b - a)};
     tvgs_out[r] = scm_blob{pb, (size_t)(c - b)};
-  }
+  });
   if (!pool_give(pk.data)) std::free(pk.data);
+  if (oom.load()) {
+    for (int64_t r = 0; r < batch; ++r) {
+      scm_blob_free(&pair_image_ids_out[r]);
+      scm_blob_free(&tvgs_out[r]);
+    }
+    set_error("malloc failed");
+    return SCM_E_NOMEM;
+  }
   ctx->t_out = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h3).count();
 #ifdef SCM_DIAG_HOST_TIMES
   SCM_HT(13);
